@@ -1,0 +1,153 @@
+/*
+ * sat_hip.h — C ABI of the MI355X-native Show-Attend-and-Tell training path.
+ *
+ * The reference (yvokeller/Show-Attend-and-Tell) has no FFI: its hot path is the
+ * PyTorch nn.Module API (encoder.py, attention.py, decoder.py) called from the
+ * inner loop of train.py.  This header is the boundary *below* that API: every
+ * entry point replaces a PyTorch op sequence of the reference, cited as
+ * file:line.  The Python package (show-attend-and-tell_amd/, imported as
+ * ``sat_amd``) keeps the reference module API and binds these symbols with
+ * ctypes; a maintainer-side binding is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - All tensor arguments are DEVICE pointers allocated by the caller (PyTorch's
+ *     caching allocator owns every buffer, including workspaces).
+ *   - ``stream`` is a hipStream_t (pass torch.cuda.current_stream().cuda_stream);
+ *     every call is asynchronous on it and performs no host synchronisation, so
+ *     calls are legal inside hipGraph stream capture.
+ *   - Return value: 0 on success, SAT_ERR_INVALID for a rejected shape/argument,
+ *     otherwise the hipError_t of the failing HIP call.  The Python layer raises
+ *     RuntimeError on non-zero, as the reference raises Python exceptions.
+ *   - dtype: SAT_F32 = exact fp32 path (parity mode, fp32-input MFMA);
+ *            SAT_BF16 = bf16 operands, fp32 accumulation (performance mode).
+ *   - Layouts are row-major; image tensors are NHWC (channels last), which makes
+ *     the encoder's permute(0,2,3,1).view(B,-1,C) (encoder.py:37-39) free.
+ */
+#ifndef SAT_HIP_H_
+#define SAT_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SAT_ABI_VERSION 1
+
+enum { SAT_F32 = 0, SAT_BF16 = 1 };
+enum { SAT_ACT_NONE = 0, SAT_ACT_RELU = 1, SAT_ACT_TANH = 2, SAT_ACT_SIGMOID = 3 };
+enum { SAT_OK = 0, SAT_ERR_INVALID = 9001 };
+
+/* Implicit-GEMM convolution geometry (NHWC input, [Cout][KH][KW][C] weights). */
+typedef struct {
+  int N, H, W, C, KH, KW, stride, pad, OH, OW;
+} SatConvGeom;
+
+/* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),
+ * A(m,k) = transA ? A[k*lda+m] : A[m*lda+k];  B(n,k) = transB ? B[k*ldb+n] : B[n*ldb+k].
+ * Optional aux output receives the same (post-activation) value in aux_dtype.
+ * Replaces torch.nn.Linear forward/backward (e.g. attention.py:15-16,
+ * decoder.py:99,125,143-146,151-158). */
+typedef struct {
+  int M, N, K, dtype;
+  const void* A; int64_t lda; int transA;
+  const void* B; int64_t ldb; int transB;
+  void* C; int64_t ldc; int c_dtype;
+  float alpha, beta;
+  const float* bias;
+  const void* add1; int64_t ld_add1; int add1_dtype;
+  int act;
+  void* aux; int64_t ld_aux; int aux_dtype;
+} SatGemmArgs;
+
+/* Decoder problem description (decoder.py:9-67 constructor flags + shapes). */
+typedef struct {
+  int B, L, D, E, V, T;       /* T = caption length; the decoder runs T-1 steps (decoder.py:77) */
+  int tf, ado, attention, bert, training;
+  int dtype;
+  int start_token;            /* 0 = <start> (decoder.py:82); 101 = [CLS] (decoder.py:80) */
+  int has_dropout_mask;       /* training: 1 = use the caller's keep-mask, 0 = draw from seed */
+  uint64_t seed;
+} SatDecoderDims;
+
+/* Element offsets of every decoder parameter inside one flat fp32 buffer.  Keys
+ * map to the reference state_dict.  Groups the kernels read as
+ * one matrix are adjacent:
+ *   init_w = [init_h.weight ; init_c.weight] [2E,D],  init_b = [init_h.bias ; init_c.bias]
+ *   hcat_w = [attention.U.weight ; f_beta.weight ; lstm.weight_hh] [E+D+4E, E]
+ *   hcat_b = [attention.U.bias ; f_beta.bias ; lstm.bias_hh]. */
+typedef struct {
+  int64_t embedding, init_w, init_b, hcat_w, hcat_b, attW_w, attW_b, v_w, v_b, wih, bih;
+  int64_t fh_w, fh_b, fz_w, fz_b, fout_w, fout_b, do_w, do_b;
+  int64_t total;
+} SatDecoderLayout;
+
+int sat_abi_version(void);
+const char* sat_error_string(int code);
+
+/* --- generic building blocks -------------------------------------------- */
+int sat_gemm(const SatGemmArgs* args, void* stream);
+/* elementwise cast between SAT_F32 and SAT_BF16 storage (n elements). */
+int sat_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, void* stream);
+
+/* mean over L: a [B,L,D] -> out_f32 [B,D] (nullable) and out_t [B,D] in dtype (nullable);
+ * img_features.mean(dim=1) of decoder.py:139 / the uniform-attention context of decoder.py:104. */
+int sat_mean_rows_abi(const void* a, int B, int L, int D, int dtype, float* out_f32, void* out_t, void* stream);
+
+/* --- encoder (encoder.py:33-40 with the torchvision trunks) ------------- */
+/* NCHW fp32 image batch -> NHWC (dtype) with channels zero-padded to Cp. */
+int sat_nchw_to_nhwc(int N, int C, int H, int W, int Cp, int dtype, const float* x, void* y, void* stream);
+/* y = act(conv(x, w) + bias [+ residual]); x NHWC [N,H,W,C], y NHWC [N,OH,OW,Cout];
+ * covers Conv2d+ReLU (VGG19) and Conv2d+BatchNorm(eval, folded)+[residual]+ReLU (ResNet152). */
+int sat_conv2d_nhwc(const SatConvGeom* g, int Cout, int dtype, const void* x, const void* w,
+                    const float* bias, const void* residual, int relu, void* y, void* stream);
+/* MaxPool2d (floor mode, -inf padding) on NHWC. */
+int sat_maxpool2d_nhwc(int N, int H, int W, int C, int k, int stride, int pad, int dtype,
+                       const void* x, void* y, int OH, int OW, void* stream);
+
+/* --- attention (attention.py:14-21), standalone module forward ----------- */
+/* Ws: workspace [B,L,E] fp32. Weights fp32 (U_w [E,E], W_w [E,D], v_w [E]); W_w_lp (bf16 copy)
+ * required when dtype == SAT_BF16. context [B,D] fp32, alpha [B,L] fp32. */
+int sat_attention_forward(int B, int L, int D, int E, int dtype, const void* img_features,
+                          const float* hidden, const float* U_w, const float* U_b,
+                          const float* W_w, const void* W_w_lp, const float* W_b,
+                          const float* v_w, const float* v_b, float* ws_scratch,
+                          float* context, float* alpha, void* stream);
+
+/* --- decoder (decoder.py:69-158) ----------------------------------------- */
+size_t sat_decoder_workspace_bytes(const SatDecoderDims* d);
+/* preds [B,T-1,V] (dtype), alphas [B,T-1,L] fp32, tokens [B,T-1] int32 = token fed at each step. */
+int sat_decoder_forward(const SatDecoderDims* d, const SatDecoderLayout* lay, const float* params,
+                        const void* params_lp, const void* img_features, const int64_t* captions,
+                        const uint8_t* dropout_mask, void* workspace, size_t workspace_bytes,
+                        void* preds, float* alphas, int32_t* tokens, void* stream);
+/* phase 1 = output-head gradients only (f_out/f_h/f_z/deep_output), 2 = the rest
+ * (needs phase 1 first), 3 = both.  accumulate=0 overwrites the active grads. */
+int sat_decoder_backward(const SatDecoderDims* d, const SatDecoderLayout* lay, const float* params,
+                         const void* params_lp, const void* img_features, void* workspace,
+                         size_t workspace_bytes, const void* preds, const float* alphas,
+                         const void* d_preds, const float* d_alphas, float* grads, int accumulate,
+                         int phase, void* stream);
+
+/* --- loss + metrics (train.py:135-162, utils.py:44-80,101-107) ----------- */
+size_t sat_caption_loss_workspace_bytes(int B, int T, int L);
+/* out[0]=loss, [1]=CE, [2]=att-reg, [3]=#top1-correct, [4]=#top5-correct, [5]=#non-pad targets,
+ * [6]=caption length (tokens not in skip_ids). */
+int sat_caption_loss_forward(int B, int T, int V, int L, int dtype, const void* preds,
+                             const float* alphas, const int64_t* captions, float alpha_c,
+                             int pad_id, int skip0, int skip1, int skip2, void* workspace,
+                             float* out, void* stream);
+int sat_caption_loss_backward(int B, int T, int V, int L, int dtype, const void* preds,
+                              const int64_t* captions, float alpha_c, void* workspace,
+                              const float* grad_out, void* d_preds, float* d_alphas, void* stream);
+
+/* --- optimiser (torch.optim.Adam single-tensor step, train.py:71,164) ---- */
+int sat_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                  void* param_lp, int64_t n, float beta1, float beta2, float eps,
+                  float step_size, float bias_correction2_sqrt, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAT_HIP_H_ */

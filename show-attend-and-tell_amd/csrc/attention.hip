@@ -1,0 +1,322 @@
+// Fused soft-attention step (attention.py:14-21) with the decoder's gating
+// scalar (decoder.py:97-100), and its backward.
+//
+// Forward, one launch per decoder step, grid (B, NS): every workgroup scores
+// all L annotation slots of its row (e_l = v . tanh(Ws[b,l,:] + U h_b) + b_v,
+// wave per slot, lanes over E, shuffle reduction), runs the softmax over L in
+// one wave, then accumulates context[b, d] = sum_l alpha_l a[b,l,d] for its
+// D-slice (lanes over d with 16-B loads, waves over l, LDS fold) and applies the
+// gate sigma(f_beta h + b).  The loop-invariant Ws = a W^T + b is hoisted out of
+// the time loop (one GEMM per batch) instead of being recomputed every step as
+// the reference does (attention.py:16 called from decoder.py:98).
+//
+// Backward, two launches per step: (1) grid (B, NS): dL/dcontext, the gate
+// gradient and per-slice partial dL/dalpha; (2) grid B: softmax backward,
+// recomputed tanh, dL/d(U h), and running sums of dL/dWs, dL/dv, dL/dv.bias
+// over the time loop (weight gradients are formed once after the loop).
+#include "sat_common.h"
+#include "sat_internal.h"
+
+namespace {
+
+constexpr int kMaxL = 1024;
+
+template <typename T> struct V16;
+template <> struct V16<float> { static constexpr int N = 4; };
+template <> struct V16<bf16> { static constexpr int N = 8; };
+
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, float* o) {
+  if constexpr (sizeof(T) == 4) {
+    float4 v = *(const float4*)p;
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  } else {
+    uint2 v = *(const uint2*)p;
+    const bf16* h = (const bf16*)&v;
+    o[0] = (float)h[0]; o[1] = (float)h[1]; o[2] = (float)h[2]; o[3] = (float)h[3];
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void loadv(const T* p, float* o) {  // 16 bytes
+  uint4 v = *(const uint4*)p;
+  const T* h = (const T*)&v;
+#pragma unroll
+  for (int j = 0; j < V16<T>::N; ++j) o[j] = (float)h[j];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
+  constexpr int VD = V16<T>::N;
+  __shared__ float s_alpha[kMaxL];
+  __shared__ float s_red[4][64 * VD];
+  const int b = blockIdx.x, s = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int L = a.L, D = a.D, E = a.E;
+  const T* Ws = (const T*)a.Ws + (long)b * L * E;
+  const float* uh = a.uh + (long)b * a.uh_ld;
+
+  // ---- scores ----
+  const float bv = a.v_b[0];
+  for (int l = w; l < L; l += 4) {
+    const T* wr = Ws + (long)l * E;
+    float acc = 0.f;
+    for (int e = lane * 4; e < E; e += 256) {
+      float x[4];
+      load4<T>(wr + e, x);
+      float4 u = *(const float4*)(uh + e);
+      float4 vv = *(const float4*)(a.v_w + e);
+      acc += vv.x * tanhf(x[0] + u.x) + vv.y * tanhf(x[1] + u.y) + vv.z * tanhf(x[2] + u.z) + vv.w * tanhf(x[3] + u.w);
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) s_alpha[l] = acc + bv;
+  }
+  __syncthreads();
+  // ---- softmax over L (one wave) ----
+  if (w == 0) {
+    float m = -INFINITY;
+    for (int l = lane; l < L; l += 64) m = fmaxf(m, s_alpha[l]);
+    m = wave_max(m);
+    float sum = 0.f;
+    for (int l = lane; l < L; l += 64) {
+      float e = expf(s_alpha[l] - m);
+      s_alpha[l] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    float inv = 1.0f / sum;
+    for (int l = lane; l < L; l += 64) {
+      float al = s_alpha[l] * inv;
+      s_alpha[l] = al;
+      if (s == 0 && a.alpha) a.alpha[(long)b * a.alpha_ld + l] = al;
+    }
+  }
+  if (s == 0 && a.uh_save) {
+    for (int e = tid; e < E; e += 256) a.uh_save[(long)b * a.uh_save_ld + e] = uh[e];
+  }
+  __syncthreads();
+  // ---- context for this D-slice ----
+  const int d0 = s * 64 * VD + lane * VD;
+  float part[VD];
+#pragma unroll
+  for (int j = 0; j < VD; ++j) part[j] = 0.f;
+  if (d0 < D) {
+    const T* ab = (const T*)a.a + (long)b * L * D + d0;
+    for (int l = w; l < L; l += 4) {
+      float x[VD];
+      loadv<T>(ab + (long)l * D, x);
+      const float al = s_alpha[l];
+#pragma unroll
+      for (int j = 0; j < VD; ++j) part[j] += al * x[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < VD; ++j) s_red[w][lane * VD + j] = part[j];
+  __syncthreads();
+  for (int i = tid; i < 64 * VD; i += 256) {
+    const int d = s * 64 * VD + i;
+    if (d >= D) continue;
+    // fixed summation order over the four wave partials
+    const float c = (s_red[0][i] + s_red[1][i]) + (s_red[2][i] + s_red[3][i]);
+    a.ctx[(long)b * a.ctx_ld + d] = c;
+    if (a.ctx_t) ((T*)a.ctx_t)[(long)b * a.ctx_t_ld + d] = (T)c;
+    if (a.gate_pre) {
+      const float g = 1.0f / (1.0f + expf(-a.gate_pre[(long)b * a.gate_ld + d]));
+      if (a.gate) a.gate[(long)b * a.gate_out_ld + d] = g;
+      if (a.gated) ((T*)a.gated)[(long)b * a.gated_ld + d] = (T)(g * c);
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd1_kernel(AttnBwdArgs a) {
+  constexpr int VD = V16<T>::N;
+  const int b = blockIdx.x, s = blockIdx.y, NS = gridDim.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int L = a.L, D = a.D, E = a.E;
+  const int d0 = s * 64 * VD + lane * VD;
+  float dctx[VD];
+#pragma unroll
+  for (int j = 0; j < VD; ++j) dctx[j] = 0.f;
+  if (d0 < D) {
+#pragma unroll
+    for (int j = 0; j < VD; ++j) {
+      const int d = d0 + j;
+      const float dg = a.d_gated[(long)b * a.d_gated_ld + d];
+      const float g = a.gate[(long)b * a.gate_ld + d];
+      const float c = a.ctx[(long)b * a.ctx_ld + d];
+      float dc = dg * g;
+      if (a.d_ctx_ext) dc += a.d_ctx_ext[(long)b * a.d_ctx_ext_ld + d];
+      dctx[j] = dc;
+      if (w == 0) {
+        const float dgp = dg * c * g * (1.f - g);
+        a.d_gpre[(long)b * a.d_gpre_ld + d] = dgp;
+        if (a.d_gpre_t) ((T*)a.d_gpre_t)[(long)b * a.d_gpre_ld + d] = (T)dgp;
+      }
+    }
+  }
+  const T* ab = (const T*)a.a + (long)b * L * D;
+  for (int l = w; l < L; l += 4) {
+    float p = 0.f;
+    if (d0 < D) {
+      float x[VD];
+      loadv<T>(ab + (long)l * D + d0, x);
+#pragma unroll
+      for (int j = 0; j < VD; ++j) p += dctx[j] * x[j];
+    }
+    p = wave_sum(p);
+    if (lane == 0) a.part[((long)b * NS + s) * L + l] = p;
+  }
+  (void)E;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
+  constexpr int kMaxE = 1024;
+  __shared__ float s_de[kMaxL];
+  __shared__ float s_red[4][kMaxE];
+  __shared__ float s_tmp[4];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int L = a.L, E = a.E;
+  const float* alpha = a.alpha + (long)b * a.alpha_ld;
+  // dL/dalpha and sum_l alpha*dalpha
+  float loc = 0.f;
+  for (int l = tid; l < L; l += 256) {
+    float da = 0.f;
+    for (int s = 0; s < NS; ++s) da += a.part[((long)b * NS + s) * L + l];
+    if (a.d_alpha_ext) da += a.d_alpha_ext[(long)b * a.d_alpha_ext_ld + l];
+    s_de[l] = da;
+    loc += alpha[l] * da;
+  }
+  loc = wave_sum(loc);
+  if (lane == 0) s_tmp[w] = loc;
+  __syncthreads();
+  const float sad = (s_tmp[0] + s_tmp[1]) + (s_tmp[2] + s_tmp[3]);
+  for (int l = tid; l < L; l += 256) s_de[l] = alpha[l] * (s_de[l] - sad);
+  __syncthreads();
+  // recompute tanh, accumulate
+  const float* uh = a.uh + (long)b * a.uh_ld;
+  const T* Ws = (const T*)a.Ws + (long)b * L * E;
+  float* dWs = a.dWs_acc + (long)b * L * E;
+  constexpr int CH = kMaxE / 256;  // e-chunks of 4 per lane
+  float duh[CH][4], dv[CH][4];
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { duh[c][j] = 0.f; dv[c][j] = 0.f; }
+  float dbv = 0.f;
+  for (int l = w; l < L; l += 4) {
+    const float de = s_de[l];
+    dbv += de;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int e = c * 256 + lane * 4;
+      if (e >= E) break;
+      float x[4];
+      load4<T>(Ws + (long)l * E + e, x);
+      float4 u = *(const float4*)(uh + e);
+      float4 vv = *(const float4*)(a.v_w + e);
+      float uu[4] = {u.x, u.y, u.z, u.w}, vw[4] = {vv.x, vv.y, vv.z, vv.w};
+      float4 acc = *(float4*)(dWs + (long)l * E + e);
+      float ac[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float t = tanhf(x[j] + uu[j]);
+        const float datt = de * vw[j] * (1.f - t * t);
+        duh[c][j] += datt;
+        dv[c][j] += de * t;
+        ac[j] += datt;
+      }
+      *(float4*)(dWs + (long)l * E + e) = make_float4(ac[0], ac[1], ac[2], ac[3]);
+    }
+  }
+  // fold waves: dU_h
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = c * 256 + lane * 4 + j;
+      if (e < E) s_red[w][e] = duh[c][j];
+    }
+  __syncthreads();
+  for (int e = tid; e < E; e += 256) {
+    const float v = (s_red[0][e] + s_red[1][e]) + (s_red[2][e] + s_red[3][e]);
+    a.d_uh[(long)b * a.d_uh_ld + e] = v;
+    if (a.d_uh_t) ((T*)a.d_uh_t)[(long)b * a.d_uh_ld + e] = (T)v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = c * 256 + lane * 4 + j;
+      if (e < E) s_red[w][e] = dv[c][j];
+    }
+  dbv = wave_sum(dbv);
+  if (lane == 0) s_tmp[w] = dbv;
+  __syncthreads();
+  for (int e = tid; e < E; e += 256)
+    a.dv_acc[(long)b * E + e] += (s_red[0][e] + s_red[1][e]) + (s_red[2][e] + s_red[3][e]);
+  if (tid == 0) a.dbv_acc[b] += (s_tmp[0] + s_tmp[1]) + (s_tmp[2] + s_tmp[3]);
+}
+
+}  // namespace
+
+int sat_attention_fwd_launch(const AttnFwdArgs& a, hipStream_t s) {
+  SAT_REQUIRE(a.L <= kMaxL && a.E % 4 == 0 && a.E <= 1024);
+  const int VD = a.dtype == SAT_BF16 ? 8 : 4;
+  SAT_REQUIRE(a.D % VD == 0);
+  const int NS = sat_cdiv(a.D, 64 * VD);
+  dim3 grid(a.B, NS);
+  if (a.dtype == SAT_BF16) hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s) {
+  SAT_REQUIRE(a.L <= kMaxL && a.E % 4 == 0 && a.E <= 1024);
+  const int VD = a.dtype == SAT_BF16 ? 8 : 4;
+  SAT_REQUIRE(a.D % VD == 0);
+  const int NS = sat_cdiv(a.D, 64 * VD);
+  if (a.dtype == SAT_BF16) {
+    hipLaunchKernelGGL(attn_bwd1_kernel<bf16>, dim3(a.B, NS), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(attn_bwd2_kernel<bf16>, dim3(a.B), dim3(256), 0, s, a, NS);
+  } else {
+    hipLaunchKernelGGL(attn_bwd1_kernel<float>, dim3(a.B, NS), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(attn_bwd2_kernel<float>, dim3(a.B), dim3(256), 0, s, a, NS);
+  }
+  return (int)hipGetLastError();
+}
+
+size_t sat_attention_part_floats(int B, int L, int D, int dtype) {
+  const int VD = dtype == SAT_BF16 ? 8 : 4;
+  return (size_t)B * sat_cdiv(D, 64 * VD) * L;
+}
+
+// Standalone Attention.forward (attention.py:14-21): two GEMMs + the fused kernel.
+extern "C" int sat_attention_forward(int B, int L, int D, int E, int dtype, const void* img_features,
+                                     const float* hidden, const float* U_w, const float* U_b, const float* W_w,
+                                     const void* W_w_lp, const float* W_b, const float* v_w, const float* v_b,
+                                     float* ws_scratch, float* context, float* alpha, void* stream) {
+  SAT_REQUIRE(img_features && hidden && U_w && W_w && v_w && v_b && ws_scratch && context && alpha);
+  SAT_REQUIRE(dtype == SAT_F32 || W_w_lp != nullptr);
+  hipStream_t s = (hipStream_t)stream;
+  // scratch layout: Ws [B*L*E] (dtype) followed by uh [B*E] fp32
+  float* uh = ws_scratch + (size_t)B * L * E;
+  SatGemm g;  // U_h = h U^T + b  (fp32 exact)
+  g.M = B; g.N = E; g.K = E; g.dtype = SAT_F32;
+  g.A = hidden; g.lda = E; g.B = U_w; g.ldb = E;
+  g.C = uh; g.ldc = E; g.c_dtype = SAT_F32; g.bias = U_b;
+  SAT_CHECK((hipError_t)sat_gemm_launch(g, s));
+  SatGemm w;  // Ws = a W^T + b
+  w.M = B * L; w.N = E; w.K = D; w.dtype = dtype;
+  w.A = img_features; w.lda = D; w.B = dtype == SAT_BF16 ? W_w_lp : (const void*)W_w; w.ldb = D;
+  w.C = ws_scratch; w.ldc = E; w.c_dtype = dtype; w.bias = W_b;
+  SAT_CHECK((hipError_t)sat_gemm_launch(w, s));
+  AttnFwdArgs a{};
+  a.B = B; a.L = L; a.D = D; a.E = E; a.dtype = dtype;
+  a.Ws = ws_scratch; a.uh = uh; a.uh_ld = E; a.v_w = v_w; a.v_b = v_b; a.a = img_features;
+  a.alpha = alpha; a.alpha_ld = L; a.ctx = context; a.ctx_ld = D;
+  return sat_attention_fwd_launch(a, s);
+}

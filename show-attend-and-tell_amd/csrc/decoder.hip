@@ -1,0 +1,439 @@
+// Decoder forward / backward orchestration (decoder.py:69-158 and the autograd
+// BPTT the reference gets from loss.backward(), train.py:163).
+//
+// The time loop runs here, in C++, so one C-ABI call launches the whole
+// sequence (no per-step Python round trips).  Work that does not depend on the
+// recurrence is hoisted out of the loop and batched over all B*(T-1) rows:
+//   * Ws = a W^T + b (attention.py:16) once per batch,
+//   * the embedding half of the LSTM input GEMM under teacher forcing,
+//   * the whole output head (dropout, f_h/f_z/f_out or deep_output) under
+//     teacher forcing, and in backward every weight gradient (one GEMM per
+//     weight with K = B*(T-1) instead of T-1 small accumulations).
+// Per step the forward runs: [h GEMM: U, f_beta, W_hh fused as one N=E+D+4E
+// product] -> fused attention + gate -> context GEMM -> LSTM pointwise (+ the
+// per-step head and greedy argmax when teacher forcing is off).  The backward
+// step mirrors it: LSTM pointwise -> context-grad GEMM -> attention backward ->
+// one dh GEMM against the same fused [U; f_beta; W_hh] weight.
+//
+// Layout: every per-step tensor is batch-major [B, T-1, X]; step t is the
+// strided slice at offset t*X with row stride (T-1)*X, so the batched head /
+// weight-gradient GEMMs read the same buffers as plain [B*(T-1), X] matrices.
+#include "sat_common.h"
+#include "sat_internal.h"
+
+namespace {
+
+struct WS {
+  // forward (saved for backward)
+  float *mean_f, *hc0, *xg, *gctx_const, *hg, *gctx, *uh_all, *gates_all, *c_in, *c_out, *h_out, *ctx_all,
+      *gate_all, *fh, *fz;
+  void *mean_t, *Ws, *emb_t, *h_in_t, *ctx_t, *gated_t, *hd_t, *comb_t;
+  int32_t* tok;
+  uint8_t* dmask;
+  // backward
+  void *dpre_t, *dfh_t, *dfz_t, *dhg_t, *dWs_t, *dpre0_t;
+  float *dcomb, *dhd, *dctx_head, *dhg, *dgated, *dh_rec, *dc, *dWs_acc, *dv_acc, *dbv_acc, *part, *demb, *dpre0,
+      *colsum;
+};
+
+struct Carver {
+  char* base;
+  size_t off = 0;
+  template <typename P>
+  void take(P*& p, size_t bytes) {
+    off = (off + 255) & ~(size_t)255;
+    p = base ? (P*)(base + off) : nullptr;
+    off += bytes;
+  }
+};
+
+size_t carve(const SatDecoderDims& d, char* base, WS* w) {
+  const size_t B = d.B, L = d.L, D = d.D, E = d.E, V = d.V, T1 = d.T - 1, R = B * T1;
+  const size_t HG = 5 * E + D;
+  const size_t ts = d.dtype == SAT_BF16 ? 2 : 4, f = 4;
+  Carver c{base};
+  c.take(w->mean_f, B * D * f);  c.take(w->mean_t, B * D * ts);
+  c.take(w->hc0, B * 2 * E * f);
+  c.take(w->Ws, B * L * E * ts);
+  c.take(w->tok, R * 4);
+  c.take(w->emb_t, R * E * ts);
+  c.take(w->xg, R * 4 * E * f);
+  c.take(w->gctx_const, B * 4 * E * f);
+  c.take(w->hg, B * HG * f);
+  c.take(w->gctx, B * 4 * E * f);
+  c.take(w->uh_all, R * E * f);
+  c.take(w->gates_all, R * 4 * E * f);
+  c.take(w->c_in, R * E * f);   c.take(w->c_out, R * E * f);
+  c.take(w->h_in_t, R * E * ts); c.take(w->h_out, R * E * f);
+  c.take(w->ctx_all, R * D * f); c.take(w->ctx_t, R * D * ts);
+  c.take(w->gate_all, R * D * f); c.take(w->gated_t, R * D * ts);
+  c.take(w->dmask, R * E);
+  c.take(w->hd_t, R * E * ts);
+  c.take(w->fh, R * E * f); c.take(w->fz, R * E * f); c.take(w->comb_t, R * E * ts);
+  // backward
+  c.take(w->dpre_t, R * V * ts);
+  c.take(w->dcomb, R * E * f);
+  c.take(w->dfh_t, R * E * ts); c.take(w->dfz_t, R * E * ts);
+  c.take(w->dhd, R * E * f);
+  c.take(w->dctx_head, R * D * f);
+  c.take(w->dhg, R * HG * f); c.take(w->dhg_t, R * HG * ts);
+  c.take(w->dgated, B * D * f);
+  c.take(w->dh_rec, B * E * f); c.take(w->dc, B * E * f);
+  c.take(w->dWs_acc, B * L * E * f); c.take(w->dWs_t, B * L * E * ts);
+  c.take(w->dv_acc, B * E * f); c.take(w->dbv_acc, B * f);
+  c.take(w->part, sat_attention_part_floats(d.B, d.L, d.D, d.dtype) * f);
+  c.take(w->demb, R * E * f);
+  c.take(w->dpre0, B * 2 * E * f); c.take(w->dpre0_t, B * 2 * E * ts);
+  size_t maxN = V > HG ? V : HG;
+  if (D > maxN) maxN = D;
+  c.take(w->colsum, sat_colsum_scratch_floats((int)R, (int)maxN) * f);
+  return c.off + 256;
+}
+
+__global__ void start_tokens_kernel(int32_t* tok, int B, int T1, int start) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) tok[(long)b * T1] = start;
+}
+
+template <typename T>
+__global__ void ado_combine_rows_kernel(const float* fh, const float* fz, const T* emb, int rows, int E, long ld,
+                                        T* comb) {
+  const long n = (long)rows * E;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / E;
+    const int e = (int)(i - r * E);
+    const long o = r * ld + e;
+    comb[o] = (T)(fh[o] + fz[o] + (float)emb[o]);
+  }
+}
+
+int combine_rows(const float* fh, const float* fz, const void* emb, int rows, int E, long ld, int dtype, void* comb,
+                 hipStream_t s) {
+  long n = (long)rows * E;
+  int g = (int)((n + 255) / 256);
+  if (g > 4096) g = 4096;
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(ado_combine_rows_kernel<bf16>, dim3(g), dim3(256), 0, s, fh, fz, (const bf16*)emb, rows, E, ld, (bf16*)comb);
+  else
+    hipLaunchKernelGGL(ado_combine_rows_kernel<float>, dim3(g), dim3(256), 0, s, fh, fz, (const float*)emb, rows, E, ld, (float*)comb);
+  return (int)hipGetLastError();
+}
+
+struct Ctx {
+  SatDecoderDims d;
+  SatDecoderLayout lay;
+  const float* P;
+  const void* LP;
+  int ts;
+  long T1, R, HG;
+  const void* W(int64_t off) const {
+    return d.dtype == SAT_BF16 ? (const void*)((const bf16*)LP + off) : (const void*)(P + off);
+  }
+  const float* F(int64_t off) const { return P + off; }
+  void* at(void* p, long elems) const { return (char*)p + elems * ts; }
+  const void* at(const void* p, long elems) const { return (const char*)p + elems * ts; }
+};
+
+// y[rows, N] (+)= x[rows, K] . W[N, K]^T  (+bias) (act) -- all strided rows
+int linear(const Ctx& c, int rows, int N, int K, const void* x, long ldx, const void* w, long ldw, const float* bias,
+           void* y, long ldy, int y_dtype, int act, hipStream_t s, const void* add1 = nullptr, long ld_add1 = 0,
+           int add1_dtype = SAT_F32, void* aux = nullptr, long ld_aux = 0, int aux_dtype = SAT_F32) {
+  SatGemm g;
+  g.M = rows; g.N = N; g.K = K; g.dtype = c.d.dtype;
+  g.A = x; g.lda = ldx; g.B = w; g.ldb = ldw;
+  g.C = y; g.ldc = ldy; g.c_dtype = y_dtype; g.bias = bias; g.act = act;
+  g.add1 = add1; g.ld_add1 = ld_add1; g.add1_dtype = add1_dtype;
+  g.aux = aux; g.ld_aux = ld_aux; g.aux_dtype = aux_dtype;
+  return sat_gemm_launch(g, s);
+}
+
+// Output head over `rows` rows starting at step t0 (batched: rows = R, t0 = 0, ld factor 1;
+// per step: rows = B, row stride T1).  decoder.py:117-125,149-158
+int head_forward(const Ctx& c, const WS& w, int rows, int t, bool per_step, void* preds, const uint8_t* mask_in,
+                 hipStream_t s) {
+  const SatDecoderDims& d = c.d;
+  const int E = d.E, D = d.D, V = d.V;
+  const long rs = per_step ? c.T1 : 1;  // row stride multiplier
+  const long oE = per_step ? (long)t * E : 0, oD = per_step ? (long)t * D : 0, oV = per_step ? (long)t * V : 0;
+  // dropout(h)
+  if (per_step)
+    SAT_CHECK((hipError_t)sat_dropout_apply(w.h_out + oE, c.T1 * E, d.B, 1, E, d.training, d.has_dropout_mask,
+                                            mask_in ? mask_in + oE : nullptr, w.dmask + oE, c.T1 * E, d.seed, t,
+                                            c.at(w.hd_t, oE), c.T1 * E, d.dtype, s));
+  else
+    SAT_CHECK((hipError_t)sat_dropout_apply(w.h_out, E, d.B, (int)c.T1, E, d.training, d.has_dropout_mask, mask_in,
+                                            w.dmask, E, d.seed, 0, w.hd_t, E, d.dtype, s));
+  if (d.ado) {
+    SAT_CHECK((hipError_t)linear(c, rows, E, E, c.at(w.hd_t, oE), rs * E, c.W(c.lay.fh_w), E, c.F(c.lay.fh_b),
+                                 w.fh + oE, rs * E, SAT_F32, SAT_ACT_RELU, s));
+    SAT_CHECK((hipError_t)linear(c, rows, E, D, c.at(w.ctx_t, oD), rs * D, c.W(c.lay.fz_w), D, c.F(c.lay.fz_b),
+                                 w.fz + oE, rs * E, SAT_F32, SAT_ACT_RELU, s));
+    SAT_CHECK((hipError_t)combine_rows(w.fh + oE, w.fz + oE, c.at(w.emb_t, oE), rows, E, rs * E, d.dtype,
+                                       c.at(w.comb_t, oE), s));
+    SAT_CHECK((hipError_t)linear(c, rows, V, E, c.at(w.comb_t, oE), rs * E, c.W(c.lay.fout_w), E,
+                                 c.F(c.lay.fout_b), c.at(preds, oV), rs * V, d.dtype, SAT_ACT_RELU, s));
+  } else {
+    SAT_CHECK((hipError_t)linear(c, rows, V, E, c.at(w.hd_t, oE), rs * E, c.W(c.lay.do_w), E, c.F(c.lay.do_b),
+                                 c.at(preds, oV), rs * V, d.dtype, SAT_ACT_NONE, s));
+  }
+  return 0;
+}
+
+int check_dims(const SatDecoderDims* d) {
+  if (!d) return SAT_ERR_INVALID;
+  if (d->B <= 0 || d->L <= 0 || d->D <= 0 || d->E <= 0 || d->V <= 0 || d->T < 3) return SAT_ERR_INVALID;
+  if (d->dtype != SAT_F32 && d->dtype != SAT_BF16) return SAT_ERR_INVALID;
+  if (d->E % 8 != 0 || d->D % 8 != 0 || d->E > 1024 || d->L > 1024) return SAT_ERR_INVALID;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" size_t sat_decoder_workspace_bytes(const SatDecoderDims* d) {
+  if (check_dims(d)) return 0;
+  WS w;
+  return carve(*d, nullptr, &w);
+}
+
+extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLayout* lay, const float* params,
+                                   const void* params_lp, const void* img_features, const int64_t* captions,
+                                   const uint8_t* dropout_mask, void* workspace, size_t workspace_bytes, void* preds,
+                                   float* alphas, int32_t* tokens, void* stream) {
+  SAT_CHECK((hipError_t)check_dims(dp));
+  SAT_REQUIRE(lay && params && img_features && captions && workspace && preds && alphas);
+  SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
+  SAT_REQUIRE(!(dp->training && dp->has_dropout_mask) || dropout_mask);
+  const SatDecoderDims& d = *dp;
+  WS w;
+  SAT_REQUIRE(carve(d, nullptr, &w) <= workspace_bytes);
+  carve(d, (char*)workspace, &w);
+  hipStream_t s = (hipStream_t)stream;
+  Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D};
+  const int B = d.B, L = d.L, D = d.D, E = d.E, T1 = d.T - 1;
+  const long HG = c.HG;
+  const bool att = d.attention != 0;
+
+  // fed tokens + embeddings
+  if (d.tf) {
+    SAT_CHECK((hipError_t)sat_tokens_from_captions(captions, B, d.T, T1, w.tok, s));
+    SAT_CHECK((hipError_t)sat_embed_gather(c.F(lay->embedding), w.tok, B, T1, T1, E, d.dtype, w.emb_t, E, s));
+  } else {
+    hipLaunchKernelGGL(start_tokens_kernel, dim3(sat_cdiv(B, 256)), dim3(256), 0, s, w.tok, B, T1, d.start_token);
+    SAT_LAUNCH_CHECK();
+    SAT_CHECK((hipError_t)sat_embed_gather(c.F(lay->embedding), w.tok, B, 1, T1, E, d.dtype, w.emb_t, (long)T1 * E, s));
+  }
+  // init_lstm_state (decoder.py:137-147)
+  SAT_CHECK((hipError_t)sat_mean_rows(img_features, B, L, D, d.dtype, w.mean_f, w.mean_t, s));
+  SAT_CHECK((hipError_t)linear(c, B, E, D, w.mean_t, D, c.W(lay->init_w), D, c.F(lay->init_b), w.hc0, 2 * E,
+                               SAT_F32, SAT_ACT_TANH, s, nullptr, 0, SAT_F32, w.h_in_t, (long)T1 * E, d.dtype));
+  SAT_CHECK((hipError_t)linear(c, B, E, D, w.mean_t, D, c.W(lay->init_w + (long)E * D), D, c.F(lay->init_b + E),
+                               w.hc0 + E, 2 * E, SAT_F32, SAT_ACT_TANH, s, nullptr, 0, SAT_F32, w.c_in,
+                               (long)T1 * E, SAT_F32));
+  if (att) {  // hoisted Ws = a W^T + b
+    SAT_CHECK((hipError_t)linear(c, B * L, E, D, img_features, D, c.W(lay->attW_w), D, c.F(lay->attW_b), w.Ws, E,
+                                 d.dtype, SAT_ACT_NONE, s));
+  } else {    // uniform attention: context = mean_L a, alpha = 1/L (decoder.py:101-105)
+    SAT_CHECK((hipError_t)linear(c, B, 4 * E, D, w.mean_t, D, c.W(lay->wih + E), E + D, nullptr, w.gctx_const, 4 * E,
+                                 SAT_F32, SAT_ACT_NONE, s));
+    SAT_CHECK((hipError_t)sat_broadcast_rows(w.mean_t, B, D, T1, d.dtype, w.gated_t, s));
+    SAT_CHECK((hipError_t)sat_broadcast_rows(w.mean_t, B, D, T1, d.dtype, w.ctx_t, s));
+    SAT_CHECK((hipError_t)sat_broadcast_rows(w.mean_f, B, D, T1, SAT_F32, w.ctx_all, s));
+    SAT_CHECK((hipError_t)sat_fill_const(alphas, (long)B * T1 * L, 1.0f / (float)L, s));
+  }
+  if (d.tf)  // embedding half of the LSTM input GEMM for all steps at once (+ b_ih)
+    SAT_CHECK((hipError_t)linear(c, (int)c.R, 4 * E, E, w.emb_t, E, c.W(lay->wih), E + D, c.F(lay->bih), w.xg, 4 * E,
+                                 SAT_F32, SAT_ACT_NONE, s));
+
+  for (int t = 0; t < T1; ++t) {
+    if (!d.tf)
+      SAT_CHECK((hipError_t)linear(c, B, 4 * E, E, c.at(w.emb_t, (long)t * E), (long)T1 * E, c.W(lay->wih), E + D,
+                                   c.F(lay->bih), w.xg + (long)t * 4 * E, (long)T1 * 4 * E, SAT_F32, SAT_ACT_NONE, s));
+    const void* h_t = c.at(w.h_in_t, (long)t * E);
+    if (att) {
+      // [U h + b_U | f_beta h + b | W_hh h + b_hh] in one GEMM
+      SAT_CHECK((hipError_t)linear(c, B, (int)HG, E, h_t, (long)T1 * E, c.W(lay->hcat_w), E, c.F(lay->hcat_b), w.hg,
+                                   HG, SAT_F32, SAT_ACT_NONE, s));
+      AttnFwdArgs a{};
+      a.B = B; a.L = L; a.D = D; a.E = E; a.dtype = d.dtype;
+      a.Ws = w.Ws; a.uh = w.hg; a.uh_ld = HG; a.v_w = c.F(lay->v_w); a.v_b = c.F(lay->v_b); a.a = img_features;
+      a.gate_pre = w.hg + E; a.gate_ld = HG;
+      a.alpha = alphas + (long)t * L; a.alpha_ld = (long)T1 * L;
+      a.ctx = w.ctx_all + (long)t * D; a.ctx_ld = (long)T1 * D;
+      a.ctx_t = c.at(w.ctx_t, (long)t * D); a.ctx_t_ld = (long)T1 * D;
+      a.gate = w.gate_all + (long)t * D; a.gate_out_ld = (long)T1 * D;
+      a.gated = c.at(w.gated_t, (long)t * D); a.gated_ld = (long)T1 * D;
+      a.uh_save = w.uh_all + (long)t * E; a.uh_save_ld = (long)T1 * E;
+      SAT_CHECK((hipError_t)sat_attention_fwd_launch(a, s));
+      SAT_CHECK((hipError_t)linear(c, B, 4 * E, D, c.at(w.gated_t, (long)t * D), (long)T1 * D, c.W(lay->wih + E),
+                                   E + D, nullptr, w.gctx, 4 * E, SAT_F32, SAT_ACT_NONE, s));
+    } else {
+      SAT_CHECK((hipError_t)linear(c, B, 4 * E, E, h_t, (long)T1 * E, c.W(lay->hcat_w + (long)(E + D) * E), E,
+                                   c.F(lay->hcat_b + E + D), w.hg + E + D, HG, SAT_F32, SAT_ACT_NONE, s));
+    }
+    LstmFwdArgs l{};
+    l.B = B; l.E = E; l.dtype = d.dtype;
+    l.hpart = w.hg + E + D; l.hpart_ld = HG;
+    l.xpart = w.xg + (long)t * 4 * E; l.xpart_ld = (long)T1 * 4 * E;
+    l.cpart = att ? w.gctx : w.gctx_const; l.cpart_ld = 4 * E;
+    l.c_prev = w.c_in + (long)t * E; l.c_prev_ld = (long)T1 * E;
+    l.gates = w.gates_all + (long)t * 4 * E; l.gates_ld = (long)T1 * 4 * E;
+    l.c_out = w.c_out + (long)t * E; l.c_out_ld = (long)T1 * E;
+    l.c_next_in = t + 1 < T1 ? w.c_in + (long)(t + 1) * E : nullptr; l.c_next_in_ld = (long)T1 * E;
+    l.h_out = w.h_out + (long)t * E; l.h_out_ld = (long)T1 * E;
+    l.h_next_in_t = t + 1 < T1 ? c.at(w.h_in_t, (long)(t + 1) * E) : nullptr; l.h_next_in_t_ld = (long)T1 * E;
+    SAT_CHECK((hipError_t)sat_lstm_fwd_launch(l, s));
+    if (!d.tf) {
+      SAT_CHECK((hipError_t)head_forward(c, w, B, t, true, preds, dropout_mask, s));
+      if (t + 1 < T1)   // greedy feedback: argmax -> next token + its embedding (decoder.py:131-133)
+        SAT_CHECK((hipError_t)sat_argmax_rows(c.at(preds, (long)t * d.V), d.dtype, (long)T1 * d.V, B, d.V,
+                                              w.tok + t + 1, T1, c.F(lay->embedding), E,
+                                              c.at(w.emb_t, (long)(t + 1) * E), (long)T1 * E, s));
+    }
+  }
+  if (d.tf) SAT_CHECK((hipError_t)head_forward(c, w, (int)c.R, 0, false, preds, dropout_mask, s));
+  if (tokens) SAT_CHECK(hipMemcpyAsync(tokens, w.tok, c.R * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLayout* lay, const float* params,
+                                    const void* params_lp, const void* img_features, void* workspace,
+                                    size_t workspace_bytes, const void* preds, const float* alphas,
+                                    const void* d_preds, const float* d_alphas, float* grads, int accumulate,
+                                    int phase, void* stream) {
+  SAT_CHECK((hipError_t)check_dims(dp));
+  SAT_REQUIRE(lay && params && img_features && workspace && preds && alphas && d_preds && d_alphas && grads);
+  SAT_REQUIRE(phase >= 1 && phase <= 3);
+  SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
+  const SatDecoderDims& d = *dp;
+  WS w;
+  SAT_REQUIRE(carve(d, nullptr, &w) <= workspace_bytes);
+  carve(d, (char*)workspace, &w);
+  hipStream_t s = (hipStream_t)stream;
+  Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D};
+  const int B = d.B, L = d.L, D = d.D, E = d.E, V = d.V, T1 = d.T - 1;
+  const int R = (int)c.R;
+  const long HG = c.HG;
+  const bool att = d.attention != 0;
+  const float beta = accumulate ? 1.f : 0.f;
+  auto G = [&](int64_t off) { return grads + off; };
+  // weight gradient: G[M,N] (+)= X[K,M]^T Y[K,N]   (X m-contig, Y n-contig)
+  auto wgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo) {
+    SatGemm g;
+    g.M = M; g.N = N; g.K = K; g.dtype = d.dtype;
+    g.A = X; g.lda = ldx; g.transA = 1;
+    g.B = Y; g.ldb = ldy; g.transB = 1;
+    g.C = out; g.ldc = ldo; g.c_dtype = SAT_F32; g.beta = beta;
+    return sat_gemm_launch(g, s);
+  };
+  // input gradient: Y[M,N] = X[M,K] W[K,N]   (W stored [K][N] row-major = torch weight [out,in])
+  auto dgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Wt, long ldw, float* out, long ldo,
+                   const float* add1 = nullptr, long ld_add1 = 0) {
+    SatGemm g;
+    g.M = M; g.N = N; g.K = K; g.dtype = d.dtype;
+    g.A = X; g.lda = ldx; g.B = Wt; g.ldb = ldw; g.transB = 1;
+    g.C = out; g.ldc = ldo; g.c_dtype = SAT_F32;
+    g.add1 = add1; g.ld_add1 = ld_add1; g.add1_dtype = SAT_F32;
+    return sat_gemm_launch(g, s);
+  };
+  auto colsum = [&](const void* X, int dt, long ld, int rows, int N, float* out, float* out2 = nullptr) {
+    return sat_colsum(X, dt, ld, rows, N, out, accumulate, out2, w.colsum, s);
+  };
+
+  if (phase & 1) {  // ---------------- output head (decoder.py:117-125,149-158) ----------------
+    if (d.ado) {
+      SAT_CHECK((hipError_t)sat_relu_mask_mul(d_preds, preds, (long)R * V, d.dtype, w.dpre_t, s));
+      SAT_CHECK((hipError_t)wgrad(V, E, R, w.dpre_t, V, w.comb_t, E, G(lay->fout_w), E));
+      SAT_CHECK((hipError_t)colsum(w.dpre_t, d.dtype, V, R, V, G(lay->fout_b)));
+      SAT_CHECK((hipError_t)dgrad(R, E, V, w.dpre_t, V, c.W(lay->fout_w), E, w.dcomb, E));
+      SAT_CHECK((hipError_t)sat_ado_bwd_split(w.dcomb, w.fh, w.fz, (long)R * E, d.dtype, w.dfh_t, w.dfz_t, s));
+      SAT_CHECK((hipError_t)wgrad(E, E, R, w.dfh_t, E, w.hd_t, E, G(lay->fh_w), E));
+      SAT_CHECK((hipError_t)colsum(w.dfh_t, d.dtype, E, R, E, G(lay->fh_b)));
+      SAT_CHECK((hipError_t)wgrad(E, D, R, w.dfz_t, E, w.ctx_t, D, G(lay->fz_w), D));
+      SAT_CHECK((hipError_t)colsum(w.dfz_t, d.dtype, E, R, E, G(lay->fz_b)));
+      SAT_CHECK((hipError_t)dgrad(R, E, E, w.dfh_t, E, c.W(lay->fh_w), E, w.dhd, E));
+      if (att) SAT_CHECK((hipError_t)dgrad(R, D, E, w.dfz_t, E, c.W(lay->fz_w), D, w.dctx_head, D));
+    } else {
+      SAT_CHECK((hipError_t)wgrad(V, E, R, d_preds, V, w.hd_t, E, G(lay->do_w), E));
+      SAT_CHECK((hipError_t)colsum(d_preds, d.dtype, V, R, V, G(lay->do_b)));
+      SAT_CHECK((hipError_t)dgrad(R, E, V, d_preds, V, c.W(lay->do_w), E, w.dhd, E));
+    }
+  }
+  if (!(phase & 2)) return 0;
+
+  // ---------------- recurrent BPTT (reverse time loop) ----------------
+  if (att) {
+    SAT_CHECK(hipMemsetAsync(w.dWs_acc, 0, (size_t)B * L * E * 4, s));
+    SAT_CHECK(hipMemsetAsync(w.dv_acc, 0, (size_t)B * E * 4, s));
+    SAT_CHECK(hipMemsetAsync(w.dbv_acc, 0, (size_t)B * 4, s));
+  }
+  for (int t = T1 - 1; t >= 0; --t) {
+    LstmBwdArgs l{};
+    l.B = B; l.E = E; l.dtype = d.dtype;
+    l.gates = w.gates_all + (long)t * 4 * E; l.gates_ld = (long)T1 * 4 * E;
+    l.c_prev = w.c_in + (long)t * E; l.c_prev_ld = (long)T1 * E;
+    l.c_new = w.c_out + (long)t * E; l.c_new_ld = (long)T1 * E;
+    l.dh_rec = t == T1 - 1 ? nullptr : w.dh_rec; l.dh_rec_ld = E;
+    l.dh_head = w.dhd + (long)t * E; l.dh_head_ld = (long)T1 * E;
+    l.mask = d.training ? w.dmask + (long)t * E : nullptr; l.mask_ld = (long)T1 * E;
+    l.dc = w.dc; l.dc_zero = t == T1 - 1;
+    l.d_gates = w.dhg + (long)t * HG + E + D; l.d_gates_ld = (long)T1 * HG;
+    l.d_gates_t = c.at(w.dhg_t, (long)t * HG + E + D); l.d_gates_t_ld = (long)T1 * HG;
+    SAT_CHECK((hipError_t)sat_lstm_bwd_launch(l, s));
+    const void* dgates_t = c.at(w.dhg_t, (long)t * HG + E + D);
+    if (att) {
+      SAT_CHECK((hipError_t)dgrad(B, D, 4 * E, dgates_t, (long)T1 * HG, c.W(lay->wih + E), E + D, w.dgated, D));
+      AttnBwdArgs a{};
+      a.B = B; a.L = L; a.D = D; a.E = E; a.dtype = d.dtype;
+      a.Ws = w.Ws; a.a = img_features;
+      a.uh = w.uh_all + (long)t * E; a.uh_ld = (long)T1 * E;
+      a.v_w = c.F(lay->v_w);
+      a.alpha = alphas + (long)t * L; a.alpha_ld = (long)T1 * L;
+      a.d_alpha_ext = d_alphas + (long)t * L; a.d_alpha_ext_ld = (long)T1 * L;
+      a.d_gated = w.dgated; a.d_gated_ld = D;
+      a.gate = w.gate_all + (long)t * D; a.gate_ld = (long)T1 * D;
+      a.ctx = w.ctx_all + (long)t * D; a.ctx_ld = (long)T1 * D;
+      a.d_ctx_ext = d.ado ? w.dctx_head + (long)t * D : nullptr; a.d_ctx_ext_ld = (long)T1 * D;
+      a.d_uh = w.dhg + (long)t * HG; a.d_uh_ld = (long)T1 * HG; a.d_uh_t = c.at(w.dhg_t, (long)t * HG);
+      a.d_gpre = w.dhg + (long)t * HG + E; a.d_gpre_ld = (long)T1 * HG; a.d_gpre_t = c.at(w.dhg_t, (long)t * HG + E);
+      a.dWs_acc = w.dWs_acc; a.dv_acc = w.dv_acc; a.dbv_acc = w.dbv_acc; a.part = w.part;
+      SAT_CHECK((hipError_t)sat_attention_bwd_launch(a, s));
+      // dh = [dU_h | d(f_beta h) | d gates] . [U ; f_beta ; W_hh]
+      SAT_CHECK((hipError_t)dgrad(B, E, (int)HG, c.at(w.dhg_t, (long)t * HG), (long)T1 * HG, c.W(lay->hcat_w), E,
+                                  w.dh_rec, E));
+    } else {
+      SAT_CHECK((hipError_t)dgrad(B, E, 4 * E, dgates_t, (long)T1 * HG, c.W(lay->hcat_w + (long)(E + D) * E), E,
+                                  w.dh_rec, E));
+    }
+  }
+
+  // ---------------- weight gradients, batched over all B*(T-1) rows ----------------
+  const void* dg_t = c.at(w.dhg_t, E + D);   // d gates rows (ld HG)
+  const float* dg_f = w.dhg + E + D;
+  if (att) {
+    SAT_CHECK((hipError_t)wgrad((int)HG, E, R, w.dhg_t, HG, w.h_in_t, E, G(lay->hcat_w), E));
+    SAT_CHECK((hipError_t)colsum(w.dhg, SAT_F32, HG, R, E + D, G(lay->hcat_b)));
+  } else {
+    SAT_CHECK((hipError_t)wgrad(4 * E, E, R, dg_t, HG, w.h_in_t, E, G(lay->hcat_w + (long)(E + D) * E), E));
+  }
+  // b_hh and b_ih receive the same gradient (sum of d gates)
+  SAT_CHECK((hipError_t)colsum(dg_f, SAT_F32, HG, R, 4 * E, G(lay->hcat_b + E + D), G(lay->bih)));
+  SAT_CHECK((hipError_t)wgrad(4 * E, E, R, dg_t, HG, w.emb_t, E, G(lay->wih), E + D));
+  SAT_CHECK((hipError_t)wgrad(4 * E, D, R, dg_t, HG, w.gated_t, D, G(lay->wih + E), E + D));
+  if (!d.bert) {  // dense embedding gradient, scatter-added by fed token (decoder.py:87,133)
+    SAT_CHECK((hipError_t)dgrad(R, E, 4 * E, dg_t, HG, c.W(lay->wih), E + D, w.demb, E, d.ado ? w.dcomb : nullptr, E));
+    if (!accumulate) SAT_CHECK(hipMemsetAsync(G(lay->embedding), 0, (size_t)V * E * 4, s));
+    SAT_CHECK((hipError_t)sat_embed_scatter_add(w.demb, w.tok, R, E, G(lay->embedding), s));
+  }
+  if (att) {
+    SAT_CHECK((hipError_t)sat_cast_launch(w.dWs_acc, SAT_F32, w.dWs_t, d.dtype, (long)B * L * E, s));
+    SAT_CHECK((hipError_t)wgrad(E, D, B * L, w.dWs_t, E, img_features, D, G(lay->attW_w), D));
+    SAT_CHECK((hipError_t)colsum(w.dWs_acc, SAT_F32, E, B * L, E, G(lay->attW_b)));
+    SAT_CHECK((hipError_t)colsum(w.dv_acc, SAT_F32, E, B, E, G(lay->v_w)));
+    SAT_CHECK((hipError_t)colsum(w.dbv_acc, SAT_F32, 1, B, 1, G(lay->v_b)));
+  }
+  // init_h / init_c (decoder.py:137-147): dh0 = dh_rec, dc0 = dc after the t = 0 step
+  SAT_CHECK((hipError_t)sat_tanh_pair_bwd(w.dh_rec, w.dc, w.hc0, B, E, w.dpre0, w.dpre0_t, d.dtype, s));
+  SAT_CHECK((hipError_t)wgrad(2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D));
+  SAT_CHECK((hipError_t)colsum(w.dpre0, SAT_F32, 2 * E, B, 2 * E, G(lay->init_b)));
+  return 0;
+}

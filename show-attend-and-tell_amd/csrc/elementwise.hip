@@ -1,0 +1,298 @@
+// Memory-bound helper kernels: layout conversion, max-pool, casts, reductions
+// over rows/columns, embedding gather / scatter-add, greedy argmax and the Adam
+// step.  All are HBM-bound streaming kernels: 16-B accesses where the layout
+// allows, grid-stride loops capped at ~8 blocks per CU.
+#include "sat_common.h"
+#include "sat_internal.h"
+
+namespace {
+
+constexpr int kMaxGrid = 2048;
+inline int grid_for(long n, int per_block = 256) {
+  long g = (n + per_block - 1) / per_block;
+  return (int)(g < 1 ? 1 : (g > kMaxGrid ? kMaxGrid : g));
+}
+
+// ---- NCHW fp32 -> NHWC (T), channels zero-padded to Cp ----------------------
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__ y, int N, int C, int H, int W,
+                                    int Cp) {
+  long total = (long)N * H * W;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
+    long n = p / ((long)H * W), hw = p - n * H * W;
+    const float* src = x + n * C * H * W + hw;
+    T* dst = y + p * Cp;
+    for (int c = 0; c < Cp; ++c) dst[c] = (T)(c < C ? src[(long)c * H * W] : 0.f);
+  }
+}
+
+// ---- max-pool NHWC (floor mode) ---------------------------------------------
+template <typename T>
+__global__ void maxpool_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W, int C, int k,
+                               int stride, int pad, int OH, int OW) {
+  long total = (long)N * OH * OW * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    long p = i / C;
+    int ow = (int)(p % OW); p /= OW;
+    int oh = (int)(p % OH); int n = (int)(p / OH);
+    float m = -INFINITY;
+    for (int kh = 0; kh < k; ++kh) {
+      int ih = oh * stride - pad + kh;
+      if (ih < 0 || ih >= H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        int iw = ow * stride - pad + kw;
+        if (iw < 0 || iw >= W) continue;
+        float v = (float)x[(((long)n * H + ih) * W + iw) * C + c];
+        m = (v > m || v != v) ? v : m;   // NaN propagates like torch max_pool2d
+      }
+    }
+    y[i] = (T)m;
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = (TO)(float)x[i];
+}
+
+// ---- mean over L: a [B,L,D] -> out [B,D] (fp32 accumulate) -------------------
+template <typename T>
+__global__ void mean_rows_kernel(const T* __restrict__ a, int L, int D, float* __restrict__ out_f32,
+                                 T* __restrict__ out_t) {
+  int b = blockIdx.y;
+  int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  const T* p = a + (long)b * L * D + d;
+  float s = 0.f;
+  for (int l = 0; l < L; ++l) s += (float)p[(long)l * D];
+  s /= (float)L;
+  if (out_f32) out_f32[(long)b * D + d] = s;
+  if (out_t) out_t[(long)b * D + d] = (T)s;
+}
+
+// ---- column sums: out[n] (+)= sum_r X[r*ld + n] ----------------------------
+// pass 1: grid (ceil(N/256), RS) partial sums over row chunks; pass 2 folds them.
+template <typename T>
+__global__ void colsum_partial_kernel(const T* __restrict__ X, long ld, int R, int N, int rows_per,
+                                      float* __restrict__ part) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  int r0 = blockIdx.y * rows_per, r1 = min(R, r0 + rows_per);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += (float)X[(long)r * ld + n];
+  part[(long)blockIdx.y * N + n] = s;
+}
+__global__ void colsum_final_kernel(const float* __restrict__ part, int RS, int N, float* __restrict__ out,
+                                    int accumulate, float* __restrict__ out2) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int i = 0; i < RS; ++i) s += part[(long)i * N + n];
+  out[n] = accumulate ? out[n] + s : s;
+  if (out2) out2[n] = accumulate ? out2[n] + s : s;
+}
+
+// ---- embedding gather: out[r, :] = W[tok[r], :] ------------------------------
+template <typename T>
+__global__ void embed_gather_kernel(const float* __restrict__ W, const int32_t* __restrict__ tok, int R,
+                                    long tok_stride_b, int T1, int E, T* __restrict__ out, long out_ld) {
+  // row r = b*T1 + t ; tokens laid out [B][T1] with row stride tok_stride_b
+  int r = blockIdx.x;
+  if (r >= R) return;
+  int b = r / T1, t = r - b * T1;
+  int id = tok[(long)b * tok_stride_b + t];
+  const float* src = W + (long)id * E;
+  T* dst = out + (long)r * out_ld;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) dst[e] = (T)src[e];
+}
+
+// ---- embedding backward: G[tok[r], :] += dX[r, :] (fp32 atomics) -------------
+__global__ void embed_scatter_kernel(const float* __restrict__ dX, const int32_t* __restrict__ tok, int R, int E,
+                                     float* __restrict__ G) {
+  int r = blockIdx.x;
+  if (r >= R) return;
+  int id = tok[r];
+  const float* src = dX + (long)r * E;
+  float* dst = G + (long)id * E;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) atomicAdd(dst + e, src[e]);
+}
+
+// ---- greedy argmax over V (first index wins ties, decoder.py:132) ----------
+template <typename T>
+__global__ void argmax_kernel(const T* __restrict__ X, long ld, int V, int32_t* __restrict__ out, long out_stride,
+                              const float* __restrict__ emb, int E, T* __restrict__ emb_out, long emb_ld) {
+  int b = blockIdx.x;
+  const T* row = X + (long)b * ld;
+  float best = -INFINITY; int bi = 0x7fffffff;
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    float x = (float)row[v];
+    if (x > best || (x == best && v < bi) || (x != x && best == best)) { best = x; bi = v; }
+  }
+  __shared__ float sv[256];
+  __shared__ int si[256];
+  sv[threadIdx.x] = best; si[threadIdx.x] = bi;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      float x = sv[threadIdx.x + o]; int xi = si[threadIdx.x + o];
+      float y = sv[threadIdx.x]; int yi = si[threadIdx.x];
+      bool take = (x > y) || (x == y && xi < yi) || (x != x && y == y) || (x != x && y != y && xi < yi);
+      if (take) { sv[threadIdx.x] = x; si[threadIdx.x] = xi; }
+    }
+    __syncthreads();
+  }
+  int id = si[0];
+  if (id < 0 || id >= V) id = 0;
+  if (threadIdx.x == 0 && out) out[(long)b * out_stride] = id;
+  if (emb_out) {
+    const float* src = emb + (long)id * E;
+    for (int e = threadIdx.x; e < E; e += blockDim.x) emb_out[(long)b * emb_ld + e] = (T)src[e];
+  }
+}
+
+// ---- Adam (torch.optim.Adam single-tensor algorithm) ------------------------
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, bf16* __restrict__ p_lp, long n, float b1, float b2, float eps,
+                            float step_size, float bc2_sqrt) {
+  const float w1 = 1.f - b1;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gi = g[i], mi = m[i], vi = v[i];
+    // exp_avg.lerp_(grad, 1-beta1): weight < 0.5 branch of at::lerp
+    mi = mi + w1 * (gi - mi);
+    vi = vi * b2 + (1.f - b2) * gi * gi;
+    float denom = sqrtf(vi) / bc2_sqrt + eps;
+    float pi = p[i] + (-step_size) * (mi / denom);
+    m[i] = mi; v[i] = vi; p[i] = pi;
+    if (p_lp) p_lp[i] = (bf16)pi;
+  }
+}
+
+}  // namespace
+
+// ============================ internal launchers ============================
+int sat_mean_rows(const void* a, int B, int L, int D, int dtype, float* out_f32, void* out_t, hipStream_t s) {
+  dim3 grid(sat_cdiv(D, 256), B);
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(mean_rows_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)a, L, D, out_f32, (bf16*)out_t);
+  else
+    hipLaunchKernelGGL(mean_rows_kernel<float>, grid, dim3(256), 0, s, (const float*)a, L, D, out_f32, (float*)out_t);
+  return (int)hipGetLastError();
+}
+
+int sat_colsum(const void* X, int dtype, long ld, int R, int N, float* out, int accumulate, float* out2,
+               float* scratch, hipStream_t s) {
+  if (N <= 0) return 0;
+  int colblocks = sat_cdiv(N, 256);
+  int RS = 1;
+  while (colblocks * RS < 512 && RS < 64 && (R + RS * 2 - 1) / (RS * 2) >= 16) RS *= 2;
+  int rows_per = sat_cdiv(R, RS);
+  RS = sat_cdiv(R, rows_per > 0 ? rows_per : 1);
+  if (R <= 0) { RS = 1; rows_per = 0; }
+  dim3 g1(colblocks, RS);
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(colsum_partial_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)X, ld, R, N, rows_per, scratch);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ld, R, N, rows_per, scratch);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(colblocks), dim3(256), 0, s, scratch, RS, N, out, accumulate, out2);
+  return (int)hipGetLastError();
+}
+size_t sat_colsum_scratch_floats(int R, int N) { (void)R; return (size_t)64 * (N > 0 ? N : 1); }
+
+int sat_embed_gather(const float* W, const int32_t* tok, int B, int T1, long tok_stride_b, int E, int dtype,
+                     void* out, long out_ld, hipStream_t s) {
+  int R = B * T1;
+  if (R <= 0) return 0;
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(embed_gather_kernel<bf16>, dim3(R), dim3(256), 0, s, W, tok, R, tok_stride_b, T1, E,
+                       (bf16*)out, out_ld);
+  else
+    hipLaunchKernelGGL(embed_gather_kernel<float>, dim3(R), dim3(256), 0, s, W, tok, R, tok_stride_b, T1, E,
+                       (float*)out, out_ld);
+  return (int)hipGetLastError();
+}
+
+int sat_embed_scatter_add(const float* dX, const int32_t* tok, int R, int E, float* G, hipStream_t s) {
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(embed_scatter_kernel, dim3(R), dim3(256), 0, s, dX, tok, R, E, G);
+  return (int)hipGetLastError();
+}
+
+int sat_argmax_rows(const void* X, int dtype, long ld, int B, int V, int32_t* out, long out_stride,
+                    const float* emb, int E, void* emb_out, long emb_ld, hipStream_t s) {
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(argmax_kernel<bf16>, dim3(B), dim3(256), 0, s, (const bf16*)X, ld, V, out, out_stride, emb, E,
+                       (bf16*)emb_out, emb_ld);
+  else
+    hipLaunchKernelGGL(argmax_kernel<float>, dim3(B), dim3(256), 0, s, (const float*)X, ld, V, out, out_stride, emb, E,
+                       (float*)emb_out, emb_ld);
+  return (int)hipGetLastError();
+}
+
+int sat_cast_launch(const void* x, int xd, void* y, int yd, long n, hipStream_t s) {
+  if (n <= 0) return 0;
+  int g = grid_for(n);
+  if (xd == SAT_F32 && yd == SAT_BF16) hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(g), dim3(256), 0, s, (const float*)x, (bf16*)y, n);
+  else if (xd == SAT_BF16 && yd == SAT_F32) hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(g), dim3(256), 0, s, (const bf16*)x, (float*)y, n);
+  else if (xd == SAT_F32) hipLaunchKernelGGL((cast_kernel<float, float>), dim3(g), dim3(256), 0, s, (const float*)x, (float*)y, n);
+  else hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(g), dim3(256), 0, s, (const bf16*)x, (bf16*)y, n);
+  return (int)hipGetLastError();
+}
+
+// ================================ C ABI =====================================
+extern "C" int sat_abi_version(void) { return SAT_ABI_VERSION; }
+
+extern "C" const char* sat_error_string(int code) {
+  if (code == 0) return "success";
+  if (code == SAT_ERR_INVALID) return "invalid argument or unsupported shape";
+  return hipGetErrorString((hipError_t)code);
+}
+
+extern "C" int sat_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, void* stream) {
+  SAT_REQUIRE(x && y && n >= 0);
+  return sat_cast_launch(x, x_dtype, y, y_dtype, n, (hipStream_t)stream);
+}
+
+extern "C" int sat_mean_rows_abi(const void* a, int B, int L, int D, int dtype, float* out_f32, void* out_t,
+                                 void* stream) {
+  SAT_REQUIRE(a && B > 0 && L > 0 && D > 0);
+  return sat_mean_rows(a, B, L, D, dtype, out_f32, out_t, (hipStream_t)stream);
+}
+
+extern "C" int sat_nchw_to_nhwc(int N, int C, int H, int W, int Cp, int dtype, const float* x, void* y,
+                                void* stream) {
+  SAT_REQUIRE(x && y && Cp >= C && C > 0);
+  long pix = (long)N * H * W;
+  int g = grid_for(pix);
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, x, (bf16*)y, N, C, H, W, Cp);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, x, (float*)y, N, C, H, W, Cp);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sat_maxpool2d_nhwc(int N, int H, int W, int C, int k, int stride, int pad, int dtype, const void* x,
+                                  void* y, int OH, int OW, void* stream) {
+  SAT_REQUIRE(x && y && k > 0 && stride > 0);
+  SAT_REQUIRE(OH == (H + 2 * pad - k) / stride + 1 && OW == (W + 2 * pad - k) / stride + 1);
+  long total = (long)N * OH * OW * C;
+  int g = grid_for(total);
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(maxpool_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, (bf16*)y, N, H,
+                       W, C, k, stride, pad, OH, OW);
+  else
+    hipLaunchKernelGGL(maxpool_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const float*)x, (float*)y, N,
+                       H, W, C, k, stride, pad, OH, OW);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sat_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* param_lp,
+                             int64_t n, float beta1, float beta2, float eps, float step_size,
+                             float bias_correction2_sqrt, void* stream) {
+  SAT_REQUIRE(param && grad && exp_avg && exp_avg_sq && n >= 0);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
+                     exp_avg_sq, (bf16*)param_lp, (long)n, beta1, beta2, eps, step_size, bias_correction2_sqrt);
+  return (int)hipGetLastError();
+}

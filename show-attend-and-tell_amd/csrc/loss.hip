@@ -1,0 +1,183 @@
+// Fused caption loss and in-loop metrics (train.py:135-162, utils.py:44-80,101-107).
+//
+//   loss = CE(preds[:, :T-2] time-major, captions[:, 1:T-1])      (pads included,
+//          last decoder step never scored: pack_padded_sequence with lengths T-2)
+//        + alpha_c * mean_{b,l} (1 - sum_t alpha[b,t,l])^2
+//
+// Forward, grid = one workgroup per (b,t) row: max / sum-exp over V, the row's
+// CE term, and the rank of the target logit (top-1 / top-5 correctness of
+// sequence_accuracy, pad-masked, over all T-1 steps) in the same pass.  A
+// single-workgroup pass folds rows in a fixed order (deterministic), forms the
+// attention regulariser and its gradient, and counts caption tokens.
+// Backward recomputes softmax from preds + the saved log-sum-exp:
+// dL/dlogit = g * (softmax - onehot) / (B*(T-2)) for scored rows.
+#include "sat_common.h"
+#include "sat_internal.h"
+
+namespace {
+
+constexpr int kStat = 5;  // lse, loss_row, top1, top5, nonpad
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < nw; ++i) s += red[i];
+  return s;
+}
+__device__ __forceinline__ float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float s = -INFINITY;
+  for (int i = 0; i < nw; ++i) s = fmaxf(s, red[i]);
+  return s;
+}
+
+template <typename TT>
+__global__ __launch_bounds__(256) void loss_rows_kernel(const TT* __restrict__ preds, const int64_t* __restrict__ caps,
+                                                        int B, int T, int V, int pad_id, float* __restrict__ stats) {
+  __shared__ float red[4];
+  const int r = blockIdx.x;
+  const int T1 = T - 1;
+  const int b = r / T1, t = r - b * T1;
+  const TT* x = preds + (long)r * V;
+  const int tgt = (int)caps[(long)b * T + t + 1];
+  const float xt = (tgt >= 0 && tgt < V) ? (float)x[tgt] : 0.f;
+  float m = -INFINITY, cnt = 0.f;
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    const float xv = (float)x[v];
+    m = fmaxf(m, xv);
+    cnt += (xv > xt || (xv == xt && v < tgt)) ? 1.f : 0.f;
+  }
+  m = block_max(m, red);
+  float se = 0.f;
+  for (int v = threadIdx.x; v < V; v += blockDim.x) se += expf((float)x[v] - m);
+  se = block_sum(se, red);
+  cnt = block_sum(cnt, red);
+  if (threadIdx.x == 0) {
+    const float lse = m + logf(se);
+    const bool nonpad = tgt != pad_id;
+    float* st = stats + (long)r * kStat;
+    st[0] = lse;
+    st[1] = (t < T1 - 1) ? lse - xt : 0.f;
+    st[2] = (nonpad && cnt < 1.f) ? 1.f : 0.f;
+    st[3] = (nonpad && cnt < 5.f) ? 1.f : 0.f;
+    st[4] = nonpad ? 1.f : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* __restrict__ stats, const float* __restrict__ alphas,
+                                                           const int64_t* __restrict__ caps, int B, int T, int L,
+                                                           float alpha_c, int s0, int s1, int s2,
+                                                           float* __restrict__ dreg, float* __restrict__ out) {
+  __shared__ float red[16];
+  const int T1 = T - 1, R = B * T1;
+  float ce = 0.f, c1 = 0.f, c5 = 0.f, np = 0.f;
+  for (int r = threadIdx.x; r < R; r += blockDim.x) {
+    const float* st = stats + (long)r * kStat;
+    ce += st[1]; c1 += st[2]; c5 += st[3]; np += st[4];
+  }
+  ce = block_sum(ce, red);
+  c1 = block_sum(c1, red);
+  c5 = block_sum(c5, red);
+  np = block_sum(np, red);
+  float reg = 0.f;
+  const float inv_bl = 1.0f / (float)(B * L);
+  for (int i = threadIdx.x; i < B * L; i += blockDim.x) {
+    const int b = i / L, l = i - b * L;
+    float ssum = 0.f;
+    for (int t = 0; t < T1; ++t) ssum += alphas[((long)b * T1 + t) * L + l];
+    const float d = 1.f - ssum;
+    reg += d * d;
+    dreg[i] = alpha_c * 2.f * (ssum - 1.f) * inv_bl;
+  }
+  reg = block_sum(reg, red);
+  float cl = 0.f;
+  for (int i = threadIdx.x; i < B * T; i += blockDim.x) {
+    const int64_t tok = caps[i];
+    cl += (tok != s0 && tok != s1 && tok != s2) ? 1.f : 0.f;
+  }
+  cl = block_sum(cl, red);
+  if (threadIdx.x == 0) {
+    const float cem = ce / (float)(B * (T1 - 1));
+    const float regm = alpha_c * (reg * inv_bl);
+    out[0] = cem + regm;
+    out[1] = cem;
+    out[2] = regm;
+    out[3] = c1; out[4] = c5; out[5] = np; out[6] = cl;
+  }
+}
+
+template <typename TT>
+__global__ __launch_bounds__(256) void loss_bwd_kernel(const TT* __restrict__ preds, const int64_t* __restrict__ caps,
+                                                       int B, int T, int V, int L, const float* __restrict__ stats,
+                                                       const float* __restrict__ dreg, const float* __restrict__ grad_out,
+                                                       TT* __restrict__ dpreds, float* __restrict__ dalphas) {
+  const int r = blockIdx.x;
+  const int T1 = T - 1;
+  const int b = r / T1, t = r - b * T1;
+  const float g = grad_out ? grad_out[0] : 1.f;
+  const TT* x = preds + (long)r * V;
+  TT* dx = dpreds + (long)r * V;
+  if (t < T1 - 1) {
+    const int tgt = (int)caps[(long)b * T + t + 1];
+    const float lse = stats[(long)r * kStat];
+    const float scale = g / (float)(B * (T1 - 1));
+    for (int v = threadIdx.x; v < V; v += blockDim.x) {
+      float p = expf((float)x[v] - lse);
+      if (v == tgt) p -= 1.f;
+      dx[v] = (TT)(p * scale);
+    }
+  } else {
+    for (int v = threadIdx.x; v < V; v += blockDim.x) dx[v] = (TT)0.0f;
+  }
+  for (int l = threadIdx.x; l < L; l += blockDim.x) dalphas[(long)r * L + l] = g * dreg[(long)b * L + l];
+}
+
+}  // namespace
+
+extern "C" size_t sat_caption_loss_workspace_bytes(int B, int T, int L) {
+  return ((size_t)B * (T - 1) * kStat + (size_t)B * L + 64) * sizeof(float);
+}
+
+extern "C" int sat_caption_loss_forward(int B, int T, int V, int L, int dtype, const void* preds, const float* alphas,
+                                        const int64_t* captions, float alpha_c, int pad_id, int skip0, int skip1,
+                                        int skip2, void* workspace, float* out, void* stream) {
+  SAT_REQUIRE(preds && alphas && captions && workspace && out && B > 0 && T >= 3 && V > 0 && L > 0);
+  hipStream_t s = (hipStream_t)stream;
+  const int R = B * (T - 1);
+  float* stats = (float*)workspace;
+  float* dreg = stats + (size_t)R * kStat;
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(loss_rows_kernel<bf16>, dim3(R), dim3(256), 0, s, (const bf16*)preds, captions, B, T, V, pad_id, stats);
+  else
+    hipLaunchKernelGGL(loss_rows_kernel<float>, dim3(R), dim3(256), 0, s, (const float*)preds, captions, B, T, V, pad_id, stats);
+  SAT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(1024), 0, s, stats, alphas, captions, B, T, L, alpha_c, skip0,
+                     skip1, skip2, dreg, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sat_caption_loss_backward(int B, int T, int V, int L, int dtype, const void* preds,
+                                         const int64_t* captions, float alpha_c, void* workspace,
+                                         const float* grad_out, void* d_preds, float* d_alphas, void* stream) {
+  SAT_REQUIRE(preds && captions && workspace && d_preds && d_alphas && B > 0 && T >= 3);
+  (void)alpha_c;
+  hipStream_t s = (hipStream_t)stream;
+  const int R = B * (T - 1);
+  const float* stats = (const float*)workspace;
+  const float* dreg = stats + (size_t)R * kStat;
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(loss_bwd_kernel<bf16>, dim3(R), dim3(256), 0, s, (const bf16*)preds, captions, B, T, V, L, stats,
+                       dreg, grad_out, (bf16*)d_preds, d_alphas);
+  else
+    hipLaunchKernelGGL(loss_bwd_kernel<float>, dim3(R), dim3(256), 0, s, (const float*)preds, captions, B, T, V, L, stats,
+                       dreg, grad_out, (float*)d_preds, d_alphas);
+  return (int)hipGetLastError();
+}

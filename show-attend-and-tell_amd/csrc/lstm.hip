@@ -1,0 +1,250 @@
+// nn.LSTMCell pointwise part (decoder.py:115) forward/backward, plus the small
+// elementwise pieces of the decoder: dropout (decoder.py:121-125), the advanced
+// deep-output combine/split (decoder.py:149-158), tanh-init backward
+// (decoder.py:137-147).  The gate GEMMs themselves run on MFMA (gemm.hip); the
+// partial gate sums meet here so no [B,4E] sum is materialised.
+#include "sat_common.h"
+#include "sat_internal.h"
+
+namespace {
+
+inline int grid_for(long n) {
+  long g = (n + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
+
+template <typename T>
+__global__ void lstm_fwd_kernel(LstmFwdArgs a) {
+  const int E = a.E;
+  const long n = (long)a.B * E;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / E), j = (int)(i - (long)b * E);
+    float sg[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = a.xpart[(long)b * a.xpart_ld + q * E + j] + a.hpart[(long)b * a.hpart_ld + q * E + j];
+      if (a.cpart) v += a.cpart[(long)b * a.cpart_ld + q * E + j];
+      sg[q] = v;
+      a.gates[(long)b * a.gates_ld + q * E + j] = v;
+    }
+    const float ig = 1.f / (1.f + expf(-sg[0]));
+    const float fg = 1.f / (1.f + expf(-sg[1]));
+    const float gg = tanhf(sg[2]);
+    const float og = 1.f / (1.f + expf(-sg[3]));
+    const float c = fg * a.c_prev[(long)b * a.c_prev_ld + j] + ig * gg;
+    const float h = og * tanhf(c);
+    a.c_out[(long)b * a.c_out_ld + j] = c;
+    if (a.c_next_in) a.c_next_in[(long)b * a.c_next_in_ld + j] = c;
+    a.h_out[(long)b * a.h_out_ld + j] = h;
+    if (a.h_out_t) ((T*)a.h_out_t)[(long)b * a.h_out_t_ld + j] = (T)h;
+    if (a.h_next_in_t) ((T*)a.h_next_in_t)[(long)b * a.h_next_in_t_ld + j] = (T)h;
+  }
+}
+
+template <typename T>
+__global__ void lstm_bwd_kernel(LstmBwdArgs a) {
+  const int E = a.E;
+  const long n = (long)a.B * E;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / E), j = (int)(i - (long)b * E);
+    const float* g = a.gates + (long)b * a.gates_ld;
+    const float ig = 1.f / (1.f + expf(-g[j]));
+    const float fg = 1.f / (1.f + expf(-g[E + j]));
+    const float gg = tanhf(g[2 * E + j]);
+    const float og = 1.f / (1.f + expf(-g[3 * E + j]));
+    const float cp = a.c_prev[(long)b * a.c_prev_ld + j];
+    const float cn = a.c_new[(long)b * a.c_new_ld + j];
+    const float tc = tanhf(cn);
+    float dh = a.dh_rec ? a.dh_rec[(long)b * a.dh_rec_ld + j] : 0.f;
+    if (a.dh_head) {
+      float hh = a.dh_head[(long)b * a.dh_head_ld + j];
+      if (a.mask) hh = a.mask[(long)b * a.mask_ld + j] ? hh * 2.f : 0.f;
+      dh += hh;
+    }
+    const float dc_in = a.dc_zero ? 0.f : a.dc[i];
+    const float dc = dc_in + dh * og * (1.f - tc * tc);
+    const float d_o = dh * tc * og * (1.f - og);
+    const float d_i = dc * gg * ig * (1.f - ig);
+    const float d_f = dc * cp * fg * (1.f - fg);
+    const float d_g = dc * ig * (1.f - gg * gg);
+    a.dc[i] = dc * fg;
+    float* dgr = a.d_gates + (long)b * a.d_gates_ld;
+    dgr[j] = d_i; dgr[E + j] = d_f; dgr[2 * E + j] = d_g; dgr[3 * E + j] = d_o;
+    if (a.d_gates_t) {
+      T* dt = (T*)a.d_gates_t + (long)b * a.d_gates_t_ld;
+      dt[j] = (T)d_i; dt[E + j] = (T)d_f; dt[2 * E + j] = (T)d_g; dt[3 * E + j] = (T)d_o;
+    }
+  }
+}
+
+// d(tanh pre) for init_h / init_c: dpre[b, 0:E] = dh (1-h^2), dpre[b, E:2E] = dc (1-c^2)
+template <typename T>
+__global__ void tanh_pair_bwd_kernel(const float* dh, const float* dc, const float* hc0, int B, int E, float* dpre,
+                                     T* dpre_t) {
+  const long n = (long)B * 2 * E;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / (2 * E)), j = (int)(i - (long)b * 2 * E);
+    const float y = hc0[i];
+    const float d = j < E ? dh[(long)b * E + j] : dc[(long)b * E + (j - E)];
+    const float v = d * (1.f - y * y);
+    dpre[i] = v;
+    if (dpre_t) dpre_t[i] = (T)v;
+  }
+}
+
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+// hd[b,t,e] = h[b,t,e] * keep * 2 (train) | h (eval); keep drawn from (seed, b, t, e) or given.
+// Rows r = b*T1 + t of this call live at r*ld in h / mask / out (per-step calls pass T1 = 1 and
+// the full-sequence row stride as ld; t_offset is then the step index).
+template <typename T>
+__global__ void dropout_kernel(const float* h, long h_ld, int B, int T1, int E, int training, int has_mask,
+                               const uint8_t* mask_in, uint8_t* mask_out, long mask_ld, uint64_t seed, int t_offset,
+                               T* out, long out_ld) {
+  const long n = (long)B * T1 * E;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int e = (int)(i % E);
+    const long r = i / E;
+    const int b = (int)(r / T1), t = (int)(r - (long)b * T1) + t_offset;
+    const float x = h[r * h_ld + e];
+    float y = x;
+    if (training) {
+      uint8_t keep;
+      if (has_mask) keep = mask_in[r * mask_ld + e];
+      else keep = (uint8_t)(mix32(seed * 0x9E3779B97F4A7C15ULL + (((uint64_t)b << 40) ^ ((uint64_t)t << 20) ^ (uint64_t)e)) & 1u);
+      if (mask_out) mask_out[r * mask_ld + e] = keep;
+      y = keep ? x * 2.f : 0.f;
+    }
+    out[r * out_ld + e] = (T)y;
+  }
+}
+
+template <typename T>
+__global__ void relu_mask_kernel(const T* d, const T* ref, long n, T* out) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = (float)ref[i] > 0.f ? d[i] : (T)0.0f;
+}
+
+template <typename T>
+__global__ void ado_split_kernel(const float* dcomb, const float* fh, const float* fz, long n, T* dfh, T* dfz) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float d = dcomb[i];
+    dfh[i] = (T)(fh[i] > 0.f ? d : 0.f);
+    dfz[i] = (T)(fz[i] > 0.f ? d : 0.f);
+  }
+}
+
+// comb = fh + fz + emb   (fz already relu'd by its GEMM epilogue)
+template <typename T>
+__global__ void ado_combine_kernel(const float* fh, const float* fz, const T* emb, long n, T* comb) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    comb[i] = (T)(fh[i] + fz[i] + (float)emb[i]);
+}
+
+__global__ void fill_kernel(float* p, long n, float v) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = v;
+}
+
+template <typename T>
+__global__ void broadcast_rows_kernel(const T* src, int B, int D, int T1, T* dst) {
+  const long n = (long)B * T1 * D;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int d = (int)(i % D);
+    const int b = (int)(i / ((long)T1 * D));
+    dst[i] = src[(long)b * D + d];
+  }
+}
+
+__global__ void row_sum_acc_kernel(const float* X, int R, int N, float* out) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += X[(long)r * N + n];
+  out[n] += s;
+}
+
+__global__ void tokens_kernel(const int64_t* caps, int B, int T, int T1, int32_t* tok) {
+  const int n = B * T1;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int b = i / T1, t = i - b * T1;
+    tok[i] = (int32_t)caps[(long)b * T + t];
+  }
+}
+
+}  // namespace
+
+#define DISPATCH_T(dtype, KERNEL, grid, ...)                                                   \
+  do {                                                                                       \
+    if ((dtype) == SAT_BF16) hipLaunchKernelGGL(KERNEL<bf16>, grid, dim3(256), 0, s, __VA_ARGS__); \
+    else hipLaunchKernelGGL(KERNEL<float>, grid, dim3(256), 0, s, __VA_ARGS__);               \
+  } while (0)
+
+int sat_lstm_fwd_launch(const LstmFwdArgs& a, hipStream_t s) {
+  DISPATCH_T(a.dtype, lstm_fwd_kernel, dim3(grid_for((long)a.B * a.E)), a);
+  return (int)hipGetLastError();
+}
+int sat_lstm_bwd_launch(const LstmBwdArgs& a, hipStream_t s) {
+  DISPATCH_T(a.dtype, lstm_bwd_kernel, dim3(grid_for((long)a.B * a.E)), a);
+  return (int)hipGetLastError();
+}
+int sat_tanh_pair_bwd(const float* d_h, const float* d_c, const float* hc0, int B, int E, float* dpre_f32,
+                      void* dpre_t, int dtype, hipStream_t s) {
+  dim3 g(grid_for((long)B * 2 * E));
+  if (dtype == SAT_BF16) hipLaunchKernelGGL(tanh_pair_bwd_kernel<bf16>, g, dim3(256), 0, s, d_h, d_c, hc0, B, E, dpre_f32, (bf16*)dpre_t);
+  else hipLaunchKernelGGL(tanh_pair_bwd_kernel<float>, g, dim3(256), 0, s, d_h, d_c, hc0, B, E, dpre_f32, (float*)dpre_t);
+  return (int)hipGetLastError();
+}
+int sat_dropout_apply(const float* h, long h_ld, int B, int T1, int E, int training, int has_mask,
+                      const uint8_t* mask_in, uint8_t* mask_out, long mask_ld, uint64_t seed, int t_offset,
+                      void* out_t, long out_ld, int dtype, hipStream_t s) {
+  dim3 g(grid_for((long)B * T1 * E));
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(dropout_kernel<bf16>, g, dim3(256), 0, s, h, h_ld, B, T1, E, training, has_mask, mask_in, mask_out, mask_ld, seed, t_offset, (bf16*)out_t, out_ld);
+  else
+    hipLaunchKernelGGL(dropout_kernel<float>, g, dim3(256), 0, s, h, h_ld, B, T1, E, training, has_mask, mask_in, mask_out, mask_ld, seed, t_offset, (float*)out_t, out_ld);
+  return (int)hipGetLastError();
+}
+int sat_relu_mask_mul(const void* d, const void* ref, long n, int dtype, void* out_t, hipStream_t s) {
+  dim3 g(grid_for(n));
+  if (dtype == SAT_BF16) hipLaunchKernelGGL(relu_mask_kernel<bf16>, g, dim3(256), 0, s, (const bf16*)d, (const bf16*)ref, n, (bf16*)out_t);
+  else hipLaunchKernelGGL(relu_mask_kernel<float>, g, dim3(256), 0, s, (const float*)d, (const float*)ref, n, (float*)out_t);
+  return (int)hipGetLastError();
+}
+int sat_ado_bwd_split(const float* d_comb, const float* fh, const float* fz, long n, int dtype, void* d_fh_t,
+                      void* d_fz_t, hipStream_t s) {
+  dim3 g(grid_for(n));
+  if (dtype == SAT_BF16) hipLaunchKernelGGL(ado_split_kernel<bf16>, g, dim3(256), 0, s, d_comb, fh, fz, n, (bf16*)d_fh_t, (bf16*)d_fz_t);
+  else hipLaunchKernelGGL(ado_split_kernel<float>, g, dim3(256), 0, s, d_comb, fh, fz, n, (float*)d_fh_t, (float*)d_fz_t);
+  return (int)hipGetLastError();
+}
+int sat_ado_combine(const float* fh, const float* fz, const void* emb, long n, int dtype, void* comb_t,
+                    hipStream_t s) {
+  dim3 g(grid_for(n));
+  if (dtype == SAT_BF16) hipLaunchKernelGGL(ado_combine_kernel<bf16>, g, dim3(256), 0, s, fh, fz, (const bf16*)emb, n, (bf16*)comb_t);
+  else hipLaunchKernelGGL(ado_combine_kernel<float>, g, dim3(256), 0, s, fh, fz, (const float*)emb, n, (float*)comb_t);
+  return (int)hipGetLastError();
+}
+int sat_fill_const(float* p, long n, float v, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, n, v);
+  return (int)hipGetLastError();
+}
+int sat_broadcast_rows(const void* src, int B, int D, int T1, int dtype, void* dst, hipStream_t s) {
+  dim3 g(grid_for((long)B * T1 * D));
+  if (dtype == SAT_BF16) hipLaunchKernelGGL(broadcast_rows_kernel<bf16>, g, dim3(256), 0, s, (const bf16*)src, B, D, T1, (bf16*)dst);
+  else hipLaunchKernelGGL(broadcast_rows_kernel<float>, g, dim3(256), 0, s, (const float*)src, B, D, T1, (float*)dst);
+  return (int)hipGetLastError();
+}
+int sat_row_sum_accumulate(const float* X, int R, int N, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(row_sum_acc_kernel, dim3(sat_cdiv(N, 256)), dim3(256), 0, s, X, R, N, out);
+  return (int)hipGetLastError();
+}
+int sat_tokens_from_captions(const int64_t* caps, int B, int T, int T1, int32_t* tok, hipStream_t s) {
+  hipLaunchKernelGGL(tokens_kernel, dim3(grid_for((long)B * T1)), dim3(256), 0, s, caps, B, T, T1, tok);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,80 @@
+// Shared definitions for the Show-Attend-and-Tell MI355X (gfx950) kernels.
+// Internal header: the public C-ABI lives in include/sat_hip.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/sat_hip.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16;
+
+#define SAT_CHECK(x)                                   \
+  do {                                                 \
+    hipError_t e__ = (x);                              \
+    if (e__ != hipSuccess) return (int)e__;            \
+  } while (0)
+#define SAT_LAUNCH_CHECK() SAT_CHECK(hipGetLastError())
+#define SAT_REQUIRE(cond)                              \
+  do {                                                 \
+    if (!(cond)) return SAT_ERR_INVALID;               \
+  } while (0)
+
+static inline int sat_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// ---- scalar load/store helpers for the two storage dtypes -------------------
+__device__ __forceinline__ float ld_as_f32(const void* p, long i, int dt) {
+  return dt == SAT_BF16 ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
+}
+__device__ __forceinline__ void st_from_f32(void* p, long i, int dt, float v) {
+  if (dt == SAT_BF16) ((bf16*)p)[i] = (bf16)v;
+  else ((float*)p)[i] = v;
+}
+template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f32(float v) { return (T)v; }
+
+__device__ __forceinline__ float sat_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case SAT_ACT_RELU: return v > 0.f ? v : 0.f;
+    case SAT_ACT_TANH: return tanhf(v);
+    case SAT_ACT_SIGMOID: return 1.0f / (1.0f + expf(-v));
+    default: return v;
+  }
+}
+
+// wave64 reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- internal GEMM descriptor (host side) -----------------------------------
+// C[m,n] = act(alpha * sum_k A(m,k) B(n,k) + bias[n] + add1[m,n] + beta*C[m,n])
+//   A(m,k): transA ? A[k*lda + m] : A[m*lda + k]   (conv: implicit im2col of NHWC input)
+//   B(n,k): transB ? B[k*ldb + n] : B[n*ldb + k]
+struct SatGemm {
+  int M = 0, N = 0, K = 0;
+  int dtype = SAT_F32;  // operand dtype of A and B
+  const void* A = nullptr; long lda = 0; int transA = 0;
+  const void* B = nullptr; long ldb = 0; int transB = 0;
+  void* C = nullptr; long ldc = 0; int c_dtype = SAT_F32;
+  float alpha = 1.f, beta = 0.f;
+  const float* bias = nullptr;
+  const void* add1 = nullptr; long ld_add1 = 0; int add1_dtype = SAT_F32;
+  int act = SAT_ACT_NONE;
+  void* aux = nullptr; long ld_aux = 0; int aux_dtype = SAT_BF16;
+  int batch = 1; long sA = 0, sB = 0, sC = 0, s_add1 = 0, s_aux = 0;
+  SatConvGeom conv{};  // conv.C > 0 selects the implicit-im2col A loader
+};
+
+int sat_gemm_launch(const SatGemm& g, hipStream_t s);

@@ -1,0 +1,101 @@
+// Internal host-side launchers shared between the kernel translation units.
+#pragma once
+#include "sat_common.h"
+
+int sat_mean_rows(const void* a, int B, int L, int D, int dtype, float* out_f32, void* out_t, hipStream_t s);
+int sat_colsum(const void* X, int dtype, long ld, int R, int N, float* out, int accumulate, float* out2,
+               float* scratch, hipStream_t s);
+size_t sat_colsum_scratch_floats(int R, int N);
+int sat_embed_gather(const float* W, const int32_t* tok, int B, int T1, long tok_stride_b, int E, int dtype,
+                     void* out, long out_ld, hipStream_t s);
+int sat_embed_scatter_add(const float* dX, const int32_t* tok, int R, int E, float* G, hipStream_t s);
+int sat_argmax_rows(const void* X, int dtype, long ld, int B, int V, int32_t* out, long out_stride,
+                    const float* emb, int E, void* emb_out, long emb_ld, hipStream_t s);
+int sat_cast_launch(const void* x, int xd, void* y, int yd, long n, hipStream_t s);
+
+// ---- attention (attention.py:14-21 + decoder.py:97-100 gate) ----
+struct AttnFwdArgs {
+  int B, L, D, E, dtype;
+  const void* Ws;            // [B,L,E]  dtype
+  const float* uh; long uh_ld;        // U h + b_U, row b at uh + b*uh_ld
+  const float* v_w; const float* v_b; // [E], [1]
+  const void* a;             // [B,L,D] dtype
+  const float* gate_pre; long gate_ld;  // f_beta h + b (nullable: plain attention)
+  float* alpha; long alpha_ld;          // [B, *, L]
+  float* ctx; long ctx_ld;              // fp32 context
+  void* ctx_t; long ctx_t_ld;           // dtype context copy (nullable)
+  float* gate; long gate_out_ld;        // sigmoid gate (nullable)
+  void* gated; long gated_ld;           // dtype gate*context (nullable)
+  float* uh_save; long uh_save_ld;      // copy of U h + b (nullable)
+};
+int sat_attention_fwd_launch(const AttnFwdArgs& a, hipStream_t s);
+
+struct AttnBwdArgs {
+  int B, L, D, E, dtype;
+  const void* Ws; const void* a;
+  const float* uh; long uh_ld;          // saved U h + b of this step
+  const float* v_w;
+  const float* alpha; long alpha_ld;    // this step's alpha rows
+  const float* d_alpha_ext; long d_alpha_ext_ld;  // loss gradient wrt alphas (this step), nullable
+  const float* d_gated; long d_gated_ld;          // dL/d(gate*context)  [B,D]
+  const float* gate; long gate_ld;
+  const float* ctx; long ctx_ld;
+  const float* d_ctx_ext; long d_ctx_ext_ld;      // extra dL/dcontext (ado head), nullable
+  float* d_uh; long d_uh_ld;            // out fp32 dL/d(U h)  (== dL/dU_b rows)
+  void* d_uh_t;                         // out dtype copy (same ld), nullable
+  float* d_gpre; long d_gpre_ld;        // out fp32 dL/d(f_beta h + b)
+  void* d_gpre_t;                       // out dtype copy, nullable
+  float* dWs_acc;                       // [B,L,E] += dL/dWs
+  float* dv_acc;                        // [B,E]  += dL/dv (per row b)
+  float* dbv_acc;                       // [B]    += dL/dv.bias
+  float* part;                          // scratch [B, NS, L]
+};
+int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s);
+
+// ---- LSTMCell pointwise (decoder.py:115, nn.LSTMCell gate order i,f,g,o) ----
+struct LstmFwdArgs {
+  int B, E, dtype;
+  const float* hpart; long hpart_ld;    // h W_hh^T + b_hh     [B,4E]
+  const float* xpart; long xpart_ld;    // emb W_ih_e^T + b_ih [B,4E]
+  const float* cpart; long cpart_ld;    // ctx W_ih_c^T        [B,4E] (ld 0 = broadcast row)
+  const float* c_prev; long c_prev_ld;
+  float* gates; long gates_ld;          // pre-activation save
+  float* c_out; long c_out_ld;
+  float* c_next_in; long c_next_in_ld;  // nullable: copy of c_out as next step's input
+  float* h_out; long h_out_ld;          // fp32
+  void* h_out_t; long h_out_t_ld;       // dtype copy (nullable)
+  void* h_next_in_t; long h_next_in_t_ld;  // dtype copy as next step's input (nullable)
+};
+int sat_lstm_fwd_launch(const LstmFwdArgs& a, hipStream_t s);
+
+struct LstmBwdArgs {
+  int B, E, dtype;
+  const float* gates; long gates_ld;
+  const float* c_prev; long c_prev_ld;
+  const float* c_new; long c_new_ld;
+  const float* dh_rec; long dh_rec_ld;  // nullable (last step)
+  const float* dh_head; long dh_head_ld;  // nullable
+  const uint8_t* mask; long mask_ld;    // dropout keep-mask for dh_head (nullable = no dropout)
+  float* dc;                            // [B,E] in: dc from step t+1 (or zeros), out: dc_prev
+  int dc_zero;                          // treat incoming dc as zero
+  float* d_gates; long d_gates_ld;      // out fp32
+  void* d_gates_t; long d_gates_t_ld;   // out dtype copy (nullable)
+};
+int sat_lstm_bwd_launch(const LstmBwdArgs& a, hipStream_t s);
+
+// ---- misc decoder elementwise ----
+int sat_tanh_pair_bwd(const float* d_h, const float* d_c, const float* hc0, int B, int E, float* dpre_f32,
+                      void* dpre_t, int dtype, hipStream_t s);
+int sat_dropout_apply(const float* h, long h_ld, int B, int T1, int E, int training, int has_mask,
+                      const uint8_t* mask_in, uint8_t* mask_out, long mask_ld, uint64_t seed, int t_offset,
+                      void* out_t, long out_ld, int dtype, hipStream_t s);
+int sat_relu_mask_mul(const void* d, const void* ref, long n, int dtype, void* out_t, hipStream_t s);
+int sat_ado_bwd_split(const float* d_comb, const float* fh, const float* fz, long n, int dtype, void* d_fh_t,
+                      void* d_fz_t, hipStream_t s);
+int sat_ado_combine(const float* fh, const float* fz, const void* emb, long n, int dtype,
+                    void* comb_t, hipStream_t s);
+int sat_fill_const(float* p, long n, float v, hipStream_t s);
+int sat_broadcast_rows(const void* src, int B, int D, int T1, int dtype, void* dst, hipStream_t s);
+int sat_row_sum_accumulate(const float* X, int R, int N, float* out, hipStream_t s);
+int sat_tokens_from_captions(const int64_t* caps, int B, int T, int T1, int32_t* tok, hipStream_t s);
+size_t sat_attention_part_floats(int B, int L, int D, int dtype);

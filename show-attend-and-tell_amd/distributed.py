@@ -1,0 +1,50 @@
+"""Data parallelism: one process per GPU, RCCL gradient all-reduce over xGMI.
+
+The reference is single-device (no torch.distributed).  Each rank
+runs the same train step on its own B/N images; the decoder gradients are
+averaged across ranks between backward and Adam, which reproduces the
+full-batch step because both loss terms are means over equal-size local sets
+(SURVEY 8e).
+
+Two buckets, launched asynchronously from inside the decoder's backward:
+  * bucket 1 = the output head (f_out/f_h/f_z or deep_output), ready right after
+    backward phase 1, so its all-reduce overlaps the whole recurrent BPTT;
+  * bucket 2 = everything else, ready when BPTT finishes.
+Both are contiguous slices of the decoder's flat gradient buffer: no packing.
+"""
+import torch
+import torch.distributed as dist
+
+
+class GradAllReduce:
+    def __init__(self, decoder, group=None):
+        self.decoder = decoder
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.works = []
+        self.buckets = []
+        self.use_avg = dist.get_backend(group) == "nccl"   # RCCL has ncclAvg; gloo does not
+        decoder._grad_hooks.append(self._on_phase)
+
+    def _on_phase(self, phase, dec):
+        bucket = dec.grad_bucket(phase)
+        op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
+        self.works.append(dist.all_reduce(bucket, op=op, group=self.group, async_op=True))
+        self.buckets.append(bucket)
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        if not self.use_avg:
+            for b in self.buckets:
+                b.div_(self.world)
+        self.works, self.buckets = [], []
+
+
+def shard_batch(tensor, rank, world):
+    """Rank r's contiguous 1/N of a global batch (global batch divisible by N)."""
+    n = tensor.shape[0]
+    if n % world:
+        raise ValueError(f"global batch {n} not divisible by world size {world}")
+    per = n // world
+    return tensor[rank * per:(rank + 1) * per]

@@ -1,0 +1,191 @@
+"""Encoder module (reference: encoder.py:5-40) on MFMA implicit-GEMM convolutions.
+
+``Encoder(network)`` keeps the reference attributes (``network``, ``net``,
+``dim``) and the torchvision 0.16 parameter layout of ``self.net``
+(``vgg19().features[:-1]`` -> keys ``net.<i>.weight``; ``resnet152`` children
+``[:-2]`` -> ``net.0`` conv1, ``net.1`` bn1, ``net.4-7`` layer1-4 Bottlenecks), so
+torchvision-derived state_dicts load unchanged.  ``forward(x[B,3,H,W]) ->
+[B, L, D]`` runs the trunk as a compiled plan of HIP kernels on NHWC
+activations:
+
+  * every Conv2d (+ eval-mode BatchNorm folded into weight/bias, + ReLU, + the
+    residual add of a Bottleneck) is ONE implicit-GEMM MFMA launch
+    (sat_conv2d_nhwc): M = B*OH*OW, N = Cout, K = KH*KW*Cin;
+  * MaxPool2d is a streaming NHWC kernel;
+  * the image is converted once to NHWC with channels zero-padded 3 -> 8 so the
+    first conv loads 16-byte vectors;
+  * the final NHWC tensor already IS ``permute(0,2,3,1).view(B,-1,C)``
+    (encoder.py:37-39): no transpose.
+
+The trunk is frozen (``requires_grad=False``) and forward-only for every
+network: the reference freezes only VGG19 (encoder.py:29-31) and lets ResNet152
+accumulate encoder gradients the optimiser never reads (train.py:71); skipping
+that dead backward leaves every trained value identical.
+Pretrained ImageNet weights are a download in the reference; here weights are
+randomly initialised with torchvision's scheme unless a state_dict is loaded.
+DenseNet161 (argparse choice, no BASELINE config) is out of scope.
+"""
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from . import ops
+
+VGG19_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M", 512, 512, 512, 512, "M"]
+IN_PAD = 8  # input channels padded 3 -> 8 (16-B bf16 vectors in the im2col loader)
+
+
+class Bottleneck(nn.Module):
+    """torchvision Bottleneck (expansion 4, stride on the 3x3: ResNet v1.5)."""
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+
+def _vgg19_features():
+    layers, cin = [], 3
+    for v in VGG19_CFG:
+        if v == "M":
+            layers.append(nn.MaxPool2d(2, 2))
+        else:
+            layers += [nn.Conv2d(cin, v, 3, padding=1), nn.ReLU(inplace=True)]
+            cin = v
+    return layers[:-1]   # encoder.py:24-27 drops the last MaxPool
+
+
+def _resnet152_trunk():
+    layers = [nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False), nn.BatchNorm2d(64), nn.ReLU(inplace=True),
+              nn.MaxPool2d(3, 2, 1)]
+    inplanes = 64
+    for li, (n, planes) in enumerate(zip([3, 8, 36, 3], [64, 128, 256, 512])):
+        stride = 1 if li == 0 else 2
+        blocks = []
+        for bi in range(n):
+            s = stride if bi == 0 else 1
+            ds = None
+            if bi == 0 and (s != 1 or inplanes != planes * 4):
+                ds = nn.Sequential(nn.Conv2d(inplanes, planes * 4, 1, stride=s, bias=False), nn.BatchNorm2d(planes * 4))
+            blocks.append(Bottleneck(inplanes, planes, s, ds))
+            inplanes = planes * 4
+        layers.append(nn.Sequential(*blocks))
+    return layers
+
+
+def _init_like_torchvision(module):
+    for m in module.modules():
+        if isinstance(m, nn.Conv2d):
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, nn.BatchNorm2d):
+            nn.init.constant_(m.weight, 1)
+            nn.init.constant_(m.bias, 0)
+
+
+class Encoder(nn.Module):
+    def __init__(self, network="vgg19", dtype=torch.float32):
+        super().__init__()
+        self.network = network
+        if network == "resnet152":
+            self.net = nn.Sequential(*_resnet152_trunk())
+            self.dim = 2048
+        elif network == "densenet161":
+            raise NotImplementedError("densenet161 is out of scope for the MI355X path (no BASELINE config)")
+        else:
+            self.net = nn.Sequential(*_vgg19_features())
+            self.dim = 512
+        _init_like_torchvision(self.net)
+        for p in self.net.parameters():   # frozen trunk (encoder.py:29-31; see module docstring)
+            p.requires_grad = False
+        self.compute_dtype = dtype
+        self._plan = None
+        self._plan_key = None
+        self.timing = None   # bench hook: list collecting (start, end) HIP events around every conv launch
+
+    def _conv(self, x, f, relu, residual=None):
+        w, b, s, p = f
+        if self.timing is None:
+            return ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual)
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        y = ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual)
+        en.record()
+        self.timing.append((st, en))
+        return y
+
+    # ---- plan: folded NHWC weights ------------------------------------------
+    @torch.no_grad()
+    def _fold(self, conv, bn, pad_in=None):
+        w = conv.weight.detach().float()
+        b = conv.bias.detach().float() if conv.bias is not None else torch.zeros(w.shape[0], device=w.device)
+        if bn is not None:  # eval-mode BatchNorm2d folded into the conv
+            scale = bn.weight.float() / torch.sqrt(bn.running_var.float() + bn.eps)
+            w = w * scale[:, None, None, None]
+            b = bn.bias.float() + (b - bn.running_mean.float()) * scale
+        w = w.permute(0, 2, 3, 1)   # [Cout, KH, KW, Cin]
+        if pad_in is not None and w.shape[3] < pad_in:
+            w = torch.nn.functional.pad(w, (0, pad_in - w.shape[3]))
+        return (w.contiguous().to(self.compute_dtype), b.contiguous(), conv.stride[0], conv.padding[0])
+
+    def _state_key(self, device, dtype):
+        return (device, dtype, tuple(p._version for p in self.net.parameters()),
+                tuple(b._version for b in self.net.buffers()))
+
+    def _build_plan(self, device, dtype):
+        self.compute_dtype = dtype
+        plan = []
+        mods = list(self.net.children())
+        if self.network == "resnet152":
+            plan.append(("conv", self._fold(mods[0], mods[1], IN_PAD), True, None))
+            plan.append(("pool", 3, 2, 1))
+            for layer in mods[4:]:
+                for blk in layer:
+                    ds = self._fold(blk.downsample[0], blk.downsample[1]) if blk.downsample is not None else None
+                    plan.append(("block", self._fold(blk.conv1, blk.bn1), self._fold(blk.conv2, blk.bn2),
+                                 self._fold(blk.conv3, blk.bn3), ds))
+        else:
+            first = True
+            for i, m in enumerate(mods):
+                if isinstance(m, nn.Conv2d):
+                    relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
+                    plan.append(("conv", self._fold(m, None, IN_PAD if first else None), relu, None))
+                    first = False
+                elif isinstance(m, nn.MaxPool2d):
+                    plan.append(("pool", m.kernel_size, m.stride, m.padding))
+        self._plan = plan
+
+    def compiled_plan(self, device, dtype):
+        key = self._state_key(device, dtype)
+        if self._plan is None or self._plan_key != key:
+            self._build_plan(device, dtype)
+            self._plan_key = key
+        return self._plan
+
+    def forward(self, x, dtype=None):
+        L.require_device(x)
+        dtype = dtype or self.compute_dtype
+        plan = self.compiled_plan(x.device, dtype)
+        y = ops.nchw_to_nhwc(x, IN_PAD, dtype)
+        for step in plan:
+            if step[0] == "conv":
+                y = self._conv(y, step[1], step[2])
+            elif step[0] == "pool":
+                y = ops.maxpool2d_nhwc(y, step[1], step[2], step[3])
+            else:
+                _, c1, c2, c3, ds = step
+                out = self._conv(y, c1, True)
+                out = self._conv(out, c2, True)
+                idn = self._conv(y, ds, False) if ds is not None else y
+                y = self._conv(out, c3, True, residual=idn)
+        B, H, W, C = y.shape
+        return y.view(B, H * W, C)

@@ -1,0 +1,85 @@
+"""Fused caption loss + in-loop metrics (reference: train.py:135-162, utils.py:44-80,101-107).
+
+``caption_loss(preds, alphas, captions, alpha_c, pad_id, skip_ids)`` returns
+``(loss, metrics)``: ``loss`` is the reference objective
+
+    CE(pack_padded_sequence(preds, T-2), pack_padded_sequence(captions[:,1:], T-2))
+      + alpha_c * ((1 - alphas.sum(1)) ** 2).mean()
+
+and ``metrics`` is a device tensor [CE, att_reg, n_top1, n_top5, n_nonpad,
+caption_length] so the train loop can report the reference's meters without
+the four per-step host syncs the reference pays.  Both come from one
+pass over the logits on the GPU; the backward recomputes softmax from the saved
+log-sum-exp (no [B,T-1,V] probability tensor is kept).
+"""
+import torch
+
+from . import _lib as L
+
+PLAIN_PAD, PLAIN_START, PLAIN_EOS = 3, 0, 1          # generate_json_data.py:45-48
+BERT_PAD, BERT_CLS, BERT_SEP = 0, 101, 102
+
+
+class _CaptionLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, preds, alphas, captions, alpha_c, pad_id, skip):
+        L.require_device(preds, alphas, captions)
+        B, T1, V = preds.shape
+        T = captions.shape[1]
+        if T1 != T - 1 or alphas.shape[:2] != (B, T1):
+            raise ValueError("caption_loss: preds [B,T-1,V], alphas [B,T-1,L], captions [B,T] expected")
+        Lf = alphas.shape[2]
+        lib = L.lib()
+        ws = torch.empty(lib.sat_caption_loss_workspace_bytes(B, T, Lf), device=preds.device, dtype=torch.uint8)
+        out = torch.empty(8, device=preds.device, dtype=torch.float32)
+        preds_c, alphas_c, caps = preds.contiguous(), alphas.contiguous().float(), captions.contiguous().long()
+        L.check(lib.sat_caption_loss_forward(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds_c), L.ptr(alphas_c),
+                                             L.ptr(caps), float(alpha_c), int(pad_id), int(skip[0]), int(skip[1]),
+                                             int(skip[2]), L.ptr(ws), L.ptr(out), L.stream_of(out)),
+                "sat_caption_loss_forward")
+        ctx.save_for_backward(preds_c, caps)
+        ctx.ws, ctx.dims, ctx.alpha_c = ws, (B, T, V, Lf), float(alpha_c)
+        loss = out[0].clone()
+        metrics = out[1:7].clone()
+        ctx.mark_non_differentiable(metrics)
+        return loss, metrics
+
+    @staticmethod
+    def backward(ctx, g_loss, g_metrics):
+        preds, caps = ctx.saved_tensors
+        B, T, V, Lf = ctx.dims
+        d_preds = torch.empty_like(preds)
+        d_alphas = torch.empty(B, T - 1, Lf, device=preds.device, dtype=torch.float32)
+        g = (g_loss if g_loss is not None else torch.ones((), device=preds.device)).float().contiguous()
+        L.check(L.lib().sat_caption_loss_backward(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds), L.ptr(caps),
+                                                  ctx.alpha_c, L.ptr(ctx.ws), L.ptr(g), L.ptr(d_preds),
+                                                  L.ptr(d_alphas), L.stream_of(d_preds)),
+                "sat_caption_loss_backward")
+        ctx.ws = None
+        return d_preds, d_alphas, None, None, None, None
+
+
+def caption_loss(preds, alphas, captions, alpha_c=1.0, pad_id=PLAIN_PAD, skip_ids=(PLAIN_PAD, PLAIN_START, PLAIN_EOS)):
+    return _CaptionLossFn.apply(preds, alphas, captions, alpha_c, pad_id, tuple(skip_ids))
+
+
+def special_ids(bert):
+    """(pad_id, skip_ids) as train.py:143,174-177 pick them."""
+    if bert:
+        return BERT_PAD, (BERT_PAD, BERT_CLS, BERT_SEP)
+    return PLAIN_PAD, (PLAIN_PAD, PLAIN_START, PLAIN_EOS)
+
+
+class StepMetrics:
+    """Host view of the metrics tensor: one D2H copy when read (not per step)."""
+
+    def __init__(self, loss, metrics):
+        self.loss, self.metrics = loss, metrics
+
+    def values(self):
+        m = self.metrics.detach().cpu().tolist()
+        ce, reg, c1, c5, nonpad, cap_len = m
+        acc1 = c1 * 100.0 / nonpad if nonpad > 0 else 0
+        acc5 = c5 * 100.0 / nonpad if nonpad > 0 else 0
+        return dict(loss=float(self.loss.detach().cpu()), ce=ce, att_reg=reg, acc1=acc1, acc5=acc5,
+                    caption_length=int(cap_len))

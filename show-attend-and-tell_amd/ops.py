@@ -1,0 +1,117 @@
+"""Tensor-level wrappers over the C ABI (shape checks, output allocation, stream).
+
+Every function here launches HIP kernels on the tensors' current stream and
+never falls back to a PyTorch compute op.
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+
+def linear(x, weight, bias=None, act=L.ACT_NONE, out_dtype=None, weight_lp=None):
+    """y = act(x @ weight.T + bias) on MFMA (nn.Linear forward).  x [M,K] (f32|bf16),
+    weight [N,K] f32 (or weight_lp bf16 when x is bf16)."""
+    L.require_device(x, weight)
+    M, K = x.shape
+    N = weight.shape[0]
+    dt = L.dtype_code(x.dtype)
+    if dt == L.SAT_F32:
+        w = weight
+    elif weight_lp is not None:
+        w = weight_lp
+    else:
+        w = cast_(weight.contiguous(), torch.empty(weight.shape, device=weight.device, dtype=torch.bfloat16))
+    out_dtype = out_dtype or torch.float32
+    y = torch.empty(M, N, device=x.device, dtype=out_dtype)
+    gemm(x, w, y, bias=bias, act=act)
+    return y
+
+
+def gemm(A, B, C, *, transA=False, transB=False, alpha=1.0, beta=0.0, bias=None, add1=None, act=L.ACT_NONE,
+         aux=None):
+    """C = act(alpha * A' B'^T + bias + add1 + beta*C) with A' = A or A^T, B'(n,k) = B[n,k] or B[k,n]."""
+    L.require_device(A, B, C)
+    dt = L.dtype_code(A.dtype)
+    if B.dtype != A.dtype:
+        raise TypeError("sat_amd.gemm: A and B must share a dtype")
+    M = A.shape[1] if transA else A.shape[0]
+    K = A.shape[0] if transA else A.shape[1]
+    N = B.shape[1] if transB else B.shape[0]
+    Kb = B.shape[0] if transB else B.shape[1]
+    if Kb != K or C.shape[0] != M or C.shape[1] != N:
+        raise ValueError(f"sat_amd.gemm: shape mismatch A{tuple(A.shape)} B{tuple(B.shape)} C{tuple(C.shape)}")
+    for t in (A, B, C, add1, aux):
+        if t is not None and t.stride(-1) != 1:
+            raise ValueError("sat_amd.gemm: operands must be row-major with unit inner stride")
+    a = L.SatGemmArgs()
+    a.M, a.N, a.K, a.dtype = M, N, K, dt
+    a.A, a.lda, a.transA = A.data_ptr(), A.stride(0), int(transA)
+    a.B, a.ldb, a.transB = B.data_ptr(), B.stride(0), int(transB)
+    a.C, a.ldc, a.c_dtype = C.data_ptr(), C.stride(0), L.dtype_code(C.dtype)
+    a.alpha, a.beta = alpha, beta
+    a.bias = bias.data_ptr() if bias is not None else None
+    if add1 is not None:
+        a.add1, a.ld_add1, a.add1_dtype = add1.data_ptr(), add1.stride(0), L.dtype_code(add1.dtype)
+    a.act = act
+    if aux is not None:
+        a.aux, a.ld_aux, a.aux_dtype = aux.data_ptr(), aux.stride(0), L.dtype_code(aux.dtype)
+    L.check(L.lib().sat_gemm(ctypes.byref(a), L.stream_of(C)), "sat_gemm")
+    return C
+
+
+def cast_(src, dst):
+    """dst.copy_(src) between float32/bfloat16 storage, on the HIP path."""
+    L.require_device(src, dst)
+    assert src.numel() == dst.numel() and src.is_contiguous() and dst.is_contiguous()
+    L.check(L.lib().sat_cast(L.ptr(src), L.dtype_code(src.dtype), L.ptr(dst), L.dtype_code(dst.dtype),
+                             src.numel(), L.stream_of(dst)), "sat_cast")
+    return dst
+
+
+def nchw_to_nhwc(x, c_pad, dtype):
+    """[N,C,H,W] f32 -> [N,H,W,c_pad] (dtype), zero-padded channels."""
+    L.require_device(x)
+    x = x.contiguous() if not x.is_contiguous() else x
+    if x.dtype != torch.float32:
+        raise TypeError("images must be float32 (post-Normalize domain, train.py:27-32)")
+    N, C, H, W = x.shape
+    y = torch.empty(N, H, W, c_pad, device=x.device, dtype=dtype)
+    L.check(L.lib().sat_nchw_to_nhwc(N, C, H, W, c_pad, L.dtype_code(dtype), L.ptr(x), L.ptr(y), L.stream_of(y)),
+            "sat_nchw_to_nhwc")
+    return y
+
+
+def conv2d_nhwc(x, w, bias, stride, pad, relu, residual=None, out=None):
+    """x [N,H,W,C] ; w [Cout,KH,KW,C] (same dtype) ; bias f32 [Cout]."""
+    L.require_device(x, w)
+    N, H, W, C = x.shape
+    Cout, KH, KW, Cw = w.shape
+    assert Cw == C, (w.shape, x.shape)
+    OH = (H + 2 * pad - KH) // stride + 1
+    OW = (W + 2 * pad - KW) // stride + 1
+    y = out if out is not None else torch.empty(N, OH, OW, Cout, device=x.device, dtype=x.dtype)
+    g = L.SatConvGeom(N, H, W, C, KH, KW, stride, pad, OH, OW)
+    if residual is not None:
+        assert residual.shape == y.shape and residual.dtype == y.dtype
+    L.check(L.lib().sat_conv2d_nhwc(ctypes.byref(g), Cout, L.dtype_code(x.dtype), L.ptr(x), L.ptr(w), L.ptr(bias),
+                                    L.ptr(residual), int(relu), L.ptr(y), L.stream_of(y)), "sat_conv2d_nhwc")
+    return y
+
+
+def maxpool2d_nhwc(x, k, stride, pad=0):
+    L.require_device(x)
+    N, H, W, C = x.shape
+    OH = (H + 2 * pad - k) // stride + 1
+    OW = (W + 2 * pad - k) // stride + 1
+    y = torch.empty(N, OH, OW, C, device=x.device, dtype=x.dtype)
+    L.check(L.lib().sat_maxpool2d_nhwc(N, H, W, C, k, stride, pad, L.dtype_code(x.dtype), L.ptr(x), L.ptr(y), OH, OW,
+                                       L.stream_of(y)), "sat_maxpool2d_nhwc")
+    return y
+
+
+def adam_step_(param, grad, exp_avg, exp_avg_sq, param_lp, beta1, beta2, eps, step_size, bc2_sqrt):
+    L.check(L.lib().sat_adam_step(L.ptr(param), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), L.ptr(param_lp),
+                                  param.numel(), beta1, beta2, eps, step_size, bc2_sqrt, L.stream_of(param)),
+            "sat_adam_step")
