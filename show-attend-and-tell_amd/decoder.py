@@ -44,11 +44,10 @@ class BertTokenizerStub:
 
 
 def _bert_tokenizer():
-    try:  # only a locally cached tokenizer; this build never downloads
-        from transformers import BertTokenizer
-        return BertTokenizer.from_pretrained("bert-base-uncased", local_files_only=True)
-    except Exception:
-        return BertTokenizerStub()
+    """bert-base-uncased special ids.  A tokenizer object resolved from whatever HF cache a
+    machine happens to hold is NOT trusted (one GPU host returned cls_token_id=2); pass
+    ``tokenizer=`` explicitly to use a real BertTokenizer."""
+    return BertTokenizerStub()
 
 
 class Decoder(nn.Module):
