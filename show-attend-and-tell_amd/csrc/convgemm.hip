@@ -1,0 +1,290 @@
+// Fast bf16 NT GEMM / implicit-GEMM convolution for gfx950 (MI355X).
+//
+//   C[M,N] = act(A[M,K] . B[N,K]^T + bias[N] + add1[M,N])
+//   A: row-major bf16 matrix (lda) or the implicit im2col of an NHWC bf16 image;
+//   B: row-major [N][K] bf16 (conv weights [Cout][KH][KW][Cin], Linear weights [out][in]).
+//
+// Design (cdna_hip_programming.md sec. 5, "glds vs register staging"):
+//   * 256 threads = 4 waves, 2x2; block tile 128 x BN (BN = 128 or 64), BK = 64;
+//   * operands move HBM -> LDS with global_load_lds_dwordx4 (16 B per lane, no VGPR round
+//     trip), one 1 KiB wave-instruction = 8 LDS rows of 128 B, two-stage ring;
+//   * the LDS image is lane-linear, so the bank swizzle is applied to the SOURCE address:
+//     LDS slot s of row r holds k-chunk s ^ ((r >> 1) & 7); the fragment reads
+//     (ds_read_b128, lane l -> row l&15, chunk 4ks + l>>4) are then conflict-free;
+//   * out-of-range rows / k-chunks / conv padding read a 16-byte zero line in HBM instead
+//     of being predicated, so every lane always issues its DMA;
+//   * im2col: when Cin % 64 == 0 a whole k-tile lies in one filter tap, so (kh, kw, ci0)
+//     are block-uniform scalars and each lane only adds its pixel's row offset;
+//   * v_mfma_f32_16x16x32_bf16, fp32 accumulation; the epilogue stages each wave's
+//     64 x BN/2 fp32 tile in LDS and writes 16-byte row segments (bias, residual add,
+//     activation and the bf16 conversion fused).
+#include "sat_common.h"
+#include "sat_internal.h"
+
+namespace {
+
+constexpr int BM = 128, BK = 64, ROWB = BK * 2;   // 128-byte LDS rows
+
+struct FArgs {
+  int M, N, K;
+  const bf16* A; long lda;
+  const bf16* B; long ldb;
+  void* C; long ldc; int c_bf16;
+  const float* bias;
+  const void* add1; long ld_add1; int add1_bf16;
+  int act;
+  // implicit im2col (amode 1: Cin % 64 == 0, amode 2: Cin % 8 == 0)
+  int amode, H, W, Cin, KW, stride, pad, OH, OW;
+  const bf16* zero16;
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_void;
+
+__device__ __forceinline__ void dma16(const void* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_dst, 16, 0, 0);
+}
+
+template <int BN>
+__global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
+  constexpr int WN = BN / 2, NJ = WN / 16, MI = 4;
+  constexpr int STAGE_A = BM * ROWB, STAGE_B = BN * ROWB, STAGE = STAGE_A + STAGE_B;
+  constexpr int A_INSTR = BM / 32, B_INSTR = BN / 32;   // 1 KiB DMA instructions per wave per stage
+  constexpr int EPI_LD = WN + 4;
+  constexpr int EPI_BYTES = 4 * 64 * EPI_LD * 4;
+  constexpr int LDS_BYTES = (2 * STAGE > EPI_BYTES) ? 2 * STAGE : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int M = a.M, N = a.N, K = a.K;
+
+  // ---- per-lane DMA row bookkeeping (rows are fixed across k-tiles) ----
+  const int lrow = lane >> 3, slot = lane & 7;
+  long a_base[A_INSTR];   // plain: element offset of the row; conv: pixel index (n*H*W) or -1
+  int a_ih[A_INSTR], a_iw[A_INSTR], a_chunk[A_INSTR];
+#pragma unroll
+  for (int j = 0; j < A_INSTR; ++j) {
+    const int r = (w * A_INSTR + j) * 8 + lrow;
+    a_chunk[j] = slot ^ ((r >> 1) & 7);
+    const int row = m0 + r;
+    if (a.amode == 0) {
+      a_base[j] = row < M ? (long)row * a.lda : -1;
+      a_ih[j] = a_iw[j] = 0;
+    } else if (row < M) {
+      const int ohw = a.OH * a.OW;
+      const int n = row / ohw, rem = row - n * ohw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      a_base[j] = (long)n * a.H * a.W;
+      a_ih[j] = oh * a.stride - a.pad;
+      a_iw[j] = ow * a.stride - a.pad;
+    } else {
+      a_base[j] = -1; a_ih[j] = a_iw[j] = 0;
+    }
+  }
+  long b_base[B_INSTR];
+  int b_chunk[B_INSTR];
+#pragma unroll
+  for (int j = 0; j < B_INSTR; ++j) {
+    const int r = (w * B_INSTR + j) * 8 + lrow;
+    b_chunk[j] = slot ^ ((r >> 1) & 7);
+    b_base[j] = (n0 + r < N) ? (long)(n0 + r) * a.ldb : -1;
+  }
+
+  auto stage = [&](int buf, int k0) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + STAGE_A;
+    if (a.amode == 1) {   // block-uniform filter tap
+      const int tap = k0 / a.Cin, ci0 = k0 - tap * a.Cin;
+      const int kh = tap / a.KW, kw = tap - kh * a.KW;
+#pragma unroll
+      for (int j = 0; j < A_INSTR; ++j) {
+        const int ih = a_ih[j] + kh, iw = a_iw[j] + kw;
+        const bool ok = a_base[j] >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const void* src = ok ? (const void*)(a.A + ((a_base[j] + (long)ih * a.W + iw) * a.Cin + ci0 + 8 * a_chunk[j]))
+                             : (const void*)a.zero16;
+        dma16(src, sa + (w * A_INSTR + j) * 1024);
+      }
+    } else if (a.amode == 2) {  // per-lane tap (small Cin, e.g. the padded 3->8 stem)
+#pragma unroll
+      for (int j = 0; j < A_INSTR; ++j) {
+        const int k = k0 + 8 * a_chunk[j];
+        bool ok = a_base[j] >= 0 && k < K;
+        long off = 0;
+        if (ok) {
+          const int tap = k / a.Cin, ci = k - tap * a.Cin;
+          const int kh = tap / a.KW, kw = tap - kh * a.KW;
+          const int ih = a_ih[j] + kh, iw = a_iw[j] + kw;
+          ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+          off = (a_base[j] + (long)ih * a.W + iw) * a.Cin + ci;
+        }
+        dma16(ok ? (const void*)(a.A + off) : (const void*)a.zero16, sa + (w * A_INSTR + j) * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < A_INSTR; ++j) {
+        const int k = k0 + 8 * a_chunk[j];
+        const bool ok = a_base[j] >= 0 && k < K;
+        dma16(ok ? (const void*)(a.A + a_base[j] + k) : (const void*)a.zero16, sa + (w * A_INSTR + j) * 1024);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < B_INSTR; ++j) {
+      const int k = k0 + 8 * b_chunk[j];
+      const bool ok = b_base[j] >= 0 && k < K;
+      dma16(ok ? (const void*)(a.B + b_base[j] + k) : (const void*)a.zero16, sb + (w * B_INSTR + j) * 1024);
+    }
+  };
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fh = lane >> 4;
+  auto compute = [&](int buf) {
+    const char* sa = smem + buf * STAGE;
+    const char* sb = sa + STAGE_A;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[MI], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int r = wm * 64 + i * 16 + fr;
+        af[i] = *(const bf16x8*)(sa + r * ROWB + 16 * ((ks * 4 + fh) ^ ((r >> 1) & 7)));
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int r = wn * WN + j * 16 + fr;
+        bfr[j] = *(const bf16x8*)(sb + r * ROWB + 16 * ((ks * 4 + fh) ^ ((r >> 1) & 7)));
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int nk = (K + BK - 1) / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+    compute(cur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: stage the wave's 64 x WN fp32 tile in LDS, write 16-B row segments ----
+  float* ep = (float*)smem + w * 64 * EPI_LD;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ep[(i * 16 + fh * 4 + r) * EPI_LD + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+  constexpr int CPR = WN / 8;               // 8-column chunks per row
+  constexpr int ITER = 64 * CPR / 64;
+  const bool vec_ok = (a.ldc % 8 == 0) && (!a.add1 || a.ld_add1 % 8 == 0);
+#pragma unroll
+  for (int it = 0; it < ITER; ++it) {
+    const int q = lane + 64 * it;
+    const int rl = q / CPR, cc = q - rl * CPR;
+    const int row = m0 + wm * 64 + rl, col = n0 + wn * WN + cc * 8;
+    if (row >= M || col >= N) continue;
+    float v[8];
+    const float4 x0 = *(const float4*)(ep + rl * EPI_LD + cc * 8);
+    const float4 x1 = *(const float4*)(ep + rl * EPI_LD + cc * 8 + 4);
+    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+    if (vec_ok && col + 8 <= N) {
+      if (a.bias) {
+        const float4 b0 = *(const float4*)(a.bias + col), b1 = *(const float4*)(a.bias + col + 4);
+        v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+      }
+      if (a.add1) {
+        if (a.add1_bf16) {
+          const uint4 u = *(const uint4*)((const bf16*)a.add1 + (long)row * a.ld_add1 + col);
+          const bf16* h = (const bf16*)&u;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += (float)h[e];
+        } else {
+          const float* p = (const float*)a.add1 + (long)row * a.ld_add1 + col;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += p[e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], a.act);
+      if (a.c_bf16) {
+        uint4 u;
+        bf16* h = (bf16*)&u;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
+        *(uint4*)((bf16*)a.C + (long)row * a.ldc + col) = u;
+      } else {
+        float* p = (float*)a.C + (long)row * a.ldc + col;
+        *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+        *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    } else {
+      for (int e = 0; e < 8 && col + e < N; ++e) {
+        float x = v[e] + (a.bias ? a.bias[col + e] : 0.f);
+        if (a.add1) x += ld_as_f32(a.add1, (long)row * a.ld_add1 + col + e, a.add1_bf16 ? SAT_BF16 : SAT_F32);
+        x = apply_act(x, a.act);
+        st_from_f32(a.C, (long)row * a.ldc + col + e, a.c_bf16 ? SAT_BF16 : SAT_F32, x);
+      }
+    }
+  }
+}
+
+__device__ __attribute__((aligned(16))) bf16 g_zero16[64];
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+// Returns 1 if the problem was handled by the fast path, 0 if the caller should use the generic kernel.
+int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
+  *err = 0;
+  if (g.dtype != SAT_BF16 || g.transA || g.transB || g.batch != 1 || g.aux || g.beta != 0.f) return 0;
+  if (g.K % 8 || g.ldb % 8 || !al16(g.B) || !al16(g.A)) return 0;
+  const bool conv = g.conv.C > 0;
+  if (!conv && g.lda % 8) return 0;
+  if (g.bias && !al16(g.bias)) return 0;
+  if (g.add1 && !al16(g.add1)) return 0;
+  const int bn = g.N <= 64 ? 64 : 128;
+  const long tiles = (long)sat_cdiv(g.M, BM) * sat_cdiv(g.N, bn);
+  if (tiles < 160) return 0;   // skinny problems: the generic kernel's split-K fills the chip better
+  static bf16* zero = nullptr;
+  if (!zero) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_zero16)) != hipSuccess) return 0;
+    zero = (bf16*)p;
+  }
+  FArgs a{};
+  a.M = g.M; a.N = g.N; a.K = g.K;
+  a.A = (const bf16*)g.A; a.lda = g.lda; a.B = (const bf16*)g.B; a.ldb = g.ldb;
+  a.C = g.C; a.ldc = g.ldc; a.c_bf16 = g.c_dtype == SAT_BF16;
+  a.bias = g.bias;
+  a.add1 = g.add1; a.ld_add1 = g.ld_add1; a.add1_bf16 = g.add1_dtype == SAT_BF16;
+  a.act = g.act;
+  a.zero16 = zero;
+  if (conv) {
+    if (g.conv.C % 8) return 0;
+    a.amode = (g.conv.C % BK == 0) ? 1 : 2;
+    a.H = g.conv.H; a.W = g.conv.W; a.Cin = g.conv.C; a.KW = g.conv.KW;
+    a.stride = g.conv.stride; a.pad = g.conv.pad; a.OH = g.conv.OH; a.OW = g.conv.OW;
+  }
+  dim3 grid(sat_cdiv(g.N, bn), sat_cdiv(g.M, BM));
+  if (bn == 64) hipLaunchKernelGGL(fast_gemm_kernel<64>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(fast_gemm_kernel<128>, grid, dim3(256), 0, s, a);
+  *err = (int)hipGetLastError();
+  return 1;
+}

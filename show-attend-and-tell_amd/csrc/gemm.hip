@@ -35,6 +35,7 @@ struct KArgs {
   long sA, sB, sC, s_add1, s_aux;
   SatConvGeom cv;
   int vecA, vecB;
+  int splitk, kchunk;   // split-K: blockIdx.z = batch*splitk + split; K range [split*kchunk, +kchunk)
 };
 
 union Vec16 {
@@ -56,10 +57,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const long z = blockIdx.z;
+  const long z = blockIdx.z / a.splitk;
+  const int split = blockIdx.z - (int)z * a.splitk;
   const T* Ag = (const T*)a.A + z * a.sA;
   const T* Bg = (const T*)a.B + z * a.sB;
-  const int M = a.M, N = a.N, K = a.K;
+  const int M = a.M, N = a.N;
+  const int kbeg = split * a.kchunk;
+  const int K = min(a.K, kbeg + a.kchunk);   // loaders treat K as the (exclusive) end of this split
 
   Vec16 ra[NA], rb[NB];
   int cv_pix[NA], cv_ih[NA], cv_iw[NA];
@@ -221,15 +225,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
     }
   };
 
-  const int nk = (K + BK - 1) / BK;
+  const int nk = K > kbeg ? (K - kbeg + BK - 1) / BK : 0;
   if (nk > 0) {
-    load_a(0); load_b(0);
+    load_a(kbeg); load_b(kbeg);
     store_a(0); store_b(0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
       const bool more = kt + 1 < nk;
-      if (more) { load_a((kt + 1) * BK); load_b((kt + 1) * BK); }
+      if (more) { load_a(kbeg + (kt + 1) * BK); load_b(kbeg + (kt + 1) * BK); }
       compute(cur);
       if (more) { store_a(cur ^ 1); store_b(cur ^ 1); }
       __syncthreads();
@@ -237,45 +241,78 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
   }
 
   // ---- epilogue ----
-  void* Cg = (char*)a.C + z * a.sC * (a.c_dtype == SAT_BF16 ? 2 : 4);
   const void* add1 = a.add1 ? (const char*)a.add1 + z * a.s_add1 * (a.add1_dtype == SAT_BF16 ? 2 : 4) : nullptr;
-  void* aux = a.aux ? (char*)a.aux + z * a.s_aux * (a.aux_dtype == SAT_BF16 ? 2 : 4) : nullptr;
+  if (a.splitk > 1) {
+    // split-K: fp32 atomic accumulation into C (pre-zeroed by the host when beta == 0);
+    // split 0 also contributes bias + add1.  Host guarantees act == NONE, fp32 C, no aux.
+    float* Cg = (float*)a.C + z * a.sC;
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int col = n0 + wn * WN + j * 16 + (lane & 15);
-      if (col >= N) continue;
-      const float bcol = a.bias ? a.bias[col] : 0.f;
+      for (int j = 0; j < NJ; ++j) {
+        const int col = n0 + wn * WN + j * 16 + (lane & 15);
+        if (col >= N) continue;
+        const float bcol = (split == 0 && a.bias) ? a.bias[col] : 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        if (row >= M) continue;
-        float v = a.alpha * acc[i][j][r] + bcol;
-        if (add1) v += ld_as_f32(add1, (long)row * a.ld_add1 + col, a.add1_dtype);
-        const long ci = (long)row * a.ldc + col;
-        if (a.beta != 0.f) v += a.beta * ld_as_f32(Cg, ci, a.c_dtype);
-        v = apply_act(v, a.act);
-        st_from_f32(Cg, ci, a.c_dtype, v);
-        if (aux) st_from_f32(aux, (long)row * a.ld_aux + col, a.aux_dtype, v);
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          if (row >= M) continue;
+          float v = a.alpha * acc[i][j][r] + bcol;
+          if (split == 0 && add1) v += ld_as_f32(add1, (long)row * a.ld_add1 + col, a.add1_dtype);
+          atomicAdd(Cg + (long)row * a.ldc + col, v);
+        }
+      }
+    return;
+  }
+  auto epi = [&](auto* Cg, auto* auxg) {
+    using CT = typename std::remove_pointer<decltype(Cg)>::type;
+    using XT = typename std::remove_pointer<decltype(auxg)>::type;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = n0 + wn * WN + j * 16 + (lane & 15);
+        if (col >= N) continue;
+        const float bcol = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          if (row >= M) continue;
+          float v = a.alpha * acc[i][j][r] + bcol;
+          if (add1) v += ld_as_f32(add1, (long)row * a.ld_add1 + col, a.add1_dtype);
+          const long ci = (long)row * a.ldc + col;
+          if (a.beta != 0.f) v += a.beta * (float)Cg[ci];
+          v = apply_act(v, a.act);
+          Cg[ci] = (CT)v;
+          if (auxg) auxg[(long)row * a.ld_aux + col] = (XT)v;
+        }
       }
     }
+  };
+  char* Cb = (char*)a.C + z * a.sC * (a.c_dtype == SAT_BF16 ? 2 : 4);
+  char* Xb = a.aux ? (char*)a.aux + z * a.s_aux * (a.aux_dtype == SAT_BF16 ? 2 : 4) : nullptr;
+  if (a.c_dtype == SAT_BF16) {
+    if (a.aux_dtype == SAT_BF16) epi((bf16*)Cb, (bf16*)Xb);
+    else epi((bf16*)Cb, (float*)Xb);
+  } else {
+    if (a.aux_dtype == SAT_BF16) epi((float*)Cb, (bf16*)Xb);
+    else epi((float*)Cb, (float*)Xb);
   }
 }
 
 template <typename T, int BM, int BN, int AMODE, bool TB>
 int launch_cfg(const KArgs& k, int batch, hipStream_t s) {
-  dim3 grid(sat_cdiv(k.N, BN), sat_cdiv(k.M, BM), batch);
+  dim3 grid(sat_cdiv(k.N, BN), sat_cdiv(k.M, BM), batch * k.splitk);
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, AMODE, TB>), grid, dim3(256), 0, s, k);
   return (int)hipGetLastError();
 }
 
 template <typename T, int AMODE, bool TB>
 int launch_tiles(const KArgs& k, int batch, hipStream_t s) {
-  long t128 = (long)sat_cdiv(k.M, 128) * sat_cdiv(k.N, 128) * batch;
-  long t64x128 = (long)sat_cdiv(k.M, 64) * sat_cdiv(k.N, 128) * batch;
-  if (t128 >= 240) return launch_cfg<T, 128, 128, AMODE, TB>(k, batch, s);
-  if (t64x128 >= 240) return launch_cfg<T, 64, 128, AMODE, TB>(k, batch, s);
+  long t128 = (long)sat_cdiv(k.M, 128) * sat_cdiv(k.N, 128) * batch * k.splitk;
+  long t64x128 = (long)sat_cdiv(k.M, 64) * sat_cdiv(k.N, 128) * batch * k.splitk;
+  if (k.splitk == 1 && t128 >= 240) return launch_cfg<T, 128, 128, AMODE, TB>(k, batch, s);
+  if (k.splitk == 1 && t64x128 >= 240) return launch_cfg<T, 64, 128, AMODE, TB>(k, batch, s);
   return launch_cfg<T, 64, 64, AMODE, TB>(k, batch, s);
 }
 
@@ -294,6 +331,10 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return 0;
   SAT_REQUIRE(g.K >= 0 && g.A && g.B && g.C);
   SAT_REQUIRE(g.dtype == SAT_F32 || g.dtype == SAT_BF16);
+  {
+    int err = 0;
+    if (sat_fast_gemm_try(g, s, &err)) return err;
+  }
   const int vec = g.dtype == SAT_BF16 ? 8 : 4;
   KArgs k{};
   k.M = g.M; k.N = g.N; k.K = g.K;
@@ -314,6 +355,29 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s) {
     k.vecA = aligned16(g.A) && (g.lda % vec == 0) && (g.batch == 1 || g.sA % vec == 0);
   }
   k.vecB = aligned16(g.B) && (g.ldb % vec == 0) && (g.batch == 1 || g.sB % vec == 0);
+  // split-K for skinny problems that cannot fill 256 CUs with 64x64 tiles
+  k.splitk = 1;
+  k.kchunk = g.K > 0 ? g.K : 1;
+  const int bk = g.dtype == SAT_BF16 ? 32 : 16;
+  const long tiles64 = (long)sat_cdiv(g.M, 64) * sat_cdiv(g.N, 64) * g.batch;
+  const bool can_split = g.act == SAT_ACT_NONE && g.c_dtype == SAT_F32 && g.aux == nullptr &&
+                         (g.beta == 0.f || g.beta == 1.f) && amode != 2 && g.batch == 1;
+  if (can_split && tiles64 < 200 && g.K >= 8 * bk) {
+    int sk = (int)((400 + tiles64 - 1) / tiles64);
+    sk = sk > 16 ? 16 : sk;
+    const int max_by_k = g.K / (4 * bk);
+    if (sk > max_by_k) sk = max_by_k;
+    if (sk > 1) {
+      int chunk = sat_cdiv(g.K, sk);
+      chunk = sat_cdiv(chunk, bk) * bk;
+      k.kchunk = chunk;
+      k.splitk = sat_cdiv(g.K, chunk);
+      if (g.beta == 0.f) {
+        if (g.ldc == g.N) SAT_CHECK(hipMemsetAsync(g.C, 0, (size_t)g.M * g.N * 4, s));
+        else SAT_CHECK(hipMemset2DAsync(g.C, (size_t)g.ldc * 4, 0, (size_t)g.N * 4, g.M, s));
+      }
+    }
+  }
   if (g.dtype == SAT_BF16) return launch_t<bf16>(k, amode, g.transB, g.batch, s);
   return launch_t<float>(k, amode, g.transB, g.batch, s);
 }

@@ -268,3 +268,44 @@ def test_bench_shape_train_step_properties(sat):
         gr = dict(dec.named_parameters())[n].grad
         assert torch.isfinite(gr).all(), n
     assert not torch.equal(before, dec.lstm.weight_ih.detach())
+
+
+# ---------------------------------------------------------------------------- bf16 fast path (LDS-DMA kernel)
+@pytest.mark.parametrize("N,C,H,Cout,k,stride,pad", [(8, 64, 56, 128, 3, 1, 1),     # uniform-tap im2col
+                                                     (8, 64, 56, 64, 3, 2, 1),      # BN=64 tile, stride 2
+                                                     (16, 8, 64, 64, 7, 2, 3),      # stem: per-lane tap (Cin=8)
+                                                     (8, 128, 56, 256, 1, 2, 0),    # strided 1x1 (downsample)
+                                                     (32, 256, 14, 200, 1, 1, 0)])  # N tail (200 % 128)
+def test_fast_conv_path(sat, N, C, H, Cout, k, stride, pad):
+    from sat_amd import ops
+    g = torch.Generator().manual_seed(N * C + Cout + k)
+    x = torch.randn(N, C, H, H, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, C, k, k, generator=g) / math.sqrt(C * k * k)).bfloat16().float()
+    b = torch.randn(Cout, generator=g)
+    ref = F.conv2d(x, w, b, stride=stride, padding=pad)
+    res = torch.randn_like(ref).bfloat16().float()
+    ref_r = torch.relu(ref + res)
+    xd = x.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    wd = w.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    rd = res.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    y = ops.conv2d_nhwc(xd, wd, b.to(DEV), stride, pad, True, residual=rd)
+    y = y.float().permute(0, 3, 1, 2).cpu()
+    # bf16 output rounding (2^-8 relative) dominates; fp32 accumulation
+    assert rel(y, ref_r) < 1e-2
+    assert ((y - ref_r).abs() <= 1e-2 * ref_r.abs() + 2e-2).all()
+
+
+@pytest.mark.parametrize("M,N,K,out", [(3000, 1000, 520, torch.float32), (4096, 64, 512, torch.bfloat16),
+                                       (2500, 1003, 256, torch.float32), (3328, 10000, 512, torch.bfloat16)])
+def test_fast_gemm_path(sat, M, N, K, out):
+    from sat_amd import ops
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    Bm = torch.randn(N, K, generator=g).bfloat16()
+    bias = torch.randn(N, generator=g)
+    add1 = torch.randn(M, N, generator=g)
+    ref = torch.relu(A.float() @ Bm.float().T + bias + add1)
+    C = torch.empty(M, N, dtype=out, device=DEV)
+    ops.gemm(A.to(DEV), Bm.to(DEV), C, bias=bias.to(DEV), add1=add1.to(DEV), act=sat._lib.ACT_RELU)
+    tol = 1e-5 if out == torch.float32 else 8e-3
+    assert rel(C.float(), ref) < tol
