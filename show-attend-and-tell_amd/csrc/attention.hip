@@ -65,6 +65,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
       float x[4];
       load4<T>(wr + e, x);
       float4 u = *(const float4*)(uh + e);
+      for (int sp = 1; sp < a.hg_splits; ++sp) {
+        const float4 u2 = *(const float4*)(uh + sp * a.hg_split_stride + e);
+        u.x += u2.x; u.y += u2.y; u.z += u2.z; u.w += u2.w;
+      }
       float4 vv = *(const float4*)(a.v_w + e);
       acc += vv.x * tanhf(x[0] + u.x) + vv.y * tanhf(x[1] + u.y) + vv.z * tanhf(x[2] + u.z) + vv.w * tanhf(x[3] + u.w);
     }
@@ -92,7 +96,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
     }
   }
   if (s == 0 && a.uh_save) {
-    for (int e = tid; e < E; e += 256) a.uh_save[(long)b * a.uh_save_ld + e] = uh[e];
+    for (int e = tid; e < E; e += 256) a.uh_save[(long)b * a.uh_save_ld + e] = sum_parts(uh, e, a.hg_splits, a.hg_split_stride);
   }
   __syncthreads();
   // ---- context for this D-slice ----
@@ -121,7 +125,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
     a.ctx[(long)b * a.ctx_ld + d] = c;
     if (a.ctx_t) ((T*)a.ctx_t)[(long)b * a.ctx_t_ld + d] = (T)c;
     if (a.gate_pre) {
-      const float g = 1.0f / (1.0f + expf(-a.gate_pre[(long)b * a.gate_ld + d]));
+      const float g = 1.0f / (1.0f + expf(-sum_parts(a.gate_pre, (long)b * a.gate_ld + d, a.hg_splits, a.hg_split_stride)));
       if (a.gate) a.gate[(long)b * a.gate_out_ld + d] = g;
       if (a.gated) ((T*)a.gated)[(long)b * a.gated_ld + d] = (T)(g * c);
     }
@@ -142,7 +146,7 @@ __global__ __launch_bounds__(256) void attn_bwd1_kernel(AttnBwdArgs a) {
 #pragma unroll
     for (int j = 0; j < VD; ++j) {
       const int d = d0 + j;
-      const float dg = a.d_gated[(long)b * a.d_gated_ld + d];
+      const float dg = sum_parts(a.d_gated, (long)b * a.d_gated_ld + d, a.dg_splits, a.dg_split_stride);
       const float g = a.gate[(long)b * a.gate_ld + d];
       const float c = a.ctx[(long)b * a.ctx_ld + d];
       float dc = dg * g;

@@ -191,33 +191,44 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
       for (int r = 0; r < 4; ++r) ep[(i * 16 + fh * 4 + r) * EPI_LD + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
   constexpr int CPR = WN / 8;               // 8-column chunks per row
-  constexpr int ITER = 64 * CPR / 64;
-  const bool vec_ok = (a.ldc % 8 == 0) && (!a.add1 || a.ld_add1 % 8 == 0);
+  constexpr int ITER = 64 * CPR / 64;        // chunks per lane; a lane's column chunk is fixed (cc = lane % CPR)
+  const int cc = lane % CPR;
+  const int col = n0 + wn * WN + cc * 8;
+  const bool vec_ok = (a.ldc % 8 == 0) && (!a.add1 || a.ld_add1 % 8 == 0) && col + 8 <= N;
+  float bias8[8];
 #pragma unroll
-  for (int it = 0; it < ITER; ++it) {
-    const int q = lane + 64 * it;
-    const int rl = q / CPR, cc = q - rl * CPR;
-    const int row = m0 + wm * 64 + rl, col = n0 + wn * WN + cc * 8;
-    if (row >= M || col >= N) continue;
-    float v[8];
-    const float4 x0 = *(const float4*)(ep + rl * EPI_LD + cc * 8);
-    const float4 x1 = *(const float4*)(ep + rl * EPI_LD + cc * 8 + 4);
-    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-    if (vec_ok && col + 8 <= N) {
-      if (a.bias) {
-        const float4 b0 = *(const float4*)(a.bias + col), b1 = *(const float4*)(a.bias + col + 4);
-        v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  for (int e = 0; e < 8; ++e) bias8[e] = (a.bias && col + e < N) ? a.bias[col + e] : 0.f;
+  if (vec_ok) {
+    // issue every residual load of this lane before the first store (C and add1 may not be
+    // proven disjoint by the compiler, which would otherwise serialise load-after-store)
+    uint4 res[ITER];
+    if (a.add1 && a.add1_bf16) {
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) {
+        const int row = m0 + wm * 64 + (lane + 64 * it) / CPR;
+        res[it] = row < M ? *(const uint4*)((const bf16*)a.add1 + (long)row * a.ld_add1 + col) : make_uint4(0, 0, 0, 0);
       }
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int rl = (lane + 64 * it) / CPR;
+      const int row = m0 + wm * 64 + rl;
+      if (row >= M) continue;
+      float v[8];
+      const float4 x0 = *(const float4*)(ep + rl * EPI_LD + cc * 8);
+      const float4 x1 = *(const float4*)(ep + rl * EPI_LD + cc * 8 + 4);
+      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bias8[e];
       if (a.add1) {
         if (a.add1_bf16) {
-          const uint4 u = *(const uint4*)((const bf16*)a.add1 + (long)row * a.ld_add1 + col);
-          const bf16* h = (const bf16*)&u;
+          const bf16* h = (const bf16*)&res[it];
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += (float)h[e];
         } else {
           const float* p = (const float*)a.add1 + (long)row * a.ld_add1 + col;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += p[e];
+          const float4 p0 = *(const float4*)p, p1 = *(const float4*)(p + 4);
+          v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w; v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
         }
       }
 #pragma unroll
@@ -233,9 +244,14 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
         *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
         *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
       }
-    } else {
+    }
+  } else if (col < N) {
+    for (int it = 0; it < ITER; ++it) {
+      const int rl = (lane + 64 * it) / CPR;
+      const int row = m0 + wm * 64 + rl;
+      if (row >= M) continue;
       for (int e = 0; e < 8 && col + e < N; ++e) {
-        float x = v[e] + (a.bias ? a.bias[col + e] : 0.f);
+        float x = ep[rl * EPI_LD + cc * 8 + e] + bias8[e];
         if (a.add1) x += ld_as_f32(a.add1, (long)row * a.ld_add1 + col + e, a.add1_bf16 ? SAT_BF16 : SAT_F32);
         x = apply_act(x, a.act);
         st_from_f32(a.C, (long)row * a.ldc + col + e, a.c_bf16 ? SAT_BF16 : SAT_F32, x);

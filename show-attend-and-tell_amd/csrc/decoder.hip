@@ -36,6 +36,28 @@ struct WS {
       *colsum;
 };
 
+// split counts of the per-step skinny GEMMs (M = B rows): enough 64x64-tile x split blocks to
+// cover the 256 CUs; fp32 (parity) mode keeps a single split.
+struct Splits { int h, c, g, dh; };
+inline int pick_splits(int M, int N, int K, int dtype) {
+  if (dtype != SAT_BF16) return 1;
+  const long tiles = (long)sat_cdiv(M, 64) * sat_cdiv(N, 64);
+  int sk = (int)((320 + tiles - 1) / tiles);
+  const int by_k = K / 128;
+  if (sk > by_k) sk = by_k;
+  if (sk > 16) sk = 16;
+  return sk < 1 ? 1 : sk;
+}
+inline Splits splits_for(const SatDecoderDims& d) {
+  const int E = d.E, D = d.D, HG = 5 * E + D;
+  Splits s;
+  s.h = pick_splits(d.B, d.attention ? HG : 4 * E, E, d.dtype);
+  s.c = pick_splits(d.B, 4 * E, D, d.dtype);
+  s.g = pick_splits(d.B, D, 4 * E, d.dtype);
+  s.dh = pick_splits(d.B, E, d.attention ? HG : 4 * E, d.dtype);
+  return s;
+}
+
 struct Carver {
   char* base;
   size_t off = 0;
@@ -51,6 +73,7 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   const size_t B = d.B, L = d.L, D = d.D, E = d.E, V = d.V, T1 = d.T - 1, R = B * T1;
   const size_t HG = 5 * E + D;
   const size_t ts = d.dtype == SAT_BF16 ? 2 : 4, f = 4;
+  const Splits sp = splits_for(d);
   Carver c{base};
   c.take(w->mean_f, B * D * f);  c.take(w->mean_t, B * D * ts);
   c.take(w->hc0, B * 2 * E * f);
@@ -59,8 +82,8 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   c.take(w->emb_t, R * E * ts);
   c.take(w->xg, R * 4 * E * f);
   c.take(w->gctx_const, B * 4 * E * f);
-  c.take(w->hg, B * HG * f);
-  c.take(w->gctx, B * 4 * E * f);
+  c.take(w->hg, sp.h * B * HG * f);
+  c.take(w->gctx, sp.c * B * 4 * E * f);
   c.take(w->uh_all, R * E * f);
   c.take(w->gates_all, R * 4 * E * f);
   c.take(w->c_in, R * E * f);   c.take(w->c_out, R * E * f);
@@ -77,8 +100,8 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   c.take(w->dhd, R * E * f);
   c.take(w->dctx_head, R * D * f);
   c.take(w->dhg, R * HG * f); c.take(w->dhg_t, R * HG * ts);
-  c.take(w->dgated, B * D * f);
-  c.take(w->dh_rec, B * E * f); c.take(w->dc, B * E * f);
+  c.take(w->dgated, sp.g * B * D * f);
+  c.take(w->dh_rec, sp.dh * B * E * f); c.take(w->dc, B * E * f);
   c.take(w->dWs_acc, B * L * E * f); c.take(w->dWs_t, B * L * E * ts);
   c.take(w->dv_acc, B * E * f); c.take(w->dbv_acc, B * f);
   c.take(w->part, sat_attention_part_floats(d.B, d.L, d.D, d.dtype) * f);
@@ -137,8 +160,10 @@ struct Ctx {
 // y[rows, N] (+)= x[rows, K] . W[N, K]^T  (+bias) (act) -- all strided rows
 int linear(const Ctx& c, int rows, int N, int K, const void* x, long ldx, const void* w, long ldw, const float* bias,
            void* y, long ldy, int y_dtype, int act, hipStream_t s, const void* add1 = nullptr, long ld_add1 = 0,
-           int add1_dtype = SAT_F32, void* aux = nullptr, long ld_aux = 0, int aux_dtype = SAT_F32) {
+           int add1_dtype = SAT_F32, void* aux = nullptr, long ld_aux = 0, int aux_dtype = SAT_F32,
+           int splits = 0, long split_stride = 0) {
   SatGemm g;
+  g.partial_splits = splits; g.split_stride = split_stride;
   g.M = rows; g.N = N; g.K = K; g.dtype = c.d.dtype;
   g.A = x; g.lda = ldx; g.B = w; g.ldb = ldw;
   g.C = y; g.ldc = ldy; g.c_dtype = y_dtype; g.bias = bias; g.act = act;
@@ -212,6 +237,7 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
   const int B = d.B, L = d.L, D = d.D, E = d.E, T1 = d.T - 1;
   const long HG = c.HG;
   const bool att = d.attention != 0;
+  const Splits sp = splits_for(d);
 
   // fed tokens + embeddings
   if (d.tf) {
@@ -252,11 +278,13 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
     if (att) {
       // [U h + b_U | f_beta h + b | W_hh h + b_hh] in one GEMM
       SAT_CHECK((hipError_t)linear(c, B, (int)HG, E, h_t, (long)T1 * E, c.W(lay->hcat_w), E, c.F(lay->hcat_b), w.hg,
-                                   HG, SAT_F32, SAT_ACT_NONE, s));
+                                   HG, SAT_F32, SAT_ACT_NONE, s, nullptr, 0, SAT_F32, nullptr, 0, SAT_F32, sp.h,
+                                   (long)B * HG));
       AttnFwdArgs a{};
       a.B = B; a.L = L; a.D = D; a.E = E; a.dtype = d.dtype;
       a.Ws = w.Ws; a.uh = w.hg; a.uh_ld = HG; a.v_w = c.F(lay->v_w); a.v_b = c.F(lay->v_b); a.a = img_features;
       a.gate_pre = w.hg + E; a.gate_ld = HG;
+      a.hg_splits = sp.h; a.hg_split_stride = (long)B * HG;
       a.alpha = alphas + (long)t * L; a.alpha_ld = (long)T1 * L;
       a.ctx = w.ctx_all + (long)t * D; a.ctx_ld = (long)T1 * D;
       a.ctx_t = c.at(w.ctx_t, (long)t * D); a.ctx_t_ld = (long)T1 * D;
@@ -265,16 +293,20 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
       a.uh_save = w.uh_all + (long)t * E; a.uh_save_ld = (long)T1 * E;
       SAT_CHECK((hipError_t)sat_attention_fwd_launch(a, s));
       SAT_CHECK((hipError_t)linear(c, B, 4 * E, D, c.at(w.gated_t, (long)t * D), (long)T1 * D, c.W(lay->wih + E),
-                                   E + D, nullptr, w.gctx, 4 * E, SAT_F32, SAT_ACT_NONE, s));
+                                   E + D, nullptr, w.gctx, 4 * E, SAT_F32, SAT_ACT_NONE, s, nullptr, 0, SAT_F32,
+                                   nullptr, 0, SAT_F32, sp.c, (long)B * 4 * E));
     } else {
       SAT_CHECK((hipError_t)linear(c, B, 4 * E, E, h_t, (long)T1 * E, c.W(lay->hcat_w + (long)(E + D) * E), E,
-                                   c.F(lay->hcat_b + E + D), w.hg + E + D, HG, SAT_F32, SAT_ACT_NONE, s));
+                                   c.F(lay->hcat_b + E + D), w.hg + E + D, HG, SAT_F32, SAT_ACT_NONE, s, nullptr, 0,
+                                   SAT_F32, nullptr, 0, SAT_F32, sp.h, (long)B * HG));
     }
     LstmFwdArgs l{};
     l.B = B; l.E = E; l.dtype = d.dtype;
     l.hpart = w.hg + E + D; l.hpart_ld = HG;
     l.xpart = w.xg + (long)t * 4 * E; l.xpart_ld = (long)T1 * 4 * E;
     l.cpart = att ? w.gctx : w.gctx_const; l.cpart_ld = 4 * E;
+    l.h_splits = sp.h; l.h_split_stride = (long)B * HG;
+    l.c_splits = att ? sp.c : 1; l.c_split_stride = (long)B * 4 * E;
     l.c_prev = w.c_in + (long)t * E; l.c_prev_ld = (long)T1 * E;
     l.gates = w.gates_all + (long)t * 4 * E; l.gates_ld = (long)T1 * 4 * E;
     l.c_out = w.c_out + (long)t * E; l.c_out_ld = (long)T1 * E;
@@ -315,6 +347,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   const long HG = c.HG;
   const bool att = d.attention != 0;
   const float beta = accumulate ? 1.f : 0.f;
+  const Splits sp = splits_for(d);
   auto G = [&](int64_t off) { return grads + off; };
   // weight gradient: G[M,N] (+)= X[K,M]^T Y[K,N]   (X m-contig, Y n-contig)
   auto wgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo) {
@@ -327,8 +360,9 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   };
   // input gradient: Y[M,N] = X[M,K] W[K,N]   (W stored [K][N] row-major = torch weight [out,in])
   auto dgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Wt, long ldw, float* out, long ldo,
-                   const float* add1 = nullptr, long ld_add1 = 0) {
+                   const float* add1 = nullptr, long ld_add1 = 0, int splits = 0, long split_stride = 0) {
     SatGemm g;
+    g.partial_splits = splits; g.split_stride = split_stride;
     g.M = M; g.N = N; g.K = K; g.dtype = d.dtype;
     g.A = X; g.lda = ldx; g.B = Wt; g.ldb = ldw; g.transB = 1;
     g.C = out; g.ldc = ldo; g.c_dtype = SAT_F32;
@@ -373,6 +407,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
     l.c_prev = w.c_in + (long)t * E; l.c_prev_ld = (long)T1 * E;
     l.c_new = w.c_out + (long)t * E; l.c_new_ld = (long)T1 * E;
     l.dh_rec = t == T1 - 1 ? nullptr : w.dh_rec; l.dh_rec_ld = E;
+    l.dh_splits = sp.dh; l.dh_split_stride = (long)B * E;
     l.dh_head = w.dhd + (long)t * E; l.dh_head_ld = (long)T1 * E;
     l.mask = d.training ? w.dmask + (long)t * E : nullptr; l.mask_ld = (long)T1 * E;
     l.dc = w.dc; l.dc_zero = t == T1 - 1;
@@ -381,7 +416,8 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
     SAT_CHECK((hipError_t)sat_lstm_bwd_launch(l, s));
     const void* dgates_t = c.at(w.dhg_t, (long)t * HG + E + D);
     if (att) {
-      SAT_CHECK((hipError_t)dgrad(B, D, 4 * E, dgates_t, (long)T1 * HG, c.W(lay->wih + E), E + D, w.dgated, D));
+      SAT_CHECK((hipError_t)dgrad(B, D, 4 * E, dgates_t, (long)T1 * HG, c.W(lay->wih + E), E + D, w.dgated, D,
+                                  nullptr, 0, sp.g, (long)B * D));
       AttnBwdArgs a{};
       a.B = B; a.L = L; a.D = D; a.E = E; a.dtype = d.dtype;
       a.Ws = w.Ws; a.a = img_features;
@@ -396,13 +432,14 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
       a.d_uh = w.dhg + (long)t * HG; a.d_uh_ld = (long)T1 * HG; a.d_uh_t = c.at(w.dhg_t, (long)t * HG);
       a.d_gpre = w.dhg + (long)t * HG + E; a.d_gpre_ld = (long)T1 * HG; a.d_gpre_t = c.at(w.dhg_t, (long)t * HG + E);
       a.dWs_acc = w.dWs_acc; a.dv_acc = w.dv_acc; a.dbv_acc = w.dbv_acc; a.part = w.part;
+      a.dg_splits = sp.g; a.dg_split_stride = (long)B * D;
       SAT_CHECK((hipError_t)sat_attention_bwd_launch(a, s));
       // dh = [dU_h | d(f_beta h) | d gates] . [U ; f_beta ; W_hh]
       SAT_CHECK((hipError_t)dgrad(B, E, (int)HG, c.at(w.dhg_t, (long)t * HG), (long)T1 * HG, c.W(lay->hcat_w), E,
-                                  w.dh_rec, E));
+                                  w.dh_rec, E, nullptr, 0, sp.dh, (long)B * E));
     } else {
       SAT_CHECK((hipError_t)dgrad(B, E, 4 * E, dgates_t, (long)T1 * HG, c.W(lay->hcat_w + (long)(E + D) * E), E,
-                                  w.dh_rec, E));
+                                  w.dh_rec, E, nullptr, 0, sp.dh, (long)B * E));
     }
   }
 
@@ -432,7 +469,8 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
     SAT_CHECK((hipError_t)colsum(w.dbv_acc, SAT_F32, 1, B, 1, G(lay->v_b)));
   }
   // init_h / init_c (decoder.py:137-147): dh0 = dh_rec, dc0 = dc after the t = 0 step
-  SAT_CHECK((hipError_t)sat_tanh_pair_bwd(w.dh_rec, w.dc, w.hc0, B, E, w.dpre0, w.dpre0_t, d.dtype, s));
+  SAT_CHECK((hipError_t)sat_tanh_pair_bwd(w.dh_rec, sp.dh, (long)B * E, w.dc, w.hc0, B, E, w.dpre0, w.dpre0_t,
+                                          d.dtype, s));
   SAT_CHECK((hipError_t)wgrad(2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D));
   SAT_CHECK((hipError_t)colsum(w.dpre0, SAT_F32, 2 * E, B, 2 * E, G(lay->init_b)));
   return 0;

@@ -14,6 +14,7 @@ inline int grid_for(long n, int per_block = 256) {
 }
 
 // ---- NCHW fp32 -> NHWC (T), channels zero-padded to Cp ----------------------
+// one pixel per thread: C coalesced channel-plane loads, one 16-B store when Cp*sizeof(T) == 16
 template <typename T>
 __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__ y, int N, int C, int H, int W,
                                     int Cp) {
@@ -22,32 +23,63 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__
     long n = p / ((long)H * W), hw = p - n * H * W;
     const float* src = x + n * C * H * W + hw;
     T* dst = y + p * Cp;
-    for (int c = 0; c < Cp; ++c) dst[c] = (T)(c < C ? src[(long)c * H * W] : 0.f);
+    if (Cp * sizeof(T) == 16) {
+      uint4 u;
+      T* h = (T*)&u;
+#pragma unroll
+      for (int c = 0; c < 16 / (int)sizeof(T); ++c) h[c] = (T)(c < C ? src[(long)c * H * W] : 0.f);
+      *(uint4*)dst = u;
+    } else {
+      for (int c = 0; c < Cp; ++c) dst[c] = (T)(c < C ? src[(long)c * H * W] : 0.f);
+    }
   }
 }
 
-// ---- max-pool NHWC (floor mode) ---------------------------------------------
+// ---- max-pool NHWC (floor mode), 8 channels per thread (16-B bf16 / 2x16-B f32 accesses) ----
 template <typename T>
 __global__ void maxpool_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W, int C, int k,
                                int stride, int pad, int OH, int OW) {
-  long total = (long)N * OH * OW * C;
+  const int C8 = C / 8;
+  long total = (long)N * OH * OW * C8;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int c = (int)(i % C);
-    long p = i / C;
-    int ow = (int)(p % OW); p /= OW;
-    int oh = (int)(p % OH); int n = (int)(p / OH);
-    float m = -INFINITY;
+    const int c8 = (int)(i % C8);
+    long p = i / C8;
+    const int ow = (int)(p % OW); p /= OW;
+    const int oh = (int)(p % OH); const int n = (int)(p / OH);
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
     for (int kh = 0; kh < k; ++kh) {
-      int ih = oh * stride - pad + kh;
+      const int ih = oh * stride - pad + kh;
       if (ih < 0 || ih >= H) continue;
       for (int kw = 0; kw < k; ++kw) {
-        int iw = ow * stride - pad + kw;
+        const int iw = ow * stride - pad + kw;
         if (iw < 0 || iw >= W) continue;
-        float v = (float)x[(((long)n * H + ih) * W + iw) * C + c];
-        m = (v > m || v != v) ? v : m;   // NaN propagates like torch max_pool2d
+        const T* src = x + (((long)n * H + ih) * W + iw) * C + c8 * 8;
+        T v[8];
+        if constexpr (sizeof(T) == 2) {
+          *(uint4*)v = *(const uint4*)src;
+        } else {
+          *(uint4*)v = *(const uint4*)src;
+          *(uint4*)(v + 4) = *(const uint4*)(src + 4);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = (float)v[e];
+          m[e] = (f > m[e] || f != f) ? f : m[e];   // NaN propagates like torch max_pool2d
+        }
       }
     }
-    y[i] = (T)m;
+    T o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (T)m[e];
+    T* dst = y + i * 8;
+    if constexpr (sizeof(T) == 2) {
+      *(uint4*)dst = *(uint4*)o;
+    } else {
+      *(uint4*)dst = *(uint4*)o;
+      *(uint4*)(dst + 4) = *(uint4*)(o + 4);
+    }
   }
 }
 
@@ -276,7 +308,8 @@ extern "C" int sat_maxpool2d_nhwc(int N, int H, int W, int C, int k, int stride,
                                   void* y, int OH, int OW, void* stream) {
   SAT_REQUIRE(x && y && k > 0 && stride > 0);
   SAT_REQUIRE(OH == (H + 2 * pad - k) / stride + 1 && OW == (W + 2 * pad - k) / stride + 1);
-  long total = (long)N * OH * OW * C;
+  SAT_REQUIRE(C % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0);
+  long total = (long)N * OH * OW * (C / 8);
   int g = grid_for(total);
   if (dtype == SAT_BF16)
     hipLaunchKernelGGL(maxpool_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, (bf16*)y, N, H,

@@ -36,6 +36,7 @@ struct KArgs {
   SatConvGeom cv;
   int vecA, vecB;
   int splitk, kchunk;   // split-K: blockIdx.z = batch*splitk + split; K range [split*kchunk, +kchunk)
+  int partial; long split_stride;   // partial-output split-K (plain stores into per-split slabs)
 };
 
 union Vec16 {
@@ -242,6 +243,26 @@ __global__ __launch_bounds__(256) void gemm_kernel(KArgs a) {
 
   // ---- epilogue ----
   const void* add1 = a.add1 ? (const char*)a.add1 + z * a.s_add1 * (a.add1_dtype == SAT_BF16 ? 2 : 4) : nullptr;
+  if (a.splitk > 1 && a.partial) {
+    float* Cg = (float*)a.C + (long)split * a.split_stride;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = n0 + wn * WN + j * 16 + (lane & 15);
+        if (col >= N) continue;
+        const float bcol = (split == 0 && a.bias) ? a.bias[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          if (row >= M) continue;
+          float v = a.alpha * acc[i][j][r] + bcol;
+          if (split == 0 && add1) v += ld_as_f32(add1, (long)row * a.ld_add1 + col, a.add1_dtype);
+          Cg[(long)row * a.ldc + col] = v;
+        }
+      }
+    return;
+  }
   if (a.splitk > 1) {
     // split-K: fp32 atomic accumulation into C (pre-zeroed by the host when beta == 0);
     // split 0 also contributes bias + add1.  Host guarantees act == NONE, fp32 C, no aux.
@@ -331,7 +352,7 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return 0;
   SAT_REQUIRE(g.K >= 0 && g.A && g.B && g.C);
   SAT_REQUIRE(g.dtype == SAT_F32 || g.dtype == SAT_BF16);
-  {
+  if (g.partial_splits <= 1) {
     int err = 0;
     if (sat_fast_gemm_try(g, s, &err)) return err;
   }
@@ -358,11 +379,22 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s) {
   // split-K for skinny problems that cannot fill 256 CUs with 64x64 tiles
   k.splitk = 1;
   k.kchunk = g.K > 0 ? g.K : 1;
+  k.partial = 0; k.split_stride = 0;
   const int bk = g.dtype == SAT_BF16 ? 32 : 16;
+  if (g.partial_splits > 1) {
+    SAT_REQUIRE(g.act == SAT_ACT_NONE && g.c_dtype == SAT_F32 && g.aux == nullptr && g.beta == 0.f &&
+                g.batch == 1 && amode != 2);
+    k.partial = 1; k.split_stride = g.split_stride;
+    k.splitk = g.partial_splits;
+    k.kchunk = sat_cdiv(sat_cdiv(g.K > 0 ? g.K : 1, g.partial_splits), bk) * bk;
+    if (g.dtype == SAT_BF16) return launch_t<bf16>(k, amode, g.transB, g.batch, s);
+    return launch_t<float>(k, amode, g.transB, g.batch, s);
+  }
   const long tiles64 = (long)sat_cdiv(g.M, 64) * sat_cdiv(g.N, 64) * g.batch;
   const bool can_split = g.act == SAT_ACT_NONE && g.c_dtype == SAT_F32 && g.aux == nullptr &&
                          (g.beta == 0.f || g.beta == 1.f) && amode != 2 && g.batch == 1;
-  if (can_split && tiles64 < 200 && g.K >= 8 * bk) {
+  // (bf16 only: the fp32 parity path stays deterministic)
+  if (can_split && g.dtype == SAT_BF16 && tiles64 < 200 && g.K >= 8 * bk) {
     int sk = (int)((400 + tiles64 - 1) / tiles64);
     sk = sk > 16 ? 16 : sk;
     const int max_by_k = g.K / (4 * bk);

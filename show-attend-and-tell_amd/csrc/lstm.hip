@@ -22,8 +22,9 @@ __global__ void lstm_fwd_kernel(LstmFwdArgs a) {
     float sg[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float v = a.xpart[(long)b * a.xpart_ld + q * E + j] + a.hpart[(long)b * a.hpart_ld + q * E + j];
-      if (a.cpart) v += a.cpart[(long)b * a.cpart_ld + q * E + j];
+      float v = a.xpart[(long)b * a.xpart_ld + q * E + j] +
+                sum_parts(a.hpart, (long)b * a.hpart_ld + q * E + j, a.h_splits, a.h_split_stride);
+      if (a.cpart) v += sum_parts(a.cpart, (long)b * a.cpart_ld + q * E + j, a.c_splits, a.c_split_stride);
       sg[q] = v;
       a.gates[(long)b * a.gates_ld + q * E + j] = v;
     }
@@ -55,7 +56,7 @@ __global__ void lstm_bwd_kernel(LstmBwdArgs a) {
     const float cp = a.c_prev[(long)b * a.c_prev_ld + j];
     const float cn = a.c_new[(long)b * a.c_new_ld + j];
     const float tc = tanhf(cn);
-    float dh = a.dh_rec ? a.dh_rec[(long)b * a.dh_rec_ld + j] : 0.f;
+    float dh = a.dh_rec ? sum_parts(a.dh_rec, (long)b * a.dh_rec_ld + j, a.dh_splits, a.dh_split_stride) : 0.f;
     if (a.dh_head) {
       float hh = a.dh_head[(long)b * a.dh_head_ld + j];
       if (a.mask) hh = a.mask[(long)b * a.mask_ld + j] ? hh * 2.f : 0.f;
@@ -79,13 +80,13 @@ __global__ void lstm_bwd_kernel(LstmBwdArgs a) {
 
 // d(tanh pre) for init_h / init_c: dpre[b, 0:E] = dh (1-h^2), dpre[b, E:2E] = dc (1-c^2)
 template <typename T>
-__global__ void tanh_pair_bwd_kernel(const float* dh, const float* dc, const float* hc0, int B, int E, float* dpre,
-                                     T* dpre_t) {
+__global__ void tanh_pair_bwd_kernel(const float* dh, int dh_splits, long dh_split_stride, const float* dc,
+                                     const float* hc0, int B, int E, float* dpre, T* dpre_t) {
   const long n = (long)B * 2 * E;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int b = (int)(i / (2 * E)), j = (int)(i - (long)b * 2 * E);
     const float y = hc0[i];
-    const float d = j < E ? dh[(long)b * E + j] : dc[(long)b * E + (j - E)];
+    const float d = j < E ? sum_parts(dh, (long)b * E + j, dh_splits, dh_split_stride) : dc[(long)b * E + (j - E)];
     const float v = d * (1.f - y * y);
     dpre[i] = v;
     if (dpre_t) dpre_t[i] = (T)v;
@@ -192,11 +193,11 @@ int sat_lstm_bwd_launch(const LstmBwdArgs& a, hipStream_t s) {
   DISPATCH_T(a.dtype, lstm_bwd_kernel, dim3(grid_for((long)a.B * a.E)), a);
   return (int)hipGetLastError();
 }
-int sat_tanh_pair_bwd(const float* d_h, const float* d_c, const float* hc0, int B, int E, float* dpre_f32,
-                      void* dpre_t, int dtype, hipStream_t s) {
+int sat_tanh_pair_bwd(const float* d_h, int dh_splits, long dh_split_stride, const float* d_c, const float* hc0,
+                      int B, int E, float* dpre_f32, void* dpre_t, int dtype, hipStream_t s) {
   dim3 g(grid_for((long)B * 2 * E));
-  if (dtype == SAT_BF16) hipLaunchKernelGGL(tanh_pair_bwd_kernel<bf16>, g, dim3(256), 0, s, d_h, d_c, hc0, B, E, dpre_f32, (bf16*)dpre_t);
-  else hipLaunchKernelGGL(tanh_pair_bwd_kernel<float>, g, dim3(256), 0, s, d_h, d_c, hc0, B, E, dpre_f32, (float*)dpre_t);
+  if (dtype == SAT_BF16) hipLaunchKernelGGL(tanh_pair_bwd_kernel<bf16>, g, dim3(256), 0, s, d_h, dh_splits, dh_split_stride, d_c, hc0, B, E, dpre_f32, (bf16*)dpre_t);
+  else hipLaunchKernelGGL(tanh_pair_bwd_kernel<float>, g, dim3(256), 0, s, d_h, dh_splits, dh_split_stride, d_c, hc0, B, E, dpre_f32, (float*)dpre_t);
   return (int)hipGetLastError();
 }
 int sat_dropout_apply(const float* h, long h_ld, int B, int T1, int E, int training, int has_mask,

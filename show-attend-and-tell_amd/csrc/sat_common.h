@@ -75,6 +75,9 @@ struct SatGemm {
   void* aux = nullptr; long ld_aux = 0; int aux_dtype = SAT_BF16;
   int batch = 1; long sA = 0, sB = 0, sC = 0, s_add1 = 0, s_aux = 0;
   SatConvGeom conv{};  // conv.C > 0 selects the implicit-im2col A loader
+  // partial-output split-K: split s writes its fp32 partial product to C + s*split_stride
+  // (bias/add1 in split 0 only, act must be NONE); the consumer sums the slabs.
+  int partial_splits = 0; long split_stride = 0;
 };
 
 int sat_gemm_launch(const SatGemm& g, hipStream_t s);

@@ -27,6 +27,7 @@ struct AttnFwdArgs {
   float* gate; long gate_out_ld;        // sigmoid gate (nullable)
   void* gated; long gated_ld;           // dtype gate*context (nullable)
   float* uh_save; long uh_save_ld;      // copy of U h + b (nullable)
+  int hg_splits; long hg_split_stride;  // uh / gate_pre are sums of hg_splits partial slabs (0|1 = plain)
 };
 int sat_attention_fwd_launch(const AttnFwdArgs& a, hipStream_t s);
 
@@ -49,6 +50,7 @@ struct AttnBwdArgs {
   float* dv_acc;                        // [B,E]  += dL/dv (per row b)
   float* dbv_acc;                       // [B]    += dL/dv.bias
   float* part;                          // scratch [B, NS, L]
+  int dg_splits; long dg_split_stride;  // d_gated = sum of dg_splits partial slabs (0|1 = plain)
 };
 int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s);
 
@@ -65,6 +67,8 @@ struct LstmFwdArgs {
   float* h_out; long h_out_ld;          // fp32
   void* h_out_t; long h_out_t_ld;       // dtype copy (nullable)
   void* h_next_in_t; long h_next_in_t_ld;  // dtype copy as next step's input (nullable)
+  int h_splits; long h_split_stride;    // hpart = sum of h_splits slabs
+  int c_splits; long c_split_stride;    // cpart = sum of c_splits slabs
 };
 int sat_lstm_fwd_launch(const LstmFwdArgs& a, hipStream_t s);
 
@@ -80,12 +84,13 @@ struct LstmBwdArgs {
   int dc_zero;                          // treat incoming dc as zero
   float* d_gates; long d_gates_ld;      // out fp32
   void* d_gates_t; long d_gates_t_ld;   // out dtype copy (nullable)
+  int dh_splits; long dh_split_stride;  // dh_rec = sum of dh_splits slabs
 };
 int sat_lstm_bwd_launch(const LstmBwdArgs& a, hipStream_t s);
 
 // ---- misc decoder elementwise ----
-int sat_tanh_pair_bwd(const float* d_h, const float* d_c, const float* hc0, int B, int E, float* dpre_f32,
-                      void* dpre_t, int dtype, hipStream_t s);
+int sat_tanh_pair_bwd(const float* d_h, int dh_splits, long dh_split_stride, const float* d_c, const float* hc0,
+                      int B, int E, float* dpre_f32, void* dpre_t, int dtype, hipStream_t s);
 int sat_dropout_apply(const float* h, long h_ld, int B, int T1, int E, int training, int has_mask,
                       const uint8_t* mask_in, uint8_t* mask_out, long mask_ld, uint64_t seed, int t_offset,
                       void* out_t, long out_ld, int dtype, hipStream_t s);
@@ -99,3 +104,10 @@ int sat_broadcast_rows(const void* src, int B, int D, int T1, int dtype, void* d
 int sat_row_sum_accumulate(const float* X, int R, int N, float* out, hipStream_t s);
 int sat_tokens_from_captions(const int64_t* caps, int B, int T, int T1, int32_t* tok, hipStream_t s);
 size_t sat_attention_part_floats(int B, int L, int D, int dtype);
+
+// sum of `n` partial slabs (n <= 1: plain read)
+__device__ __forceinline__ float sum_parts(const float* p, long idx, int n, long stride) {
+  float v = p[idx];
+  for (int s = 1; s < n; ++s) v += p[idx + s * stride];
+  return v;
+}
