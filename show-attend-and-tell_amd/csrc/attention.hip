@@ -37,6 +37,17 @@ __device__ __forceinline__ void load4(const T* p, float* o) {
   }
 }
 
+// tanh: exact libm in the fp32 parity path; exp-based (v_exp_f32 + v_rcp_f32, ~1e-6 rel) in bf16 mode.
+template <typename T>
+__device__ __forceinline__ float tanh_t(float x) {
+  if constexpr (sizeof(T) == 4) {
+    return tanhf(x);
+  } else {
+    const float e = __expf(2.f * x);
+    return 1.f - 2.f * __frcp_rn(e + 1.f);
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void loadv(const T* p, float* o) {  // 16 bytes
   uint4 v = *(const uint4*)p;
@@ -56,21 +67,35 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
   const T* Ws = (const T*)a.Ws + (long)b * L * E;
   const float* uh = a.uh + (long)b * a.uh_ld;
 
-  // ---- scores ----
+  // ---- scores: lane holds its E-chunks of (U h + b) and v in registers ----
+  constexpr int CH = 4;   // E <= 1024 = 4 chunks of 64 lanes x 4
+  float u_r[CH][4], v_r[CH][4];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int e = c * 256 + lane * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { u_r[c][j] = 0.f; v_r[c][j] = 0.f; }
+    if (e < E) {
+      for (int sp = 0; sp < (a.hg_splits > 1 ? a.hg_splits : 1); ++sp) {
+        const float4 u2 = *(const float4*)(uh + sp * a.hg_split_stride + e);
+        u_r[c][0] += u2.x; u_r[c][1] += u2.y; u_r[c][2] += u2.z; u_r[c][3] += u2.w;
+      }
+      const float4 vv = *(const float4*)(a.v_w + e);
+      v_r[c][0] = vv.x; v_r[c][1] = vv.y; v_r[c][2] = vv.z; v_r[c][3] = vv.w;
+    }
+  }
   const float bv = a.v_b[0];
   for (int l = w; l < L; l += 4) {
     const T* wr = Ws + (long)l * E;
     float acc = 0.f;
-    for (int e = lane * 4; e < E; e += 256) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int e = c * 256 + lane * 4;
+      if (e >= E) break;
       float x[4];
       load4<T>(wr + e, x);
-      float4 u = *(const float4*)(uh + e);
-      for (int sp = 1; sp < a.hg_splits; ++sp) {
-        const float4 u2 = *(const float4*)(uh + sp * a.hg_split_stride + e);
-        u.x += u2.x; u.y += u2.y; u.z += u2.z; u.w += u2.w;
-      }
-      float4 vv = *(const float4*)(a.v_w + e);
-      acc += vv.x * tanhf(x[0] + u.x) + vv.y * tanhf(x[1] + u.y) + vv.z * tanhf(x[2] + u.z) + vv.w * tanhf(x[3] + u.w);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc += v_r[c][j] * tanh_t<T>(x[j] + u_r[c][j]);
     }
     acc = wave_sum(acc);
     if (lane == 0) s_alpha[l] = acc + bv;
@@ -143,19 +168,33 @@ __global__ __launch_bounds__(256) void attn_bwd1_kernel(AttnBwdArgs a) {
 #pragma unroll
   for (int j = 0; j < VD; ++j) dctx[j] = 0.f;
   if (d0 < D) {
+    float dg[VD], g[VD], c[VD], dx[VD];
+#pragma unroll
+    for (int j = 0; j < VD; j += 4) {
+      float4 q = *(const float4*)(a.d_gated + (long)b * a.d_gated_ld + d0 + j);
+      for (int sp = 1; sp < a.dg_splits; ++sp) {
+        const float4 q2 = *(const float4*)(a.d_gated + sp * a.dg_split_stride + (long)b * a.d_gated_ld + d0 + j);
+        q.x += q2.x; q.y += q2.y; q.z += q2.z; q.w += q2.w;
+      }
+      const float4 gg = *(const float4*)(a.gate + (long)b * a.gate_ld + d0 + j);
+      const float4 cc = *(const float4*)(a.ctx + (long)b * a.ctx_ld + d0 + j);
+      dg[j] = q.x; dg[j + 1] = q.y; dg[j + 2] = q.z; dg[j + 3] = q.w;
+      g[j] = gg.x; g[j + 1] = gg.y; g[j + 2] = gg.z; g[j + 3] = gg.w;
+      c[j] = cc.x; c[j + 1] = cc.y; c[j + 2] = cc.z; c[j + 3] = cc.w;
+      if (a.d_ctx_ext) {
+        const float4 xx = *(const float4*)(a.d_ctx_ext + (long)b * a.d_ctx_ext_ld + d0 + j);
+        dx[j] = xx.x; dx[j + 1] = xx.y; dx[j + 2] = xx.z; dx[j + 3] = xx.w;
+      } else {
+        dx[j] = dx[j + 1] = dx[j + 2] = dx[j + 3] = 0.f;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < VD; ++j) {
-      const int d = d0 + j;
-      const float dg = sum_parts(a.d_gated, (long)b * a.d_gated_ld + d, a.dg_splits, a.dg_split_stride);
-      const float g = a.gate[(long)b * a.gate_ld + d];
-      const float c = a.ctx[(long)b * a.ctx_ld + d];
-      float dc = dg * g;
-      if (a.d_ctx_ext) dc += a.d_ctx_ext[(long)b * a.d_ctx_ext_ld + d];
-      dctx[j] = dc;
+      dctx[j] = dg[j] * g[j] + dx[j];
       if (w == 0) {
-        const float dgp = dg * c * g * (1.f - g);
-        a.d_gpre[(long)b * a.d_gpre_ld + d] = dgp;
-        if (a.d_gpre_t) ((T*)a.d_gpre_t)[(long)b * a.d_gpre_ld + d] = (T)dgp;
+        const float dgp = dg[j] * c[j] * g[j] * (1.f - g[j]);
+        a.d_gpre[(long)b * a.d_gpre_ld + d0 + j] = dgp;
+        if (a.d_gpre_t) ((T*)a.d_gpre_t)[(long)b * a.d_gpre_ld + d0 + j] = (T)dgp;
       }
     }
   }
@@ -226,7 +265,7 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
       float ac[4] = {acc.x, acc.y, acc.z, acc.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float t = tanhf(x[j] + uu[j]);
+        const float t = tanh_t<T>(x[j] + uu[j]);
         const float datt = de * vw[j] * (1.f - t * t);
         duh[c][j] += datt;
         dv[c][j] += de * t;

@@ -36,16 +36,42 @@ struct FArgs {
   // implicit im2col (amode 1: Cin % 64 == 0, amode 2: Cin % 8 == 0)
   int amode, H, W, Cin, KW, stride, pad, OH, OW;
   const bf16* zero16;
+  int splitk, kchunk;      // atomic split-K (fp32 C, act NONE): blockIdx.z = split
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+// k-major ("transposed") operand tile: 64 k-rows x 128 elements = 256-B rows, 16-B chunk ch of
+// row r stored at slot ch ^ swz(r) (cdna_hip_programming.md T10, image (b)): conflict-free for
+// ds_read_b64_tr_b16 fragment reads.
+__device__ __forceinline__ int swz256(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+// MFMA 16x16x32 operand fragment (8 consecutive k of one row x) from a k-major tile:
+// two transposing reads of 4 k-rows x 16 columns each.
+__device__ __forceinline__ bf16x8 frag_tr(const char* tile, int kbase, int xt, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int ch = (xt >> 3) + (p >> 1);
+  const int r0 = kbase + 8 * g + q, r1 = r0 + 4;
+  const char* a0 = tile + r0 * 256 + 16 * (ch ^ swz256(r0)) + 8 * (p & 1);
+  const char* a1 = tile + r1 * 256 + 16 * (ch ^ swz256(r1)) + 8 * (p & 1);
+  const bf16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(uintptr_t)(const void*)a0);
+  const bf16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(uintptr_t)(const void*)a1);
+  bf16x8 r;
+  r[0] = v0[0]; r[1] = v0[1]; r[2] = v0[2]; r[3] = v0[3];
+  r[4] = v1[0]; r[5] = v1[1]; r[6] = v1[2]; r[7] = v1[3];
+  return r;
+}
 typedef __attribute__((address_space(1))) const void gbl_void;
 
 __device__ __forceinline__ void dma16(const void* src, char* lds_dst) {
   __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_dst, 16, 0, 0);
 }
 
-template <int BN>
+// AT: A stored [K][M] (m-contiguous); BT: B stored [K][N] (n-contiguous).  Transposed operands
+// need a 128-wide tile (256-B k-rows) and M, N multiples of 8.
+template <int BN, bool AT, bool BT>
 __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
   constexpr int WN = BN / 2, NJ = WN / 16, MI = 4;
   constexpr int STAGE_A = BM * ROWB, STAGE_B = BN * ROWB, STAGE = STAGE_A + STAGE_B;
@@ -59,7 +85,10 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int M = a.M, N = a.N, K = a.K;
+  const int M = a.M, N = a.N;
+  const int split = blockIdx.z;
+  const int kbeg = split * a.kchunk;
+  const int K = min(a.K, kbeg + a.kchunk);
 
   // ---- per-lane DMA row bookkeeping (rows are fixed across k-tiles) ----
   const int lrow = lane >> 3, slot = lane & 7;
@@ -93,10 +122,22 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
     b_base[j] = (n0 + r < N) ? (long)(n0 + r) * a.ldb : -1;
   }
 
+  // k-major operands: lane -> (k-row within the 4-row DMA piece, chunk slot)
+  const int trow = lane >> 4, tslot = lane & 15;
+
   auto stage = [&](int buf, int k0) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + STAGE_A;
-    if (a.amode == 1) {   // block-uniform filter tap
+    if constexpr (AT) {
+#pragma unroll
+      for (int j = 0; j < A_INSTR; ++j) {
+        const int r = (w * A_INSTR + j) * 4 + trow;       // k-row of the tile
+        const int ch = tslot ^ swz256(r);
+        const int k = k0 + r, m = m0 + 8 * ch;
+        const bool ok = k < K && m + 8 <= M;
+        dma16(ok ? (const void*)(a.A + (long)k * a.lda + m) : (const void*)a.zero16, sa + (w * A_INSTR + j) * 1024);
+      }
+    } else if (a.amode == 1) {   // block-uniform filter tap
       const int tap = k0 / a.Cin, ci0 = k0 - tap * a.Cin;
       const int kh = tap / a.KW, kw = tap - kh * a.KW;
 #pragma unroll
@@ -130,11 +171,22 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
         dma16(ok ? (const void*)(a.A + a_base[j] + k) : (const void*)a.zero16, sa + (w * A_INSTR + j) * 1024);
       }
     }
+    if constexpr (BT) {
 #pragma unroll
-    for (int j = 0; j < B_INSTR; ++j) {
-      const int k = k0 + 8 * b_chunk[j];
-      const bool ok = b_base[j] >= 0 && k < K;
-      dma16(ok ? (const void*)(a.B + b_base[j] + k) : (const void*)a.zero16, sb + (w * B_INSTR + j) * 1024);
+      for (int j = 0; j < B_INSTR; ++j) {
+        const int r = (w * B_INSTR + j) * 4 + trow;
+        const int ch = tslot ^ swz256(r);
+        const int k = k0 + r, n = n0 + 8 * ch;
+        const bool ok = k < K && n + 8 <= N;
+        dma16(ok ? (const void*)(a.B + (long)k * a.ldb + n) : (const void*)a.zero16, sb + (w * B_INSTR + j) * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < B_INSTR; ++j) {
+        const int k = k0 + 8 * b_chunk[j];
+        const bool ok = b_base[j] >= 0 && k < K;
+        dma16(ok ? (const void*)(a.B + b_base[j] + k) : (const void*)a.zero16, sb + (w * B_INSTR + j) * 1024);
+      }
     }
   };
 
@@ -153,13 +205,21 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
       bf16x8 af[MI], bfr[NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const int r = wm * 64 + i * 16 + fr;
-        af[i] = *(const bf16x8*)(sa + r * ROWB + 16 * ((ks * 4 + fh) ^ ((r >> 1) & 7)));
+        if constexpr (AT) {
+          af[i] = frag_tr(sa, ks * 32, wm * 64 + i * 16, lane);
+        } else {
+          const int r = wm * 64 + i * 16 + fr;
+          af[i] = *(const bf16x8*)(sa + r * ROWB + 16 * ((ks * 4 + fh) ^ ((r >> 1) & 7)));
+        }
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int r = wn * WN + j * 16 + fr;
-        bfr[j] = *(const bf16x8*)(sb + r * ROWB + 16 * ((ks * 4 + fh) ^ ((r >> 1) & 7)));
+        if constexpr (BT) {
+          bfr[j] = frag_tr(sb, ks * 32, wn * WN + j * 16, lane);
+        } else {
+          const int r = wn * WN + j * 16 + fr;
+          bfr[j] = *(const bf16x8*)(sb + r * ROWB + 16 * ((ks * 4 + fh) ^ ((r >> 1) & 7)));
+        }
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -169,18 +229,34 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
     }
   };
 
-  const int nk = (K + BK - 1) / BK;
-  stage(0, 0);
+  const int nk = K > kbeg ? (K - kbeg + BK - 1) / BK : 0;
+  if (nk > 0) stage(0, kbeg);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+    if (kt + 1 < nk) stage(cur ^ 1, kbeg + (kt + 1) * BK);
     compute(cur);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
+  if (a.splitk > 1) {   // atomic split-K: fp32 C, bias in split 0, act NONE (host-checked)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = n0 + wn * WN + j * 16 + fr;
+        if (col >= N) continue;
+        const float bcol = (split == 0 && a.bias) ? a.bias[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * 64 + i * 16 + fh * 4 + r;
+          if (row < M) atomicAdd((float*)a.C + (long)row * a.ldc + col, acc[i][j][r] + bcol);
+        }
+      }
+    return;
+  }
   // ---- epilogue: stage the wave's 64 x WN fp32 tile in LDS, write 16-B row segments ----
   float* ep = (float*)smem + w * 64 * EPI_LD;
 #pragma unroll
@@ -269,15 +345,33 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // Returns 1 if the problem was handled by the fast path, 0 if the caller should use the generic kernel.
 int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   *err = 0;
-  if (g.dtype != SAT_BF16 || g.transA || g.transB || g.batch != 1 || g.aux || g.beta != 0.f) return 0;
-  if (g.K % 8 || g.ldb % 8 || !al16(g.B) || !al16(g.A)) return 0;
+  if (g.dtype != SAT_BF16 || g.batch != 1 || g.aux) return 0;
+  if (!al16(g.B) || !al16(g.A)) return 0;
   const bool conv = g.conv.C > 0;
-  if (!conv && g.lda % 8) return 0;
+  const bool at = g.transA != 0, bt = g.transB != 0;
+  if (conv && at) return 0;
+  if (at && (g.M % 8 || g.lda % 8)) return 0;
+  if (bt && (g.N % 8 || g.ldb % 8)) return 0;
+  if (!at && (g.K % 8 || (!conv && g.lda % 8))) return 0;
+  if (!bt && (g.K % 8 || g.ldb % 8)) return 0;
   if (g.bias && !al16(g.bias)) return 0;
   if (g.add1 && !al16(g.add1)) return 0;
-  const int bn = g.N <= 64 ? 64 : 128;
+  const int bn = (g.N <= 64 && !at && !bt) ? 64 : 128;
   const long tiles = (long)sat_cdiv(g.M, BM) * sat_cdiv(g.N, bn);
-  if (tiles < 160) return 0;   // skinny problems: the generic kernel's split-K fills the chip better
+  // atomic split-K for weight-gradient-like problems (long K, few tiles, fp32 output)
+  int splitk = 1;
+  const bool can_split = g.c_dtype == SAT_F32 && g.act == SAT_ACT_NONE && !g.add1 && (g.beta == 0.f || g.beta == 1.f) && !conv;
+  if (g.beta != 0.f && !(can_split && g.beta == 1.f)) return 0;
+  if (tiles < 160) {
+    if (!can_split || g.K < 1024) return 0;
+    splitk = (int)((320 + tiles - 1) / tiles);
+    const int by_k = g.K / 256;
+    if (splitk > by_k) splitk = by_k;
+    if (splitk > 16) splitk = 16;
+    if (splitk < 2) return 0;
+  } else if (g.beta != 0.f) {
+    splitk = 1;   // beta == 1 accumulate through the atomic epilogue with a single split
+  }
   static bf16* zero = nullptr;
   if (!zero) {
     void* p = nullptr;
@@ -292,15 +386,33 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   a.add1 = g.add1; a.ld_add1 = g.ld_add1; a.add1_bf16 = g.add1_dtype == SAT_BF16;
   a.act = g.act;
   a.zero16 = zero;
+  const bool atomic = splitk > 1 || g.beta != 0.f;
+  a.splitk = atomic ? (splitk > 1 ? splitk : 2) : 1;   // the atomic epilogue is selected by splitk > 1
+  a.kchunk = g.K;
+  if (atomic) {
+    const int chunks = splitk > 1 ? splitk : 1;
+    a.kchunk = sat_cdiv(sat_cdiv(g.K, chunks), BK) * BK;
+    a.splitk = chunks > 1 ? sat_cdiv(g.K, a.kchunk) : 1;
+    if (a.splitk == 1) {   // beta == 1, single split: still accumulate atomically
+      a.splitk = 2; a.kchunk = sat_cdiv(g.K, BK) * BK;   // split 1 has an empty K range and adds 0
+    }
+    if (g.beta == 0.f) {
+      if (g.ldc == g.N) { SAT_CHECK(hipMemsetAsync(g.C, 0, (size_t)g.M * g.N * 4, s)); }
+      else { SAT_CHECK(hipMemset2DAsync(g.C, (size_t)g.ldc * 4, 0, (size_t)g.N * 4, g.M, s)); }
+    }
+  }
   if (conv) {
     if (g.conv.C % 8) return 0;
     a.amode = (g.conv.C % BK == 0) ? 1 : 2;
     a.H = g.conv.H; a.W = g.conv.W; a.Cin = g.conv.C; a.KW = g.conv.KW;
     a.stride = g.conv.stride; a.pad = g.conv.pad; a.OH = g.conv.OH; a.OW = g.conv.OW;
   }
-  dim3 grid(sat_cdiv(g.N, bn), sat_cdiv(g.M, BM));
-  if (bn == 64) hipLaunchKernelGGL(fast_gemm_kernel<64>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(fast_gemm_kernel<128>, grid, dim3(256), 0, s, a);
+  dim3 grid(sat_cdiv(g.N, bn), sat_cdiv(g.M, BM), a.splitk);
+  if (at && bt) hipLaunchKernelGGL((fast_gemm_kernel<128, true, true>), grid, dim3(256), 0, s, a);
+  else if (at) hipLaunchKernelGGL((fast_gemm_kernel<128, true, false>), grid, dim3(256), 0, s, a);
+  else if (bt) hipLaunchKernelGGL((fast_gemm_kernel<128, false, true>), grid, dim3(256), 0, s, a);
+  else if (bn == 64) hipLaunchKernelGGL((fast_gemm_kernel<64, false, false>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((fast_gemm_kernel<128, false, false>), grid, dim3(256), 0, s, a);
   *err = (int)hipGetLastError();
   return 1;
 }

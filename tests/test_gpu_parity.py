@@ -309,3 +309,26 @@ def test_fast_gemm_path(sat, M, N, K, out):
     ops.gemm(A.to(DEV), Bm.to(DEV), C, bias=bias.to(DEV), add1=add1.to(DEV), act=sat._lib.ACT_RELU)
     tol = 1e-5 if out == torch.float32 else 8e-3
     assert rel(C.float(), ref) < tol
+
+
+@pytest.mark.parametrize("M,N,K,transA,transB,beta", [
+    (10000, 512, 3328, True, True, 0.0),    # dW_fout-like, 316 tiles
+    (4608, 512, 3328, True, True, 1.0),     # dW_hcat-like, accumulate into existing grads
+    (512, 512, 3328, True, True, 0.0),      # tiny-tile weight grad -> atomic split-K
+    (2048, 2048, 1040, True, True, 0.0),
+    (3328, 512, 10000, False, True, 0.0),   # d_comb-like: B n-contiguous, split-K
+    (3328, 2048, 512, False, True, 0.0),
+    (1024, 1024, 2048, True, False, 0.0)])
+def test_fast_gemm_transposed_operands(sat, M, N, K, transA, transB, beta):
+    from sat_amd import ops
+    g = torch.Generator().manual_seed(M + 3 * N + 7 * K)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    Bm = torch.randn(N, K, generator=g).bfloat16()
+    C0 = torch.randn(M, N, generator=g)
+    ref = A.double() @ Bm.double().T + beta * C0.double()
+    Ad = (A.T.contiguous() if transA else A).to(DEV)
+    Bd = (Bm.T.contiguous() if transB else Bm).to(DEV)
+    C = C0.clone().to(DEV)
+    ops.gemm(Ad, Bd, C, transA=transA, transB=transB, beta=beta)
+    torch.cuda.synchronize()
+    assert rel(C, ref) < 2e-5
