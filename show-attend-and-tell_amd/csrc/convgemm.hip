@@ -71,14 +71,29 @@ __device__ __forceinline__ void dma16(const void* src, char* lds_dst) {
 
 // AT: A stored [K][M] (m-contiguous); BT: B stored [K][N] (n-contiguous).  Transposed operands
 // need a 128-wide tile (256-B k-rows) and M, N multiples of 8.
-template <int BN, bool AT, bool BT>
+// Wait until at most N of this wave's vector-memory ops are outstanding, then barrier.  Raw
+// s_barrier (not __syncthreads, whose fence would drain every in-flight LDS-DMA stage).
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 18) asm volatile("s_waitcnt vmcnt(18)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)\n\ts_barrier" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+
+template <int BN, bool AT, bool BT, int NS>
 __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
   constexpr int WN = BN / 2, NJ = WN / 16, MI = 4;
   constexpr int STAGE_A = BM * ROWB, STAGE_B = BN * ROWB, STAGE = STAGE_A + STAGE_B;
   constexpr int A_INSTR = BM / 32, B_INSTR = BN / 32;   // 1 KiB DMA instructions per wave per stage
+  constexpr int INSTR = A_INSTR + B_INSTR;
   constexpr int EPI_LD = WN + 4;
   constexpr int EPI_BYTES = 4 * 64 * EPI_LD * 4;
-  constexpr int LDS_BYTES = (2 * STAGE > EPI_BYTES) ? 2 * STAGE : EPI_BYTES;
+  constexpr int LDS_BYTES = (NS * STAGE > EPI_BYTES) ? NS * STAGE : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -229,17 +244,27 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
     }
   };
 
+  // NS-stage LDS-DMA ring: NS-1 k-tiles in flight while one is consumed.
   const int nk = K > kbeg ? (K - kbeg + BK - 1) / BK : 0;
-  if (nk > 0) stage(0, kbeg);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) stage(p, kbeg + p * BK);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, kbeg + (kt + 1) * BK);
-    compute(cur);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    const int after = min(NS - 2, nk - 1 - kt);   // stages issued after tile kt (uniform)
+    if constexpr (NS >= 4) {
+      if (after >= 2) wait_vm_barrier<2 * INSTR>();
+      else if (after == 1) wait_vm_barrier<INSTR>();
+      else wait_vm_barrier<0>();
+    } else if constexpr (NS == 3) {
+      if (after == 1) wait_vm_barrier<INSTR>();
+      else wait_vm_barrier<0>();
+    } else {
+      wait_vm_barrier<0>();
+    }
+    if (kt + NS - 1 < nk) stage((kt + NS - 1) % NS, kbeg + (kt + NS - 1) * BK);
+    compute(kt % NS);
   }
+  __syncthreads();   // every wave done reading the ring before the epilogue reuses the LDS
 
   if (a.splitk > 1) {   // atomic split-K: fp32 C, bias in split 0, act NONE (host-checked)
 #pragma unroll
@@ -338,6 +363,24 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
 
 __device__ __attribute__((aligned(16))) bf16 g_zero16[64];
 
+// experiment override (tools/bench_conv.py): 0 = automatic
+int g_force_stages = 0, g_force_bn = 0;
+
+template <bool AT, bool BT, int NS>
+void launch_fast(int bn, dim3 grid, hipStream_t s, const FArgs& a) {
+  if constexpr (!AT && !BT) {
+    if (bn == 64) { hipLaunchKernelGGL((fast_gemm_kernel<64, false, false, NS>), grid, dim3(256), 0, s, a); return; }
+  }
+  hipLaunchKernelGGL((fast_gemm_kernel<128, AT, BT, NS>), grid, dim3(256), 0, s, a);
+}
+
+template <bool AT, bool BT>
+void launch_fast_ns(int ns, int bn, dim3 grid, hipStream_t s, const FArgs& a) {
+  if (ns >= 4) launch_fast<AT, BT, 4>(bn, grid, s, a);
+  else if (ns == 3) launch_fast<AT, BT, 3>(bn, grid, s, a);
+  else launch_fast<AT, BT, 2>(bn, grid, s, a);
+}
+
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
@@ -356,7 +399,8 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   if (!bt && (g.K % 8 || g.ldb % 8)) return 0;
   if (g.bias && !al16(g.bias)) return 0;
   if (g.add1 && !al16(g.add1)) return 0;
-  const int bn = (g.N <= 64 && !at && !bt) ? 64 : 128;
+  int bn = (g.N <= 64 && !at && !bt) ? 64 : 128;
+  if (g_force_bn && !at && !bt) bn = g_force_bn;
   const long tiles = (long)sat_cdiv(g.M, BM) * sat_cdiv(g.N, bn);
   // atomic split-K for weight-gradient-like problems (long K, few tiles, fp32 output)
   int splitk = 1;
@@ -408,11 +452,17 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
     a.stride = g.conv.stride; a.pad = g.conv.pad; a.OH = g.conv.OH; a.OW = g.conv.OW;
   }
   dim3 grid(sat_cdiv(g.N, bn), sat_cdiv(g.M, BM), a.splitk);
-  if (at && bt) hipLaunchKernelGGL((fast_gemm_kernel<128, true, true>), grid, dim3(256), 0, s, a);
-  else if (at) hipLaunchKernelGGL((fast_gemm_kernel<128, true, false>), grid, dim3(256), 0, s, a);
-  else if (bt) hipLaunchKernelGGL((fast_gemm_kernel<128, false, true>), grid, dim3(256), 0, s, a);
-  else if (bn == 64) hipLaunchKernelGGL((fast_gemm_kernel<64, false, false>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((fast_gemm_kernel<128, false, false>), grid, dim3(256), 0, s, a);
+  const int ns = g_force_stages ? g_force_stages : 2;
+  if (at && bt) launch_fast_ns<true, true>(ns, bn, grid, s, a);
+  else if (at) launch_fast_ns<true, false>(ns, bn, grid, s, a);
+  else if (bt) launch_fast_ns<false, true>(ns, bn, grid, s, a);
+  else launch_fast_ns<false, false>(ns, bn, grid, s, a);
   *err = (int)hipGetLastError();
   return 1;
+}
+
+extern "C" int sat_fast_gemm_set_config(int stages, int bn) {
+  g_force_stages = stages;
+  g_force_bn = bn;
+  return 0;
 }
