@@ -87,8 +87,9 @@ int sat_abi_version(void);
 const char* sat_error_string(int code);
 
 /* --- generic building blocks -------------------------------------------- */
-/* tuning hook for the bf16 LDS-DMA GEMM: LDS ring depth (2..4) and N tile (64|128); 0 = automatic. */
-int sat_fast_gemm_set_config(int stages, int bn);
+/* tuning hook for the bf16 LDS-DMA GEMM: LDS ring depth (2|3), N tile (64|128), waves per block
+ * (4|8); 0 = automatic. */
+int sat_fast_gemm_set_config(int stages, int bn, int waves);
 int sat_gemm(const SatGemmArgs* args, void* stream);
 /* elementwise cast between SAT_F32 and SAT_BF16 storage (n elements). */
 int sat_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, void* stream);

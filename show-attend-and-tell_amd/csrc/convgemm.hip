@@ -68,6 +68,11 @@ typedef __attribute__((address_space(1))) const void gbl_void;
 __device__ __forceinline__ void dma16(const void* src, char* lds_dst) {
   __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_dst, 16, 0, 0);
 }
+// select the DMA source without control flow (v_cndmask on the address, one DMA per lane)
+__device__ __forceinline__ const void* sel(bool ok, const void* p, const void* z) {
+  const uintptr_t a = (uintptr_t)p, b = (uintptr_t)z;
+  return (const void*)(ok ? a : b);
+}
 
 // AT: A stored [K][M] (m-contiguous); BT: B stored [K][N] (n-contiguous).  Transposed operands
 // need a 128-wide tile (256-B k-rows) and M, N multiples of 8.
@@ -76,6 +81,8 @@ __device__ __forceinline__ void dma16(const void* src, char* lds_dst) {
 template <int N>
 __device__ __forceinline__ void wait_vm_barrier() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
@@ -85,20 +92,23 @@ __device__ __forceinline__ void wait_vm_barrier() {
   else static_assert(N < 0, "unsupported vmcnt");
 }
 
-template <int BN, bool AT, bool BT, int NS>
-__global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
-  constexpr int WN = BN / 2, NJ = WN / 16, MI = 4;
+template <int BN, bool AT, bool BT, int NS, int NW>
+__global__ __launch_bounds__(NW * 64) void fast_gemm_kernel(FArgs a) {
+  constexpr int WCOLS = NW / 2;                       // waves along N (2 along M, 64 rows each)
+  constexpr int WN = BN / WCOLS, NJ = WN / 16, MI = 4;
   constexpr int STAGE_A = BM * ROWB, STAGE_B = BN * ROWB, STAGE = STAGE_A + STAGE_B;
-  constexpr int A_INSTR = BM / 32, B_INSTR = BN / 32;   // 1 KiB DMA instructions per wave per stage
+  constexpr int A_INSTR = 16 / NW;                    // 1 KiB DMA instructions per wave per stage
+  constexpr int B_INSTR = BT ? 16 / NW : BN / (8 * NW);
+  static_assert(A_INSTR >= 1 && B_INSTR >= 1 && NJ >= 1, "tile/wave mismatch");
   constexpr int INSTR = A_INSTR + B_INSTR;
-  constexpr int EPI_LD = WN + 4;
-  constexpr int EPI_BYTES = 4 * 64 * EPI_LD * 4;
+  constexpr int EPI_LD = BN + 4;
+  constexpr int EPI_BYTES = BM * EPI_LD * 4;
   constexpr int LDS_BYTES = (NS * STAGE > EPI_BYTES) ? NS * STAGE : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / WCOLS, wn = w % WCOLS;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int M = a.M, N = a.N;
   const int split = blockIdx.z;
@@ -150,7 +160,7 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
         const int ch = tslot ^ swz256(r);
         const int k = k0 + r, m = m0 + 8 * ch;
         const bool ok = k < K && m + 8 <= M;
-        dma16(ok ? (const void*)(a.A + (long)k * a.lda + m) : (const void*)a.zero16, sa + (w * A_INSTR + j) * 1024);
+        dma16(sel(ok, a.A + (long)k * a.lda + m, a.zero16), sa + (w * A_INSTR + j) * 1024);
       }
     } else if (a.amode == 1) {   // block-uniform filter tap
       const int tap = k0 / a.Cin, ci0 = k0 - tap * a.Cin;
@@ -159,8 +169,7 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
       for (int j = 0; j < A_INSTR; ++j) {
         const int ih = a_ih[j] + kh, iw = a_iw[j] + kw;
         const bool ok = a_base[j] >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        const void* src = ok ? (const void*)(a.A + ((a_base[j] + (long)ih * a.W + iw) * a.Cin + ci0 + 8 * a_chunk[j]))
-                             : (const void*)a.zero16;
+        const void* src = sel(ok, a.A + ((a_base[j] + (long)ih * a.W + iw) * a.Cin + ci0 + 8 * a_chunk[j]), a.zero16);
         dma16(src, sa + (w * A_INSTR + j) * 1024);
       }
     } else if (a.amode == 2) {  // per-lane tap (small Cin, e.g. the padded 3->8 stem)
@@ -176,14 +185,14 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
           ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
           off = (a_base[j] + (long)ih * a.W + iw) * a.Cin + ci;
         }
-        dma16(ok ? (const void*)(a.A + off) : (const void*)a.zero16, sa + (w * A_INSTR + j) * 1024);
+        dma16(sel(ok, a.A + off, a.zero16), sa + (w * A_INSTR + j) * 1024);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < A_INSTR; ++j) {
         const int k = k0 + 8 * a_chunk[j];
         const bool ok = a_base[j] >= 0 && k < K;
-        dma16(ok ? (const void*)(a.A + a_base[j] + k) : (const void*)a.zero16, sa + (w * A_INSTR + j) * 1024);
+        dma16(sel(ok, a.A + a_base[j] + k, a.zero16), sa + (w * A_INSTR + j) * 1024);
       }
     }
     if constexpr (BT) {
@@ -193,14 +202,14 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
         const int ch = tslot ^ swz256(r);
         const int k = k0 + r, n = n0 + 8 * ch;
         const bool ok = k < K && n + 8 <= N;
-        dma16(ok ? (const void*)(a.B + (long)k * a.ldb + n) : (const void*)a.zero16, sb + (w * B_INSTR + j) * 1024);
+        dma16(sel(ok, a.B + (long)k * a.ldb + n, a.zero16), sb + (w * B_INSTR + j) * 1024);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < B_INSTR; ++j) {
         const int k = k0 + 8 * b_chunk[j];
         const bool ok = b_base[j] >= 0 && k < K;
-        dma16(ok ? (const void*)(a.B + b_base[j] + k) : (const void*)a.zero16, sb + (w * B_INSTR + j) * 1024);
+        dma16(sel(ok, a.B + b_base[j] + k, a.zero16), sb + (w * B_INSTR + j) * 1024);
       }
     }
   };
@@ -282,38 +291,41 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
       }
     return;
   }
-  // ---- epilogue: stage the wave's 64 x WN fp32 tile in LDS, write 16-B row segments ----
-  float* ep = (float*)smem + w * 64 * EPI_LD;
+  // ---- epilogue: stage the block's 128 x BN fp32 tile in LDS, then every thread writes
+  //      16-byte pieces of full BN-wide row segments (bias, residual, activation, bf16 fused) ----
+  float* ep = (float*)smem;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) ep[(i * 16 + fh * 4 + r) * EPI_LD + j * 16 + fr] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r)
+        ep[(wm * 64 + i * 16 + fh * 4 + r) * EPI_LD + wn * WN + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
-  constexpr int CPR = WN / 8;               // 8-column chunks per row
-  constexpr int ITER = 64 * CPR / 64;        // chunks per lane; a lane's column chunk is fixed (cc = lane % CPR)
-  const int cc = lane % CPR;
-  const int col = n0 + wn * WN + cc * 8;
+  constexpr int CPR = BN / 8;                  // 8-column chunks per tile row
+  constexpr int RPP = NW * 64 / CPR;           // rows per pass
+  constexpr int ITER = BM / RPP;
+  const int tid2 = threadIdx.x;
+  const int cc = tid2 % CPR, r0 = tid2 / CPR;
+  const int col = n0 + cc * 8;
   const bool vec_ok = (a.ldc % 8 == 0) && (!a.add1 || a.ld_add1 % 8 == 0) && col + 8 <= N;
   float bias8[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bias8[e] = (a.bias && col + e < N) ? a.bias[col + e] : 0.f;
   if (vec_ok) {
-    // issue every residual load of this lane before the first store (C and add1 may not be
-    // proven disjoint by the compiler, which would otherwise serialise load-after-store)
+    // all residual loads of this thread go out before the first store
     uint4 res[ITER];
     if (a.add1 && a.add1_bf16) {
 #pragma unroll
       for (int it = 0; it < ITER; ++it) {
-        const int row = m0 + wm * 64 + (lane + 64 * it) / CPR;
+        const int row = m0 + r0 + it * RPP;
         res[it] = row < M ? *(const uint4*)((const bf16*)a.add1 + (long)row * a.ld_add1 + col) : make_uint4(0, 0, 0, 0);
       }
     }
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
-      const int rl = (lane + 64 * it) / CPR;
-      const int row = m0 + wm * 64 + rl;
+      const int rl = r0 + it * RPP;
+      const int row = m0 + rl;
       if (row >= M) continue;
       float v[8];
       const float4 x0 = *(const float4*)(ep + rl * EPI_LD + cc * 8);
@@ -348,8 +360,8 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
     }
   } else if (col < N) {
     for (int it = 0; it < ITER; ++it) {
-      const int rl = (lane + 64 * it) / CPR;
-      const int row = m0 + wm * 64 + rl;
+      const int rl = r0 + it * RPP;
+      const int row = m0 + rl;
       if (row >= M) continue;
       for (int e = 0; e < 8 && col + e < N; ++e) {
         float x = ep[rl * EPI_LD + cc * 8 + e] + bias8[e];
@@ -364,21 +376,25 @@ __global__ __launch_bounds__(256) void fast_gemm_kernel(FArgs a) {
 __device__ __attribute__((aligned(16))) bf16 g_zero16[64];
 
 // experiment override (tools/bench_conv.py): 0 = automatic
-int g_force_stages = 0, g_force_bn = 0;
+int g_force_stages = 0, g_force_bn = 0, g_force_waves = 0;
 
-template <bool AT, bool BT, int NS>
+template <bool AT, bool BT, int NS, int NW>
 void launch_fast(int bn, dim3 grid, hipStream_t s, const FArgs& a) {
   if constexpr (!AT && !BT) {
-    if (bn == 64) { hipLaunchKernelGGL((fast_gemm_kernel<64, false, false, NS>), grid, dim3(256), 0, s, a); return; }
+    if (bn == 64) { hipLaunchKernelGGL((fast_gemm_kernel<64, false, false, NS, NW>), grid, dim3(NW * 64), 0, s, a); return; }
   }
-  hipLaunchKernelGGL((fast_gemm_kernel<128, AT, BT, NS>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((fast_gemm_kernel<128, AT, BT, NS, NW>), grid, dim3(NW * 64), 0, s, a);
 }
 
 template <bool AT, bool BT>
-void launch_fast_ns(int ns, int bn, dim3 grid, hipStream_t s, const FArgs& a) {
-  if (ns >= 4) launch_fast<AT, BT, 4>(bn, grid, s, a);
-  else if (ns == 3) launch_fast<AT, BT, 3>(bn, grid, s, a);
-  else launch_fast<AT, BT, 2>(bn, grid, s, a);
+void launch_fast_ns(int ns, int nw, int bn, dim3 grid, hipStream_t s, const FArgs& a) {
+  if (nw == 8) {
+    if (ns == 3) launch_fast<AT, BT, 3, 8>(bn, grid, s, a);
+    else launch_fast<AT, BT, 2, 8>(bn, grid, s, a);
+  } else {
+    if (ns == 3) launch_fast<AT, BT, 3, 4>(bn, grid, s, a);
+    else launch_fast<AT, BT, 2, 4>(bn, grid, s, a);
+  }
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -453,16 +469,18 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   }
   dim3 grid(sat_cdiv(g.N, bn), sat_cdiv(g.M, BM), a.splitk);
   const int ns = g_force_stages ? g_force_stages : 2;
-  if (at && bt) launch_fast_ns<true, true>(ns, bn, grid, s, a);
-  else if (at) launch_fast_ns<true, false>(ns, bn, grid, s, a);
-  else if (bt) launch_fast_ns<false, true>(ns, bn, grid, s, a);
-  else launch_fast_ns<false, false>(ns, bn, grid, s, a);
+  const int nw = g_force_waves ? g_force_waves : 8;
+  if (at && bt) launch_fast_ns<true, true>(ns, nw, bn, grid, s, a);
+  else if (at) launch_fast_ns<true, false>(ns, nw, bn, grid, s, a);
+  else if (bt) launch_fast_ns<false, true>(ns, nw, bn, grid, s, a);
+  else launch_fast_ns<false, false>(ns, nw, bn, grid, s, a);
   *err = (int)hipGetLastError();
   return 1;
 }
 
-extern "C" int sat_fast_gemm_set_config(int stages, int bn) {
+extern "C" int sat_fast_gemm_set_config(int stages, int bn, int waves) {
   g_force_stages = stages;
   g_force_bn = bn;
+  g_force_waves = waves;
   return 0;
 }
