@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--seq", type=int, default=27)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=2, help="images in the bounded CPU-baseline sample")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     return ap.parse_args()
 
 
@@ -107,9 +108,10 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
     import sat_amd
     from sat_amd.data import synthetic_captions, synthetic_images
-    from sat_amd.distributed import GradAllReduce
+    from sat_amd.distributed import allreduce_grads
 
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream
     D = 2048 if args.network == "resnet152" else 512
@@ -117,33 +119,73 @@ def main():
     torch.manual_seed(42)          # identical decoder init on every rank
     dec = sat_amd.Decoder(args.vocab, D, tf=True, ado=True, attention=True).to(dev).train()
     opt = sat_amd.Adam(dec.parameters(), lr=1e-4)
-    reducer = GradAllReduce(dec) if world > 1 else None
     g = torch.Generator().manual_seed(1000 + rank)
     B = args.batch
     imgs = synthetic_images(B, generator=g, device=dev)
     caps = synthetic_captions(B, args.seq, args.vocab, generator=g, device=dev)
     torch.cuda.synchronize()
 
-    def step():
+    def fwd_bwd():
         with torch.no_grad():
             feats = enc(imgs)
-        opt.zero_grad()
         preds, alphas = dec(feats, caps)
         loss, metrics = sat_amd.caption_loss(preds, alphas, caps)
         loss.backward()
-        if reducer is not None:
-            reducer.wait()
+        return loss
+
+    # eager warm-up (builds the encoder plan, caches, allocator pools)
+    for _ in range(args.warmup):
+        opt.zero_grad()
+        loss = fwd_bwd()
+        if world > 1:
+            allreduce_grads(dec)
+        opt.step()
+    torch.cuda.synchronize()
+
+    use_graph = not args.no_graph
+    if use_graph:
+        # Two hipGraphs: the encoder trunk (so its kernels can be bracketed with events) and
+        # decoder fwd + loss + BPTT.  Adam and the RCCL all-reduce run eagerly after replay
+        # (Adam's bias corrections are step-dependent host scalars).
+        opt.zero_grad(set_to_none=True)
+        g_enc, g_dec = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_enc):
+            with torch.no_grad():
+                feats_static = enc(imgs)
+        with torch.cuda.graph(g_dec, pool=g_enc.pool()):
+            preds, alphas = dec(feats_static, caps)
+            loss_static, _ = sat_amd.caption_loss(preds, alphas, caps)
+            loss_static.backward()
+        torch.cuda.synchronize()
+
+    enc_events = []
+
+    def step():
+        if use_graph:
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st.record()
+            g_enc.replay()
+            en.record()
+            enc_events.append((st, en))
+            g_dec.replay()
+            loss = loss_static
+        else:
+            opt.zero_grad()
+            loss = fwd_bwd()
+        if world > 1:
+            allreduce_grads(dec)
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
+    for _ in range(2):   # replay warm-up
         step()
+    enc_events.clear()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # conv launches are bracketed with HIP events on the encoder's stream during the timed steps
-    enc.timing = []
+    if not use_graph:
+        enc.timing = []   # eager: bracket every conv launch
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -151,15 +193,22 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    timing, enc.timing = enc.timing, None
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    conv_ms = sum(s.elapsed_time(e) for s, e in timing)
-    flops = conv_flops(enc, B) * args.steps
-    n_launch = len(timing)
-    achieved = sum(flops) / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    per_img_conv = conv_flops(enc, B)
+    if use_graph:
+        enc_ms = sum(s.elapsed_time(e) for s, e in enc_events)
+        n_launch = len(per_img_conv) * args.steps
+        kernel_desc = "encoder trunk hipGraph (155 implicit-GEMM conv launches fast_gemm_kernel<*,0,0,2,8> + pool/layout)"
+    else:
+        enc_ms = sum(s.elapsed_time(e) for s, e in enc.timing)
+        n_launch = len(enc.timing)
+        enc.timing = None
+        kernel_desc = "fast_gemm_kernel<*,0,0,2,8> (implicit-GEMM conv), per-launch events"
+    flops = sum(per_img_conv) * args.steps
+    achieved = flops / (enc_ms * 1e-3) / 1e12 if enc_ms > 0 else 0.0
     loss_v = loss.item()
     if rank == 0:
         out = {
@@ -173,12 +222,12 @@ def main():
             "config": {"workload": f"COCO-shaped {args.network} encoder (bf16 fwd) + attention/tf/ado decoder train "
                                    f"step, V={args.vocab}, T={args.seq}",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": args.seq,
-                       "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "gemm_kernel<bf16,*,*,2,false> (implicit-GEMM conv)",
+                       "parallelism": f"dp{world}", "hip_graph": use_graph},
+            "roofline": {"bound": "mfma", "kernel": kernel_desc,
                          "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
-                         "launches": n_launch, "avg_launch_ms": round(conv_ms / max(1, n_launch), 4),
-                         "algorithmic_flops_per_launch": sum(flops) / max(1, n_launch), "traffic": None},
+                         "launches": n_launch, "avg_launch_ms": round(enc_ms / max(1, n_launch), 4),
+                         "algorithmic_flops_per_launch": flops / max(1, n_launch), "traffic": None},
             "loss": round(loss_v, 4),
         }
         if not args.no_cpu_baseline and world == 1:

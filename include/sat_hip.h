@@ -69,6 +69,9 @@ typedef struct {
   int start_token;            /* 0 = <start> (decoder.py:82); 101 = [CLS] (decoder.py:80) */
   int has_dropout_mask;       /* training: 1 = use the caller's keep-mask, 0 = draw from seed */
   uint64_t seed;
+  /* optional device counter: when set, masks are drawn from (seed ^ *seed_ptr) and the forward
+   * increments *seed_ptr on the stream, so a hipGraph replay draws fresh masks every step. */
+  uint64_t* seed_ptr;
 } SatDecoderDims;
 
 /* Element offsets of every decoder parameter inside one flat fp32 buffer.  Keys

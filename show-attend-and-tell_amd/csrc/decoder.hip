@@ -183,11 +183,12 @@ int head_forward(const Ctx& c, const WS& w, int rows, int t, bool per_step, void
   // dropout(h)
   if (per_step)
     SAT_CHECK((hipError_t)sat_dropout_apply(w.h_out + oE, c.T1 * E, d.B, 1, E, d.training, d.has_dropout_mask,
-                                            mask_in ? mask_in + oE : nullptr, w.dmask + oE, c.T1 * E, d.seed, t,
+                                            mask_in ? mask_in + oE : nullptr, w.dmask + oE, c.T1 * E, d.seed,
+                                            d.seed_ptr, t,
                                             c.at(w.hd_t, oE), c.T1 * E, d.dtype, s));
   else
     SAT_CHECK((hipError_t)sat_dropout_apply(w.h_out, E, d.B, (int)c.T1, E, d.training, d.has_dropout_mask, mask_in,
-                                            w.dmask, E, d.seed, 0, w.hd_t, E, d.dtype, s));
+                                            w.dmask, E, d.seed, d.seed_ptr, 0, w.hd_t, E, d.dtype, s));
   if (d.ado) {
     SAT_CHECK((hipError_t)linear(c, rows, E, E, c.at(w.hd_t, oE), rs * E, c.W(c.lay.fh_w), E, c.F(c.lay.fh_b),
                                  w.fh + oE, rs * E, SAT_F32, SAT_ACT_RELU, s));
@@ -323,6 +324,7 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
     }
   }
   if (d.tf) SAT_CHECK((hipError_t)head_forward(c, w, (int)c.R, 0, false, preds, dropout_mask, s));
+  if (d.training && d.seed_ptr) SAT_CHECK((hipError_t)sat_bump_seed(d.seed_ptr, s));
   if (tokens) SAT_CHECK(hipMemcpyAsync(tokens, w.tok, c.R * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
   return 0;
 }

@@ -105,9 +105,10 @@ __device__ __forceinline__ uint32_t mix32(uint64_t x) {
 // the full-sequence row stride as ld; t_offset is then the step index).
 template <typename T>
 __global__ void dropout_kernel(const float* h, long h_ld, int B, int T1, int E, int training, int has_mask,
-                               const uint8_t* mask_in, uint8_t* mask_out, long mask_ld, uint64_t seed, int t_offset,
-                               T* out, long out_ld) {
+                               const uint8_t* mask_in, uint8_t* mask_out, long mask_ld, uint64_t seed,
+                               const uint64_t* seed_ptr, int t_offset, T* out, long out_ld) {
   const long n = (long)B * T1 * E;
+  if (seed_ptr) seed ^= *seed_ptr * 0xD1B54A32D192ED03ULL;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int e = (int)(i % E);
     const long r = i / E;
@@ -147,6 +148,15 @@ __global__ void ado_combine_kernel(const float* fh, const float* fz, const T* em
     comb[i] = (T)(fh[i] + fz[i] + (float)emb[i]);
 }
 
+__global__ void bump_seed_kernel(uint64_t* p) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *p += 1;
+}
+}  // namespace
+int sat_bump_seed(uint64_t* p, hipStream_t s) {
+  hipLaunchKernelGGL(bump_seed_kernel, dim3(1), dim3(64), 0, s, p);
+  return (int)hipGetLastError();
+}
+namespace {
 __global__ void fill_kernel(float* p, long n, float v) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -201,13 +211,13 @@ int sat_tanh_pair_bwd(const float* d_h, int dh_splits, long dh_split_stride, con
   return (int)hipGetLastError();
 }
 int sat_dropout_apply(const float* h, long h_ld, int B, int T1, int E, int training, int has_mask,
-                      const uint8_t* mask_in, uint8_t* mask_out, long mask_ld, uint64_t seed, int t_offset,
-                      void* out_t, long out_ld, int dtype, hipStream_t s) {
+                      const uint8_t* mask_in, uint8_t* mask_out, long mask_ld, uint64_t seed,
+                      const uint64_t* seed_ptr, int t_offset, void* out_t, long out_ld, int dtype, hipStream_t s) {
   dim3 g(grid_for((long)B * T1 * E));
   if (dtype == SAT_BF16)
-    hipLaunchKernelGGL(dropout_kernel<bf16>, g, dim3(256), 0, s, h, h_ld, B, T1, E, training, has_mask, mask_in, mask_out, mask_ld, seed, t_offset, (bf16*)out_t, out_ld);
+    hipLaunchKernelGGL(dropout_kernel<bf16>, g, dim3(256), 0, s, h, h_ld, B, T1, E, training, has_mask, mask_in, mask_out, mask_ld, seed, seed_ptr, t_offset, (bf16*)out_t, out_ld);
   else
-    hipLaunchKernelGGL(dropout_kernel<float>, g, dim3(256), 0, s, h, h_ld, B, T1, E, training, has_mask, mask_in, mask_out, mask_ld, seed, t_offset, (float*)out_t, out_ld);
+    hipLaunchKernelGGL(dropout_kernel<float>, g, dim3(256), 0, s, h, h_ld, B, T1, E, training, has_mask, mask_in, mask_out, mask_ld, seed, seed_ptr, t_offset, (float*)out_t, out_ld);
   return (int)hipGetLastError();
 }
 int sat_relu_mask_mul(const void* d, const void* ref, long n, int dtype, void* out_t, hipStream_t s) {

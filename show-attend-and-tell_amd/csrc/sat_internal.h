@@ -92,8 +92,9 @@ int sat_lstm_bwd_launch(const LstmBwdArgs& a, hipStream_t s);
 int sat_tanh_pair_bwd(const float* d_h, int dh_splits, long dh_split_stride, const float* d_c, const float* hc0,
                       int B, int E, float* dpre_f32, void* dpre_t, int dtype, hipStream_t s);
 int sat_dropout_apply(const float* h, long h_ld, int B, int T1, int E, int training, int has_mask,
-                      const uint8_t* mask_in, uint8_t* mask_out, long mask_ld, uint64_t seed, int t_offset,
-                      void* out_t, long out_ld, int dtype, hipStream_t s);
+                      const uint8_t* mask_in, uint8_t* mask_out, long mask_ld, uint64_t seed,
+                      const uint64_t* seed_ptr, int t_offset, void* out_t, long out_ld, int dtype, hipStream_t s);
+int sat_bump_seed(uint64_t* p, hipStream_t s);
 int sat_relu_mask_mul(const void* d, const void* ref, long n, int dtype, void* out_t, hipStream_t s);
 int sat_ado_bwd_split(const float* d_comb, const float* fh, const float* fz, long n, int dtype, void* d_fh_t,
                       void* d_fz_t, hipStream_t s);

@@ -100,6 +100,8 @@ class Decoder(nn.Module):
         self._offsets = {}
         self._grad_hooks = []          # callables(phase, decoder): DDP bucket all-reduce
         self.dropout_mask = None       # test hook: uint8 keep-mask [B, T-1, E] used in training mode
+        self._seed_host = None
+        self._seed_dev = None
         self.last_tokens = None        # int32 [B, T-1]: token fed at each step of the last forward
 
     # ------------------------------------------------------------------ layout
@@ -234,7 +236,15 @@ class Decoder(nn.Module):
         d.dtype = L.dtype_code(feats.dtype)
         d.start_token = self.tokenizer.cls_token_id if self.use_bert else 0
         d.has_dropout_mask = int(self.training and self.dropout_mask is not None)
-        d.seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if self.training else 0
+        # dropout masks: host seed drawn once per module from torch's RNG (train.py:37-43 seeding)
+        # XOR a device step counter the forward itself advances -> graph replays draw fresh masks
+        if self.training:
+            if self._seed_host is None:
+                self._seed_host = int(torch.randint(0, 2 ** 62, (1,)).item())
+            if self._seed_dev is None or self._seed_dev.device != feats.device:
+                self._seed_dev = torch.zeros(1, dtype=torch.int64, device=feats.device)
+            d.seed = self._seed_host
+            d.seed_ptr = self._seed_dev.data_ptr()
         return d
 
     def forward(self, img_features, captions):

@@ -48,3 +48,15 @@ def shard_batch(tensor, rank, world):
         raise ValueError(f"global batch {n} not divisible by world size {world}")
     per = n // world
     return tensor[rank * per:(rank + 1) * per]
+
+
+def allreduce_grads(decoder, group=None):
+    """Synchronous mean all-reduce of the decoder's two gradient buckets (used after a hipGraph
+    replay of fwd+bwd, where the in-backward hooks of GradAllReduce cannot run)."""
+    world = dist.get_world_size(group)
+    avg = dist.get_backend(group) == "nccl"
+    for phase in (1, 2):
+        bucket = decoder.grad_bucket(phase)
+        dist.all_reduce(bucket, op=dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM, group=group)
+        if not avg:
+            bucket.div_(world)
