@@ -47,7 +47,7 @@ def conv_flops(enc, B, H=224, W=224):
     """Algorithmic FLOPs of every conv launch of one encoder forward (real Cin, not the padded one)."""
     flops = []
     h, w = H, W
-    for step in enc.compiled_plan(torch.device("cuda"), torch.bfloat16):
+    for step in enc._plan:   # the plan the timed steps ran (built during warm-up)
         if step[0] == "conv":
             wt, _, s, p = step[1]
             co, kh, kw, ci = wt.shape
