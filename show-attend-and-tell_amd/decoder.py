@@ -36,8 +36,10 @@ class BertTokenizerStub:
     pad_token_id = 0
     unk_token_id = 100
 
+    _SPECIAL = {101: "[CLS]", 102: "[SEP]", 0: "[PAD]", 100: "[UNK]"}
+
     def convert_ids_to_tokens(self, ids):
-        return [f"[{i}]" for i in ids]
+        return [self._SPECIAL.get(int(i), f"tok{int(i)}") for i in ids]
 
     def convert_tokens_to_string(self, tokens):
         return " ".join(tokens)
