@@ -1,0 +1,262 @@
+"""Training CLI with the reference's flags (train.py:438-472) on the MI355X path.
+
+    python show-attend-and-tell_amd/train.py --data data/flickr8k --network vgg19 --tf --ado --attention
+    python show-attend-and-tell_amd/train.py --synthetic 512 --network resnet152 --tf --ado --attention
+
+Same flags and defaults as the reference (``--perform-test`` is store_true with default True,
+so it cannot be disabled, as in train.py:450), plus:
+  --synthetic N   N synthetic images (5 captions each is not needed: one caption per row) instead
+                  of the Karpathy-JSON dataset;  --vocab for its vocabulary size
+  --dtype         bf16 (default, performance) | fp32 (exact parity mode)
+  --max-steps     cap batches per epoch (smoke runs)
+Multi-GPU: ``python -m torch.distributed.run --nproc-per-node N show-attend-and-tell_amd/train.py ...``
+(RCCL data parallel; the batch size is per GPU).  W&B logging is not part of this build; the
+reference's scalar names are printed / written as JSON lines instead.
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+if __package__ in (None, ""):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import sat_amd  # noqa: E402
+else:
+    import sat_amd  # noqa: E402
+from sat_amd import bleu as bleu_mod  # noqa: E402
+from sat_amd import distributed as sat_dist  # noqa: E402
+from sat_amd.data import synthetic_captions, synthetic_images  # noqa: E402
+
+MEAN = np.array([0.485, 0.456, 0.406], dtype=np.float32)   # train.py:27-32
+STD = np.array([0.229, 0.224, 0.225], dtype=np.float32)
+
+
+class AverageMeter:
+    """utils.py:4-19"""
+
+    def __init__(self):
+        self.val = self.avg = self.sum = 0
+        self.count = 0
+
+    def update(self, val, n=1):
+        self.val = val
+        self.sum += val * n
+        self.count += n
+        self.avg = self.sum / self.count if self.count else 0
+
+
+class JsonCaptionDataset(torch.utils.data.Dataset):
+    """The reference's on-disk layout (generate_json_data.py:51-63, dataset.py:15-52), loaded
+    lazily per item (the reference decodes every image eagerly into RAM, which does not fit COCO)."""
+
+    def __init__(self, data_path, split_type="train", fraction=1.0, bert=False):
+        self.paths = json.load(open(os.path.join(data_path, f"{split_type}_img_paths.json")))
+        name = f"{split_type}_captions_bert.json" if bert else f"{split_type}_captions.json"
+        self.captions = json.load(open(os.path.join(data_path, name)))
+        if fraction != 1.0:
+            self.paths = self.paths[:int(len(self.paths) * fraction)]
+            self.captions = self.captions[:int(len(self.captions) * fraction)]
+        by_path = {}
+        for p, c in zip(self.paths, self.captions):
+            by_path.setdefault(p, []).append(c)
+        self.all_captions = [by_path[p] for p in self.paths]
+
+    def __len__(self):
+        return len(self.paths)
+
+    def __getitem__(self, i):
+        from PIL import Image
+        with open(self.paths[i], "rb") as f:
+            img = Image.open(f).convert("RGB").resize((224, 224), Image.BILINEAR)
+        x = (np.asarray(img, dtype=np.float32) / 255.0 - MEAN) / STD
+        return torch.from_numpy(x.transpose(2, 0, 1).copy()), torch.tensor(self.captions[i]), \
+            torch.tensor(self.all_captions[i])
+
+
+class SyntheticDataset(torch.utils.data.Dataset):
+    def __init__(self, n, vocab, T, bert, seed):
+        g = torch.Generator().manual_seed(seed)
+        self.caps = synthetic_captions(n, T, vocab, generator=g, bert=bert)
+        self.seed = seed
+
+    def __len__(self):
+        return self.caps.shape[0]
+
+    def __getitem__(self, i):
+        g = torch.Generator().manual_seed(self.seed * 100003 + i)
+        return synthetic_images(1, generator=g)[0], self.caps[i], self.caps[i:i + 1]
+
+
+def set_seed(seed):
+    """train.py:37-43"""
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    random.seed(seed)
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(description="Show, Attend and Tell (MI355X)")
+    p.add_argument("--batch-size", type=int, default=64)
+    p.add_argument("--epochs", type=int, default=10)
+    p.add_argument("--lr", type=float, default=1e-4)
+    p.add_argument("--step-size", type=int, default=5)
+    p.add_argument("--alpha-c", type=float, default=1)
+    p.add_argument("--perform-test", action="store_true", default=True)
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--log-interval", type=int, default=100)
+    p.add_argument("--data", type=str, default="data/coco")
+    p.add_argument("--network", choices=["vgg19", "resnet152", "densenet161"], default="vgg19")
+    p.add_argument("--model", type=str)
+    p.add_argument("--tf", action="store_true", default=False)
+    p.add_argument("--ado", action="store_true", default=False)
+    p.add_argument("--fraction", type=float, default=1.0)
+    p.add_argument("--bert", action="store_true", default=False)
+    p.add_argument("--attention", action="store_true", default=False)
+    # MI355X build
+    p.add_argument("--synthetic", type=int, default=0)
+    p.add_argument("--vocab", type=int, default=10000)
+    p.add_argument("--seq", type=int, default=27)
+    p.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    p.add_argument("--max-steps", type=int, default=0)
+    p.add_argument("--out", type=str, default="model")
+    return p.parse_args(argv)
+
+
+def build(args, device):
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    word_dict = None
+    if args.bert:
+        vocab = sat_amd.Decoder.BERT_VOCAB
+    elif args.synthetic:
+        vocab = args.vocab
+    else:
+        word_dict = json.load(open(os.path.join(args.data, "word_dict.json")))
+        vocab = len(word_dict)
+    encoder = sat_amd.Encoder(args.network, dtype=dt)
+    decoder = sat_amd.Decoder(vocab, encoder.dim, tf=args.tf, ado=args.ado, bert=args.bert, attention=args.attention)
+    if args.model:   # train.py:65-67 (reference checkpoints load unchanged)
+        decoder.load_state_dict(torch.load(args.model, map_location="cpu", weights_only=True))
+    return encoder.to(device).eval(), decoder.to(device), word_dict, dt
+
+
+def loaders(args, split, rank, world):
+    if args.synthetic:
+        ds = SyntheticDataset(args.synthetic if split == "train" else max(args.batch_size, args.synthetic // 8),
+                              args.vocab if not args.bert else sat_amd.Decoder.BERT_VOCAB,
+                              32 if args.bert else args.seq, args.bert, seed=args.seed + hash(split) % 1000)
+    else:
+        ds = JsonCaptionDataset(args.data, split, args.fraction, args.bert)
+    sampler = torch.utils.data.distributed.DistributedSampler(ds, world, rank, shuffle=True) if world > 1 else None
+    return torch.utils.data.DataLoader(ds, batch_size=args.batch_size, shuffle=sampler is None, sampler=sampler,
+                                       num_workers=4 if not args.synthetic else 0, pin_memory=True, drop_last=True)
+
+
+def train_epoch(epoch, encoder, decoder, opt, loader, args, device, dt, world, log):
+    """train.py:119-192"""
+    encoder.eval()
+    decoder.train()
+    pad, skip = sat_amd.special_ids(args.bert)
+    losses, top1, top5 = AverageMeter(), AverageMeter(), AverageMeter()
+    for batch_idx, (imgs, captions, _) in enumerate(loader):
+        if args.max_steps and batch_idx >= args.max_steps:
+            break
+        imgs = imgs.to(device, non_blocking=True)
+        captions = captions.to(device, non_blocking=True)
+        with torch.no_grad():
+            feats = encoder(imgs, dtype=dt)
+        opt.zero_grad()
+        preds, alphas = decoder(feats, captions)
+        loss, metrics = sat_amd.caption_loss(preds, alphas, captions, args.alpha_c, pad, skip)
+        loss.backward()
+        if world > 1:
+            sat_dist.allreduce_grads(decoder)
+        opt.step()
+        if batch_idx % args.log_interval == 0:   # one host read per logged step (reference: 4 per step)
+            m = sat_amd.StepMetrics(loss, metrics).values()
+            n = m["caption_length"]
+            losses.update(m["loss"], n); top1.update(m["acc1"], n); top5.update(m["acc5"], n)
+            log(dict(epoch=epoch, batch=batch_idx, train_loss=losses.avg, train_top1_acc=top1.avg,
+                     train_top5_acc=top5.avg, train_loss_raw=losses.val))
+    return losses.avg
+
+
+def evaluate(epoch, encoder, decoder, loader, args, device, dt, word_dict, mode, log):
+    """train.py:198-347 (teacher-forced greedy hypotheses, BLEU-1..4)."""
+    encoder.eval()
+    decoder.eval()
+    pad, skip = sat_amd.special_ids(args.bert)
+    losses, top1, top5 = AverageMeter(), AverageMeter(), AverageMeter()
+    refs, hyps = [], []
+    tok = decoder.tokenizer if args.bert else None
+    inv = {i: w for w, i in word_dict.items()} if word_dict else None
+    with torch.no_grad():
+        for batch_idx, (imgs, captions, all_caps) in enumerate(loader):
+            if args.max_steps and batch_idx >= args.max_steps:
+                break
+            imgs, captions = imgs.to(device), captions.to(device)
+            preds, alphas = decoder(encoder(imgs, dtype=dt), captions)
+            loss, metrics = sat_amd.caption_loss(preds, alphas, captions, args.alpha_c, pad, skip)
+            m = sat_amd.StepMetrics(loss, metrics).values()
+            n = m["caption_length"]
+            losses.update(m["loss"], n); top1.update(m["acc1"], n); top5.update(m["acc5"], n)
+            ids = preds.argmax(dim=2).cpu().tolist()
+            if args.bert:
+                dec = lambda c: bleu_mod.decode_bert(c, tok)  # noqa: E731
+            elif word_dict:
+                dec = lambda c: bleu_mod.decode_plain(c, word_dict, inv)  # noqa: E731
+            else:
+                dec = lambda c: [str(t) for t in c if t not in (0, 3)][:c.index(1) if 1 in c else None]  # noqa: E731
+            refs += [[dec(c) for c in cs] for cs in all_caps.tolist()]
+            hyps += [dec(c) for c in ids]
+    b1, b2, b3, b4 = bleu_mod.bleu_1_to_4(refs, hyps)
+    log({"epoch": epoch, f"{mode}_loss": losses.avg, f"{mode}_top1_acc": top1.avg, f"{mode}_top5_acc": top5.avg,
+         f"{mode}_bleu1": b1, f"{mode}_bleu2": b2, f"{mode}_bleu3": b3, f"{mode}_bleu4": b4})
+    return b4
+
+
+def main(argv=None):
+    args = parse(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    set_seed(args.seed)
+
+    def log(rec):
+        if rank == 0:
+            print(json.dumps(rec), flush=True)
+
+    encoder, decoder, word_dict, dt = build(args, device)
+    opt = sat_amd.Adam(decoder.parameters(), lr=args.lr)
+    sched = torch.optim.lr_scheduler.StepLR(opt, args.step_size)
+    train_loader = loaders(args, "train", rank, world)
+    val_loader = loaders(args, "val", rank, world)
+    os.makedirs(args.out, exist_ok=True)
+    for epoch in range(1, args.epochs + 1):
+        t0 = time.time()
+        train_epoch(epoch, encoder, decoder, opt, train_loader, args, device, dt, world, log)
+        evaluate(epoch, encoder, decoder, val_loader, args, device, dt, word_dict, "val", log)
+        sched.step()
+        if rank == 0:   # train.py:103-110
+            torch.save(decoder.state_dict(), os.path.join(args.out, f"model_{args.network}_{epoch}.pth"))
+            with open(os.path.join(args.out, "model_config.json"), "w") as f:
+                json.dump(vars(args), f)
+        log({"epoch": epoch, "epoch_seconds": time.time() - t0})
+    if args.perform_test:
+        test_loader = loaders(args, "test", rank, world)
+        evaluate(args.epochs, encoder, decoder, test_loader, args, device, dt, word_dict, "test", log)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

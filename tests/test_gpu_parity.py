@@ -332,3 +332,19 @@ def test_fast_gemm_transposed_operands(sat, M, N, K, transA, transB, beta):
     ops.gemm(Ad, Bd, C, transA=transA, transB=transB, beta=beta)
     torch.cuda.synchronize()
     assert rel(C, ref) < 2e-5
+
+
+def test_train_cli_smoke(sat, tmp_path):
+    """The reference-flag CLI runs end to end (synthetic data, 2 steps/epoch, BLEU eval, checkpoint)."""
+    import json, subprocess, sys, os
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(repo, "show-attend-and-tell_amd", "train.py"),
+                          "--synthetic", "64", "--batch-size", "16", "--epochs", "1", "--max-steps", "2",
+                          "--network", "vgg19", "--tf", "--ado", "--attention", "--vocab", "300",
+                          "--log-interval", "1", "--out", str(tmp_path)], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    recs = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert any("val_bleu4" in r for r in recs) and any("test_bleu4" in r for r in recs)
+    assert (tmp_path / "model_vgg19_1.pth").exists() and (tmp_path / "model_config.json").exists()
+    sd = torch.load(tmp_path / "model_vgg19_1.pth", weights_only=True)
+    assert "lstm.weight_ih" in sd and "f_out.weight" in sd
