@@ -136,6 +136,24 @@ int sat_decoder_backward(const SatDecoderDims* d, const SatDecoderLayout* lay, c
                          const void* d_preds, const float* d_alphas, float* grads, int accumulate,
                          int phase, void* stream);
 
+/* --- beam-search captioning (decoder.py:160-269, Decoder.caption; generate_caption.py:86-88) ---
+ * img_features: DEVICE [beam_size, L, D] (the reference expands one image to beam rows).
+ * Uses d->L, D, E, V, ado, attention, bert, dtype, start_token; d->B, T, tf, training are ignored
+ * (caption() applies no dropout).  Runs up to max_step + 1 decoder steps (the reference: 50),
+ * synchronising `stream` once per step to retire/compact beams, so it is NOT capturable.
+ * Results are written to HOST memory:
+ *   out_ids    [max_step + 2]        best completed sentence incl. the start token
+ *   out_alphas [(max_step + 2) * L]  its alpha rows (first row = ones, as in decoder.py:173)
+ *   out_score                        its summed raw logits; -inf when no beam completed, in which
+ *                                    case out_ids = [0] and out_alphas holds the last step's
+ *                                    *out_alpha_rows alpha rows (decoder.py:256-258).
+ * Requires 1 <= beam_size <= min(64, max_step + 2). */
+size_t sat_decoder_beam_workspace_bytes(const SatDecoderDims* d, int beam_size);
+int sat_decoder_beam_search(const SatDecoderDims* d, const SatDecoderLayout* lay, const float* params,
+                            const void* params_lp, const void* img_features, int beam_size, int max_step,
+                            void* workspace, size_t workspace_bytes, int32_t* out_ids, int* out_len,
+                            float* out_alphas, int* out_alpha_rows, float* out_score, void* stream);
+
 /* --- loss + metrics (train.py:135-162, utils.py:44-80,101-107) ----------- */
 size_t sat_caption_loss_workspace_bytes(int B, int T, int L);
 /* out[0]=loss, [1]=CE, [2]=att-reg, [3]=#top1-correct, [4]=#top5-correct, [5]=#non-pad targets,

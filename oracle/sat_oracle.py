@@ -211,6 +211,66 @@ def decoder_forward(p, img_features, captions, *, tf, ado, attention, bert=False
     return preds, alphas, in_tokens
 
 
+def beam_search(p, img_features, beam_size, *, ado, attention, bert=False, max_step=50):
+    """decoder.py:160-269 (Decoder.caption).  img_features: [beam_size, L, D].
+
+    Returns (sentence ids incl. the start token, alpha rows [len][L] incl. the leading ones row,
+    score) for the best completed beam; ([0], last alpha rows, -inf) when none completed.  Scores
+    are summed RAW logits (decoder.py:204); ties inside topk go to the lower flat index."""
+    L = img_features.shape[1]
+    V = p["embedding.weight"].shape[0]
+    start = SPECIAL_BERT["start"] if bert else SPECIAL_PLAIN["start"]
+    prev_words = torch.full((beam_size,), start, dtype=torch.long)       # decoder.py:166-169
+    sentences = prev_words.unsqueeze(1)
+    top_preds = torch.zeros(beam_size, 1)
+    alphas = torch.ones(beam_size, 1, L)
+    done, done_alpha, done_score = [], [], []
+    h, c = init_lstm_state(p, img_features)
+    feats = img_features
+    step = 1
+    while True:
+        emb = F.embedding(prev_words, p["embedding.weight"])
+        k = feats.shape[0]
+        if attention:
+            context, alpha = attention_forward(p, feats, h)
+            gated = torch.sigmoid(linear(h, p, "f_beta")) * context
+        else:
+            alpha = torch.full((k, L), 1.0 / L)
+            context = feats.mean(dim=1)
+            gated = context
+        h, c = lstm_cell(p, torch.cat((emb, gated), dim=1), h, c)
+        out = advanced_deep_output(p, h, context, emb) if ado else linear(h, p, "deep_output")
+        out = top_preds.expand_as(out) + out                             # decoder.py:204
+        flat = out[0] if step == 1 else out.reshape(-1)
+        # sorted top-k with ties to the lower index: stable sort on -value
+        order = torch.sort(-flat, stable=True).indices[:k]
+        top_vals, top_words = flat[order], order
+        prev_idx, next_idx = top_words // V, top_words % V                  # decoder.py:210-211
+        sentences = torch.cat((sentences[prev_idx], next_idx.unsqueeze(1)), dim=1)
+        alphas = torch.cat((alphas[prev_idx], alpha[prev_idx].unsqueeze(1)), dim=1)
+        ends = (1, 0) if bert else (1, 102)                                 # decoder.py:224-229
+        incomplete = [i for i, w in enumerate(next_idx.tolist()) if w not in ends]
+        complete = sorted(set(range(k)) - set(incomplete))
+        for i in complete:
+            done.append(sentences[i].tolist())
+            done_alpha.append(alphas[i].tolist())
+            done_score.append(float(top_vals[i]))
+        if len(incomplete) == 0:
+            break
+        sentences, alphas = sentences[incomplete], alphas[incomplete]
+        sel = prev_idx[incomplete]
+        h, c, feats = h[sel], c[sel], feats[sel]
+        top_preds = top_vals[incomplete].unsqueeze(1)
+        prev_words = next_idx[incomplete]
+        if step > max_step:
+            break
+        step += 1
+    if not done:
+        return [0], alpha.tolist(), float("-inf")
+    best = done_score.index(max(done_score))
+    return done[best], done_alpha[best], done_score[best]
+
+
 # ----------------------------------------------------------------------------
 # Loss, metrics, optimiser (train.py, utils.py, torch.optim.Adam)
 # ----------------------------------------------------------------------------

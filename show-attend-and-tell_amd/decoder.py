@@ -257,6 +257,46 @@ class Decoder(nn.Module):
         params = [p for n, p in self.named_parameters()]
         return _DecoderFn.apply(img_features.contiguous(), captions.contiguous().long(), self, *params)
 
+    def caption(self, img_features, beam_size, max_step=50):
+        """Beam search (decoder.py:160-269) as one C-ABI call (sat_decoder_beam_search).
+
+        ``img_features`` [beam_size, L, D] (one image expanded, generate_caption.py:87).  Returns
+        ``(sentence, alpha)``: word ids including the start token and the alpha rows (a list of
+        lists, first row all ones) of the best completed beam; like the reference it prints a
+        notice and returns ``[0]`` and the last step's alpha rows when no beam completed."""
+        import numpy as np
+        L.require_device(img_features)
+        feats = img_features.contiguous()
+        if feats.dim() != 3 or feats.shape[0] != beam_size:
+            raise ValueError(f"img_features must be [beam_size={beam_size}, L, D], got {tuple(feats.shape)}")
+        self._ensure_flat(feats.device)
+        if feats.dtype == torch.bfloat16:
+            self._ensure_lp()
+        dims = self._dims(feats, torch.empty(1, 3, dtype=torch.long))
+        dims.training = 0
+        lay = self._layout()
+        lib = L.lib()
+        ws_bytes = lib.sat_decoder_beam_workspace_bytes(ctypes.byref(dims), int(beam_size))
+        if ws_bytes == 0:
+            raise RuntimeError("sat_amd.Decoder.caption: unsupported shape / beam size (1..64)")
+        ws = torch.empty(ws_bytes, device=feats.device, dtype=torch.uint8)
+        cap = max_step + 2
+        ids = np.zeros(cap, dtype=np.int32)
+        alphas = np.zeros(cap * dims.L, dtype=np.float32)
+        n_ids, n_rows, score = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_float(0)
+        lp = self._flat_lp if dims.dtype == L.SAT_BF16 else None
+        L.check(lib.sat_decoder_beam_search(ctypes.byref(dims), ctypes.byref(lay), L.ptr(self._flat), L.ptr(lp),
+                                            L.ptr(feats), int(beam_size), int(max_step), L.ptr(ws), ws_bytes,
+                                            ids.ctypes.data, ctypes.byref(n_ids), alphas.ctypes.data,
+                                            ctypes.byref(n_rows), ctypes.byref(score), L.stream_of(feats)),
+                "sat_decoder_beam_search")
+        self.last_caption_score = score.value
+        alpha = alphas[:n_rows.value * dims.L].reshape(n_rows.value, dims.L)
+        if score.value == float("-inf"):
+            print("No completed sentences found")
+            return [0], torch.from_numpy(alpha.copy())
+        return ids[:n_ids.value].tolist(), alpha.tolist()
+
     def get_init_lstm_state(self, img_features):
         """decoder.py:137-147 on HIP GEMMs (inference helper)."""
         from .ops import linear

@@ -37,3 +37,27 @@ def masks_for(cfg):
 
 def t(x):
     return torch.from_numpy(np.asarray(x))
+
+
+def beam_paths():
+    return sorted(glob.glob(os.path.join(GOLDEN, "beam_*.npz")))
+
+
+def beam_ids():
+    return [os.path.basename(p)[len("beam_"):-4] for p in beam_paths()]
+
+
+def load_beam(path):
+    """Beam fixture (make_golden_beam.py) + its regenerated weights (end-token bias applied)."""
+    from oracle import sat_oracle as O
+    z = np.load(path, allow_pickle=False)
+    d = {k: z[k] for k in z.files}
+    cfg = d["cfg"] = json.loads(str(d["meta"]))
+    p = O.make_decoder_params(cfg["V"], cfg["D"], cfg["E"], cfg["ado"], cfg["seed"], scale=cfg["scale"])
+    head_b = "f_out.bias" if cfg["ado"] else "deep_output.bias"
+    for i in cfg["eos_ids"]:
+        if i < cfg["V"]:
+            p[head_b][i] += cfg["eos_bias"]
+    d["params"] = p
+    d["feats"] = torch.from_numpy(d["img_features"]).expand(cfg["beam"], cfg["L"], cfg["D"]).contiguous()
+    return d

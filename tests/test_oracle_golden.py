@@ -83,3 +83,20 @@ def test_resnet152_shapes_and_params():
     x = torch.randn(1, 3, 64, 64)
     assert O.resnet152_forward(p, x).shape == (1, 4, 2048)
     assert O.vgg19_forward(O.make_vgg19_params(0), x).shape == (1, 16, 512)
+
+
+@pytest.mark.parametrize("path", __import__("golden_util").beam_paths(), ids=__import__("golden_util").beam_ids())
+def test_oracle_beam_search(path):
+    """oracle.beam_search == reference Decoder.caption (decoder.py:160-269) on the golden cases."""
+    from golden_util import load_beam
+    g = load_beam(path)
+    cfg = g["cfg"]
+    with torch.no_grad():
+        ids, al, score = O.beam_search(g["params"], g["feats"], cfg["beam"], ado=cfg["ado"],
+                                       attention=cfg["attention"], bert=cfg["bert"])
+    assert ids == g["sentence"].tolist()
+    np.testing.assert_allclose(np.array(al, dtype=np.float32), g["alphas"], rtol=1e-5, atol=1e-6)
+    if math.isinf(float(g["score"])):
+        assert math.isinf(score)
+    else:
+        assert abs(score - float(g["score"])) <= 1e-5 * max(1.0, abs(score))
