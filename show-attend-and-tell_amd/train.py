@@ -133,8 +133,10 @@ def build(args, device):
     word_dict = None
     if args.bert:
         vocab = sat_amd.Decoder.BERT_VOCAB
-    elif args.synthetic:
+    elif args.synthetic:   # generate_json_data.py:45-48 special ids + placeholder words
         vocab = args.vocab
+        word_dict = {"<start>": 0, "<eos>": 1, "<unk>": 2, "<pad>": 3}
+        word_dict.update({f"w{i}": i for i in range(4, vocab)})
     else:
         word_dict = json.load(open(os.path.join(args.data, "word_dict.json")))
         vocab = len(word_dict)
@@ -248,8 +250,13 @@ def main(argv=None):
         sched.step()
         if rank == 0:   # train.py:103-110
             torch.save(decoder.state_dict(), os.path.join(args.out, f"model_{args.network}_{epoch}.pth"))
+            cfg = dict(vars(args))
+            if args.synthetic and word_dict:   # generate_caption.py reads <data>/word_dict.json
+                cfg["data"] = args.out
+                with open(os.path.join(args.out, "word_dict.json"), "w") as f:
+                    json.dump(word_dict, f)
             with open(os.path.join(args.out, "model_config.json"), "w") as f:
-                json.dump(vars(args), f)
+                json.dump(cfg, f)
         log({"epoch": epoch, "epoch_seconds": time.time() - t0})
     if args.perform_test:
         test_loader = loaders(args, "test", rank, world)

@@ -89,3 +89,23 @@ def test_synthetic_caption_layout():
         assert 8 <= eos - 1 <= 25
     bert = synthetic_captions(4, 32, 30522, torch.Generator().manual_seed(0), bert=True)
     assert (bert[:, 0] == 101).all() and (bert[:, -1] == 102).all()
+
+
+def test_cli_flags_mirror_reference():
+    """train.py:438-472 and generate_caption.py:153-160 flags parse with the reference defaults."""
+    import importlib.util, os
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "show-attend-and-tell_amd")
+    spec = importlib.util.spec_from_file_location("sat_train_cli", os.path.join(pkg, "train.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    a = m.parse([])
+    assert (a.batch_size, a.epochs, a.lr, a.step_size, a.alpha_c, a.seed, a.log_interval) == (64, 10, 1e-4, 5, 1, 42, 100)
+    assert (a.data, a.network, a.tf, a.ado, a.fraction, a.bert, a.attention, a.perform_test) == \
+        ("data/coco", "vgg19", False, False, 1.0, False, False, True)
+    a = m.parse(["--tf", "--ado", "--attention", "--network", "resnet152"])
+    assert a.tf and a.ado and a.attention and a.network == "resnet152"
+    spec = importlib.util.spec_from_file_location("sat_gen_cli", os.path.join(pkg, "generate_caption.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    with pytest.raises(SystemExit):
+        g.main(["--img-path", "x.png", "--wandb-run", "a/b/c", "--wandb-model", "m"])

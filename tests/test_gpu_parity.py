@@ -396,3 +396,24 @@ def test_beam_search_bf16_and_bench_shape(sat):
         assert torch.allclose(a[1:].sum(1), torch.ones(a.shape[0] - 1), atol=1e-3)
     s32, a32 = dec.caption(feats.float(), 3)
     assert 1 <= len(s32) <= 52 and len(a32) == len(s32) or dec.last_caption_score == float("-inf")
+
+
+def test_generate_caption_cli(sat, tmp_path):
+    """train.py checkpoint + model_config.json -> generate_caption.py beam search on a PNG."""
+    import json, subprocess, sys, os
+    from PIL import Image
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(repo, "show-attend-and-tell_amd")
+    r = subprocess.run([sys.executable, os.path.join(pkg, "train.py"), "--synthetic", "32", "--batch-size", "16",
+                        "--epochs", "1", "--max-steps", "1", "--network", "vgg19", "--ado", "--attention",
+                        "--vocab", "200", "--out", str(tmp_path)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    img = tmp_path / "img.png"
+    Image.fromarray((np.random.default_rng(0).random((300, 260, 3)) * 255).astype(np.uint8)).save(img)
+    r = subprocess.run([sys.executable, os.path.join(pkg, "generate_caption.py"), "--img-path", str(img),
+                        "--model", str(tmp_path / "model_vgg19_1.pth"), "--plot", str(tmp_path / "att.png")],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["ids"][0] == 0 and out["caption"].split()[0] == "<start>"
+    assert (tmp_path / "att.png").exists()
