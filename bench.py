@@ -73,6 +73,17 @@ def conv_flops(enc, B, H=224, W=224):
     return flops
 
 
+def pmc_traffic(network):
+    """HBM bytes per conv launch from the committed PMC passes (tools/pmc_traffic.py; a PMC run
+    cannot share a process with the timed bench), or None when none was collected for this trunk."""
+    path = os.path.join(REPO, "profiles", f"pmc_traffic_{network}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        rec = json.load(f)
+    return rec.get("hbm_bytes_per_conv_launch"), os.path.relpath(path, REPO)
+
+
 def cpu_baseline(args):
     """Bounded CPU sample of the same step through the oracle (torch-CPU fp32 port)."""
     from oracle import sat_oracle as O
@@ -210,6 +221,7 @@ def main():
     flops = sum(per_img_conv) * args.steps
     achieved = flops / (enc_ms * 1e-3) / 1e12 if enc_ms > 0 else 0.0
     loss_v = loss.item()
+    traffic, t_src = pmc_traffic(args.network)
     if rank == 0:
         out = {
             "metric": "train images/sec on COCO batch=128 at 1/2/4/8 MI355X",
@@ -227,7 +239,8 @@ def main():
                          "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
                          "launches": n_launch, "avg_launch_ms": round(enc_ms / max(1, n_launch), 4),
-                         "algorithmic_flops_per_launch": flops / max(1, n_launch), "traffic": None},
+                         "algorithmic_flops_per_launch": flops / max(1, n_launch),
+                         "traffic": traffic, "traffic_unit": "HBM bytes per conv launch", "traffic_source": t_src},
             "loss": round(loss_v, 4),
         }
         if not args.no_cpu_baseline and world == 1:
