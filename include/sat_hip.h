@@ -90,9 +90,10 @@ int sat_abi_version(void);
 const char* sat_error_string(int code);
 
 /* --- generic building blocks -------------------------------------------- */
-/* tuning hook for the bf16 LDS-DMA GEMM: LDS ring depth (2|3), N tile (64|128), waves per block
- * (4|8); 0 = automatic. */
-int sat_fast_gemm_set_config(int stages, int bn, int waves);
+/* tuning hook for the bf16 LDS-DMA GEMM (process-global): LDS ring depth (0 = auto | 2 | 3), tile
+ * configuration (0 = auto, 1 = 128x128 / 8 waves, 2 = 128x64 / 8, 3 = 128x128 / 4, 4 = 128x256 / 8,
+ * 5 = 256x128 / 8; k-major operands use 1 or 3), XCD-aware tile order (0 | 1, default 1). */
+int sat_fast_gemm_set_config(int stages, int tile, int xcd_remap);
 int sat_gemm(const SatGemmArgs* args, void* stream);
 /* elementwise cast between SAT_F32 and SAT_BF16 storage (n elements). */
 int sat_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, void* stream);

@@ -23,7 +23,7 @@
 
 namespace {
 
-constexpr int BM = 128, BK = 64, ROWB = BK * 2;   // 128-byte LDS rows
+constexpr int BK = 64, ROWB = BK * 2;   // 128-byte LDS rows
 
 struct FArgs {
   int M, N, K;
@@ -37,6 +37,7 @@ struct FArgs {
   int amode, H, W, Cin, KW, stride, pad, OH, OW;
   const bf16* zero16;
   int splitk, kchunk;      // atomic split-K (fp32 C, act NONE): blockIdx.z = split
+  int xcd_remap;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -92,14 +93,17 @@ __device__ __forceinline__ void wait_vm_barrier() {
   else static_assert(N < 0, "unsupported vmcnt");
 }
 
-template <int BN, bool AT, bool BT, int NS, int NW>
-__global__ __launch_bounds__(NW * 64) void fast_gemm_kernel(FArgs a) {
-  constexpr int WCOLS = NW / 2;                       // waves along N (2 along M, 64 rows each)
-  constexpr int WN = BN / WCOLS, NJ = WN / 16, MI = 4;
+// Tile configurations: BM x BN block tile, WGM x WGN waves (wave tile BM/WGM x BN/WGN).
+template <int BM, int BN, int WGM, int WGN, bool AT, bool BT, int NS>
+__global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
+  constexpr int NW = WGM * WGN;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int MI = WTM / 16, NJ = WTN / 16;
   constexpr int STAGE_A = BM * ROWB, STAGE_B = BN * ROWB, STAGE = STAGE_A + STAGE_B;
-  constexpr int A_INSTR = 16 / NW;                    // 1 KiB DMA instructions per wave per stage
+  constexpr int A_INSTR = AT ? 16 / NW : BM / (8 * NW);   // 1 KiB DMA instructions per wave per stage
   constexpr int B_INSTR = BT ? 16 / NW : BN / (8 * NW);
-  static_assert(A_INSTR >= 1 && B_INSTR >= 1 && NJ >= 1, "tile/wave mismatch");
+  static_assert(A_INSTR >= 1 && B_INSTR >= 1 && MI >= 1 && NJ >= 1, "tile/wave mismatch");
+  static_assert(!(AT || BT) || (BM == 128 && BN == 128), "k-major operands need 128-wide tiles");
   constexpr int INSTR = A_INSTR + B_INSTR;
   constexpr int EPI_LD = BN + 4;
   constexpr int EPI_BYTES = BM * EPI_LD * 4;
@@ -108,8 +112,16 @@ __global__ __launch_bounds__(NW * 64) void fast_gemm_kernel(FArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w / WCOLS, wn = w % WCOLS;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int wm = w / WGN, wn = w % WGN;
+  // XCD-aware tile order (cdna_hip_programming.md T1, bijective form): dispatch round-robins
+  // consecutive workgroups over the 8 XCDs; give each XCD a contiguous run of row-major tiles so
+  // the blocks sharing an A row-panel share one L2.
+  int tile = blockIdx.y * gridDim.x + blockIdx.x;
+  if (a.xcd_remap) {
+    const int nwg = gridDim.x * gridDim.y, q = nwg / 8, r = nwg % 8, x = tile % 8;
+    tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
+  }
+  const int m0 = (tile / gridDim.x) * BM, n0 = (tile % gridDim.x) * BN;
   const int M = a.M, N = a.N;
   const int split = blockIdx.z;
   const int kbeg = split * a.kchunk;
@@ -230,18 +242,18 @@ __global__ __launch_bounds__(NW * 64) void fast_gemm_kernel(FArgs a) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         if constexpr (AT) {
-          af[i] = frag_tr(sa, ks * 32, wm * 64 + i * 16, lane);
+          af[i] = frag_tr(sa, ks * 32, wm * WTM + i * 16, lane);
         } else {
-          const int r = wm * 64 + i * 16 + fr;
+          const int r = wm * WTM + i * 16 + fr;
           af[i] = *(const bf16x8*)(sa + r * ROWB + 16 * ((ks * 4 + fh) ^ ((r >> 1) & 7)));
         }
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         if constexpr (BT) {
-          bfr[j] = frag_tr(sb, ks * 32, wn * WN + j * 16, lane);
+          bfr[j] = frag_tr(sb, ks * 32, wn * WTN + j * 16, lane);
         } else {
-          const int r = wn * WN + j * 16 + fr;
+          const int r = wn * WTN + j * 16 + fr;
           bfr[j] = *(const bf16x8*)(sb + r * ROWB + 16 * ((ks * 4 + fh) ^ ((r >> 1) & 7)));
         }
       }
@@ -280,12 +292,12 @@ __global__ __launch_bounds__(NW * 64) void fast_gemm_kernel(FArgs a) {
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int col = n0 + wn * WN + j * 16 + fr;
+        const int col = n0 + wn * WTN + j * 16 + fr;
         if (col >= N) continue;
         const float bcol = (split == 0 && a.bias) ? a.bias[col] : 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm * 64 + i * 16 + fh * 4 + r;
+          const int row = m0 + wm * WTM + i * 16 + fh * 4 + r;
           if (row < M) atomicAdd((float*)a.C + (long)row * a.ldc + col, acc[i][j][r] + bcol);
         }
       }
@@ -300,7 +312,7 @@ __global__ __launch_bounds__(NW * 64) void fast_gemm_kernel(FArgs a) {
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        ep[(wm * 64 + i * 16 + fh * 4 + r) * EPI_LD + wn * WN + j * 16 + fr] = acc[i][j][r];
+        ep[(wm * WTM + i * 16 + fh * 4 + r) * EPI_LD + wn * WTN + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
   constexpr int CPR = BN / 8;                  // 8-column chunks per tile row
   constexpr int RPP = NW * 64 / CPR;           // rows per pass
@@ -375,25 +387,33 @@ __global__ __launch_bounds__(NW * 64) void fast_gemm_kernel(FArgs a) {
 
 __device__ __attribute__((aligned(16))) bf16 g_zero16[64];
 
-// experiment override (tools/bench_conv.py): 0 = automatic
-int g_force_stages = 0, g_force_bn = 0, g_force_waves = 0;
+// experiment overrides (tools/bench_conv.py): 0 = automatic
+int g_force_stages = 0, g_force_tile = 0, g_xcd_remap = 1;
 
-template <bool AT, bool BT, int NS, int NW>
-void launch_fast(int bn, dim3 grid, hipStream_t s, const FArgs& a) {
-  if constexpr (!AT && !BT) {
-    if (bn == 64) { hipLaunchKernelGGL((fast_gemm_kernel<64, false, false, NS, NW>), grid, dim3(NW * 64), 0, s, a); return; }
-  }
-  hipLaunchKernelGGL((fast_gemm_kernel<128, AT, BT, NS, NW>), grid, dim3(NW * 64), 0, s, a);
+// tile configurations (ids of sat_fast_gemm_set_config)
+enum { T_AUTO = 0, T128x128W8 = 1, T128x64W8 = 2, T128x128W4 = 3, T128x256W8 = 4, T256x128W8 = 5 };
+inline int tile_bm(int t) { return t == T256x128W8 ? 256 : 128; }
+inline int tile_bn(int t) { return t == T128x64W8 ? 64 : t == T128x256W8 ? 256 : 128; }
+
+template <int BM, int BN, int WGM, int WGN, bool AT, bool BT>
+void launch_ns(int ns, dim3 grid, hipStream_t s, const FArgs& a) {
+  if (ns == 3) hipLaunchKernelGGL((fast_gemm_kernel<BM, BN, WGM, WGN, AT, BT, 3>), grid, dim3(WGM * WGN * 64), 0, s, a);
+  else hipLaunchKernelGGL((fast_gemm_kernel<BM, BN, WGM, WGN, AT, BT, 2>), grid, dim3(WGM * WGN * 64), 0, s, a);
 }
 
 template <bool AT, bool BT>
-void launch_fast_ns(int ns, int nw, int bn, dim3 grid, hipStream_t s, const FArgs& a) {
-  if (nw == 8) {
-    if (ns == 3) launch_fast<AT, BT, 3, 8>(bn, grid, s, a);
-    else launch_fast<AT, BT, 2, 8>(bn, grid, s, a);
+void launch_tile(int t, int ns, dim3 grid, hipStream_t s, const FArgs& a) {
+  if constexpr (AT || BT) {
+    if (t == T128x128W4) launch_ns<128, 128, 2, 2, AT, BT>(ns, grid, s, a);
+    else launch_ns<128, 128, 2, 4, AT, BT>(ns, grid, s, a);
   } else {
-    if (ns == 3) launch_fast<AT, BT, 3, 4>(bn, grid, s, a);
-    else launch_fast<AT, BT, 2, 4>(bn, grid, s, a);
+    switch (t) {
+      case T128x64W8: launch_ns<128, 64, 2, 4, false, false>(ns, grid, s, a); break;
+      case T128x128W4: launch_ns<128, 128, 2, 2, false, false>(ns, grid, s, a); break;
+      case T128x256W8: launch_ns<128, 256, 2, 4, false, false>(2, grid, s, a); break;
+      case T256x128W8: launch_ns<256, 128, 4, 2, false, false>(2, grid, s, a); break;
+      default: launch_ns<128, 128, 2, 4, false, false>(ns, grid, s, a); break;
+    }
   }
 }
 
@@ -415,9 +435,11 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   if (!bt && (g.K % 8 || g.ldb % 8)) return 0;
   if (g.bias && !al16(g.bias)) return 0;
   if (g.add1 && !al16(g.add1)) return 0;
-  int bn = (g.N <= 64 && !at && !bt) ? 64 : 128;
-  if (g_force_bn && !at && !bt) bn = g_force_bn;
-  const long tiles = (long)sat_cdiv(g.M, BM) * sat_cdiv(g.N, bn);
+  int tcfg = (g.N <= 64 && !at && !bt) ? T128x64W8 : T128x128W8;
+  if (g_force_tile) tcfg = g_force_tile;
+  if ((at || bt) && tcfg != T128x128W4) tcfg = T128x128W8;
+  const int bm = tile_bm(tcfg), bn = tile_bn(tcfg);
+  const long tiles = (long)sat_cdiv(g.M, bm) * sat_cdiv(g.N, bn);
   // atomic split-K for weight-gradient-like problems (long K, few tiles, fp32 output)
   int splitk = 1;
   const bool can_split = g.c_dtype == SAT_F32 && g.act == SAT_ACT_NONE && !g.add1 && (g.beta == 0.f || g.beta == 1.f) && !conv;
@@ -467,20 +489,21 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
     a.H = g.conv.H; a.W = g.conv.W; a.Cin = g.conv.C; a.KW = g.conv.KW;
     a.stride = g.conv.stride; a.pad = g.conv.pad; a.OH = g.conv.OH; a.OW = g.conv.OW;
   }
-  dim3 grid(sat_cdiv(g.N, bn), sat_cdiv(g.M, BM), a.splitk);
+  a.xcd_remap = g_xcd_remap;
+  dim3 grid(sat_cdiv(g.N, bn), sat_cdiv(g.M, bm), a.splitk);
   const int ns = g_force_stages ? g_force_stages : 2;
-  const int nw = g_force_waves ? g_force_waves : 8;
-  if (at && bt) launch_fast_ns<true, true>(ns, nw, bn, grid, s, a);
-  else if (at) launch_fast_ns<true, false>(ns, nw, bn, grid, s, a);
-  else if (bt) launch_fast_ns<false, true>(ns, nw, bn, grid, s, a);
-  else launch_fast_ns<false, false>(ns, nw, bn, grid, s, a);
+  if (at && bt) launch_tile<true, true>(tcfg, ns, grid, s, a);
+  else if (at) launch_tile<true, false>(tcfg, ns, grid, s, a);
+  else if (bt) launch_tile<false, true>(tcfg, ns, grid, s, a);
+  else launch_tile<false, false>(tcfg, ns, grid, s, a);
   *err = (int)hipGetLastError();
   return 1;
 }
 
-extern "C" int sat_fast_gemm_set_config(int stages, int bn, int waves) {
+extern "C" int sat_fast_gemm_set_config(int stages, int tile, int xcd_remap) {
+  if (stages < 0 || stages > 3 || stages == 1 || tile < 0 || tile > T256x128W8) return SAT_ERR_INVALID;
   g_force_stages = stages;
-  g_force_bn = bn;
-  g_force_waves = waves;
+  g_force_tile = tile;
+  g_xcd_remap = xcd_remap != 0;
   return 0;
 }

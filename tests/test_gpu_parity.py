@@ -417,3 +417,52 @@ def test_generate_caption_cli(sat, tmp_path):
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["ids"][0] == 0 and out["caption"].split()[0] == "<start>"
     assert (tmp_path / "att.png").exists()
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("xcd", [0, 1])
+@pytest.mark.parametrize("N,C,H,Cout,k,stride,pad", [(8, 64, 28, 256, 3, 1, 1), (6, 256, 14, 200, 1, 1, 0),
+                                                     (4, 8, 40, 64, 7, 2, 3)])
+def test_fast_conv_tile_configs(sat, tile, xcd, N, C, H, Cout, k, stride, pad):
+    """Every tile configuration of the LDS-DMA kernel (sat_fast_gemm_set_config) with and without
+    the XCD tile remap, including M/N tails and the per-lane-tap stem mode."""
+    from sat_amd import ops
+    lib = sat._lib.lib()
+    g = torch.Generator().manual_seed(N * C + Cout + k + tile)
+    x = torch.randn(N, C, H, H, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, C, k, k, generator=g) / math.sqrt(C * k * k)).bfloat16().float()
+    b = torch.randn(Cout, generator=g)
+    ref = F.conv2d(x, w, b, stride=stride, padding=pad)
+    res = torch.randn_like(ref).bfloat16().float()
+    ref_r = torch.relu(ref + res)
+    xd = x.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    wd = w.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    rd = res.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    assert lib.sat_fast_gemm_set_config(2, tile, xcd) == 0
+    try:
+        y = ops.conv2d_nhwc(xd, wd, b.to(DEV), stride, pad, True, residual=rd)
+        torch.cuda.synchronize()
+    finally:
+        lib.sat_fast_gemm_set_config(0, 0, 1)
+    y = y.float().permute(0, 3, 1, 2).cpu()
+    assert ((y - ref_r).abs() <= 1e-2 * ref_r.abs() + 2e-2).all()
+
+
+@pytest.mark.parametrize("tile", [1, 3, 4, 5])
+def test_fast_gemm_tile_configs_fp32_out(sat, tile):
+    from sat_amd import ops
+    lib = sat._lib.lib()
+    g = torch.Generator().manual_seed(tile)
+    M, N, K = 1100, 700, 576
+    A = torch.randn(M, K, generator=g).bfloat16()
+    Bm = torch.randn(N, K, generator=g).bfloat16()
+    bias = torch.randn(N, generator=g)
+    ref = A.double() @ Bm.double().T + bias.double()
+    C = torch.empty(M, N, device=DEV)
+    assert lib.sat_fast_gemm_set_config(3 if tile in (1, 3) else 2, tile, 1) == 0
+    try:
+        ops.gemm(A.to(DEV), Bm.to(DEV), C, bias=bias.to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        lib.sat_fast_gemm_set_config(0, 0, 1)
+    assert rel(C, ref) < 2e-5

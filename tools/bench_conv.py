@@ -1,4 +1,4 @@
-"""A/B the bf16 LDS-DMA conv kernel configs (ring depth x N tile) on the ResNet152 conv shapes (B=128).
+"""A/B the bf16 LDS-DMA conv kernel configs (ring depth x tile x XCD remap) on the ResNet152 conv shapes (B=128).
 Interleaved rounds in one process (cdna_hip_programming.md 5.4 rule 24); median of rounds."""
 import os, sys, statistics
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -13,7 +13,9 @@ SHAPES = [("L1_c1", 56, 256, 64, 1, 1, 0, 0), ("L1_c2", 56, 64, 64, 3, 1, 1, 0),
           ("L2_c2", 28, 128, 128, 3, 1, 1, 0), ("L2_c3", 28, 128, 512, 1, 1, 0, 1), ("L2_c1", 28, 512, 128, 1, 1, 0, 0),
           ("L3_c1", 14, 1024, 256, 1, 1, 0, 0), ("L3_c2", 14, 256, 256, 3, 1, 1, 0), ("L3_c3", 14, 256, 1024, 1, 1, 0, 1),
           ("L4_c2", 7, 512, 512, 3, 1, 1, 0), ("stem", 224, 8, 64, 7, 2, 3, 0)]
-CONFIGS = [(2, 0, 4), (2, 64, 4), (2, 0, 8), (2, 64, 8)]
+# (stages, tile, xcd_remap); tile ids: 1 128x128/8w, 2 128x64/8w, 3 128x128/4w, 4 128x256/8w, 5 256x128/8w
+CONFIGS = [(2, 1, 0), (2, 1, 1), (3, 1, 1), (2, 2, 1), (2, 3, 1), (2, 4, 1), (2, 5, 1)]
+TNAME = {1: "128x128w8", 2: "128x64w8", 3: "128x128w4", 4: "128x256w8", 5: "256x128w8"}
 lib = sat_amd._lib.lib()
 res = {}
 for name, H, C, Co, k, s, p, r in SHAPES:
@@ -35,9 +37,9 @@ for name, H, C, Co, k, s, p, r in SHAPES:
                 ops.conv2d_nhwc(x, w, b, s, p, True, residual=resid, out=y)
             en.record(); en.synchronize()
             times[cfg].append(st.elapsed_time(en) / 5)
-    lib.sat_fast_gemm_set_config(0, 0, 0)
+    lib.sat_fast_gemm_set_config(0, 0, 1)
     line = f"{name:6s} M={B*OH*OH:7d} N={Co:5d} K={k*k*C:5d} "
     for cfg in CONFIGS:
         ms = statistics.median(times[cfg])
-        line += f" s{cfg[0]}n{cfg[1] or 128}w{cfg[2]}:{ms*1e3:6.1f}us/{flops/ms/1e9:4.0f}TF"
+        line += f" {TNAME[cfg[1]]}/s{cfg[0]}/x{cfg[2]}:{ms*1e3:6.1f}us/{flops/ms/1e9:4.0f}TF"
     print(line, flush=True)
