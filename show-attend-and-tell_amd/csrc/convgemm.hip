@@ -38,6 +38,7 @@ struct FArgs {
   const bf16* zero16;
   int splitk, kchunk;      // atomic split-K (fp32 C, act NONE): blockIdx.z = split
   int xcd_remap;
+  int partial; long split_stride;   // partial-output split-K: split s stores plain into C + s*split_stride
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
   }
   __syncthreads();   // every wave done reading the ring before the epilogue reuses the LDS
 
-  if (a.splitk > 1) {   // atomic split-K: fp32 C, bias in split 0, act NONE (host-checked)
+  if (a.splitk > 1 && !a.partial) {   // atomic split-K: fp32 C, bias in split 0, act NONE (host-checked)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -321,9 +322,11 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
   const int cc = tid2 % CPR, r0 = tid2 / CPR;
   const int col = n0 + cc * 8;
   const bool vec_ok = (a.ldc % 8 == 0) && (!a.add1 || a.ld_add1 % 8 == 0) && col + 8 <= N;
+  void* const Cb = a.partial ? (void*)((float*)a.C + split * a.split_stride) : a.C;
+  const float* const bias = (a.partial && split > 0) ? nullptr : a.bias;
   float bias8[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bias8[e] = (a.bias && col + e < N) ? a.bias[col + e] : 0.f;
+  for (int e = 0; e < 8; ++e) bias8[e] = (bias && col + e < N) ? bias[col + e] : 0.f;
   if (vec_ok) {
     // all residual loads of this thread go out before the first store
     uint4 res[ITER];
@@ -363,9 +366,9 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
         bf16* h = (bf16*)&u;
 #pragma unroll
         for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
-        *(uint4*)((bf16*)a.C + (long)row * a.ldc + col) = u;
+        *(uint4*)((bf16*)Cb + (long)row * a.ldc + col) = u;
       } else {
-        float* p = (float*)a.C + (long)row * a.ldc + col;
+        float* p = (float*)Cb + (long)row * a.ldc + col;
         *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
         *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
       }
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
         float x = ep[rl * EPI_LD + cc * 8 + e] + bias8[e];
         if (a.add1) x += ld_as_f32(a.add1, (long)row * a.ld_add1 + col + e, a.add1_bf16 ? SAT_BF16 : SAT_F32);
         x = apply_act(x, a.act);
-        st_from_f32(a.C, (long)row * a.ldc + col + e, a.c_bf16 ? SAT_BF16 : SAT_F32, x);
+        st_from_f32(Cb, (long)row * a.ldc + col + e, a.c_bf16 ? SAT_BF16 : SAT_F32, x);
       }
     }
   }
@@ -435,8 +438,11 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   if (!bt && (g.K % 8 || g.ldb % 8)) return 0;
   if (g.bias && !al16(g.bias)) return 0;
   if (g.add1 && !al16(g.add1)) return 0;
-  int tcfg = (g.N <= 64 && !at && !bt) ? T128x64W8 : T128x128W8;
-  if (g_force_tile) tcfg = g_force_tile;
+  const bool partial = g.partial_splits > 1;
+  if (partial && (g.c_dtype != SAT_F32 || g.act != SAT_ACT_NONE || g.add1 || g.beta != 0.f || conv)) return 0;
+  // skinny partial-split problems (per-step decoder GEMMs): narrow N tiles for more blocks
+  int tcfg = ((g.N <= 64 || partial) && !at && !bt) ? T128x64W8 : T128x128W8;
+  if (g_force_tile && !partial) tcfg = g_force_tile;
   if ((at || bt) && tcfg != T128x128W4) tcfg = T128x128W8;
   const int bm = tile_bm(tcfg), bn = tile_bn(tcfg);
   const long tiles = (long)sat_cdiv(g.M, bm) * sat_cdiv(g.N, bn);
@@ -444,7 +450,9 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   int splitk = 1;
   const bool can_split = g.c_dtype == SAT_F32 && g.act == SAT_ACT_NONE && !g.add1 && (g.beta == 0.f || g.beta == 1.f) && !conv;
   if (g.beta != 0.f && !(can_split && g.beta == 1.f)) return 0;
-  if (tiles < 160) {
+  if (partial) {
+    splitk = 1;
+  } else if (tiles < 160) {
     if (!can_split || g.K < 1024) return 0;
     splitk = (int)((320 + tiles - 1) / tiles);
     const int by_k = g.K / 256;
@@ -482,6 +490,12 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
       if (g.ldc == g.N) { SAT_CHECK(hipMemsetAsync(g.C, 0, (size_t)g.M * g.N * 4, s)); }
       else { SAT_CHECK(hipMemset2DAsync(g.C, (size_t)g.ldc * 4, 0, (size_t)g.N * 4, g.M, s)); }
     }
+  }
+  a.partial = partial ? 1 : 0;
+  a.split_stride = g.split_stride;
+  if (partial) {   // every split writes its slab (an empty K range writes zeros): grid z = splits
+    a.splitk = g.partial_splits;
+    a.kchunk = sat_cdiv(sat_cdiv(g.K, g.partial_splits), BK) * BK;
   }
   if (conv) {
     if (g.conv.C % 8) return 0;

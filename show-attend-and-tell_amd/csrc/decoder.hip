@@ -36,25 +36,29 @@ struct WS {
       *colsum;
 };
 
-// split counts of the per-step skinny GEMMs (M = B rows): enough 64x64-tile x split blocks to
-// cover the 256 CUs; fp32 (parity) mode keeps a single split.
+// split counts of the per-step skinny GEMMs (M = B rows).  bf16: the LDS-DMA kernel (128 x 64
+// tiles, 128 x 128 for k-major weights) with partial-output split-K -- aim for ~1.5 waves of
+// blocks over the 256 CUs with splits that divide K into whole 64-deep k-tiles; fp32 (parity)
+// mode keeps a single split.
 struct Splits { int h, c, g, dh; };
-inline int pick_splits(int M, int N, int K, int dtype) {
-  if (dtype != SAT_BF16) return 1;
-  const long tiles = (long)sat_cdiv(M, 64) * sat_cdiv(N, 64);
-  int sk = (int)((320 + tiles - 1) / tiles);
-  const int by_k = K / 128;
-  if (sk > by_k) sk = by_k;
-  if (sk > 16) sk = 16;
-  return sk < 1 ? 1 : sk;
+inline int pick_splits(int M, int N, int K, int dtype, bool kmajor_w) {
+  if (dtype != SAT_BF16 || K % 64) return 1;
+  const long tiles = (long)sat_cdiv(M, 128) * sat_cdiv(N, kmajor_w ? 128 : 64);
+  long want = (384 + tiles - 1) / tiles;
+  if (want > 32) want = 32;
+  const int kt = K / 64;
+  int best = 1;
+  for (int s = 1; s <= kt && s <= want; ++s)
+    if (kt % s == 0) best = s;
+  return best;
 }
 inline Splits splits_for(const SatDecoderDims& d) {
   const int E = d.E, D = d.D, HG = 5 * E + D;
   Splits s;
-  s.h = pick_splits(d.B, d.attention ? HG : 4 * E, E, d.dtype);
-  s.c = pick_splits(d.B, 4 * E, D, d.dtype);
-  s.g = pick_splits(d.B, D, 4 * E, d.dtype);
-  s.dh = pick_splits(d.B, E, d.attention ? HG : 4 * E, d.dtype);
+  s.h = pick_splits(d.B, d.attention ? HG : 4 * E, E, d.dtype, false);
+  s.c = pick_splits(d.B, 4 * E, D, d.dtype, false);
+  s.g = pick_splits(d.B, D, 4 * E, d.dtype, true);
+  s.dh = pick_splits(d.B, E, d.attention ? HG : 4 * E, d.dtype, true);
   return s;
 }
 

@@ -352,7 +352,7 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return 0;
   SAT_REQUIRE(g.K >= 0 && g.A && g.B && g.C);
   SAT_REQUIRE(g.dtype == SAT_F32 || g.dtype == SAT_BF16);
-  if (g.partial_splits <= 1) {
+  {
     int err = 0;
     if (sat_fast_gemm_try(g, s, &err)) return err;
   }
