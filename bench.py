@@ -43,45 +43,100 @@ def parse():
     return ap.parse_args()
 
 
-def conv_flops(enc, B, H=224, W=224):
-    """Algorithmic FLOPs of every conv launch of one encoder forward (real Cin, not the padded one)."""
-    flops = []
-    h, w = H, W
-    for step in enc._plan:   # the plan the timed steps ran (built during warm-up)
-        if step[0] == "conv":
-            wt, _, s, p = step[1]
-            co, kh, kw, ci = wt.shape
-            ci = 3 if ci == 8 else ci
-            oh, ow = (h + 2 * p - kh) // s + 1, (w + 2 * p - kw) // s + 1
-            flops.append(2.0 * B * oh * ow * co * kh * kw * ci)
-            h, w = oh, ow
-        elif step[0] == "pool":
-            k, s, p = step[1], step[2], step[3]
-            h, w = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
-        else:
-            _, c1, c2, c3, ds = step
-            s = c2[2]
-            oh, ow = (h + 2 - 3) // s + 1, (w + 2 - 3) // s + 1
-            for (wt, _, st, pd), (hh, ww, oo) in ((c1, (h, w, (h, w))), (c2, (h, w, (oh, ow))),
-                                                   (c3, (oh, ow, (oh, ow)))):
-                co, kh, kw, ci = wt.shape
-                flops.append(2.0 * B * oo[0] * oo[1] * co * kh * kw * ci)
-            if ds is not None:
-                co, kh, kw, ci = ds[0].shape
-                flops.append(2.0 * B * oh * ow * co * ci)
-            h, w = oh, ow
-    return flops
+PEAK_HBM_ACHIEVABLE_GBS = 6300.0   # MI355X_MICROARCH.md §HBM (floor estimates only)
 
 
-def pmc_traffic(network):
-    """HBM bytes per conv launch from the committed PMC passes (tools/pmc_traffic.py; a PMC run
-    cannot share a process with the timed bench), or None when none was collected for this trunk."""
+def conv_launches(network, B, H=224):
+    """Every conv launch of one encoder forward, in launch order (encoder.py forward: per
+    bottleneck c1, c2, downsample, c3), with its algorithmic work: FLOPs = 2*M*N*K (real Cin=3
+    for the first conv) and bytes = input activation read once + weights + output (+ residual),
+    bf16.  ``bound`` is the roofline that is larger at 2.5 PFLOP/s / 6.3 TB/s."""
+    out = []
+
+    def add(name, M, N, K, in_elems, res=False, real_k=None):
+        f = 2.0 * M * N * (real_k or K)
+        by = 2.0 * (in_elems + N * K + M * N * (2 if res else 1))
+        bound = "mfma" if f / (BF16_DENSE_PEAK_TFLOPS * 1e12) > by / (PEAK_HBM_ACHIEVABLE_GBS * 1e9) else "hbm"
+        out.append(dict(cls=f"{name} {M}x{N}x{K}", flops=f, bytes=by, bound=bound))
+
+    if network == "resnet152":
+        h = H // 2
+        add("stem7x7s2", B * h * h, 64, 7 * 7 * 8, B * H * H * 8, real_k=147)
+        h //= 2
+        cin = 64
+        for li, (n, pl) in enumerate(zip([3, 8, 36, 3], [64, 128, 256, 512])):
+            for bi in range(n):
+                s = (1 if li == 0 else 2) if bi == 0 else 1
+                oh = h // s
+                add(f"L{li + 1}c1", B * h * h, pl, cin, B * h * h * cin)
+                add(f"L{li + 1}c2{'s2' if s == 2 else ''}", B * oh * oh, pl, 9 * pl, B * h * h * pl)
+                if bi == 0:
+                    add(f"L{li + 1}ds{'s2' if s == 2 else ''}", B * oh * oh, 4 * pl, cin, B * h * h * cin)
+                add(f"L{li + 1}c3+res", B * oh * oh, 4 * pl, pl, B * oh * oh * pl, res=True)
+                cin, h = 4 * pl, oh
+    else:   # vgg19 features[:-1]: 16 3x3 convs, 4 pools (encoder.py:23-27)
+        h, cin = H, 8
+        for i, co in enumerate([64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M",
+                                512, 512, 512, 512, "M", 512, 512, 512, 512]):
+            if co == "M":
+                h //= 2
+                continue
+            add(f"conv{i}", B * h * h, co, 9 * cin, B * h * h * cin, real_k=27 if cin == 8 else None)
+            cin = co
+    return out
+
+
+def trunk_roofline(enc, imgs, launches, reps=3):
+    """Per-launch HIP events around every conv of `reps` eager forwards (on the launch stream)
+    -> per-class average duration, the dominant class and its roofline, and the whole trunk's
+    measured conv time against its roofline floor."""
+    enc.timing = []
+    with torch.no_grad():
+        for _ in range(reps):
+            enc(imgs)
+    torch.cuda.synchronize()
+    ev, enc.timing = enc.timing, None
+    n = len(launches)
+    assert len(ev) == reps * n, (len(ev), n)
+    dur = [0.0] * n
+    for r in range(reps):
+        for i in range(n):
+            st, en = ev[r * n + i]
+            dur[i] += st.elapsed_time(en) / reps   # ms
+    cls = {}
+    for l, d in zip(launches, dur):
+        c = cls.setdefault(l["cls"], dict(n=0, ms=0.0, flops=l["flops"], bytes=l["bytes"], bound=l["bound"]))
+        c["n"] += 1
+        c["ms"] += d
+    name, dom = max(cls.items(), key=lambda kv: kv[1]["ms"])
+    avg_s = dom["ms"] / dom["n"] * 1e-3
+    if dom["bound"] == "hbm":
+        achieved, peak, unit = dom["bytes"] / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
+    else:
+        achieved, peak, unit = dom["flops"] / avg_s / 1e12, BF16_DENSE_PEAK_TFLOPS, "TFLOP/s"
+    floor_us = sum(max(l["flops"] / (BF16_DENSE_PEAK_TFLOPS * 1e12), l["bytes"] / (PEAK_HBM_ACHIEVABLE_GBS * 1e9))
+                   for l in launches) * 1e6
+    trunk_us = sum(dur) * 1e3
+    return dict(kernel=f"fast_gemm_kernel, conv class {name} ({dom['n']} launches/forward)", cls=name,
+                bound=dom["bound"], achieved=round(achieved, 2), peak=peak, unit=unit,
+                frac=round(achieved / peak, 4), avg_launch_us=round(avg_s * 1e6, 2),
+                algorithmic_bytes_per_launch=dom["bytes"], algorithmic_flops_per_launch=dom["flops"]), \
+        dict(conv_us_per_forward=round(trunk_us, 1), roofline_floor_us=round(floor_us, 1),
+             frac_of_floor=round(floor_us / trunk_us, 4),
+             classes={k: dict(n=v["n"], us=round(v["ms"] * 1e3, 1)) for k, v in
+                      sorted(cls.items(), key=lambda kv: -kv[1]["ms"])})
+
+
+def pmc_traffic(network, cls):
+    """HBM bytes per launch of conv class `cls` from the committed PMC passes
+    (tools/pmc_traffic.py; a PMC run cannot share a process with the timed bench), else None."""
     path = os.path.join(REPO, "profiles", f"pmc_traffic_{network}.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         rec = json.load(f)
-    return rec.get("hbm_bytes_per_conv_launch"), os.path.relpath(path, REPO)
+    per = rec.get("classes", {}).get(cls)
+    return (per["hbm_bytes_per_launch"] if per else None), os.path.relpath(path, REPO)
 
 
 def cpu_baseline(args):
@@ -195,8 +250,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if not use_graph:
-        enc.timing = []   # eager: bracket every conv launch
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -208,21 +261,12 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    per_img_conv = conv_flops(enc, B)
-    if use_graph:
-        enc_ms = sum(s.elapsed_time(e) for s, e in enc_events)
-        n_launch = len(per_img_conv) * args.steps
-        kernel_desc = "encoder trunk hipGraph (155 implicit-GEMM conv launches fast_gemm_kernel<*,0,0,2,8> + pool/layout)"
-    else:
-        enc_ms = sum(s.elapsed_time(e) for s, e in enc.timing)
-        n_launch = len(enc.timing)
-        enc.timing = None
-        kernel_desc = "fast_gemm_kernel<*,0,0,2,8> (implicit-GEMM conv), per-launch events"
-    flops = sum(per_img_conv) * args.steps
-    achieved = flops / (enc_ms * 1e-3) / 1e12 if enc_ms > 0 else 0.0
+    launches = conv_launches(args.network, B)
+    enc_ms = sum(s.elapsed_time(e) for s, e in enc_events) if use_graph else None
     loss_v = loss.item()
-    traffic, t_src = pmc_traffic(args.network)
+    roof, trunk = trunk_roofline(enc, imgs, launches) if rank == 0 else (None, None)
     if rank == 0:
+        roof["traffic"], roof["traffic_source"] = pmc_traffic(args.network, roof["cls"])
         out = {
             "metric": "train images/sec on COCO batch=128 at 1/2/4/8 MI355X",
             "value": round(B * world * args.steps / elapsed, 2),
@@ -235,12 +279,8 @@ def main():
                                    f"step, V={args.vocab}, T={args.seq}",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": args.seq,
                        "parallelism": f"dp{world}", "hip_graph": use_graph},
-            "roofline": {"bound": "mfma", "kernel": kernel_desc,
-                         "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
-                         "launches": n_launch, "avg_launch_ms": round(enc_ms / max(1, n_launch), 4),
-                         "algorithmic_flops_per_launch": flops / max(1, n_launch),
-                         "traffic": traffic, "traffic_unit": "HBM bytes per conv launch", "traffic_source": t_src},
+            "roofline": roof,
+            "encoder_trunk": dict(trunk, graph_ms_per_step=(round(enc_ms / args.steps, 3) if enc_ms else None)),
             "loss": round(loss_v, 4),
         }
         if not args.no_cpu_baseline and world == 1:

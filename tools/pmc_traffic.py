@@ -1,14 +1,14 @@
-"""HBM traffic of the encoder's conv launches from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+"""HBM traffic per encoder conv class from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
 
-    python tools/pmc_traffic.py gpurun_out/<tag>/pmc_fetch gpurun_out/<tag>/pmc_write [out.json]
+    python tools/pmc_traffic.py <pmc_fetch dir> <pmc_write dir> [resnet152|vgg19] [B] [out.json]
 
-Counters follow MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half the bytes of a wide (16 B/lane)
-streaming read on gfx950 -> doubled here; WRITE_SIZE is exact for 16-B stores.  Both are in KiB
-per dispatch (rocprofv3 derived-counter unit); the NCHW->NHWC input conversion (a pure stream of
-known size) is printed beside them as a unit/calibration check.
+Counters per MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports half the bytes of a wide
+(16 B/lane) streaming read -> doubled here; WRITE_SIZE is exact for 16-B stores.  rocprofv3's
+derived FETCH_SIZE / WRITE_SIZE are in KiB.  The NCHW->NHWC conversion (a plain stream of known
+size: B*3*224*224*4 B read, B*224*224*8*2 B written) is reported beside them as the unit check.
 
-Encoder dispatches = from each ``nchw_to_nhwc_kernel`` up to the decoder's first
-``mean_rows_kernel``; the conv launches among them are the ``fast_gemm_kernel`` ones.
+Dispatch mapping as tools/conv_shapes.py: last complete encoder forward in each pass, its
+fast_gemm_kernel dispatches in order onto bench.conv_launches().
 """
 import csv
 import glob
@@ -16,29 +16,27 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import conv_launches  # noqa: E402
+
 
 def read_counter(d, name):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
-    rows = []
+    per = {}
     for f in files:
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if r.get("Counter_Name") == name:
-                    rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
-    rows.sort()
-    # one value per dispatch (sum over per-XCD / per-instance rows if any)
-    out = {}
-    for did, k, v in rows:
-        if did in out:
-            out[did] = (k, out[did][1] + v)
-        else:
-            out[did] = (k, v)
-    return [(did, k, v) for did, (k, v) in sorted(out.items())]
+                if r.get("Counter_Name") != name:
+                    continue
+                did = int(r["Dispatch_Id"])
+                k, v = per.get(did, (r["Kernel_Name"], 0.0))
+                per[did] = (k, v + float(r["Counter_Value"]))
+    return [(did, k, v) for did, (k, v) in sorted(per.items())]
 
 
-def encoder_groups(rows):
+def last_forward(rows, n_conv):
     groups, cur = [], None
     for did, k, v in rows:
         if "nchw_to_nhwc" in k:
@@ -47,34 +45,46 @@ def encoder_groups(rows):
         elif "mean_rows" in k:
             cur = None
         if cur is not None:
-            cur.append((did, k, v))
-    return groups
+            cur.append((k, v))
+    groups = [g for g in groups if sum("fast_gemm" in k for k, _ in g) == n_conv]
+    if not groups:
+        raise SystemExit("no complete encoder forward")
+    return groups[-1]
 
 
 def main():
     fdir, wdir = sys.argv[1], sys.argv[2]
-    out_path = sys.argv[3] if len(sys.argv) > 3 else None
-    fetch = read_counter(fdir, "FETCH_SIZE")
-    write = read_counter(wdir, "WRITE_SIZE")
-    res = {}
-    for name, rows, scale in (("fetch", fetch, 2.0), ("write", write, 1.0)):
-        gs = [g for g in encoder_groups(rows) if g]
-        g = gs[-1]   # last (steady-state) encoder forward
-        conv = [v for _, k, v in g if "fast_gemm_kernel" in k]
-        layout = [v for _, k, v in g if "nchw_to_nhwc" in k]
-        res[name] = dict(encoder_forwards_seen=len(gs), conv_launches=len(conv),
-                         conv_kib_total=sum(conv) * scale, conv_kib_per_launch=sum(conv) * scale / max(1, len(conv)),
-                         nchw_to_nhwc_kib=(layout[0] * scale if layout else None), scale_applied=scale)
-    n = res["fetch"]["conv_launches"]
-    per_launch = (res["fetch"]["conv_kib_total"] + res["write"]["conv_kib_total"]) * 1024 / max(1, n)
-    summary = dict(source="rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), --kernel-trace, "
-                          "bench.py --no-graph; FETCH_SIZE x2 (gfx950 correction)",
-                   conv_launches=n, hbm_bytes_per_conv_launch=per_launch,
-                   hbm_bytes_encoder_convs=per_launch * n, detail=res)
-    print(json.dumps(summary, indent=1))
-    if out_path:
-        with open(out_path, "w") as f:
-            json.dump(summary, f, indent=1)
+    network = sys.argv[3] if len(sys.argv) > 3 else "resnet152"
+    B = int(sys.argv[4]) if len(sys.argv) > 4 else 128
+    launches = conv_launches(network, B)
+    n = len(launches)
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes, --kernel-trace), "
+                     "bench.py --no-graph; FETCH_SIZE x2 (gfx950), KiB -> bytes",
+           "network": network, "batch": B, "classes": {}}
+    fetch = last_forward(read_counter(fdir, "FETCH_SIZE"), n)
+    write = last_forward(read_counter(wdir, "WRITE_SIZE"), n)
+    unit = {}
+    for tag, g, scale in (("fetch", fetch, 2.0), ("write", write, 1.0)):
+        layout = [v for k, v in g if "nchw_to_nhwc" in k]
+        unit[tag] = layout[0] * scale * 1024 if layout else None
+        conv = [v * scale * 1024 for k, v in g if "fast_gemm" in k]
+        for l, b in zip(launches, conv):
+            c = out["classes"].setdefault(l["cls"], {"n": 0, "fetch": 0.0, "write": 0.0, "alg_bytes": l["bytes"]})
+            if tag == "fetch":
+                c["n"] += 1
+            c[tag] += b
+    tot = 0.0
+    for name, c in out["classes"].items():
+        c["hbm_bytes_per_launch"] = (c["fetch"] + c["write"]) / c["n"]
+        c["ratio_to_algorithmic"] = round(c["hbm_bytes_per_launch"] / c["alg_bytes"], 3)
+        tot += c["fetch"] + c["write"]
+    out["hbm_bytes_encoder_convs"] = tot
+    out["unit_check_nchw_to_nhwc"] = {"fetch_bytes": unit["fetch"], "expected_read": B * 3 * 224 * 224 * 4,
+                                      "write_bytes": unit["write"], "expected_write": B * 224 * 224 * 8 * 2}
+    print(json.dumps(out, indent=1))
+    if len(sys.argv) > 5:
+        with open(sys.argv[5], "w") as f:
+            json.dump(out, f, indent=1)
 
 
 if __name__ == "__main__":
