@@ -30,9 +30,9 @@ for s in $STEPS; do
     profg) run profg 600 rocprofv3 --kernel-trace --stats -d "$OUT/profg" -o run --output-format csv -- \
                python bench.py --steps 10 --warmup 3 --no-cpu-baseline || exit $? ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- \
-               python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-graph || exit $?
+               python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-graph || exit $?
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- \
-               python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-graph || exit $? ;;
+               python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-graph || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
