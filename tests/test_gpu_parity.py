@@ -145,6 +145,16 @@ def test_decoder_eval_matches_reference(sat, path):
     assert m["caption_length"] == int(g["caption_length"])
 
 
+def _fp64_oracle_grads(g):
+    """The oracle's gradients for a golden case computed in float64 (the fp32 noise gauge)."""
+    c = g["cfg"]
+    p = {k: v.double() for k, v in params_for(c).items()}
+    _, grads, _, _, _ = O.train_step(p, tt(g["img_features"]).double(), tt(g["captions"]), tf=c["tf"], ado=c["ado"],
+                                     attention=c["attention"], bert=c["bert"], alpha_c=c["alpha_c"], lr=c["lr"],
+                                     training=True, dropout_masks=masks_for(c).double(), adam_state={})
+    return {k: v.reshape(-1).double() for k, v in grads.items()}
+
+
 @pytest.mark.parametrize("path", fixture_paths(), ids=fixture_ids())
 def test_decoder_train_step_matches_reference(sat, path):
     g = load(path); c = g["cfg"]
@@ -165,16 +175,24 @@ def test_decoder_train_step_matches_reference(sat, path):
     params = dict(dec.named_parameters())
     have = sorted(n for n, p in params.items() if p.grad is not None)
     assert have == sorted(g["grad_names"])
+    g64 = _fp64_oracle_grads(g)
     for name in g["grad_names"]:
         gr = params[name].grad.detach().reshape(-1).double().cpu()
         ref_norm = math.sqrt(float(g[f"gsq::{name}"]))
         if ref_norm < 1e-7:    # attention.v.bias: analytically zero (softmax shift invariance)
             assert gr.abs().max().item() < 1e-5
             continue
-        assert abs(gr.norm().item() - ref_norm) <= 2e-4 * ref_norm, name
         idx = torch.from_numpy(g[f"gidx::{name}"])
-        err = (gr[idx] - torch.from_numpy(g[f"gval::{name}"]).double()).abs().max().item()
-        assert err <= 1e-3 * gr.abs().max().item() + 1e-9, name  # fp32 reduction-order noise
+        ref_s = torch.from_numpy(g[f"gval::{name}"]).double()
+        # Tolerances: 2e-4 of the norm / 1e-3 of max|g| per sampled element, or twice the distance
+        # between the fp32 reference and the same math in fp64 when that is larger -- some BPTT
+        # gradients (e.g. init_h under greedy + ado) are conditioned so that ANY fp32 summation
+        # order lands ~5e-4 away from the reference's own fp32 result.
+        noise_norm = abs(g64[name].norm().item() - ref_norm) / ref_norm
+        noise_elem = (g64[name][idx] - ref_s).abs().max().item()
+        assert abs(gr.norm().item() - ref_norm) <= max(2e-4, 2 * noise_norm) * ref_norm, name
+        err = (gr[idx] - ref_s).abs().max().item()
+        assert err <= max(1e-3 * gr.abs().max().item(), 2 * noise_elem) + 1e-9, name
     opt.step()
     torch.cuda.synchronize()
     for name in g["grad_names"]:
