@@ -444,7 +444,8 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   int tcfg = ((g.N <= 64 || partial) && !at && !bt) ? T128x64W8 : T128x128W8;
   if (g_force_tile && !partial) tcfg = g_force_tile;
   if ((at || bt) && tcfg != T128x128W4) tcfg = T128x128W8;
-  const int bm = tile_bm(tcfg), bn = tile_bn(tcfg);
+  const int bm = tile_bm(tcfg);
+  int bn = tile_bn(tcfg);
   const long tiles = (long)sat_cdiv(g.M, bm) * sat_cdiv(g.N, bn);
   // atomic split-K for weight-gradient-like problems (long K, few tiles, fp32 output)
   int splitk = 1;
@@ -453,12 +454,19 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   if (partial) {
     splitk = 1;
   } else if (tiles < 160) {
-    if (!can_split || g.K < 1024) return 0;
-    splitk = (int)((320 + tiles - 1) / tiles);
-    const int by_k = g.K / 256;
-    if (splitk > by_k) splitk = by_k;
-    if (splitk > 16) splitk = 16;
-    if (splitk < 2) return 0;
+    if (can_split && g.K >= 1024) {
+      splitk = (int)((320 + tiles - 1) / tiles);
+      const int by_k = g.K / 256;
+      if (splitk > by_k) splitk = by_k;
+      if (splitk > 16) splitk = 16;
+      if (splitk < 2) splitk = 1;
+    }
+    // no split: still the LDS-DMA kernel (the register-staged one is slower per tile); narrow
+    // N tiles double the block count of non-transposed problems
+    if (splitk == 1 && !at && !bt && !g_force_tile && tcfg == T128x128W8) {
+      tcfg = T128x64W8;
+      bn = tile_bn(tcfg);
+    }
   } else if (g.beta != 0.f) {
     splitk = 1;   // beta == 1 accumulate through the atomic epilogue with a single split
   }

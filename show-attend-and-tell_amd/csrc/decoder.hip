@@ -25,7 +25,7 @@ namespace {
 
 struct WS {
   // forward (saved for backward)
-  float *mean_f, *hc0, *xg, *gctx_const, *hg, *gctx, *uh_all, *gates_all, *c_in, *c_out, *h_out, *ctx_all,
+  float *mean_f, *hc0, *hc0pre, *xg, *gctx_const, *hg, *gctx, *uh_all, *gates_all, *c_in, *c_out, *h_out, *ctx_all,
       *gate_all, *fh, *fz;
   void *mean_t, *Ws, *emb_t, *h_in_t, *ctx_t, *gated_t, *hd_t, *comb_t;
   int32_t* tok;
@@ -40,7 +40,7 @@ struct WS {
 // tiles, 128 x 128 for k-major weights) with partial-output split-K -- aim for ~1.5 waves of
 // blocks over the 256 CUs with splits that divide K into whole 64-deep k-tiles; fp32 (parity)
 // mode keeps a single split.
-struct Splits { int h, c, g, dh; };
+struct Splits { int h, c, g, dh, i; };
 inline int pick_splits(int M, int N, int K, int dtype, bool kmajor_w) {
   if (dtype != SAT_BF16 || K % 64) return 1;
   const long tiles = (long)sat_cdiv(M, 128) * sat_cdiv(N, kmajor_w ? 128 : 64);
@@ -59,6 +59,7 @@ inline Splits splits_for(const SatDecoderDims& d) {
   s.c = pick_splits(d.B, 4 * E, D, d.dtype, false);
   s.g = pick_splits(d.B, D, 4 * E, d.dtype, true);
   s.dh = pick_splits(d.B, E, d.attention ? HG : 4 * E, d.dtype, true);
+  s.i = pick_splits(d.B, 2 * E, D, d.dtype, false);
   return s;
 }
 
@@ -81,6 +82,7 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   Carver c{base};
   c.take(w->mean_f, B * D * f);  c.take(w->mean_t, B * D * ts);
   c.take(w->hc0, B * 2 * E * f);
+  c.take(w->hc0pre, sp.i * B * 2 * E * f);
   c.take(w->Ws, B * L * E * ts);
   c.take(w->tok, R * 4);
   c.take(w->emb_t, R * E * ts);
@@ -144,6 +146,21 @@ int combine_rows(const float* fh, const float* fz, const void* emb, int rows, in
   else
     hipLaunchKernelGGL(ado_combine_rows_kernel<float>, dim3(g), dim3(256), 0, s, fh, fz, (const float*)emb, rows, E, ld, (float*)comb);
   return (int)hipGetLastError();
+}
+
+// tanh of the [init_h | init_c] pre-activations (sum of `splits` slabs): hc0 (fp32, kept for the
+// backward), h into step 0's GEMM-input slot (dtype), c into step 0's cell slot (fp32).
+template <typename T>
+__global__ void init_state_kernel(const float* pre, int splits, long stride, int B, int E, float* hc0, T* h_t,
+                                  long h_ld, float* c_in, long c_ld) {
+  const long n = (long)B * 2 * E;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / (2 * E)), j = (int)(i - (long)b * 2 * E);
+    const float v = tanhf(sum_parts(pre, i, splits, stride));
+    hc0[i] = v;
+    if (j < E) h_t[(long)b * h_ld + j] = (T)v;
+    else c_in[(long)b * c_ld + j - E] = v;
+  }
 }
 
 struct Ctx {
@@ -255,11 +272,21 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
   }
   // init_lstm_state (decoder.py:137-147)
   SAT_CHECK((hipError_t)sat_mean_rows(img_features, B, L, D, d.dtype, w.mean_f, w.mean_t, s));
-  SAT_CHECK((hipError_t)linear(c, B, E, D, w.mean_t, D, c.W(lay->init_w), D, c.F(lay->init_b), w.hc0, 2 * E,
-                               SAT_F32, SAT_ACT_TANH, s, nullptr, 0, SAT_F32, w.h_in_t, (long)T1 * E, d.dtype));
-  SAT_CHECK((hipError_t)linear(c, B, E, D, w.mean_t, D, c.W(lay->init_w + (long)E * D), D, c.F(lay->init_b + E),
-                               w.hc0 + E, 2 * E, SAT_F32, SAT_ACT_TANH, s, nullptr, 0, SAT_F32, w.c_in,
-                               (long)T1 * E, SAT_F32));
+  // [init_h; init_c] as one N = 2E product (split-K slabs), tanh + scatter in one pass
+  SAT_CHECK((hipError_t)linear(c, B, 2 * E, D, w.mean_t, D, c.W(lay->init_w), D, c.F(lay->init_b), w.hc0pre, 2 * E,
+                               SAT_F32, SAT_ACT_NONE, s, nullptr, 0, SAT_F32, nullptr, 0, SAT_F32, sp.i,
+                               (long)B * 2 * E));
+  {
+    const long n = (long)B * 2 * E;
+    const int g = (int)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+    if (d.dtype == SAT_BF16)
+      hipLaunchKernelGGL(init_state_kernel<bf16>, dim3(g), dim3(256), 0, s, (const float*)w.hc0pre, sp.i,
+                         (long)B * 2 * E, B, E, w.hc0, (bf16*)w.h_in_t, (long)T1 * E, w.c_in, (long)T1 * E);
+    else
+      hipLaunchKernelGGL(init_state_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)w.hc0pre, sp.i,
+                         (long)B * 2 * E, B, E, w.hc0, (float*)w.h_in_t, (long)T1 * E, w.c_in, (long)T1 * E);
+    SAT_LAUNCH_CHECK();
+  }
   if (att) {  // hoisted Ws = a W^T + b
     SAT_CHECK((hipError_t)linear(c, B * L, E, D, img_features, D, c.W(lay->attW_w), D, c.F(lay->attW_b), w.Ws, E,
                                  d.dtype, SAT_ACT_NONE, s));

@@ -116,6 +116,39 @@ __global__ void colsum_partial_kernel(const T* __restrict__ X, long ld, int R, i
   for (int r = r0; r < r1; ++r) s += (float)X[(long)r * ld + n];
   part[(long)blockIdx.y * N + n] = s;
 }
+// 16-byte rows chunks per thread (VEC columns), 4 rows in flight per iteration
+template <typename T>
+__global__ void colsum_partial_vec_kernel(const T* __restrict__ X, long ld, int R, int N, int rows_per,
+                                          float* __restrict__ part) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * VEC;
+  if (n >= N) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(R, r0 + rows_per);
+  float acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  int r = r0;
+  for (; r + 4 <= r1; r += 4) {
+    uint4 u[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) u[q] = *(const uint4*)(X + (long)(r + q) * ld + n);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const T* h = (const T*)&u[q];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += (float)h[j];
+    }
+  }
+  for (; r < r1; ++r) {
+    uint4 u = *(const uint4*)(X + (long)r * ld + n);
+    const T* h = (const T*)&u;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] += (float)h[j];
+  }
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) part[(long)blockIdx.y * N + n + j] = acc[j];
+}
+
 __global__ void colsum_final_kernel(const float* __restrict__ part, int RS, int N, float* __restrict__ out,
                                     int accumulate, float* __restrict__ out2) {
   int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -216,18 +249,25 @@ int sat_mean_rows(const void* a, int B, int L, int D, int dtype, float* out_f32,
 int sat_colsum(const void* X, int dtype, long ld, int R, int N, float* out, int accumulate, float* out2,
                float* scratch, hipStream_t s) {
   if (N <= 0) return 0;
-  int colblocks = sat_cdiv(N, 256);
+  const int vec = dtype == SAT_BF16 ? 8 : 4;
+  const bool vok = N % vec == 0 && ld % vec == 0 && ((uintptr_t)X & 15) == 0;
+  const int colblocks = sat_cdiv(N, 256 * (vok ? vec : 1));
   int RS = 1;
   while (colblocks * RS < 512 && RS < 64 && (R + RS * 2 - 1) / (RS * 2) >= 16) RS *= 2;
   int rows_per = sat_cdiv(R, RS);
   RS = sat_cdiv(R, rows_per > 0 ? rows_per : 1);
   if (R <= 0) { RS = 1; rows_per = 0; }
   dim3 g1(colblocks, RS);
-  if (dtype == SAT_BF16)
+  if (vok) {
+    if (dtype == SAT_BF16)
+      hipLaunchKernelGGL(colsum_partial_vec_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)X, ld, R, N, rows_per, scratch);
+    else
+      hipLaunchKernelGGL(colsum_partial_vec_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ld, R, N, rows_per, scratch);
+  } else if (dtype == SAT_BF16)
     hipLaunchKernelGGL(colsum_partial_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)X, ld, R, N, rows_per, scratch);
   else
     hipLaunchKernelGGL(colsum_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ld, R, N, rows_per, scratch);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(colblocks), dim3(256), 0, s, scratch, RS, N, out, accumulate, out2);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(sat_cdiv(N, 256)), dim3(256), 0, s, scratch, RS, N, out, accumulate, out2);
   return (int)hipGetLastError();
 }
 size_t sat_colsum_scratch_floats(int R, int N) { (void)R; return (size_t)64 * (N > 0 ? N : 1); }

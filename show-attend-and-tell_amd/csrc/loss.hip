@@ -39,43 +39,100 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return s;
 }
 
+// one pass over the row: online (max, sum-exp) per thread, then a block-level merge; rows with
+// V % (16 / sizeof(T)) == 0 are read as 16-byte vectors.
+__device__ __forceinline__ void online_add(float& m, float& se, float x) {
+  if (x > m) { se = se * expf(m - x) + 1.f; m = x; }
+  else se += expf(x - m);
+}
+
 template <typename TT>
 __global__ __launch_bounds__(256) void loss_rows_kernel(const TT* __restrict__ preds, const int64_t* __restrict__ caps,
                                                         int B, int T, int V, int pad_id, float* __restrict__ stats) {
-  __shared__ float red[4];
+  __shared__ float red_m[4], red_s[4], red_c[4];
   const int r = blockIdx.x;
   const int T1 = T - 1;
   const int b = r / T1, t = r - b * T1;
   const TT* x = preds + (long)r * V;
   const int tgt = (int)caps[(long)b * T + t + 1];
   const float xt = (tgt >= 0 && tgt < V) ? (float)x[tgt] : 0.f;
-  float m = -INFINITY, cnt = 0.f;
-  for (int v = threadIdx.x; v < V; v += blockDim.x) {
-    const float xv = (float)x[v];
-    m = fmaxf(m, xv);
-    cnt += (xv > xt || (xv == xt && v < tgt)) ? 1.f : 0.f;
+  float m = -INFINITY, se = 0.f, cnt = 0.f;
+  constexpr int VEC = 16 / sizeof(TT);
+  if (V % VEC == 0) {
+    for (int c = threadIdx.x; c < V / VEC; c += blockDim.x) {
+      uint4 u = *(const uint4*)(x + (long)c * VEC);
+      const TT* h = (const TT*)&u;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float xv = (float)h[j];
+        const int v = c * VEC + j;
+        online_add(m, se, xv);
+        cnt += (xv > xt || (xv == xt && v < tgt)) ? 1.f : 0.f;
+      }
+    }
+  } else {
+    for (int v = threadIdx.x; v < V; v += blockDim.x) {
+      const float xv = (float)x[v];
+      online_add(m, se, xv);
+      cnt += (xv > xt || (xv == xt && v < tgt)) ? 1.f : 0.f;
+    }
   }
-  m = block_max(m, red);
-  float se = 0.f;
-  for (int v = threadIdx.x; v < V; v += blockDim.x) se += expf((float)x[v] - m);
-  se = block_sum(se, red);
-  cnt = block_sum(cnt, red);
+  // merge (m, se) pairs: across the wave, then the 4 waves in a fixed order
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64), os = __shfl_xor(se, o, 64);
+    const float nm = fmaxf(m, om);
+    se = (nm == -INFINITY) ? 0.f : se * expf(m - nm) + os * expf(om - nm);
+    m = nm;
+    cnt += __shfl_xor(cnt, o, 64);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) { red_m[w] = m; red_s[w] = se; red_c[w] = cnt; }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    const float lse = m + logf(se);
+    float M = red_m[0], S = red_s[0], C = red_c[0];
+    for (int i = 1; i < 4; ++i) {
+      const float nm = fmaxf(M, red_m[i]);
+      S = S * expf(M - nm) + red_s[i] * expf(red_m[i] - nm);
+      M = nm;
+      C += red_c[i];
+    }
+    const float lse = M + logf(S);
     const bool nonpad = tgt != pad_id;
     float* st = stats + (long)r * kStat;
     st[0] = lse;
     st[1] = (t < T1 - 1) ? lse - xt : 0.f;
-    st[2] = (nonpad && cnt < 1.f) ? 1.f : 0.f;
-    st[3] = (nonpad && cnt < 5.f) ? 1.f : 0.f;
+    st[2] = (nonpad && C < 1.f) ? 1.f : 0.f;
+    st[3] = (nonpad && C < 5.f) ? 1.f : 0.f;
     st[4] = nonpad ? 1.f : 0.f;
   }
 }
 
-__global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* __restrict__ stats, const float* __restrict__ alphas,
-                                                           const int64_t* __restrict__ caps, int B, int T, int L,
-                                                           float alpha_c, int s0, int s1, int s2,
-                                                           float* __restrict__ dreg, float* __restrict__ out) {
+// attention regulariser, one thread per (b, l): the sum over steps, its gradient, and a block
+// partial of sum (1 - s)^2 (folded in a fixed order by loss_reduce_kernel).
+__global__ __launch_bounds__(256) void loss_reg_kernel(const float* __restrict__ alphas, int B, int T1, int L,
+                                                       float alpha_c, float* __restrict__ dreg,
+                                                       float* __restrict__ part) {
+  __shared__ float red[4];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const float inv_bl = 1.0f / (float)(B * L);
+  float reg = 0.f;
+  if (i < B * L) {
+    const int b = i / L, l = i - b * L;
+    float ssum = 0.f;
+    for (int t = 0; t < T1; ++t) ssum += alphas[((long)b * T1 + t) * L + l];
+    const float d = 1.f - ssum;
+    reg = d * d;
+    dreg[i] = alpha_c * 2.f * (ssum - 1.f) * inv_bl;
+  }
+  reg = block_sum(reg, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = reg;
+}
+
+__global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* __restrict__ stats, const float* __restrict__ part,
+                                                           int nparts, const int64_t* __restrict__ caps, int B, int T,
+                                                           int L, float alpha_c, int s0, int s1, int s2,
+                                                           float* __restrict__ out) {
   __shared__ float red[16];
   const int T1 = T - 1, R = B * T1;
   float ce = 0.f, c1 = 0.f, c5 = 0.f, np = 0.f;
@@ -88,15 +145,7 @@ __global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* __restri
   c5 = block_sum(c5, red);
   np = block_sum(np, red);
   float reg = 0.f;
-  const float inv_bl = 1.0f / (float)(B * L);
-  for (int i = threadIdx.x; i < B * L; i += blockDim.x) {
-    const int b = i / L, l = i - b * L;
-    float ssum = 0.f;
-    for (int t = 0; t < T1; ++t) ssum += alphas[((long)b * T1 + t) * L + l];
-    const float d = 1.f - ssum;
-    reg += d * d;
-    dreg[i] = alpha_c * 2.f * (ssum - 1.f) * inv_bl;
-  }
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) reg += part[i];
   reg = block_sum(reg, red);
   float cl = 0.f;
   for (int i = threadIdx.x; i < B * T; i += blockDim.x) {
@@ -106,7 +155,7 @@ __global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* __restri
   cl = block_sum(cl, red);
   if (threadIdx.x == 0) {
     const float cem = ce / (float)(B * (T1 - 1));
-    const float regm = alpha_c * (reg * inv_bl);
+    const float regm = alpha_c * (reg * (1.0f / (float)(B * L)));
     out[0] = cem + regm;
     out[1] = cem;
     out[2] = regm;
@@ -143,7 +192,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const TT* __restrict__ pr
 }  // namespace
 
 extern "C" size_t sat_caption_loss_workspace_bytes(int B, int T, int L) {
-  return ((size_t)B * (T - 1) * kStat + (size_t)B * L + 64) * sizeof(float);
+  return ((size_t)B * (T - 1) * kStat + (size_t)B * L + sat_cdiv((long)B * L, 256) + 64) * sizeof(float);
 }
 
 extern "C" int sat_caption_loss_forward(int B, int T, int V, int L, int dtype, const void* preds, const float* alphas,
@@ -159,8 +208,12 @@ extern "C" int sat_caption_loss_forward(int B, int T, int V, int L, int dtype, c
   else
     hipLaunchKernelGGL(loss_rows_kernel<float>, dim3(R), dim3(256), 0, s, (const float*)preds, captions, B, T, V, pad_id, stats);
   SAT_LAUNCH_CHECK();
-  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(1024), 0, s, stats, alphas, captions, B, T, L, alpha_c, skip0,
-                     skip1, skip2, dreg, out);
+  float* part = dreg + (size_t)B * L;
+  const int nparts = sat_cdiv((long)B * L, 256);
+  hipLaunchKernelGGL(loss_reg_kernel, dim3(nparts), dim3(256), 0, s, alphas, B, T - 1, L, alpha_c, dreg, part);
+  SAT_LAUNCH_CHECK();
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(1024), 0, s, stats, (const float*)part, nparts, captions, B, T,
+                     L, alpha_c, skip0, skip1, skip2, out);
   return (int)hipGetLastError();
 }
 

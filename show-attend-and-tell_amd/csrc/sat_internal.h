@@ -106,9 +106,17 @@ int sat_row_sum_accumulate(const float* X, int R, int N, float* out, hipStream_t
 int sat_tokens_from_captions(const int64_t* caps, int B, int T, int T1, int32_t* tok, hipStream_t s);
 size_t sat_attention_part_floats(int B, int L, int D, int dtype);
 
-// sum of `n` partial slabs (n <= 1: plain read)
+// sum of `n` partial slabs (n <= 1: plain read).  Three independent accumulators keep several
+// slab loads in flight (a single running sum serialises one L2 round trip per slab).
 __device__ __forceinline__ float sum_parts(const float* p, long idx, int n, long stride) {
-  float v = p[idx];
-  for (int s = 1; s < n; ++s) v += p[idx + s * stride];
-  return v;
+  float a0 = p[idx];
+  if (n <= 1) return a0;
+  float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = 1;
+  for (; s + 2 < n; s += 3) {
+    const float x1 = p[idx + s * stride], x2 = p[idx + (s + 1) * stride], x3 = p[idx + (s + 2) * stride];
+    a1 += x1; a2 += x2; a3 += x3;
+  }
+  for (; s < n; ++s) a1 += p[idx + s * stride];
+  return (a0 + a1) + (a2 + a3);
 }
