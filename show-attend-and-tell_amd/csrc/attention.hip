@@ -56,49 +56,81 @@ __device__ __forceinline__ void loadv(const T* p, float* o) {  // 16 bytes
   for (int j = 0; j < V16<T>::N; ++j) o[j] = (float)h[j];
 }
 
+// Loops over the L annotation slots keep UNR slots' loads in flight per wave (the scores, the
+// context and the backward reductions are otherwise one L2 round trip per slot).
+constexpr int UNR = 4;
+
+template <typename T>
+__device__ __forceinline__ uint4 ld16(const T* p, bool ok) {
+  return ok ? *(const uint4*)p : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// 16-byte float4 pair / quad of `n` partial slabs with two independent accumulators
+__device__ __forceinline__ float4 f4add(float4 x, float4 y) { return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w); }
+__device__ __forceinline__ float4 sum_parts4(const float* p, long idx, int n, long stride) {
+  float4 a0 = *(const float4*)(p + idx);
+  if (n <= 1) return a0;
+  float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f);
+  int sp = 1;
+  for (; sp + 1 < n; sp += 2) {
+    const float4 x = *(const float4*)(p + idx + sp * stride), y = *(const float4*)(p + idx + (sp + 1) * stride);
+    a0 = f4add(a0, x); a1 = f4add(a1, y);
+  }
+  if (sp < n) a0 = f4add(a0, *(const float4*)(p + idx + sp * stride));
+  return f4add(a0, a1);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
-  constexpr int VD = V16<T>::N;
+  constexpr int VN = V16<T>::N;            // elements per 16-byte vector
+  constexpr int CH = 1024 / (64 * VN);     // e-chunks per lane for E <= 1024
   __shared__ float s_alpha[kMaxL];
-  __shared__ float s_red[4][64 * VD];
+  __shared__ float s_red[4][64 * VN];
   const int b = blockIdx.x, s = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = a.L, D = a.D, E = a.E;
   const T* Ws = (const T*)a.Ws + (long)b * L * E;
   const float* uh = a.uh + (long)b * a.uh_ld;
 
-  // ---- scores: lane holds its E-chunks of (U h + b) and v in registers ----
-  constexpr int CH = 4;   // E <= 1024 = 4 chunks of 64 lanes x 4
-  float u_r[CH][4], v_r[CH][4];
+  // ---- scores: lane owns VN consecutive e per chunk; (U h + b) and v live in registers ----
+  float u_r[CH][VN], v_r[CH][VN];
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
-    const int e = c * 256 + lane * 4;
+    const int e = c * 64 * VN + lane * VN;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { u_r[c][j] = 0.f; v_r[c][j] = 0.f; }
-    if (e < E) {
-      for (int sp = 0; sp < (a.hg_splits > 1 ? a.hg_splits : 1); ++sp) {
-        const float4 u2 = *(const float4*)(uh + sp * a.hg_split_stride + e);
-        u_r[c][0] += u2.x; u_r[c][1] += u2.y; u_r[c][2] += u2.z; u_r[c][3] += u2.w;
+    for (int j = 0; j < VN; j += 4) {
+      float4 u4 = make_float4(0.f, 0.f, 0.f, 0.f), v4 = u4;
+      if (e < E) {
+        u4 = sum_parts4(uh, e + j, a.hg_splits, a.hg_split_stride);
+        v4 = *(const float4*)(a.v_w + e + j);
       }
-      const float4 vv = *(const float4*)(a.v_w + e);
-      v_r[c][0] = vv.x; v_r[c][1] = vv.y; v_r[c][2] = vv.z; v_r[c][3] = vv.w;
+      u_r[c][j] = u4.x; u_r[c][j + 1] = u4.y; u_r[c][j + 2] = u4.z; u_r[c][j + 3] = u4.w;
+      v_r[c][j] = v4.x; v_r[c][j + 1] = v4.y; v_r[c][j + 2] = v4.z; v_r[c][j + 3] = v4.w;
     }
   }
   const float bv = a.v_b[0];
-  for (int l = w; l < L; l += 4) {
-    const T* wr = Ws + (long)l * E;
-    float acc = 0.f;
+  for (int l0 = w; l0 < L; l0 += 4 * UNR) {
+    uint4 xv[UNR][CH];
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int e = c * 256 + lane * 4;
-      if (e >= E) break;
-      float x[4];
-      load4<T>(wr + e, x);
+    for (int u = 0; u < UNR; ++u)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc += v_r[c][j] * tanh_t<T>(x[j] + u_r[c][j]);
+      for (int c = 0; c < CH; ++c) {
+        const int l = l0 + 4 * u, e = c * 64 * VN + lane * VN;
+        xv[u][c] = ld16(Ws + (long)l * E + e, l < L && e < E);
+      }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const T* h = (const T*)&xv[u][c];
+#pragma unroll
+        for (int j = 0; j < VN; ++j) acc += v_r[c][j] * tanh_t<T>((float)h[j] + u_r[c][j]);   // v = 0 past E
+      }
+      acc = wave_sum(acc);
+      const int l = l0 + 4 * u;
+      if (lane == 0 && l < L) s_alpha[l] = acc + bv;
     }
-    acc = wave_sum(acc);
-    if (lane == 0) s_alpha[l] = acc + bv;
   }
   __syncthreads();
   // ---- softmax over L (one wave) ----
@@ -124,26 +156,32 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
     for (int e = tid; e < E; e += 256) a.uh_save[(long)b * a.uh_save_ld + e] = sum_parts(uh, e, a.hg_splits, a.hg_split_stride);
   }
   __syncthreads();
-  // ---- context for this D-slice ----
-  const int d0 = s * 64 * VD + lane * VD;
-  float part[VD];
+  // ---- context for this D-slice: lanes over d (16-byte loads), waves over l ----
+  const int d0 = s * 64 * VN + lane * VN;
+  float part[VN];
 #pragma unroll
-  for (int j = 0; j < VD; ++j) part[j] = 0.f;
-  if (d0 < D) {
-    const T* ab = (const T*)a.a + (long)b * L * D + d0;
-    for (int l = w; l < L; l += 4) {
-      float x[VD];
-      loadv<T>(ab + (long)l * D, x);
-      const float al = s_alpha[l];
+  for (int j = 0; j < VN; ++j) part[j] = 0.f;
+  const T* ab = (const T*)a.a + (long)b * L * D + d0;
+  for (int l0 = w; l0 < L; l0 += 4 * UNR) {
+    uint4 xa[UNR];
 #pragma unroll
-      for (int j = 0; j < VD; ++j) part[j] += al * x[j];
+    for (int u = 0; u < UNR; ++u) xa[u] = ld16(ab + (long)(l0 + 4 * u) * D, l0 + 4 * u < L && d0 < D);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int l = l0 + 4 * u;
+      if (l < L) {
+        const float al = s_alpha[l];
+        const T* h = (const T*)&xa[u];
+#pragma unroll
+        for (int j = 0; j < VN; ++j) part[j] += al * (float)h[j];
+      }
     }
   }
 #pragma unroll
-  for (int j = 0; j < VD; ++j) s_red[w][lane * VD + j] = part[j];
+  for (int j = 0; j < VN; ++j) s_red[w][lane * VN + j] = part[j];
   __syncthreads();
-  for (int i = tid; i < 64 * VD; i += 256) {
-    const int d = s * 64 * VD + i;
+  for (int i = tid; i < 64 * VN; i += 256) {
+    const int d = s * 64 * VN + i;
     if (d >= D) continue;
     // fixed summation order over the four wave partials
     const float c = (s_red[0][i] + s_red[1][i]) + (s_red[2][i] + s_red[3][i]);
@@ -171,11 +209,7 @@ __global__ __launch_bounds__(256) void attn_bwd1_kernel(AttnBwdArgs a) {
     float dg[VD], g[VD], c[VD], dx[VD];
 #pragma unroll
     for (int j = 0; j < VD; j += 4) {
-      float4 q = *(const float4*)(a.d_gated + (long)b * a.d_gated_ld + d0 + j);
-      for (int sp = 1; sp < a.dg_splits; ++sp) {
-        const float4 q2 = *(const float4*)(a.d_gated + sp * a.dg_split_stride + (long)b * a.d_gated_ld + d0 + j);
-        q.x += q2.x; q.y += q2.y; q.z += q2.z; q.w += q2.w;
-      }
+      const float4 q = sum_parts4(a.d_gated, (long)b * a.d_gated_ld + d0 + j, a.dg_splits, a.dg_split_stride);
       const float4 gg = *(const float4*)(a.gate + (long)b * a.gate_ld + d0 + j);
       const float4 cc = *(const float4*)(a.ctx + (long)b * a.ctx_ld + d0 + j);
       dg[j] = q.x; dg[j + 1] = q.y; dg[j + 2] = q.z; dg[j + 3] = q.w;
@@ -198,34 +232,39 @@ __global__ __launch_bounds__(256) void attn_bwd1_kernel(AttnBwdArgs a) {
       }
     }
   }
-  const T* ab = (const T*)a.a + (long)b * L * D;
-  for (int l = w; l < L; l += 4) {
-    float p = 0.f;
-    if (d0 < D) {
-      float x[VD];
-      loadv<T>(ab + (long)l * D + d0, x);
+  const T* ab = (const T*)a.a + (long)b * L * D + d0;
+  for (int l0 = w; l0 < L; l0 += 4 * UNR) {
+    uint4 xa[UNR];
 #pragma unroll
-      for (int j = 0; j < VD; ++j) p += dctx[j] * x[j];
+    for (int u = 0; u < UNR; ++u) xa[u] = ld16(ab + (long)(l0 + 4 * u) * D, l0 + 4 * u < L && d0 < D);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const T* h = (const T*)&xa[u];
+      float p = 0.f;
+#pragma unroll
+      for (int j = 0; j < VD; ++j) p += dctx[j] * (float)h[j];
+      p = wave_sum(p);
+      const int l = l0 + 4 * u;
+      if (lane == 0 && l < L) a.part[((long)b * NS + s) * L + l] = p;
     }
-    p = wave_sum(p);
-    if (lane == 0) a.part[((long)b * NS + s) * L + l] = p;
   }
   (void)E;
 }
 
+// one workgroup of 8 waves per batch row; lane owns VN consecutive e per chunk
 template <typename T>
-__global__ __launch_bounds__(256) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
-  constexpr int kMaxE = 1024;
+__global__ __launch_bounds__(512) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
+  constexpr int NW = 8, VN = V16<T>::N, CH = 1024 / (64 * VN);
   __shared__ float s_de[kMaxL];
-  __shared__ float s_red[4][kMaxE];
-  __shared__ float s_tmp[4];
+  __shared__ float s_red[NW][1024];
+  __shared__ float s_tmp[NW];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = a.L, E = a.E;
   const float* alpha = a.alpha + (long)b * a.alpha_ld;
   // dL/dalpha and sum_l alpha*dalpha
   float loc = 0.f;
-  for (int l = tid; l < L; l += 256) {
+  for (int l = tid; l < L; l += NW * 64) {
     float da = 0.f;
     for (int s = 0; s < NS; ++s) da += a.part[((long)b * NS + s) * L + l];
     if (a.d_alpha_ext) da += a.d_alpha_ext[(long)b * a.d_alpha_ext_ld + l];
@@ -235,56 +274,81 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
   loc = wave_sum(loc);
   if (lane == 0) s_tmp[w] = loc;
   __syncthreads();
-  const float sad = (s_tmp[0] + s_tmp[1]) + (s_tmp[2] + s_tmp[3]);
-  for (int l = tid; l < L; l += 256) s_de[l] = alpha[l] * (s_de[l] - sad);
+  float sad = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; i += 2) sad += s_tmp[i] + s_tmp[i + 1];
   __syncthreads();
-  // recompute tanh, accumulate
+  for (int l = tid; l < L; l += NW * 64) s_de[l] = alpha[l] * (s_de[l] - sad);
+  __syncthreads();
+  // recompute tanh, accumulate (U h + b and v are loop-invariant: registers)
   const float* uh = a.uh + (long)b * a.uh_ld;
   const T* Ws = (const T*)a.Ws + (long)b * L * E;
   float* dWs = a.dWs_acc + (long)b * L * E;
-  constexpr int CH = kMaxE / 256;  // e-chunks of 4 per lane
-  float duh[CH][4], dv[CH][4];
+  float uu[CH][VN], vw[CH][VN], duh[CH][VN], dv[CH][VN];
 #pragma unroll
-  for (int c = 0; c < CH; ++c)
+  for (int c = 0; c < CH; ++c) {
+    const int e = c * 64 * VN + lane * VN;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { duh[c][j] = 0.f; dv[c][j] = 0.f; }
-  float dbv = 0.f;
-  for (int l = w; l < L; l += 4) {
-    const float de = s_de[l];
-    dbv += de;
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int e = c * 256 + lane * 4;
-      if (e >= E) break;
-      float x[4];
-      load4<T>(Ws + (long)l * E + e, x);
-      float4 u = *(const float4*)(uh + e);
-      float4 vv = *(const float4*)(a.v_w + e);
-      float uu[4] = {u.x, u.y, u.z, u.w}, vw[4] = {vv.x, vv.y, vv.z, vv.w};
-      float4 acc = *(float4*)(dWs + (long)l * E + e);
-      float ac[4] = {acc.x, acc.y, acc.z, acc.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float t = tanh_t<T>(x[j] + uu[j]);
-        const float datt = de * vw[j] * (1.f - t * t);
-        duh[c][j] += datt;
-        dv[c][j] += de * t;
-        ac[j] += datt;
-      }
-      *(float4*)(dWs + (long)l * E + e) = make_float4(ac[0], ac[1], ac[2], ac[3]);
+    for (int j = 0; j < VN; ++j) {
+      uu[c][j] = e < E ? uh[e + j] : 0.f;
+      vw[c][j] = e < E ? a.v_w[e + j] : 0.f;
+      duh[c][j] = 0.f;
+      dv[c][j] = 0.f;
     }
   }
-  // fold waves: dU_h
+  float dbv = 0.f;
+  for (int l0 = w; l0 < L; l0 += NW * 2) {
+    uint4 xw[2][CH];
+    float4 acc[2][CH][VN / 4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int l = l0 + NW * u, e = c * 64 * VN + lane * VN;
+        const bool ok = l < L && e < E;
+        xw[u][c] = ld16(Ws + (long)l * E + e, ok);
+#pragma unroll
+        for (int q = 0; q < VN / 4; ++q)
+          acc[u][c][q] = ok ? *(const float4*)(dWs + (long)l * E + e + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int l = l0 + NW * u;
+      if (l >= L) continue;
+      const float de = s_de[l];
+      dbv += de;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int e = c * 64 * VN + lane * VN;
+        if (e >= E) continue;
+        const T* h = (const T*)&xw[u][c];
+        float* ac = (float*)&acc[u][c][0];
+#pragma unroll
+        for (int j = 0; j < VN; ++j) {
+          const float t = tanh_t<T>((float)h[j] + uu[c][j]);
+          const float datt = de * vw[c][j] * (1.f - t * t);
+          duh[c][j] += datt;
+          dv[c][j] += de * t;
+          ac[j] += datt;
+        }
+#pragma unroll
+        for (int q = 0; q < VN / 4; ++q) *(float4*)(dWs + (long)l * E + e + 4 * q) = acc[u][c][q];
+      }
+    }
+  }
+  // fold the waves (fixed order): dU_h, then dv
 #pragma unroll
   for (int c = 0; c < CH; ++c)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = c * 256 + lane * 4 + j;
+    for (int j = 0; j < VN; ++j) {
+      const int e = c * 64 * VN + lane * VN + j;
       if (e < E) s_red[w][e] = duh[c][j];
     }
   __syncthreads();
-  for (int e = tid; e < E; e += 256) {
-    const float v = (s_red[0][e] + s_red[1][e]) + (s_red[2][e] + s_red[3][e]);
+  for (int e = tid; e < E; e += NW * 64) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; i += 2) v += s_red[i][e] + s_red[i + 1][e];
     a.d_uh[(long)b * a.d_uh_ld + e] = v;
     if (a.d_uh_t) ((T*)a.d_uh_t)[(long)b * a.d_uh_ld + e] = (T)v;
   }
@@ -292,23 +356,33 @@ __global__ __launch_bounds__(256) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
 #pragma unroll
   for (int c = 0; c < CH; ++c)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int e = c * 256 + lane * 4 + j;
+    for (int j = 0; j < VN; ++j) {
+      const int e = c * 64 * VN + lane * VN + j;
       if (e < E) s_red[w][e] = dv[c][j];
     }
   dbv = wave_sum(dbv);
   if (lane == 0) s_tmp[w] = dbv;
   __syncthreads();
-  for (int e = tid; e < E; e += 256)
-    a.dv_acc[(long)b * E + e] += (s_red[0][e] + s_red[1][e]) + (s_red[2][e] + s_red[3][e]);
-  if (tid == 0) a.dbv_acc[b] += (s_tmp[0] + s_tmp[1]) + (s_tmp[2] + s_tmp[3]);
+  for (int e = tid; e < E; e += NW * 64) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; i += 2) v += s_red[i][e] + s_red[i + 1][e];
+    a.dv_acc[(long)b * E + e] += v;
+  }
+  if (tid == 0) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; i += 2) v += s_tmp[i] + s_tmp[i + 1];
+    a.dbv_acc[b] += v;
+  }
 }
 
 }  // namespace
 
 int sat_attention_fwd_launch(const AttnFwdArgs& a, hipStream_t s) {
-  SAT_REQUIRE(a.L <= kMaxL && a.E % 4 == 0 && a.E <= 1024);
   const int VD = a.dtype == SAT_BF16 ? 8 : 4;
+  SAT_REQUIRE(a.L <= kMaxL && a.E % VD == 0 && a.E <= 1024);
+  SAT_REQUIRE((a.uh_ld % 4) == 0 && (a.hg_splits <= 1 || a.hg_split_stride % 4 == 0));
   SAT_REQUIRE(a.D % VD == 0);
   const int NS = sat_cdiv(a.D, 64 * VD);
   dim3 grid(a.B, NS);
@@ -318,16 +392,16 @@ int sat_attention_fwd_launch(const AttnFwdArgs& a, hipStream_t s) {
 }
 
 int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s) {
-  SAT_REQUIRE(a.L <= kMaxL && a.E % 4 == 0 && a.E <= 1024);
   const int VD = a.dtype == SAT_BF16 ? 8 : 4;
+  SAT_REQUIRE(a.L <= kMaxL && a.E % VD == 0 && a.E <= 1024);
   SAT_REQUIRE(a.D % VD == 0);
   const int NS = sat_cdiv(a.D, 64 * VD);
   if (a.dtype == SAT_BF16) {
     hipLaunchKernelGGL(attn_bwd1_kernel<bf16>, dim3(a.B, NS), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd2_kernel<bf16>, dim3(a.B), dim3(256), 0, s, a, NS);
+    hipLaunchKernelGGL(attn_bwd2_kernel<bf16>, dim3(a.B), dim3(512), 0, s, a, NS);
   } else {
     hipLaunchKernelGGL(attn_bwd1_kernel<float>, dim3(a.B, NS), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd2_kernel<float>, dim3(a.B), dim3(256), 0, s, a, NS);
+    hipLaunchKernelGGL(attn_bwd2_kernel<float>, dim3(a.B), dim3(512), 0, s, a, NS);
   }
   return (int)hipGetLastError();
 }
