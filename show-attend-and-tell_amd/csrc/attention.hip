@@ -70,27 +70,39 @@ __device__ __forceinline__ float4 f4add(float4 x, float4 y) { return make_float4
 __device__ __forceinline__ float4 sum_parts4(const float* p, long idx, int n, long stride) {
   float4 a0 = *(const float4*)(p + idx);
   if (n <= 1) return a0;
-  float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f), a2 = a1, a3 = a1;
   int sp = 1;
-  for (; sp + 1 < n; sp += 2) {
-    const float4 x = *(const float4*)(p + idx + sp * stride), y = *(const float4*)(p + idx + (sp + 1) * stride);
-    a0 = f4add(a0, x); a1 = f4add(a1, y);
+  for (; sp + 2 < n; sp += 3) {
+    const float4 x = *(const float4*)(p + idx + sp * stride), y = *(const float4*)(p + idx + (sp + 1) * stride),
+                 z = *(const float4*)(p + idx + (sp + 2) * stride);
+    a1 = f4add(a1, x); a2 = f4add(a2, y); a3 = f4add(a3, z);
   }
-  if (sp < n) a0 = f4add(a0, *(const float4*)(p + idx + sp * stride));
-  return f4add(a0, a1);
+  for (; sp < n; ++sp) a1 = f4add(a1, *(const float4*)(p + idx + sp * stride));
+  return f4add(f4add(a0, a1), f4add(a2, a3));
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
+// 8 waves per (row, D-slice) workgroup; each wave scores / accumulates FU slots per batch, and
+// the context rows of the first batch are requested before the scores are computed (they do not
+// depend on alpha), so a step costs ~2 dependent memory round trips for L <= 64.
+constexpr int ANW = 8, FU = 8;
+
+template <typename T, int CH>   // CH = e-chunks of 64 x 16 bytes per lane covering E
+__global__ __launch_bounds__(ANW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
   constexpr int VN = V16<T>::N;            // elements per 16-byte vector
-  constexpr int CH = 1024 / (64 * VN);     // e-chunks per lane for E <= 1024
   __shared__ float s_alpha[kMaxL];
-  __shared__ float s_red[4][64 * VN];
+  __shared__ float s_red[ANW][64 * VN];
   const int b = blockIdx.x, s = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = a.L, D = a.D, E = a.E;
   const T* Ws = (const T*)a.Ws + (long)b * L * E;
   const float* uh = a.uh + (long)b * a.uh_ld;
+  const int d0 = s * 64 * VN + lane * VN;
+  const T* ab = (const T*)a.a + (long)b * L * D + d0;
+
+  // context rows of the first batch: in flight while the scores are formed
+  uint4 xa[FU];
+#pragma unroll
+  for (int u = 0; u < FU; ++u) xa[u] = ld16(ab + (long)(w + ANW * u) * D, w + ANW * u < L && d0 < D);
 
   // ---- scores: lane owns VN consecutive e per chunk; (U h + b) and v live in registers ----
   float u_r[CH][VN], v_r[CH][VN];
@@ -109,17 +121,17 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
     }
   }
   const float bv = a.v_b[0];
-  for (int l0 = w; l0 < L; l0 += 4 * UNR) {
-    uint4 xv[UNR][CH];
+  for (int l0 = w; l0 < L; l0 += ANW * FU) {
+    uint4 xv[FU][CH];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u)
+    for (int u = 0; u < FU; ++u)
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
-        const int l = l0 + 4 * u, e = c * 64 * VN + lane * VN;
+        const int l = l0 + ANW * u, e = c * 64 * VN + lane * VN;
         xv[u][c] = ld16(Ws + (long)l * E + e, l < L && e < E);
       }
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
+    for (int u = 0; u < FU; ++u) {
       float acc = 0.f;
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
@@ -128,7 +140,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
         for (int j = 0; j < VN; ++j) acc += v_r[c][j] * tanh_t<T>((float)h[j] + u_r[c][j]);   // v = 0 past E
       }
       acc = wave_sum(acc);
-      const int l = l0 + 4 * u;
+      const int l = l0 + ANW * u;
       if (lane == 0 && l < L) s_alpha[l] = acc + bv;
     }
   }
@@ -153,22 +165,21 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
     }
   }
   if (s == 0 && a.uh_save) {
-    for (int e = tid; e < E; e += 256) a.uh_save[(long)b * a.uh_save_ld + e] = sum_parts(uh, e, a.hg_splits, a.hg_split_stride);
+    for (int e = tid; e < E; e += ANW * 64) a.uh_save[(long)b * a.uh_save_ld + e] = sum_parts(uh, e, a.hg_splits, a.hg_split_stride);
   }
   __syncthreads();
   // ---- context for this D-slice: lanes over d (16-byte loads), waves over l ----
-  const int d0 = s * 64 * VN + lane * VN;
   float part[VN];
 #pragma unroll
   for (int j = 0; j < VN; ++j) part[j] = 0.f;
-  const T* ab = (const T*)a.a + (long)b * L * D + d0;
-  for (int l0 = w; l0 < L; l0 += 4 * UNR) {
-    uint4 xa[UNR];
+  for (int l0 = w; l0 < L; l0 += ANW * FU) {
+    if (l0 != w) {
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) xa[u] = ld16(ab + (long)(l0 + 4 * u) * D, l0 + 4 * u < L && d0 < D);
+      for (int u = 0; u < FU; ++u) xa[u] = ld16(ab + (long)(l0 + ANW * u) * D, l0 + ANW * u < L && d0 < D);
+    }
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int l = l0 + 4 * u;
+    for (int u = 0; u < FU; ++u) {
+      const int l = l0 + ANW * u;
       if (l < L) {
         const float al = s_alpha[l];
         const T* h = (const T*)&xa[u];
@@ -180,11 +191,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
 #pragma unroll
   for (int j = 0; j < VN; ++j) s_red[w][lane * VN + j] = part[j];
   __syncthreads();
-  for (int i = tid; i < 64 * VN; i += 256) {
+  for (int i = tid; i < 64 * VN; i += ANW * 64) {
     const int d = s * 64 * VN + i;
     if (d >= D) continue;
-    // fixed summation order over the four wave partials
-    const float c = (s_red[0][i] + s_red[1][i]) + (s_red[2][i] + s_red[3][i]);
+    // fixed summation order over the wave partials
+    float c = 0.f;
+#pragma unroll
+    for (int q = 0; q < ANW; q += 2) c += s_red[q][i] + s_red[q + 1][i];
     a.ctx[(long)b * a.ctx_ld + d] = c;
     if (a.ctx_t) ((T*)a.ctx_t)[(long)b * a.ctx_t_ld + d] = (T)c;
     if (a.gate_pre) {
@@ -196,12 +209,17 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnFwdArgs a) {
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void attn_bwd1_kernel(AttnBwdArgs a) {
+__global__ __launch_bounds__(ANW * 64) void attn_bwd1_kernel(AttnBwdArgs a) {
   constexpr int VD = V16<T>::N;
   const int b = blockIdx.x, s = blockIdx.y, NS = gridDim.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = a.L, D = a.D, E = a.E;
   const int d0 = s * 64 * VD + lane * VD;
+  const T* ab = (const T*)a.a + (long)b * L * D + d0;
+  // annotation rows of the first batch: independent of dL/dcontext, requested first
+  uint4 xa[FU];
+#pragma unroll
+  for (int u = 0; u < FU; ++u) xa[u] = ld16(ab + (long)(w + ANW * u) * D, w + ANW * u < L && d0 < D);
   float dctx[VD];
 #pragma unroll
   for (int j = 0; j < VD; ++j) dctx[j] = 0.f;
@@ -232,19 +250,19 @@ __global__ __launch_bounds__(256) void attn_bwd1_kernel(AttnBwdArgs a) {
       }
     }
   }
-  const T* ab = (const T*)a.a + (long)b * L * D + d0;
-  for (int l0 = w; l0 < L; l0 += 4 * UNR) {
-    uint4 xa[UNR];
+  for (int l0 = w; l0 < L; l0 += ANW * FU) {
+    if (l0 != w) {
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) xa[u] = ld16(ab + (long)(l0 + 4 * u) * D, l0 + 4 * u < L && d0 < D);
+      for (int u = 0; u < FU; ++u) xa[u] = ld16(ab + (long)(l0 + ANW * u) * D, l0 + ANW * u < L && d0 < D);
+    }
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
+    for (int u = 0; u < FU; ++u) {
       const T* h = (const T*)&xa[u];
       float p = 0.f;
 #pragma unroll
       for (int j = 0; j < VD; ++j) p += dctx[j] * (float)h[j];
       p = wave_sum(p);
-      const int l = l0 + 4 * u;
+      const int l = l0 + ANW * u;
       if (lane == 0 && l < L) a.part[((long)b * NS + s) * L + l] = p;
     }
   }
@@ -252,9 +270,9 @@ __global__ __launch_bounds__(256) void attn_bwd1_kernel(AttnBwdArgs a) {
 }
 
 // one workgroup of 8 waves per batch row; lane owns VN consecutive e per chunk
-template <typename T>
+template <typename T, int CH>
 __global__ __launch_bounds__(512) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
-  constexpr int NW = 8, VN = V16<T>::N, CH = 1024 / (64 * VN);
+  constexpr int NW = 8, VN = V16<T>::N;
   __shared__ float s_de[kMaxL];
   __shared__ float s_red[NW][1024];
   __shared__ float s_tmp[NW];
@@ -377,6 +395,25 @@ __global__ __launch_bounds__(512) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
   }
 }
 
+// e-chunks per lane: 1, 2 or 4 (E <= 1024)
+inline int e_chunks(int E, int VN) {
+  const int c = sat_cdiv(E, 64 * VN);
+  return c <= 1 ? 1 : (c <= 2 ? 2 : 4);
+}
+
+template <typename T>
+void launch_fwd(int ch, dim3 grid, hipStream_t s, const AttnFwdArgs& a) {
+  if (ch == 1) hipLaunchKernelGGL((attn_fwd_kernel<T, 1>), grid, dim3(ANW * 64), 0, s, a);
+  else if (ch == 2) hipLaunchKernelGGL((attn_fwd_kernel<T, 2>), grid, dim3(ANW * 64), 0, s, a);
+  else hipLaunchKernelGGL((attn_fwd_kernel<T, 4>), grid, dim3(ANW * 64), 0, s, a);
+}
+template <typename T>
+void launch_bwd2(int ch, dim3 grid, hipStream_t s, const AttnBwdArgs& a, int NS) {
+  if (ch == 1) hipLaunchKernelGGL((attn_bwd2_kernel<T, 1>), grid, dim3(512), 0, s, a, NS);
+  else if (ch == 2) hipLaunchKernelGGL((attn_bwd2_kernel<T, 2>), grid, dim3(512), 0, s, a, NS);
+  else hipLaunchKernelGGL((attn_bwd2_kernel<T, 4>), grid, dim3(512), 0, s, a, NS);
+}
+
 }  // namespace
 
 int sat_attention_fwd_launch(const AttnFwdArgs& a, hipStream_t s) {
@@ -386,8 +423,8 @@ int sat_attention_fwd_launch(const AttnFwdArgs& a, hipStream_t s) {
   SAT_REQUIRE(a.D % VD == 0);
   const int NS = sat_cdiv(a.D, 64 * VD);
   dim3 grid(a.B, NS);
-  if (a.dtype == SAT_BF16) hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, s, a);
+  if (a.dtype == SAT_BF16) launch_fwd<bf16>(e_chunks(a.E, 8), grid, s, a);
+  else launch_fwd<float>(e_chunks(a.E, 4), grid, s, a);
   return (int)hipGetLastError();
 }
 
@@ -397,11 +434,11 @@ int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s) {
   SAT_REQUIRE(a.D % VD == 0);
   const int NS = sat_cdiv(a.D, 64 * VD);
   if (a.dtype == SAT_BF16) {
-    hipLaunchKernelGGL(attn_bwd1_kernel<bf16>, dim3(a.B, NS), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd2_kernel<bf16>, dim3(a.B), dim3(512), 0, s, a, NS);
+    hipLaunchKernelGGL(attn_bwd1_kernel<bf16>, dim3(a.B, NS), dim3(ANW * 64), 0, s, a);
+    launch_bwd2<bf16>(e_chunks(a.E, 8), dim3(a.B), s, a, NS);
   } else {
-    hipLaunchKernelGGL(attn_bwd1_kernel<float>, dim3(a.B, NS), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd2_kernel<float>, dim3(a.B), dim3(512), 0, s, a, NS);
+    hipLaunchKernelGGL(attn_bwd1_kernel<float>, dim3(a.B, NS), dim3(ANW * 64), 0, s, a);
+    launch_bwd2<float>(e_chunks(a.E, 4), dim3(a.B), s, a, NS);
   }
   return (int)hipGetLastError();
 }

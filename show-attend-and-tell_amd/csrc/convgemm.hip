@@ -513,7 +513,9 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   }
   a.xcd_remap = g_xcd_remap;
   dim3 grid(sat_cdiv(g.N, bn), sat_cdiv(g.M, bm), a.splitk);
-  const int ns = g_force_stages ? g_force_stages : 2;
+  // skinny partial-split GEMMs run 2-4 k-tiles per block: a 3-deep ring puts the first two in
+  // flight at once (their block counts leave LDS occupancy irrelevant)
+  const int ns = g_force_stages ? g_force_stages : (partial ? 3 : 2);
   if (at && bt) launch_tile<true, true>(tcfg, ns, grid, s, a);
   else if (at) launch_tile<true, false>(tcfg, ns, grid, s, a);
   else if (bt) launch_tile<false, true>(tcfg, ns, grid, s, a);

@@ -146,13 +146,15 @@ def test_decoder_eval_matches_reference(sat, path):
 
 
 def _fp64_oracle_grads(g):
-    """The oracle's gradients for a golden case computed in float64 (the fp32 noise gauge)."""
+    """The oracle's gradients and post-Adam weights for a golden case computed in float64 (the
+    fp32 noise gauge)."""
     c = g["cfg"]
     p = {k: v.double() for k, v in params_for(c).items()}
-    _, grads, _, _, _ = O.train_step(p, tt(g["img_features"]).double(), tt(g["captions"]), tf=c["tf"], ado=c["ado"],
+    _, grads, newp, _, _ = O.train_step(p, tt(g["img_features"]).double(), tt(g["captions"]), tf=c["tf"], ado=c["ado"],
                                      attention=c["attention"], bert=c["bert"], alpha_c=c["alpha_c"], lr=c["lr"],
                                      training=True, dropout_masks=masks_for(c).double(), adam_state={})
-    return {k: v.reshape(-1).double() for k, v in grads.items()}
+    return ({k: v.reshape(-1).double() for k, v in grads.items()},
+            {k: v.reshape(-1).double() for k, v in newp.items()})
 
 
 @pytest.mark.parametrize("path", fixture_paths(), ids=fixture_ids())
@@ -175,7 +177,7 @@ def test_decoder_train_step_matches_reference(sat, path):
     params = dict(dec.named_parameters())
     have = sorted(n for n, p in params.items() if p.grad is not None)
     assert have == sorted(g["grad_names"])
-    g64 = _fp64_oracle_grads(g)
+    g64, w64 = _fp64_oracle_grads(g)
     for name in g["grad_names"]:
         gr = params[name].grad.detach().reshape(-1).double().cpu()
         ref_norm = math.sqrt(float(g[f"gsq::{name}"]))
@@ -200,8 +202,12 @@ def test_decoder_train_step_matches_reference(sat, path):
             continue
         idx = torch.from_numpy(g[f"gidx::{name}"])
         w = params[name].detach().reshape(-1).cpu()[idx].double()
-        # an Adam update is bounded by ~lr: compare the post-step weights at lr scale
-        assert (w - torch.from_numpy(g[f"pval::{name}"]).double()).abs().max().item() <= 2e-3 * c["lr"] + 1e-6, name
+        ref_w = torch.from_numpy(g[f"pval::{name}"]).double()
+        # an Adam update is bounded by ~lr: compare the post-step weights at lr scale, or at the
+        # reference's own fp32-vs-fp64 distance where a near-zero gradient makes the first Adam
+        # step (g / (|g| + eps)) rounding-sensitive
+        noise = (w64[name][idx] - ref_w).abs().max().item()
+        assert (w - ref_w).abs().max().item() <= max(2e-3 * c["lr"] + 1e-6, 2 * noise), name
 
 
 @pytest.mark.parametrize("path", fixture_paths()[:3], ids=fixture_ids()[:3])
