@@ -153,8 +153,17 @@ __global__ void colsum_final_kernel(const float* __restrict__ part, int RS, int 
                                     int accumulate, float* __restrict__ out2) {
   int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
-  float s = 0.f;
-  for (int i = 0; i < RS; ++i) s += part[(long)i * N + n];
+  // four independent partial sums (a single chain serialises RS L2 round trips), fixed order
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int i = 0;
+  for (; i + 4 <= RS; i += 4) {
+    s0 += part[(long)i * N + n];
+    s1 += part[(long)(i + 1) * N + n];
+    s2 += part[(long)(i + 2) * N + n];
+    s3 += part[(long)(i + 3) * N + n];
+  }
+  for (; i < RS; ++i) s0 += part[(long)i * N + n];
+  const float s = (s0 + s1) + (s2 + s3);
   out[n] = accumulate ? out[n] + s : s;
   if (out2) out2[n] = accumulate ? out2[n] + s : s;
 }
