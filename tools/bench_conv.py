@@ -14,7 +14,7 @@ SHAPES = [("L1_c1", 56, 256, 64, 1, 1, 0, 0), ("L1_c2", 56, 64, 64, 3, 1, 1, 0),
           ("L3_c1", 14, 1024, 256, 1, 1, 0, 0), ("L3_c2", 14, 256, 256, 3, 1, 1, 0), ("L3_c3", 14, 256, 1024, 1, 1, 0, 1),
           ("L4_c2", 7, 512, 512, 3, 1, 1, 0), ("stem", 224, 8, 64, 7, 2, 3, 0)]
 # (stages, tile, xcd_remap); tile ids: 1 128x128/8w, 2 128x64/8w, 3 128x128/4w, 4 128x256/8w, 5 256x128/8w
-CONFIGS = [(2, 1, 0), (2, 1, 1), (3, 1, 1), (2, 2, 1), (2, 3, 1), (2, 4, 1), (2, 5, 1)]
+CONFIGS = [tuple(int(v) for v in c.split(',')) for c in os.environ.get('CONFIGS', '2,1,1;3,2,1;2,2,1').split(';')]
 TNAME = {1: "128x128w8", 2: "128x64w8", 3: "128x128w4", 4: "128x256w8", 5: "256x128w8"}
 lib = sat_amd._lib.lib()
 res = {}
