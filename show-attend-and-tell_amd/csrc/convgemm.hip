@@ -83,8 +83,6 @@ __device__ __forceinline__ const void* sel(bool ok, const void* p, const void* z
 template <int N>
 __device__ __forceinline__ void wait_vm_barrier() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)\n\ts_barrier" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
@@ -281,26 +279,17 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
   const int cc = tid % CPR, r0 = tid / CPR;
   const int col = n0 + cc * 8;
   const bool vec_ok = (a.ldc % 8 == 0) && (!a.add1 || a.ld_add1 % 8 == 0) && col + 8 <= N;
-  // the bf16 residual (the bottleneck's identity branch) is requested right after the DMA of the
-  // LAST k-tile, so its HBM latency overlaps that tile's wait + compute; the wait for the last
-  // tile then leaves these ITER loads outstanding (2-stage ring only)
+  // the bf16 residual (the bottleneck's identity branch) is requested now, so its HBM latency
+  // overlaps the main loop instead of sitting in the epilogue
   uint4 res[ITER];
-  // wave-uniform condition (kernel arguments only): every lane of every wave issues the loads
-  const bool res_pre = NS == 2 && a.add1 && a.add1_bf16 && a.splitk <= 1 && nk >= 1 && a.ldc % 8 == 0 &&
-                       a.ld_add1 % 8 == 0 && N % 8 == 0;
-  const int col_c = min(col, N - 8);   // lanes past N load a valid (unused) chunk
-  auto load_res = [&]() {   // exactly ITER loads per wave (rows clamped), as the counted wait assumes
-    // keep them younger than the last tile's DMA in issue order (vmcnt(ITER) relies on it)
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
+  const bool res_pre = a.add1 && a.add1_bf16 && vec_ok && a.splitk <= 1;
+  if (res_pre) {
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
-      const int row = min(m0 + r0 + it * RPP, M - 1);
-      res[it] = *(const uint4*)((const bf16*)a.add1 + (long)row * a.ld_add1 + col_c);
+      const int row = m0 + r0 + it * RPP;
+      res[it] = row < M ? *(const uint4*)((const bf16*)a.add1 + (long)row * a.ld_add1 + col) : make_uint4(0, 0, 0, 0);
     }
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  if (res_pre && nk == 1) load_res();
+  }
   for (int kt = 0; kt < nk; ++kt) {
     const int after = min(NS - 2, nk - 1 - kt);   // stages issued after tile kt (uniform)
     if constexpr (NS >= 4) {
@@ -311,13 +300,9 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
       if (after == 1) wait_vm_barrier<INSTR>();
       else wait_vm_barrier<0>();
     } else {
-      if (res_pre && kt == nk - 1) wait_vm_barrier<ITER>();
-      else wait_vm_barrier<0>();
+      wait_vm_barrier<0>();
     }
-    if (kt + NS - 1 < nk) {
-      stage((kt + NS - 1) % NS, kbeg + (kt + NS - 1) * BK);
-      if (res_pre && kt + NS - 1 == nk - 1) load_res();
-    }
+    if (kt + NS - 1 < nk) stage((kt + NS - 1) % NS, kbeg + (kt + NS - 1) * BK);
     compute(kt % NS);
   }
   __syncthreads();   // every wave done reading the ring before the epilogue reuses the LDS
