@@ -271,25 +271,6 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < nk) stage(p, kbeg + p * BK);
-
-  // epilogue mapping: every thread owns 16-byte pieces of BN-wide row segments
-  constexpr int CPR = BN / 8;                  // 8-column chunks per tile row
-  constexpr int RPP = NW * 64 / CPR;           // rows per pass
-  constexpr int ITER = BM / RPP;
-  const int cc = tid % CPR, r0 = tid / CPR;
-  const int col = n0 + cc * 8;
-  const bool vec_ok = (a.ldc % 8 == 0) && (!a.add1 || a.ld_add1 % 8 == 0) && col + 8 <= N;
-  // the bf16 residual (the bottleneck's identity branch) is requested now, so its HBM latency
-  // overlaps the main loop instead of sitting in the epilogue
-  uint4 res[ITER];
-  const bool res_pre = a.add1 && a.add1_bf16 && vec_ok && a.splitk <= 1;
-  if (res_pre) {
-#pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-      const int row = m0 + r0 + it * RPP;
-      res[it] = row < M ? *(const uint4*)((const bf16*)a.add1 + (long)row * a.ld_add1 + col) : make_uint4(0, 0, 0, 0);
-    }
-  }
   for (int kt = 0; kt < nk; ++kt) {
     const int after = min(NS - 2, nk - 1 - kt);   // stages issued after tile kt (uniform)
     if constexpr (NS >= 4) {
@@ -334,13 +315,22 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
       for (int r = 0; r < 4; ++r)
         ep[(wm * WTM + i * 16 + fh * 4 + r) * EPI_LD + wn * WTN + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
+  constexpr int CPR = BN / 8;                  // 8-column chunks per tile row
+  constexpr int RPP = NW * 64 / CPR;           // rows per pass
+  constexpr int ITER = BM / RPP;
+  const int tid2 = threadIdx.x;
+  const int cc = tid2 % CPR, r0 = tid2 / CPR;
+  const int col = n0 + cc * 8;
+  const bool vec_ok = (a.ldc % 8 == 0) && (!a.add1 || a.ld_add1 % 8 == 0) && col + 8 <= N;
   void* const Cb = a.partial ? (void*)((float*)a.C + split * a.split_stride) : a.C;
   const float* const bias = (a.partial && split > 0) ? nullptr : a.bias;
   float bias8[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bias8[e] = (bias && col + e < N) ? bias[col + e] : 0.f;
   if (vec_ok) {
-    if (a.add1 && a.add1_bf16 && !res_pre) {
+    // all residual loads of this thread go out before the first store
+    uint4 res[ITER];
+    if (a.add1 && a.add1_bf16) {
 #pragma unroll
       for (int it = 0; it < ITER; ++it) {
         const int row = m0 + r0 + it * RPP;
