@@ -490,3 +490,35 @@ def test_fast_gemm_tile_configs_fp32_out(sat, tile):
     finally:
         lib.sat_fast_gemm_set_config(0, 0, 1)
     assert rel(C, ref) < 2e-5
+
+
+def test_bleu4_parity_teacher_forced(sat):
+    """The BLEU-4 half of the metric: teacher-forced evaluation (train.py:198-336) of a
+    fixed synthetic validation set through the HIP path (fp32) and the oracle gives identical
+    greedy ids, hence identical BLEU-1..4 under the restated corpus_bleu (non-trivial scores:
+    references are the oracle's own ids with every fifth token replaced)."""
+    from sat_amd import bleu as B
+    V, D, L, Bn, T = 300, 64, 16, 12, 14
+    p = O.make_decoder_params(V, D, 512, True, 23)
+    dec = sat.Decoder(V, D, tf=True, ado=True, attention=True)
+    dec.load_state_dict(p, strict=True)
+    dec = dec.to(DEV).eval()
+    feats = torch.from_numpy(np.random.default_rng(24).standard_normal((Bn, L, D)).astype(np.float32))
+    caps = O.make_captions(Bn, T, V, 25)
+    with torch.no_grad():
+        preds, _ = dec(feats.to(DEV), caps.to(DEV))
+        ref_preds, _, _ = O.decoder_forward(p, feats, caps, tf=True, ado=True, attention=True)
+    ids, ref_ids = preds.argmax(2).cpu(), ref_preds.argmax(2)
+    assert torch.equal(ids, ref_ids)
+    word_dict = {"<start>": 0, "<eos>": 1, "<unk>": 2, "<pad>": 3}
+    word_dict.update({f"w{i}": i for i in range(4, V)})
+    inv = {i: w for w, i in word_dict.items()}
+    refs = [[B.decode_plain([(t + 7) % V if k % 5 == 4 else t for k, t in enumerate(row)], word_dict, inv)]
+            for row in ref_ids.tolist()]
+    hyp = [B.decode_plain(r, word_dict, inv) for r in ids.tolist()]
+    hyp_o = [B.decode_plain(r, word_dict, inv) for r in ref_ids.tolist()]
+    ours = B.bleu_1_to_4(refs, hyp)
+    theirs = tuple(O.corpus_bleu(refs, hyp_o, weights=w) for w in
+                   ((1, 0, 0, 0), (0.5, 0.5, 0, 0), (0.33, 0.33, 0.33, 0), (0.25, 0.25, 0.25, 0.25)))
+    assert ours == theirs
+    assert 0.0 < ours[3] < 1.0
