@@ -11,7 +11,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsat_hip.so")
+LIB_PATH = os.environ.get("SAT_HIP_LIB_TUNING") or os.path.join(_HERE, "libsat_hip.so")   # override: A/B builds only
 
 SAT_F32, SAT_BF16 = 0, 1
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_SIGMOID = 0, 1, 2, 3

@@ -18,6 +18,13 @@
 //   * v_mfma_f32_16x16x32_bf16, fp32 accumulation; the epilogue stages each wave's
 //     64 x BN/2 fp32 tile in LDS and writes 16-byte row segments (bias, residual add,
 //     activation and the bf16 conversion fused).
+// Measured limits (profiles/r1_s8_conv_ablation.txt, taken with a temporary ablation build): the
+// main loop is bound by the per-CU L2 -> LDS DMA rate and the LDS fragment traffic of 64x32 wave
+// tiles; the residual 1x1 convs by their epilogue traffic, which runs after the main loop of the
+// same workgroups.  Variants that did not beat this kernel on the ResNet152 shapes: all fragment
+// reads issued before the DMA (sched_barrier-pinned), a persistent-tile variant with register
+// epilogue, non-temporal epilogue traffic, 16-wave and 4-wave (128x64 wave tile, in-wave
+// pipelined) 256x128 tiles.
 #include "sat_common.h"
 #include "sat_internal.h"
 

@@ -14,6 +14,9 @@ SHAPES = [("L1_c1", 56, 256, 64, 1, 1, 0, 0), ("L1_c2", 56, 64, 64, 3, 1, 1, 0),
           ("L3_c1", 14, 1024, 256, 1, 1, 0, 0), ("L3_c2", 14, 256, 256, 3, 1, 1, 0), ("L3_c3", 14, 256, 1024, 1, 1, 0, 1),
           ("L4_c2", 7, 512, 512, 3, 1, 1, 0), ("stem", 224, 8, 64, 7, 2, 3, 0)]
 # (stages, tile, xcd_remap); tile ids: 1 128x128/8w, 2 128x64/8w, 3 128x128/4w, 4 128x256/8w, 5 256x128/8w
+ONLY = os.environ.get("SHAPES")
+if ONLY:
+    SHAPES = [t for t in SHAPES if t[0] in ONLY.split(",")]
 CONFIGS = [tuple(int(v) for v in c.split(',')) for c in os.environ.get('CONFIGS', '2,1,1;3,2,1;2,2,1').split(';')]
 TNAME = {1: "128x128w8", 2: "128x64w8", 3: "128x128w4", 4: "128x256w8", 5: "256x128w8"}
 lib = sat_amd._lib.lib()
@@ -29,7 +32,7 @@ for name, H, C, Co, k, s, p, r in SHAPES:
     times = {c: [] for c in CONFIGS}
     for rnd in range(5):
         for cfg in CONFIGS:
-            lib.sat_fast_gemm_set_config(*cfg)
+            lib.sat_fast_gemm_set_config(*cfg[:3])
             ops.conv2d_nhwc(x, w, b, s, p, True, residual=resid, out=y)
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             st.record()
@@ -41,5 +44,5 @@ for name, H, C, Co, k, s, p, r in SHAPES:
     line = f"{name:6s} M={B*OH*OH:7d} N={Co:5d} K={k*k*C:5d} "
     for cfg in CONFIGS:
         ms = statistics.median(times[cfg])
-        line += f" {TNAME[cfg[1]]}/s{cfg[0]}/x{cfg[2]}:{ms*1e3:6.1f}us/{flops/ms/1e9:4.0f}TF"
+        line += f" {TNAME.get(cfg[1], 'auto')}/s{cfg[0]}/x{cfg[2]}:{ms*1e3:6.1f}us/{flops/ms/1e9:4.0f}TF"
     print(line, flush=True)
