@@ -65,21 +65,6 @@ __device__ __forceinline__ uint4 ld16(const T* p, bool ok) {
   return ok ? *(const uint4*)p : make_uint4(0u, 0u, 0u, 0u);
 }
 
-// 16-byte float4 pair / quad of `n` partial slabs with two independent accumulators
-__device__ __forceinline__ float4 f4add(float4 x, float4 y) { return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w); }
-__device__ __forceinline__ float4 sum_parts4(const float* p, long idx, int n, long stride) {
-  float4 a0 = *(const float4*)(p + idx);
-  if (n <= 1) return a0;
-  float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f), a2 = a1, a3 = a1;
-  int sp = 1;
-  for (; sp + 2 < n; sp += 3) {
-    const float4 x = *(const float4*)(p + idx + sp * stride), y = *(const float4*)(p + idx + (sp + 1) * stride),
-                 z = *(const float4*)(p + idx + (sp + 2) * stride);
-    a1 = f4add(a1, x); a2 = f4add(a2, y); a3 = f4add(a3, z);
-  }
-  for (; sp < n; ++sp) a1 = f4add(a1, *(const float4*)(p + idx + sp * stride));
-  return f4add(f4add(a0, a1), f4add(a2, a3));
-}
 
 // 8 waves per (row, D-slice) workgroup; each wave scores / accumulates FU slots per batch, and
 // the context rows of the first batch are requested before the scores are computed (they do not

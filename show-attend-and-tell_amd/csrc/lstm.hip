@@ -13,68 +13,90 @@ inline int grid_for(long n) {
   return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
 }
 
+// Gate-parallel forward: a 256-thread block covers 64 units; thread (q, u) sums gate q of unit u
+// over its split-K slabs (4x the loads in flight of a unit-per-thread kernel: 9.5 -> 5.7 us per
+// step at B=128, E=512, 4 + 8 slabs), the cell update reads the four gates back from LDS.
 template <typename T>
-__global__ void lstm_fwd_kernel(LstmFwdArgs a) {
+__global__ __launch_bounds__(256) void lstm_fwd_gp_kernel(LstmFwdArgs a) {
+  __shared__ float sg[4][64];
   const int E = a.E;
-  const long n = (long)a.B * E;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int b = (int)(i / E), j = (int)(i - (long)b * E);
-    float sg[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
+  const int q = threadIdx.x >> 6, u = threadIdx.x & 63;
+  const long units = (long)a.B * E;
+  for (long base = (long)blockIdx.x * 64; base < units; base += (long)gridDim.x * 64) {
+    const long i = base + u;
+    const bool ok = i < units;
+    const int b = ok ? (int)(i / E) : 0, j = ok ? (int)(i - (long)b * E) : 0;
+    if (ok) {
       float v = a.xpart[(long)b * a.xpart_ld + q * E + j] +
                 sum_parts(a.hpart, (long)b * a.hpart_ld + q * E + j, a.h_splits, a.h_split_stride);
       if (a.cpart) v += sum_parts(a.cpart, (long)b * a.cpart_ld + q * E + j, a.c_splits, a.c_split_stride);
-      sg[q] = v;
+      sg[q][u] = v;
       a.gates[(long)b * a.gates_ld + q * E + j] = v;
     }
-    const float ig = 1.f / (1.f + expf(-sg[0]));
-    const float fg = 1.f / (1.f + expf(-sg[1]));
-    const float gg = tanhf(sg[2]);
-    const float og = 1.f / (1.f + expf(-sg[3]));
-    const float c = fg * a.c_prev[(long)b * a.c_prev_ld + j] + ig * gg;
-    const float h = og * tanhf(c);
-    a.c_out[(long)b * a.c_out_ld + j] = c;
-    if (a.c_next_in) a.c_next_in[(long)b * a.c_next_in_ld + j] = c;
-    a.h_out[(long)b * a.h_out_ld + j] = h;
-    if (a.h_out_t) ((T*)a.h_out_t)[(long)b * a.h_out_t_ld + j] = (T)h;
-    if (a.h_next_in_t) ((T*)a.h_next_in_t)[(long)b * a.h_next_in_t_ld + j] = (T)h;
+    __syncthreads();
+    if (q == 0 && ok) {
+      const float ig = 1.f / (1.f + expf(-sg[0][u]));
+      const float fg = 1.f / (1.f + expf(-sg[1][u]));
+      const float gg = tanhf(sg[2][u]);
+      const float og = 1.f / (1.f + expf(-sg[3][u]));
+      const float c = fg * a.c_prev[(long)b * a.c_prev_ld + j] + ig * gg;
+      const float h = og * tanhf(c);
+      a.c_out[(long)b * a.c_out_ld + j] = c;
+      if (a.c_next_in) a.c_next_in[(long)b * a.c_next_in_ld + j] = c;
+      a.h_out[(long)b * a.h_out_ld + j] = h;
+      if (a.h_out_t) ((T*)a.h_out_t)[(long)b * a.h_out_t_ld + j] = (T)h;
+      if (a.h_next_in_t) ((T*)a.h_next_in_t)[(long)b * a.h_next_in_t_ld + j] = (T)h;
+    }
+    __syncthreads();
   }
 }
 
+// Gate-parallel backward (layout as lstm_fwd_gp_kernel): thread (q, u) loads gate q and the
+// slabs s = q, q+4, ... of the recurrent dh; the four partial sums meet in LDS in a fixed order.
 template <typename T>
-__global__ void lstm_bwd_kernel(LstmBwdArgs a) {
+__global__ __launch_bounds__(256) void lstm_bwd_gp_kernel(LstmBwdArgs a) {
+  __shared__ float sg[4][64], sdh[4][64];
   const int E = a.E;
-  const long n = (long)a.B * E;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int b = (int)(i / E), j = (int)(i - (long)b * E);
-    const float* g = a.gates + (long)b * a.gates_ld;
-    const float ig = 1.f / (1.f + expf(-g[j]));
-    const float fg = 1.f / (1.f + expf(-g[E + j]));
-    const float gg = tanhf(g[2 * E + j]);
-    const float og = 1.f / (1.f + expf(-g[3 * E + j]));
-    const float cp = a.c_prev[(long)b * a.c_prev_ld + j];
-    const float cn = a.c_new[(long)b * a.c_new_ld + j];
-    const float tc = tanhf(cn);
-    float dh = a.dh_rec ? sum_parts(a.dh_rec, (long)b * a.dh_rec_ld + j, a.dh_splits, a.dh_split_stride) : 0.f;
-    if (a.dh_head) {
-      float hh = a.dh_head[(long)b * a.dh_head_ld + j];
-      if (a.mask) hh = a.mask[(long)b * a.mask_ld + j] ? hh * 2.f : 0.f;
-      dh += hh;
+  const int q = threadIdx.x >> 6, u = threadIdx.x & 63;
+  const long units = (long)a.B * E;
+  for (long base = (long)blockIdx.x * 64; base < units; base += (long)gridDim.x * 64) {
+    const long i = base + u;
+    const bool ok = i < units;
+    const int b = ok ? (int)(i / E) : 0, j = ok ? (int)(i - (long)b * E) : 0;
+    float cp = 0.f, cn = 0.f, dcin = 0.f, hh = 0.f;
+    if (ok) {
+      sg[q][u] = a.gates[(long)b * a.gates_ld + q * E + j];
+      float p = 0.f;
+      if (a.dh_rec)
+        for (int sp = q; sp < a.dh_splits; sp += 4) p += a.dh_rec[(long)b * a.dh_rec_ld + j + sp * a.dh_split_stride];
+      sdh[q][u] = p;
+      cp = a.c_prev[(long)b * a.c_prev_ld + j];
+      cn = a.c_new[(long)b * a.c_new_ld + j];
+      dcin = a.dc_zero ? 0.f : a.dc[i];
+      if (a.dh_head) {
+        hh = a.dh_head[(long)b * a.dh_head_ld + j];
+        if (a.mask) hh = a.mask[(long)b * a.mask_ld + j] ? hh * 2.f : 0.f;
+      }
     }
-    const float dc_in = a.dc_zero ? 0.f : a.dc[i];
-    const float dc = dc_in + dh * og * (1.f - tc * tc);
-    const float d_o = dh * tc * og * (1.f - og);
-    const float d_i = dc * gg * ig * (1.f - ig);
-    const float d_f = dc * cp * fg * (1.f - fg);
-    const float d_g = dc * ig * (1.f - gg * gg);
-    a.dc[i] = dc * fg;
-    float* dgr = a.d_gates + (long)b * a.d_gates_ld;
-    dgr[j] = d_i; dgr[E + j] = d_f; dgr[2 * E + j] = d_g; dgr[3 * E + j] = d_o;
-    if (a.d_gates_t) {
-      T* dt = (T*)a.d_gates_t + (long)b * a.d_gates_t_ld;
-      dt[j] = (T)d_i; dt[E + j] = (T)d_f; dt[2 * E + j] = (T)d_g; dt[3 * E + j] = (T)d_o;
+    __syncthreads();
+    if (ok) {
+      const float ig = 1.f / (1.f + expf(-sg[0][u]));
+      const float fg = 1.f / (1.f + expf(-sg[1][u]));
+      const float gg = tanhf(sg[2][u]);
+      const float og = 1.f / (1.f + expf(-sg[3][u]));
+      const float tc = tanhf(cn);
+      const float dh = ((sdh[0][u] + sdh[1][u]) + (sdh[2][u] + sdh[3][u])) + hh;
+      const float dc = dcin + dh * og * (1.f - tc * tc);
+      float dq;
+      if (q == 0) dq = dc * gg * ig * (1.f - ig);
+      else if (q == 1) dq = dc * cp * fg * (1.f - fg);
+      else if (q == 2) dq = dc * ig * (1.f - gg * gg);
+      else dq = dh * tc * og * (1.f - og);
+      a.d_gates[(long)b * a.d_gates_ld + q * E + j] = dq;
+      if (a.d_gates_t) ((T*)a.d_gates_t)[(long)b * a.d_gates_t_ld + q * E + j] = (T)dq;
+      if (q == 0) a.dc[i] = dc * fg;
     }
+    __syncthreads();
   }
 }
 
@@ -196,11 +218,15 @@ __global__ void tokens_kernel(const int64_t* caps, int B, int T, int T1, int32_t
   } while (0)
 
 int sat_lstm_fwd_launch(const LstmFwdArgs& a, hipStream_t s) {
-  DISPATCH_T(a.dtype, lstm_fwd_kernel, dim3(grid_for((long)a.B * a.E)), a);
+  long blocks = ((long)a.B * a.E + 63) / 64;
+  if (blocks > 4096) blocks = 4096;
+  DISPATCH_T(a.dtype, lstm_fwd_gp_kernel, dim3((int)blocks), a);
   return (int)hipGetLastError();
 }
 int sat_lstm_bwd_launch(const LstmBwdArgs& a, hipStream_t s) {
-  DISPATCH_T(a.dtype, lstm_bwd_kernel, dim3(grid_for((long)a.B * a.E)), a);
+  long blocks = ((long)a.B * a.E + 63) / 64;
+  if (blocks > 4096) blocks = 4096;
+  DISPATCH_T(a.dtype, lstm_bwd_gp_kernel, dim3((int)blocks), a);
   return (int)hipGetLastError();
 }
 int sat_tanh_pair_bwd(const float* d_h, int dh_splits, long dh_split_stride, const float* d_c, const float* hc0,

@@ -120,3 +120,19 @@ __device__ __forceinline__ float sum_parts(const float* p, long idx, int n, long
   for (; s < n; ++s) a1 += p[idx + s * stride];
   return (a0 + a1) + (a2 + a3);
 }
+
+// 16-byte form of sum_parts (same summation order per element)
+__device__ __forceinline__ float4 f4add(float4 x, float4 y) { return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w); }
+__device__ __forceinline__ float4 sum_parts4(const float* p, long idx, int n, long stride) {
+  float4 a0 = *(const float4*)(p + idx);
+  if (n <= 1) return a0;
+  float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f), a2 = a1, a3 = a1;
+  int sp = 1;
+  for (; sp + 2 < n; sp += 3) {
+    const float4 x = *(const float4*)(p + idx + sp * stride), y = *(const float4*)(p + idx + (sp + 1) * stride),
+                 z = *(const float4*)(p + idx + (sp + 2) * stride);
+    a1 = f4add(a1, x); a2 = f4add(a2, y); a3 = f4add(a3, z);
+  }
+  for (; sp < n; ++sp) a1 = f4add(a1, *(const float4*)(p + idx + sp * stride));
+  return f4add(f4add(a0, a1), f4add(a2, a3));
+}
