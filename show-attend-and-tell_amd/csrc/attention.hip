@@ -5,8 +5,8 @@
 // all L annotation slots of its row (e_l = v . tanh(Ws[b,l,:] + U h_b) + b_v,
 // wave per slot, lanes over E, shuffle reduction), runs the softmax over L in
 // one wave, then accumulates context[b, d] = sum_l alpha_l a[b,l,d] for its
-// D-slice (lanes over d with 16-B loads, waves over l, LDS fold) and applies the
-// gate sigma(f_beta h + b).  The loop-invariant Ws = a W^T + b is hoisted out of
+// D-slice of 64*2 16-B vectors (lanes over d, waves over l, LDS fold) and applies
+// the gate sigma(f_beta h + b).  The loop-invariant Ws = a W^T + b is hoisted out of
 // the time loop (one GEMM per batch) instead of being recomputed every step as
 // the reference does (attention.py:16 called from decoder.py:98).
 //
@@ -66,28 +66,46 @@ __device__ __forceinline__ uint4 ld16(const T* p, bool ok) {
 }
 
 
-// 8 waves per (row, D-slice) workgroup; each wave scores / accumulates FU slots per batch, and
-// the context rows of the first batch are requested before the scores are computed (they do not
-// depend on alpha), so a step costs ~2 dependent memory round trips for L <= 64.
+// Backward kernels: 8 waves per (row, D-slice) workgroup; each wave accumulates FU slots per
+// batch, the annotation rows of the first batch requested before anything else.
 constexpr int ANW = 8, FU = 8;
 
+// Forward: 16 waves per (row, D-slice) workgroup and two 16-byte context vectors per lane, so a
+// row's scores are computed by cdiv(D, 64*VN*2) workgroups (2 at D = 2048 in bf16) instead of 4:
+// the score pass (v . tanh, VALU / transcendental-bound) is half as redundant and one workgroup
+// per CU still streams its 100 KB annotation slice.  Slots past L skip their score work (the
+// wave-uniform test), and everything the epilogue needs from HBM (gate pre-activation slabs) is
+// requested at kernel entry with the first annotation rows, so a step is one dependent memory
+// round trip plus the score / softmax / context phases.
+constexpr int FNW = 16, FDV = 2, FFU = 4;
+
 template <typename T, int CH>   // CH = e-chunks of 64 x 16 bytes per lane covering E
-__global__ __launch_bounds__(ANW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
+__global__ __launch_bounds__(FNW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
   constexpr int VN = V16<T>::N;            // elements per 16-byte vector
+  constexpr int COLS = 64 * VN * FDV;      // context columns of one workgroup
   __shared__ float s_alpha[kMaxL];
-  __shared__ float s_red[ANW][64 * VN];
+  __shared__ float s_red[FNW][COLS];
   const int b = blockIdx.x, s = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = a.L, D = a.D, E = a.E;
   const T* Ws = (const T*)a.Ws + (long)b * L * E;
   const float* uh = a.uh + (long)b * a.uh_ld;
-  const int d0 = s * 64 * VN + lane * VN;
-  const T* ab = (const T*)a.a + (long)b * L * D + d0;
+  const int c0 = s * COLS;
+  const T* ab = (const T*)a.a + (long)b * L * D + c0 + lane * VN;
+
+  // epilogue operand: gate pre-activation of this thread's output column
+  const int dout = c0 + tid;
+  const bool out_ok = tid < COLS && dout < D;
+  float gpre = 0.f;
+  if (a.gate_pre && out_ok) gpre = sum_parts(a.gate_pre, (long)b * a.gate_ld + dout, a.hg_splits, a.hg_split_stride);
 
   // context rows of the first batch: in flight while the scores are formed
-  uint4 xa[FU];
+  uint4 xa[FFU][FDV];
 #pragma unroll
-  for (int u = 0; u < FU; ++u) xa[u] = ld16(ab + (long)(w + ANW * u) * D, w + ANW * u < L && d0 < D);
+  for (int u = 0; u < FFU; ++u)
+#pragma unroll
+    for (int v = 0; v < FDV; ++v)
+      xa[u][v] = ld16(ab + (long)(w + FNW * u) * D + v * 64 * VN, w + FNW * u < L && c0 + v * 64 * VN + lane * VN < D);
 
   // ---- scores: lane owns VN consecutive e per chunk; (U h + b) and v live in registers ----
   float u_r[CH][VN], v_r[CH][VN];
@@ -106,17 +124,19 @@ __global__ __launch_bounds__(ANW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
     }
   }
   const float bv = a.v_b[0];
-  for (int l0 = w; l0 < L; l0 += ANW * FU) {
-    uint4 xv[FU][CH];
+  for (int l0 = w; l0 < L; l0 += FNW * FFU) {
+    uint4 xv[FFU][CH];
 #pragma unroll
-    for (int u = 0; u < FU; ++u)
+    for (int u = 0; u < FFU; ++u)
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
-        const int l = l0 + ANW * u, e = c * 64 * VN + lane * VN;
+        const int l = l0 + FNW * u, e = c * 64 * VN + lane * VN;
         xv[u][c] = ld16(Ws + (long)l * E + e, l < L && e < E);
       }
 #pragma unroll
-    for (int u = 0; u < FU; ++u) {
+    for (int u = 0; u < FFU; ++u) {
+      const int l = l0 + FNW * u;
+      if (l >= L) break;   // wave-uniform
       float acc = 0.f;
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
@@ -125,8 +145,17 @@ __global__ __launch_bounds__(ANW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
         for (int j = 0; j < VN; ++j) acc += v_r[c][j] * tanh_t<T>((float)h[j] + u_r[c][j]);   // v = 0 past E
       }
       acc = wave_sum(acc);
-      const int l = l0 + ANW * u;
-      if (lane == 0 && l < L) s_alpha[l] = acc + bv;
+      if (lane == 0) s_alpha[l] = acc + bv;
+    }
+  }
+  if (s == 0 && w == 1 && a.uh_save) {   // U h + b of this row (the registers every wave holds)
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int e = c * 64 * VN + lane * VN;
+      if (e < E) {
+#pragma unroll
+        for (int j = 0; j < VN; ++j) a.uh_save[(long)b * a.uh_save_ld + e + j] = u_r[c][j];
+      }
     }
   }
   __syncthreads();
@@ -149,46 +178,52 @@ __global__ __launch_bounds__(ANW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
       if (s == 0 && a.alpha) a.alpha[(long)b * a.alpha_ld + l] = al;
     }
   }
-  if (s == 0 && a.uh_save) {
-    for (int e = tid; e < E; e += ANW * 64) a.uh_save[(long)b * a.uh_save_ld + e] = sum_parts(uh, e, a.hg_splits, a.hg_split_stride);
-  }
   __syncthreads();
   // ---- context for this D-slice: lanes over d (16-byte loads), waves over l ----
-  float part[VN];
+  float part[FDV][VN];
 #pragma unroll
-  for (int j = 0; j < VN; ++j) part[j] = 0.f;
-  for (int l0 = w; l0 < L; l0 += ANW * FU) {
+  for (int v = 0; v < FDV; ++v)
+#pragma unroll
+    for (int j = 0; j < VN; ++j) part[v][j] = 0.f;
+  for (int l0 = w; l0 < L; l0 += FNW * FFU) {
     if (l0 != w) {
 #pragma unroll
-      for (int u = 0; u < FU; ++u) xa[u] = ld16(ab + (long)(l0 + ANW * u) * D, l0 + ANW * u < L && d0 < D);
+      for (int u = 0; u < FFU; ++u)
+#pragma unroll
+        for (int v = 0; v < FDV; ++v)
+          xa[u][v] = ld16(ab + (long)(l0 + FNW * u) * D + v * 64 * VN,
+                          l0 + FNW * u < L && c0 + v * 64 * VN + lane * VN < D);
     }
 #pragma unroll
-    for (int u = 0; u < FU; ++u) {
-      const int l = l0 + ANW * u;
+    for (int u = 0; u < FFU; ++u) {
+      const int l = l0 + FNW * u;
       if (l < L) {
         const float al = s_alpha[l];
-        const T* h = (const T*)&xa[u];
 #pragma unroll
-        for (int j = 0; j < VN; ++j) part[j] += al * (float)h[j];
+        for (int v = 0; v < FDV; ++v) {
+          const T* h = (const T*)&xa[u][v];
+#pragma unroll
+          for (int j = 0; j < VN; ++j) part[v][j] += al * (float)h[j];
+        }
       }
     }
   }
 #pragma unroll
-  for (int j = 0; j < VN; ++j) s_red[w][lane * VN + j] = part[j];
+  for (int v = 0; v < FDV; ++v)
+#pragma unroll
+    for (int j = 0; j < VN; ++j) s_red[w][v * 64 * VN + lane * VN + j] = part[v][j];
   __syncthreads();
-  for (int i = tid; i < 64 * VN; i += ANW * 64) {
-    const int d = s * 64 * VN + i;
-    if (d >= D) continue;
+  if (out_ok) {
     // fixed summation order over the wave partials
     float c = 0.f;
 #pragma unroll
-    for (int q = 0; q < ANW; q += 2) c += s_red[q][i] + s_red[q + 1][i];
-    a.ctx[(long)b * a.ctx_ld + d] = c;
-    if (a.ctx_t) ((T*)a.ctx_t)[(long)b * a.ctx_t_ld + d] = (T)c;
+    for (int q = 0; q < FNW; q += 2) c += s_red[q][tid] + s_red[q + 1][tid];
+    a.ctx[(long)b * a.ctx_ld + dout] = c;
+    if (a.ctx_t) ((T*)a.ctx_t)[(long)b * a.ctx_t_ld + dout] = (T)c;
     if (a.gate_pre) {
-      const float g = 1.0f / (1.0f + expf(-sum_parts(a.gate_pre, (long)b * a.gate_ld + d, a.hg_splits, a.hg_split_stride)));
-      if (a.gate) a.gate[(long)b * a.gate_out_ld + d] = g;
-      if (a.gated) ((T*)a.gated)[(long)b * a.gated_ld + d] = (T)(g * c);
+      const float g = 1.0f / (1.0f + expf(-gpre));
+      if (a.gate) a.gate[(long)b * a.gate_out_ld + dout] = g;
+      if (a.gated) ((T*)a.gated)[(long)b * a.gated_ld + dout] = (T)(g * c);
     }
   }
 }
@@ -388,9 +423,9 @@ inline int e_chunks(int E, int VN) {
 
 template <typename T>
 void launch_fwd(int ch, dim3 grid, hipStream_t s, const AttnFwdArgs& a) {
-  if (ch == 1) hipLaunchKernelGGL((attn_fwd_kernel<T, 1>), grid, dim3(ANW * 64), 0, s, a);
-  else if (ch == 2) hipLaunchKernelGGL((attn_fwd_kernel<T, 2>), grid, dim3(ANW * 64), 0, s, a);
-  else hipLaunchKernelGGL((attn_fwd_kernel<T, 4>), grid, dim3(ANW * 64), 0, s, a);
+  if (ch == 1) hipLaunchKernelGGL((attn_fwd_kernel<T, 1>), grid, dim3(FNW * 64), 0, s, a);
+  else if (ch == 2) hipLaunchKernelGGL((attn_fwd_kernel<T, 2>), grid, dim3(FNW * 64), 0, s, a);
+  else hipLaunchKernelGGL((attn_fwd_kernel<T, 4>), grid, dim3(FNW * 64), 0, s, a);
 }
 template <typename T>
 void launch_bwd2(int ch, dim3 grid, hipStream_t s, const AttnBwdArgs& a, int NS) {
@@ -406,7 +441,7 @@ int sat_attention_fwd_launch(const AttnFwdArgs& a, hipStream_t s) {
   SAT_REQUIRE(a.L <= kMaxL && a.E % VD == 0 && a.E <= 1024);
   SAT_REQUIRE((a.uh_ld % 4) == 0 && (a.hg_splits <= 1 || a.hg_split_stride % 4 == 0));
   SAT_REQUIRE(a.D % VD == 0);
-  const int NS = sat_cdiv(a.D, 64 * VD);
+  const int NS = sat_cdiv(a.D, 64 * VD * FDV);
   dim3 grid(a.B, NS);
   if (a.dtype == SAT_BF16) launch_fwd<bf16>(e_chunks(a.E, 8), grid, s, a);
   else launch_fwd<float>(e_chunks(a.E, 4), grid, s, a);
