@@ -289,20 +289,47 @@ __global__ __launch_bounds__(ANW * 64) void attn_bwd1_kernel(AttnBwdArgs a) {
   (void)E;
 }
 
-// one workgroup of 8 waves per batch row; lane owns VN consecutive e per chunk
-template <typename T, int CH>
-__global__ __launch_bounds__(512) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
-  constexpr int NW = 8, VN = V16<T>::N;
+// grid (B, E / 256): a workgroup of 8 waves per (row, 256-wide e-slice); lane owns 4 consecutive
+// e, waves take BFU slots each per batch, so a row's 49 slots are two batches of loads in flight.
+// The softmax backward (a few hundred flops per row) is recomputed by each slice.
+constexpr int BNW = 8, BFU = 4, BEV = 4, BSLICE = 64 * BEV;
+
+template <typename T>
+__device__ __forceinline__ void load_e4(const T* p, bool ok, float* o) {
+  if (!ok) { o[0] = o[1] = o[2] = o[3] = 0.f; return; }
+  load4<T>(p, o);
+}
+
+template <typename T>
+__global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
   __shared__ float s_de[kMaxL];
-  __shared__ float s_red[NW][1024];
-  __shared__ float s_tmp[NW];
-  const int b = blockIdx.x;
+  __shared__ float s_red[BNW][BSLICE];
+  __shared__ float s_tmp[BNW];
+  const int b = blockIdx.x, eslice = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = a.L, E = a.E;
+  const int e = eslice * BSLICE + lane * BEV;
+  const bool eok = e < E;
   const float* alpha = a.alpha + (long)b * a.alpha_ld;
+  const float* uh = a.uh + (long)b * a.uh_ld;
+  const T* Ws = (const T*)a.Ws + (long)b * L * E;
+  float* dWs = a.dWs_acc + (long)b * L * E;
+  // loop invariants and the first batch of slots: requested before the softmax backward
+  float uu[BEV], vw[BEV];
+  load_e4<float>(uh + e, eok, uu);
+  load_e4<float>(a.v_w + e, eok, vw);
+  float xw[BFU][BEV];
+  float4 acc[BFU];
+#pragma unroll
+  for (int u = 0; u < BFU; ++u) {
+    const int l = w + BNW * u;
+    const bool ok = l < L && eok;
+    load_e4<T>(Ws + (long)l * E + e, ok, xw[u]);
+    acc[u] = ok ? *(const float4*)(dWs + (long)l * E + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   // dL/dalpha and sum_l alpha*dalpha
   float loc = 0.f;
-  for (int l = tid; l < L; l += NW * 64) {
+  for (int l = tid; l < L; l += BNW * 64) {
     float da = 0.f;
     for (int s = 0; s < NS; ++s) da += a.part[((long)b * NS + s) * L + l];
     if (a.d_alpha_ext) da += a.d_alpha_ext[(long)b * a.d_alpha_ext_ld + l];
@@ -314,103 +341,72 @@ __global__ __launch_bounds__(512) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
   __syncthreads();
   float sad = 0.f;
 #pragma unroll
-  for (int i = 0; i < NW; i += 2) sad += s_tmp[i] + s_tmp[i + 1];
+  for (int i = 0; i < BNW; i += 2) sad += s_tmp[i] + s_tmp[i + 1];
   __syncthreads();
-  for (int l = tid; l < L; l += NW * 64) s_de[l] = alpha[l] * (s_de[l] - sad);
+  for (int l = tid; l < L; l += BNW * 64) s_de[l] = alpha[l] * (s_de[l] - sad);
   __syncthreads();
-  // recompute tanh, accumulate (U h + b and v are loop-invariant: registers)
-  const float* uh = a.uh + (long)b * a.uh_ld;
-  const T* Ws = (const T*)a.Ws + (long)b * L * E;
-  float* dWs = a.dWs_acc + (long)b * L * E;
-  float uu[CH][VN], vw[CH][VN], duh[CH][VN], dv[CH][VN];
+  // recompute tanh, accumulate
+  float duh[BEV], dv[BEV];
 #pragma unroll
-  for (int c = 0; c < CH; ++c) {
-    const int e = c * 64 * VN + lane * VN;
-#pragma unroll
-    for (int j = 0; j < VN; ++j) {
-      uu[c][j] = e < E ? uh[e + j] : 0.f;
-      vw[c][j] = e < E ? a.v_w[e + j] : 0.f;
-      duh[c][j] = 0.f;
-      dv[c][j] = 0.f;
-    }
-  }
+  for (int j = 0; j < BEV; ++j) duh[j] = dv[j] = 0.f;
   float dbv = 0.f;
-  for (int l0 = w; l0 < L; l0 += NW * 2) {
-    uint4 xw[2][CH];
-    float4 acc[2][CH][VN / 4];
+  for (int l0 = w; l0 < L; l0 += BNW * BFU) {
+    if (l0 != w) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        const int l = l0 + NW * u, e = c * 64 * VN + lane * VN;
-        const bool ok = l < L && e < E;
-        xw[u][c] = ld16(Ws + (long)l * E + e, ok);
-#pragma unroll
-        for (int q = 0; q < VN / 4; ++q)
-          acc[u][c][q] = ok ? *(const float4*)(dWs + (long)l * E + e + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int u = 0; u < BFU; ++u) {
+        const int l = l0 + BNW * u;
+        const bool ok = l < L && eok;
+        load_e4<T>(Ws + (long)l * E + e, ok, xw[u]);
+        acc[u] = ok ? *(const float4*)(dWs + (long)l * E + e) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
+    }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int l = l0 + NW * u;
-      if (l >= L) continue;
+    for (int u = 0; u < BFU; ++u) {
+      const int l = l0 + BNW * u;
+      if (l >= L) break;   // wave-uniform
       const float de = s_de[l];
       dbv += de;
+      if (!eok) continue;
+      float* ac = (float*)&acc[u];
 #pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        const int e = c * 64 * VN + lane * VN;
-        if (e >= E) continue;
-        const T* h = (const T*)&xw[u][c];
-        float* ac = (float*)&acc[u][c][0];
-#pragma unroll
-        for (int j = 0; j < VN; ++j) {
-          const float t = tanh_t<T>((float)h[j] + uu[c][j]);
-          const float datt = de * vw[c][j] * (1.f - t * t);
-          duh[c][j] += datt;
-          dv[c][j] += de * t;
-          ac[j] += datt;
-        }
-#pragma unroll
-        for (int q = 0; q < VN / 4; ++q) *(float4*)(dWs + (long)l * E + e + 4 * q) = acc[u][c][q];
+      for (int j = 0; j < BEV; ++j) {
+        const float t = tanh_t<T>(xw[u][j] + uu[j]);
+        const float datt = de * vw[j] * (1.f - t * t);
+        duh[j] += datt;
+        dv[j] += de * t;
+        ac[j] += datt;
       }
+      *(float4*)(dWs + (long)l * E + e) = acc[u];
     }
   }
   // fold the waves (fixed order): dU_h, then dv
 #pragma unroll
-  for (int c = 0; c < CH; ++c)
-#pragma unroll
-    for (int j = 0; j < VN; ++j) {
-      const int e = c * 64 * VN + lane * VN + j;
-      if (e < E) s_red[w][e] = duh[c][j];
-    }
+  for (int j = 0; j < BEV; ++j) s_red[w][lane * BEV + j] = duh[j];
   __syncthreads();
-  for (int e = tid; e < E; e += NW * 64) {
+  const int eo = eslice * BSLICE + tid;
+  if (tid < BSLICE && eo < E) {
     float v = 0.f;
 #pragma unroll
-    for (int i = 0; i < NW; i += 2) v += s_red[i][e] + s_red[i + 1][e];
-    a.d_uh[(long)b * a.d_uh_ld + e] = v;
-    if (a.d_uh_t) ((T*)a.d_uh_t)[(long)b * a.d_uh_ld + e] = (T)v;
+    for (int i = 0; i < BNW; i += 2) v += s_red[i][tid] + s_red[i + 1][tid];
+    a.d_uh[(long)b * a.d_uh_ld + eo] = v;
+    if (a.d_uh_t) ((T*)a.d_uh_t)[(long)b * a.d_uh_ld + eo] = (T)v;
   }
   __syncthreads();
 #pragma unroll
-  for (int c = 0; c < CH; ++c)
-#pragma unroll
-    for (int j = 0; j < VN; ++j) {
-      const int e = c * 64 * VN + lane * VN + j;
-      if (e < E) s_red[w][e] = dv[c][j];
-    }
+  for (int j = 0; j < BEV; ++j) s_red[w][lane * BEV + j] = dv[j];
   dbv = wave_sum(dbv);
   if (lane == 0) s_tmp[w] = dbv;
   __syncthreads();
-  for (int e = tid; e < E; e += NW * 64) {
+  if (tid < BSLICE && eo < E) {
     float v = 0.f;
 #pragma unroll
-    for (int i = 0; i < NW; i += 2) v += s_red[i][e] + s_red[i + 1][e];
-    a.dv_acc[(long)b * E + e] += v;
+    for (int i = 0; i < BNW; i += 2) v += s_red[i][tid] + s_red[i + 1][tid];
+    a.dv_acc[(long)b * E + eo] += v;
   }
-  if (tid == 0) {
+  if (tid == 0 && eslice == 0) {
     float v = 0.f;
 #pragma unroll
-    for (int i = 0; i < NW; i += 2) v += s_tmp[i] + s_tmp[i + 1];
+    for (int i = 0; i < BNW; i += 2) v += s_tmp[i] + s_tmp[i + 1];
     a.dbv_acc[b] += v;
   }
 }
@@ -426,12 +422,6 @@ void launch_fwd(int ch, dim3 grid, hipStream_t s, const AttnFwdArgs& a) {
   if (ch == 1) hipLaunchKernelGGL((attn_fwd_kernel<T, 1>), grid, dim3(FNW * 64), 0, s, a);
   else if (ch == 2) hipLaunchKernelGGL((attn_fwd_kernel<T, 2>), grid, dim3(FNW * 64), 0, s, a);
   else hipLaunchKernelGGL((attn_fwd_kernel<T, 4>), grid, dim3(FNW * 64), 0, s, a);
-}
-template <typename T>
-void launch_bwd2(int ch, dim3 grid, hipStream_t s, const AttnBwdArgs& a, int NS) {
-  if (ch == 1) hipLaunchKernelGGL((attn_bwd2_kernel<T, 1>), grid, dim3(512), 0, s, a, NS);
-  else if (ch == 2) hipLaunchKernelGGL((attn_bwd2_kernel<T, 2>), grid, dim3(512), 0, s, a, NS);
-  else hipLaunchKernelGGL((attn_bwd2_kernel<T, 4>), grid, dim3(512), 0, s, a, NS);
 }
 
 }  // namespace
@@ -455,10 +445,10 @@ int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s) {
   const int NS = sat_cdiv(a.D, 64 * VD);
   if (a.dtype == SAT_BF16) {
     hipLaunchKernelGGL(attn_bwd1_kernel<bf16>, dim3(a.B, NS), dim3(ANW * 64), 0, s, a);
-    launch_bwd2<bf16>(e_chunks(a.E, 8), dim3(a.B), s, a, NS);
+    hipLaunchKernelGGL(attn_bwd2_kernel<bf16>, dim3(a.B, sat_cdiv(a.E, BSLICE)), dim3(BNW * 64), 0, s, a, NS);
   } else {
     hipLaunchKernelGGL(attn_bwd1_kernel<float>, dim3(a.B, NS), dim3(ANW * 64), 0, s, a);
-    launch_bwd2<float>(e_chunks(a.E, 4), dim3(a.B), s, a, NS);
+    hipLaunchKernelGGL(attn_bwd2_kernel<float>, dim3(a.B, sat_cdiv(a.E, BSLICE)), dim3(BNW * 64), 0, s, a, NS);
   }
   return (int)hipGetLastError();
 }
