@@ -228,48 +228,42 @@ __global__ __launch_bounds__(FNW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
   }
 }
 
+// grid (B, NS): dL/dcontext for the workgroup's D-slice is formed ONCE (thread per column: the
+// gated-context slabs, gate, context, head term; the gate gradient written on the way) into LDS,
+// then every wave dots it with its slots' annotation rows (requested at kernel entry).
 template <typename T>
 __global__ __launch_bounds__(ANW * 64) void attn_bwd1_kernel(AttnBwdArgs a) {
   constexpr int VD = V16<T>::N;
+  constexpr int COLS = 64 * VD;
+  __shared__ float s_dctx[COLS];
   const int b = blockIdx.x, s = blockIdx.y, NS = gridDim.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int L = a.L, D = a.D, E = a.E;
-  const int d0 = s * 64 * VD + lane * VD;
+  const int L = a.L, D = a.D;
+  const int d0 = s * COLS + lane * VD;
   const T* ab = (const T*)a.a + (long)b * L * D + d0;
   // annotation rows of the first batch: independent of dL/dcontext, requested first
   uint4 xa[FU];
 #pragma unroll
   for (int u = 0; u < FU; ++u) xa[u] = ld16(ab + (long)(w + ANW * u) * D, w + ANW * u < L && d0 < D);
+  for (int i = tid; i < COLS; i += ANW * 64) {
+    const int d = s * COLS + i;
+    float dctx = 0.f;
+    if (d < D) {
+      const float dg = sum_parts(a.d_gated, (long)b * a.d_gated_ld + d, a.dg_splits, a.dg_split_stride);
+      const float g = a.gate[(long)b * a.gate_ld + d];
+      const float c = a.ctx[(long)b * a.ctx_ld + d];
+      const float dx = a.d_ctx_ext ? a.d_ctx_ext[(long)b * a.d_ctx_ext_ld + d] : 0.f;
+      dctx = dg * g + dx;
+      const float dgp = dg * c * g * (1.f - g);
+      a.d_gpre[(long)b * a.d_gpre_ld + d] = dgp;
+      if (a.d_gpre_t) ((T*)a.d_gpre_t)[(long)b * a.d_gpre_ld + d] = (T)dgp;
+    }
+    s_dctx[i] = dctx;
+  }
+  __syncthreads();
   float dctx[VD];
 #pragma unroll
-  for (int j = 0; j < VD; ++j) dctx[j] = 0.f;
-  if (d0 < D) {
-    float dg[VD], g[VD], c[VD], dx[VD];
-#pragma unroll
-    for (int j = 0; j < VD; j += 4) {
-      const float4 q = sum_parts4(a.d_gated, (long)b * a.d_gated_ld + d0 + j, a.dg_splits, a.dg_split_stride);
-      const float4 gg = *(const float4*)(a.gate + (long)b * a.gate_ld + d0 + j);
-      const float4 cc = *(const float4*)(a.ctx + (long)b * a.ctx_ld + d0 + j);
-      dg[j] = q.x; dg[j + 1] = q.y; dg[j + 2] = q.z; dg[j + 3] = q.w;
-      g[j] = gg.x; g[j + 1] = gg.y; g[j + 2] = gg.z; g[j + 3] = gg.w;
-      c[j] = cc.x; c[j + 1] = cc.y; c[j + 2] = cc.z; c[j + 3] = cc.w;
-      if (a.d_ctx_ext) {
-        const float4 xx = *(const float4*)(a.d_ctx_ext + (long)b * a.d_ctx_ext_ld + d0 + j);
-        dx[j] = xx.x; dx[j + 1] = xx.y; dx[j + 2] = xx.z; dx[j + 3] = xx.w;
-      } else {
-        dx[j] = dx[j + 1] = dx[j + 2] = dx[j + 3] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < VD; ++j) {
-      dctx[j] = dg[j] * g[j] + dx[j];
-      if (w == 0) {
-        const float dgp = dg[j] * c[j] * g[j] * (1.f - g[j]);
-        a.d_gpre[(long)b * a.d_gpre_ld + d0 + j] = dgp;
-        if (a.d_gpre_t) ((T*)a.d_gpre_t)[(long)b * a.d_gpre_ld + d0 + j] = (T)dgp;
-      }
-    }
-  }
+  for (int j = 0; j < VD; ++j) dctx[j] = s_dctx[lane * VD + j];
   for (int l0 = w; l0 < L; l0 += ANW * FU) {
     if (l0 != w) {
 #pragma unroll
@@ -277,16 +271,16 @@ __global__ __launch_bounds__(ANW * 64) void attn_bwd1_kernel(AttnBwdArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < FU; ++u) {
+      const int l = l0 + ANW * u;
+      if (l >= L) break;   // wave-uniform
       const T* h = (const T*)&xa[u];
       float p = 0.f;
 #pragma unroll
       for (int j = 0; j < VD; ++j) p += dctx[j] * (float)h[j];
       p = wave_sum(p);
-      const int l = l0 + ANW * u;
-      if (lane == 0 && l < L) a.part[((long)b * NS + s) * L + l] = p;
+      if (lane == 0) a.part[((long)b * NS + s) * L + l] = p;
     }
   }
-  (void)E;
 }
 
 // grid (B, E / 256): a workgroup of 8 waves per (row, 256-wide e-slice); lane owns 4 consecutive
