@@ -123,6 +123,10 @@ int sat_attention_forward(int B, int L, int D, int E, int dtype, const void* img
                           float* context, float* alpha, void* stream);
 
 /* --- decoder (decoder.py:69-158) ----------------------------------------- */
+/* tuning hook (process-global): split-K counts of the per-step bf16 decoder GEMMs -- h: [U; f_beta; W_hh] h,
+ * c: context part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic.  Must be set
+ * before sat_decoder_workspace_bytes. */
+int sat_decoder_set_splits(int h, int c, int g, int dh);
 size_t sat_decoder_workspace_bytes(const SatDecoderDims* d);
 /* preds [B,T-1,V] (dtype), alphas [B,T-1,L] fp32, tokens [B,T-1] int32 = token fed at each step. */
 int sat_decoder_forward(const SatDecoderDims* d, const SatDecoderLayout* lay, const float* params,

@@ -37,14 +37,15 @@ struct WS {
 };
 
 // split counts of the per-step skinny GEMMs (M = B rows).  bf16: the LDS-DMA kernel (128 x 64
-// tiles, 128 x 128 for k-major weights) with partial-output split-K -- aim for ~1.5 waves of
-// blocks over the 256 CUs with splits that divide K into whole 64-deep k-tiles; fp32 (parity)
-// mode keeps a single split.
+// tiles, 128 x 128 for k-major weights) with partial-output split-K -- aim for ~0.75 waves of
+// blocks over the 256 CUs with splits that divide K into whole 64-deep k-tiles (fewer, longer
+// splits write and re-read fewer fp32 slabs: tools/bench_decoder_splits.py, B=128 bench shape
+// -1.3 % decoder time against ~1.5 waves); fp32 (parity) mode keeps a single split.
 struct Splits { int h, c, g, dh, i; };
 inline int pick_splits(int M, int N, int K, int dtype, bool kmajor_w) {
   if (dtype != SAT_BF16 || K % 64) return 1;
   const long tiles = (long)sat_cdiv(M, 128) * sat_cdiv(N, kmajor_w ? 128 : 64);
-  long want = (384 + tiles - 1) / tiles;
+  long want = (192 + tiles - 1) / tiles;
   if (want > 32) want = 32;
   const int kt = K / 64;
   int best = 1;
@@ -52,14 +53,23 @@ inline int pick_splits(int M, int N, int K, int dtype, bool kmajor_w) {
     if (kt % s == 0) best = s;
   return best;
 }
+Splits g_force_splits{0, 0, 0, 0, 0};   // tuning override (sat_decoder_set_splits), 0 = automatic
+inline int forced(int f, int K, int auto_s) { return (f > 0 && K % 64 == 0 && (K / 64) % f == 0) ? f : auto_s; }
 inline Splits splits_for(const SatDecoderDims& d) {
   const int E = d.E, D = d.D, HG = 5 * E + D;
+  const bool bf = d.dtype == SAT_BF16;
   Splits s;
   s.h = pick_splits(d.B, d.attention ? HG : 4 * E, E, d.dtype, false);
   s.c = pick_splits(d.B, 4 * E, D, d.dtype, false);
   s.g = pick_splits(d.B, D, 4 * E, d.dtype, true);
   s.dh = pick_splits(d.B, E, d.attention ? HG : 4 * E, d.dtype, true);
   s.i = pick_splits(d.B, 2 * E, D, d.dtype, false);
+  if (bf) {
+    s.h = forced(g_force_splits.h, E, s.h);
+    s.c = forced(g_force_splits.c, D, s.c);
+    s.g = forced(g_force_splits.g, 4 * E, s.g);
+    s.dh = forced(g_force_splits.dh, d.attention ? HG : 4 * E, s.dh);
+  }
   return s;
 }
 
@@ -235,6 +245,14 @@ int check_dims(const SatDecoderDims* d) {
 }
 
 }  // namespace
+
+// tuning hook: split-K counts of the per-step bf16 GEMMs (h: [U;f_beta;W_hh] h, c: context gate
+// GEMM, g: dL/d gated context, dh: recurrent dL/dh); 0 = automatic.  Set before the workspace query.
+extern "C" int sat_decoder_set_splits(int h, int c, int g, int dh) {
+  if (h < 0 || c < 0 || g < 0 || dh < 0 || h > 64 || c > 64 || g > 64 || dh > 64) return SAT_ERR_INVALID;
+  g_force_splits = Splits{h, c, g, dh, 0};
+  return 0;
+}
 
 extern "C" size_t sat_decoder_workspace_bytes(const SatDecoderDims* d) {
   if (check_dims(d)) return 0;

@@ -14,7 +14,7 @@ for f in sorted(glob.glob(os.path.join(out, "*", "**", "*counter_collection.csv"
     shape = os.path.relpath(f, out).split(os.sep)[0].rsplit("_", 1)[0]
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(f)):
-        if "fast_gemm" not in r["Kernel_Name"]:
+        if os.environ.get("KFILTER", "fast_gemm") not in r["Kernel_Name"]:
             continue
         per[r["Counter_Name"]][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
     for c, d in per.items():
