@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=2, help="images in the bounded CPU-baseline sample")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="graph mode: run the next batch's encoder after, not beside, this batch's decoder")
     return ap.parse_args()
 
 
@@ -152,7 +154,7 @@ def cpu_baseline(args):
     x = torch.randn(B, 3, 224, 224)
     caps = O.make_captions(B, args.seq, args.vocab, 0)
     iters, t_total = 0, 0.0
-    while iters < 2 or (t_total < 10.0 and iters < 5):
+    while iters < 2 or (t_total < 12.0 and iters < 60):   # ~12 s of host work
         t0 = time.perf_counter()
         with torch.no_grad():
             feats = fwd(enc_p, x)
@@ -209,50 +211,83 @@ def main():
     torch.cuda.synchronize()
 
     use_graph = not args.no_graph
+    overlap = use_graph and not args.no_overlap
     if use_graph:
-        # Two hipGraphs: the encoder trunk (so its kernels can be bracketed with events) and
-        # decoder fwd + loss + BPTT.  Adam and the RCCL all-reduce run eagerly after replay
-        # (Adam's bias corrections are step-dependent host scalars).
-        opt.zero_grad(set_to_none=True)
-        g_enc, g_dec = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_enc):
-            with torch.no_grad():
-                feats_static = enc(imgs)
-        with torch.cuda.graph(g_dec, pool=g_enc.pool()):
-            preds, alphas = dec(feats_static, caps)
-            loss_static, _ = sat_amd.caption_loss(preds, alphas, caps)
-            loss_static.backward()
+        # hipGraphs: the encoder trunk (so its kernels can be bracketed with events) and decoder
+        # fwd + loss + BPTT.  Adam and the RCCL all-reduce run eagerly after replay (Adam's bias
+        # corrections are step-dependent host scalars).  With --overlap (default) there are two of
+        # each, over two feature buffers: the frozen encoder of batch i+1 runs on its own stream
+        # while the decoder of batch i, its all-reduce and Adam run on the main stream (the
+        # encoder does not read any decoder parameter), so the latency-bound decoder kernels and
+        # the gradient exchange share the chip with the conv trunk.
+        nbuf = 2 if overlap else 1
+        enc_pool, dec_pool = torch.cuda.graph_pool_handle(), torch.cuda.graph_pool_handle()
+        g_enc = [torch.cuda.CUDAGraph() for _ in range(nbuf)]
+        g_dec = [torch.cuda.CUDAGraph() for _ in range(nbuf)]
+        feats_static, loss_static = [], []
+        for k in range(nbuf):
+            with torch.cuda.graph(g_enc[k], pool=enc_pool):
+                with torch.no_grad():
+                    feats_static.append(enc(imgs))
+        for k in range(nbuf):
+            opt.zero_grad(set_to_none=True)   # each capture overwrites the gradients (beta = 0)
+            with torch.cuda.graph(g_dec[k], pool=dec_pool):
+                preds, alphas = dec(feats_static[k], caps)
+                loss_k, _ = sat_amd.caption_loss(preds, alphas, caps)
+                loss_k.backward()
+            loss_static.append(loss_k)
         torch.cuda.synchronize()
 
     enc_events = []
+    s_main = torch.cuda.current_stream()
+    s_enc = torch.cuda.Stream() if overlap else s_main
+    ev_enc = [torch.cuda.Event() for _ in range(2)]
+    ev_dec = [torch.cuda.Event() for _ in range(2)]
 
-    def step():
-        if use_graph:
+    def replay_encoder(k, wait_dec):
+        with torch.cuda.stream(s_enc):
+            if wait_dec:   # feature buffer k was last read by the decoder two batches ago
+                s_enc.wait_event(ev_dec[k])
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            st.record()
-            g_enc.replay()
-            en.record()
-            enc_events.append((st, en))
-            g_dec.replay()
-            loss = loss_static
-        else:
-            opt.zero_grad()
-            loss = fwd_bwd()
-        if world > 1:
-            allreduce_grads(dec)
-        opt.step()
+            st.record(s_enc)
+            g_enc[k].replay()
+            en.record(s_enc)
+            ev_enc[k].record(s_enc)
+        enc_events.append((st, en))
+
+    def run(n):
+        """n full train steps (encoder fwd, decoder fwd + loss + bwd, all-reduce, Adam)."""
+        loss = None
+        if use_graph:
+            replay_encoder(0, False)
+        for i in range(n):
+            if use_graph:
+                k = i % len(g_enc)
+                s_main.wait_event(ev_enc[k])
+                g_dec[k].replay()
+                ev_dec[k].record(s_main)
+                loss = loss_static[k]
+                if i + 1 < n:
+                    if overlap:
+                        replay_encoder((i + 1) % 2, i >= 1)
+                    else:
+                        replay_encoder(0, False)
+            else:
+                opt.zero_grad()
+                loss = fwd_bwd()
+            if world > 1:
+                allreduce_grads(dec)
+            opt.step()
         return loss
 
-    for _ in range(2):   # replay warm-up
-        step()
+    run(2)   # replay warm-up
     enc_events.clear()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
+    loss = run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -278,7 +313,8 @@ def main():
             "config": {"workload": f"COCO-shaped {args.network} encoder (bf16 fwd) + attention/tf/ado decoder train "
                                    f"step, V={args.vocab}, T={args.seq}",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": args.seq,
-                       "parallelism": f"dp{world}", "hip_graph": use_graph},
+                       "parallelism": f"dp{world}", "hip_graph": use_graph,
+                       "encoder_decoder_overlap": overlap},
             "roofline": roof,
             "encoder_trunk": dict(trunk, graph_ms_per_step=(round(enc_ms / args.steps, 3) if enc_ms else None)),
             "loss": round(loss_v, 4),
