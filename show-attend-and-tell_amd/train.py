@@ -9,6 +9,8 @@ so it cannot be disabled, as in train.py:450), plus:
                   of the Karpathy-JSON dataset;  --vocab for its vocabulary size
   --dtype         bf16 (default, performance) | fp32 (exact parity mode)
   --max-steps     cap batches per epoch (smoke runs)
+  --no-overlap    encode each batch just before its decoder step (default: the frozen encoder of
+                  batch i+1 runs on a side stream beside batch i's decoder step)
 Multi-GPU: ``python -m torch.distributed.run --nproc-per-node N show-attend-and-tell_amd/train.py ...``
 (RCCL data parallel; the batch size is per GPU).  W&B logging is not part of this build; the
 reference's scalar names are printed / written as JSON lines instead.
@@ -125,6 +127,8 @@ def parse(argv=None):
     p.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     p.add_argument("--max-steps", type=int, default=0)
     p.add_argument("--out", type=str, default="model")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="encode each batch right before its decoder step instead of one batch ahead on a side stream")
     return p.parse_args(argv)
 
 
@@ -159,19 +163,49 @@ def loaders(args, split, rank, world):
                                        num_workers=4 if not args.synthetic else 0, pin_memory=True, drop_last=True)
 
 
+def encoded_batches(loader, encoder, device, dt, max_steps, overlap):
+    """(batch_idx, features, captions) of every training batch.  With ``overlap`` the frozen
+    encoder forward (and the host-to-device copy) of batch i+1 is issued on a side stream before
+    batch i is handed out, so it runs on the GPU beside batch i's decoder step, all-reduce and
+    Adam (the encoder reads no decoder parameter; train.py:29-31 freezes it for VGG19 and the
+    reference never optimises ResNet152's)."""
+    main = torch.cuda.current_stream(device)
+    side = torch.cuda.Stream(device) if overlap else main
+
+    def encode(imgs, captions):
+        with torch.cuda.stream(side), torch.no_grad():
+            imgs = imgs.to(device, non_blocking=True)
+            captions = captions.to(device, non_blocking=True)
+            feats = encoder(imgs, dtype=dt)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        return feats, captions, ev
+
+    pending = None
+    for batch_idx, (imgs, captions, _) in enumerate(loader):
+        if max_steps and batch_idx >= max_steps:
+            break
+        nxt = encode(imgs, captions)
+        if pending is not None:
+            yield pending
+        feats, caps, ev = nxt
+        main.wait_event(ev)
+        if side is not main:   # produced on the side stream, consumed on the main one
+            feats.record_stream(main)
+            caps.record_stream(main)
+        pending = (batch_idx, feats, caps)
+    if pending is not None:
+        yield pending
+
+
 def train_epoch(epoch, encoder, decoder, opt, loader, args, device, dt, world, log):
     """train.py:119-192"""
     encoder.eval()
     decoder.train()
     pad, skip = sat_amd.special_ids(args.bert)
     losses, top1, top5 = AverageMeter(), AverageMeter(), AverageMeter()
-    for batch_idx, (imgs, captions, _) in enumerate(loader):
-        if args.max_steps and batch_idx >= args.max_steps:
-            break
-        imgs = imgs.to(device, non_blocking=True)
-        captions = captions.to(device, non_blocking=True)
-        with torch.no_grad():
-            feats = encoder(imgs, dtype=dt)
+    for batch_idx, feats, captions in encoded_batches(loader, encoder, device, dt, args.max_steps,
+                                                      not args.no_overlap):
         opt.zero_grad()
         preds, alphas = decoder(feats, captions)
         loss, metrics = sat_amd.caption_loss(preds, alphas, captions, args.alpha_c, pad, skip)
