@@ -60,6 +60,10 @@ __device__ __forceinline__ void loadv(const T* p, float* o) {  // 16 bytes
 // context and the backward reductions are otherwise one L2 round trip per slot).
 constexpr int UNR = 4;
 
+// Workgroup barrier that orders LDS only: outstanding global loads stay in flight across it
+// (__syncthreads may also drain vmcnt).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 template <typename T>
 __device__ __forceinline__ uint4 ld16(const T* p, bool ok) {
   return ok ? *(const uint4*)p : make_uint4(0u, 0u, 0u, 0u);
@@ -93,19 +97,17 @@ __global__ __launch_bounds__(FNW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
   const int c0 = s * COLS;
   const T* ab = (const T*)a.a + (long)b * L * D + c0 + lane * VN;
 
-  // epilogue operand: gate pre-activation of this thread's output column
-  const int dout = c0 + tid;
-  const bool out_ok = tid < COLS && dout < D;
-  float gpre = 0.f;
-  if (a.gate_pre && out_ok) gpre = sum_parts(a.gate_pre, (long)b * a.gate_ld + dout, a.hg_splits, a.hg_split_stride);
-
-  // context rows of the first batch: in flight while the scores are formed
-  uint4 xa[FFU][FDV];
+  // Issue order = order of first use (vmcnt retires loads in order): the first batch of score
+  // rows, then U h + b and v, then the context rows and the gate pre-activation, which stay in
+  // flight while the scores and the softmax are computed.
+  uint4 xv[FFU][CH];
 #pragma unroll
   for (int u = 0; u < FFU; ++u)
 #pragma unroll
-    for (int v = 0; v < FDV; ++v)
-      xa[u][v] = ld16(ab + (long)(w + FNW * u) * D + v * 64 * VN, w + FNW * u < L && c0 + v * 64 * VN + lane * VN < D);
+    for (int c = 0; c < CH; ++c) {
+      const int l = w + FNW * u, e = c * 64 * VN + lane * VN;
+      xv[u][c] = ld16(Ws + (long)l * E + e, l < L && e < E);
+    }
 
   // ---- scores: lane owns VN consecutive e per chunk; (U h + b) and v live in registers ----
   float u_r[CH][VN], v_r[CH][VN];
@@ -123,16 +125,30 @@ __global__ __launch_bounds__(FNW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
       v_r[c][j] = v4.x; v_r[c][j + 1] = v4.y; v_r[c][j + 2] = v4.z; v_r[c][j + 3] = v4.w;
     }
   }
+
+  // context rows of the first batch and the epilogue's gate pre-activation (this thread's column)
+  uint4 xa[FFU][FDV];
+#pragma unroll
+  for (int u = 0; u < FFU; ++u)
+#pragma unroll
+    for (int v = 0; v < FDV; ++v)
+      xa[u][v] = ld16(ab + (long)(w + FNW * u) * D + v * 64 * VN, w + FNW * u < L && c0 + v * 64 * VN + lane * VN < D);
+  const int dout = c0 + tid;
+  const bool out_ok = tid < COLS && dout < D;
+  float gpre = 0.f;
+  if (a.gate_pre && out_ok) gpre = sum_parts(a.gate_pre, (long)b * a.gate_ld + dout, a.hg_splits, a.hg_split_stride);
+
   const float bv = a.v_b[0];
   for (int l0 = w; l0 < L; l0 += FNW * FFU) {
-    uint4 xv[FFU][CH];
+    if (l0 != w) {
 #pragma unroll
-    for (int u = 0; u < FFU; ++u)
+      for (int u = 0; u < FFU; ++u)
 #pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        const int l = l0 + FNW * u, e = c * 64 * VN + lane * VN;
-        xv[u][c] = ld16(Ws + (long)l * E + e, l < L && e < E);
-      }
+        for (int c = 0; c < CH; ++c) {
+          const int l = l0 + FNW * u, e = c * 64 * VN + lane * VN;
+          xv[u][c] = ld16(Ws + (long)l * E + e, l < L && e < E);
+        }
+    }
 #pragma unroll
     for (int u = 0; u < FFU; ++u) {
       const int l = l0 + FNW * u;
@@ -241,26 +257,32 @@ __global__ __launch_bounds__(ANW * 64) void attn_bwd1_kernel(AttnBwdArgs a) {
   const int L = a.L, D = a.D;
   const int d0 = s * COLS + lane * VD;
   const T* ab = (const T*)a.a + (long)b * L * D + d0;
-  // annotation rows of the first batch: independent of dL/dcontext, requested first
+  // issue order = order of first use (vmcnt retires in order): this thread's column operands,
+  // then the annotation rows of the first batch, which stay in flight through the LDS exchange
+  static_assert(COLS <= ANW * 64, "at most one column per thread");
+  const int dcol = s * COLS + tid;
+  const bool col_ok = tid < COLS && dcol < D;
+  float dg = 0.f, g = 0.f, cx = 0.f, dx = 0.f;
+  if (col_ok) {
+    dg = sum_parts(a.d_gated, (long)b * a.d_gated_ld + dcol, a.dg_splits, a.dg_split_stride);
+    g = a.gate[(long)b * a.gate_ld + dcol];
+    cx = a.ctx[(long)b * a.ctx_ld + dcol];
+    if (a.d_ctx_ext) dx = a.d_ctx_ext[(long)b * a.d_ctx_ext_ld + dcol];
+  }
   uint4 xa[FU];
 #pragma unroll
   for (int u = 0; u < FU; ++u) xa[u] = ld16(ab + (long)(w + ANW * u) * D, w + ANW * u < L && d0 < D);
-  for (int i = tid; i < COLS; i += ANW * 64) {
-    const int d = s * COLS + i;
+  if (tid < COLS) {
     float dctx = 0.f;
-    if (d < D) {
-      const float dg = sum_parts(a.d_gated, (long)b * a.d_gated_ld + d, a.dg_splits, a.dg_split_stride);
-      const float g = a.gate[(long)b * a.gate_ld + d];
-      const float c = a.ctx[(long)b * a.ctx_ld + d];
-      const float dx = a.d_ctx_ext ? a.d_ctx_ext[(long)b * a.d_ctx_ext_ld + d] : 0.f;
+    if (col_ok) {
       dctx = dg * g + dx;
-      const float dgp = dg * c * g * (1.f - g);
-      a.d_gpre[(long)b * a.d_gpre_ld + d] = dgp;
-      if (a.d_gpre_t) ((T*)a.d_gpre_t)[(long)b * a.d_gpre_ld + d] = (T)dgp;
+      const float dgp = dg * cx * g * (1.f - g);
+      a.d_gpre[(long)b * a.d_gpre_ld + dcol] = dgp;
+      if (a.d_gpre_t) ((T*)a.d_gpre_t)[(long)b * a.d_gpre_ld + dcol] = (T)dgp;
     }
-    s_dctx[i] = dctx;
+    s_dctx[tid] = dctx;
   }
-  __syncthreads();
+  lds_barrier();   // the annotation rows stay in flight
   float dctx[VD];
 #pragma unroll
   for (int j = 0; j < VD; ++j) dctx[j] = s_dctx[lane * VD + j];
