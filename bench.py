@@ -62,8 +62,8 @@ def conv_launches(network, B, H=224):
         out.append(dict(cls=f"{name} {M}x{N}x{K}", flops=f, bytes=by, bound=bound))
 
     if network == "resnet152":
-        h = H // 2
-        add("stem7x7s2", B * h * h, 64, 7 * 7 * 8, B * H * H * 8, real_k=147)
+        h = H // 2   # stem: 4x4 conv over the 2x2 space-to-depth input (16 channels, 12 real)
+        add("stem7x7s2", B * h * h, 64, 4 * 4 * 16, B * h * h * 16, real_k=147)
         h //= 2
         cin = 64
         for li, (n, pl) in enumerate(zip([3, 8, 36, 3], [64, 128, 256, 512])):

@@ -105,7 +105,12 @@ int sat_mean_rows_abi(const void* a, int B, int L, int D, int dtype, float* out_
 /* --- encoder (encoder.py:33-40 with the torchvision trunks) ------------- */
 /* NCHW fp32 image batch -> NHWC (dtype) with channels zero-padded to Cp. */
 int sat_nchw_to_nhwc(int N, int C, int H, int W, int Cp, int dtype, const float* x, void* y, void* stream);
-/* y = act(conv(x, w) + bias [+ residual]); x NHWC [N,H,W,C], y NHWC [N,OH,OW,Cout];
+/* NCHW fp32 (C <= 4, H and W even) -> space-to-depth NHWC [N, H/2, W/2, 16] (dtype): channel
+ * (sy*2 + sx)*C + c holds x[n, c, 2*by + sy, 2*bx + sx], channels 4C..15 zero.  Feeds the ResNet152
+ * stem as a 4x4 / stride-1 / top-left-pad-2 conv (encoder.py:13-17 conv1, re-laid out). */
+int sat_nchw_to_s2d(int N, int C, int H, int W, int dtype, const float* x, void* y, void* stream);
+/* y = act(conv(x, w) + bias [+ residual]); x NHWC [N,H,W,C], y NHWC [N,OH,OW,Cout]; pad is the
+ * top/left padding, OH/OW are taken as given (bottom/right padding = whatever they imply);
  * covers Conv2d+ReLU (VGG19) and Conv2d+BatchNorm(eval, folded)+[residual]+ReLU (ResNet152). */
 int sat_conv2d_nhwc(const SatConvGeom* g, int Cout, int dtype, const void* x, const void* w,
                     const float* bias, const void* residual, int relu, void* y, void* stream);

@@ -35,6 +35,33 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__
   }
 }
 
+// ---- NCHW fp32 -> space-to-depth NHWC (T): [N, H/2, W/2, 16], channel (sy*2+sx)*C + c ----------
+// The ResNet stem (7x7 / stride 2, Cin = 3) becomes a 4x4 / stride 1 conv over 16 channels
+// (12 real): K = 256 instead of 7*7*8 = 392, and half the input bytes of the 8-channel layout.
+// One output pixel (32 B) per thread.
+template <typename T>
+__global__ void nchw_to_s2d16_kernel(const float* __restrict__ x, T* __restrict__ y, int N, int C, int H, int W) {
+  const int H2 = H / 2, W2 = W / 2;
+  const long total = (long)N * H2 * W2;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
+    const long n = p / ((long)H2 * W2), r = p - n * H2 * W2;
+    const int by = (int)(r / W2), bx = (int)(r - (long)by * W2);
+    const float* src = x + n * C * H * W;
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = 0.f;
+#pragma unroll
+    for (int sy = 0; sy < 2; ++sy)
+#pragma unroll
+      for (int sx = 0; sx < 2; ++sx)
+        for (int c = 0; c < C; ++c)
+          v[(sy * 2 + sx) * C + c] = src[((long)c * H + 2 * by + sy) * W + 2 * bx + sx];
+    T* dst = y + p * 16;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dst[q] = (T)v[q];
+  }
+}
+
 // ---- max-pool NHWC (floor mode), 8 channels per thread (16-B bf16 / 2x16-B f32 accesses) ----
 template <typename T>
 __global__ void maxpool_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W, int C, int k,
@@ -350,6 +377,16 @@ extern "C" int sat_nchw_to_nhwc(int N, int C, int H, int W, int Cp, int dtype, c
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, x, (bf16*)y, N, C, H, W, Cp);
   else
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, x, (float*)y, N, C, H, W, Cp);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sat_nchw_to_s2d(int N, int C, int H, int W, int dtype, const float* x, void* y, void* stream) {
+  SAT_REQUIRE(x && y && C > 0 && 4 * C <= 16 && H % 2 == 0 && W % 2 == 0);
+  const int g = grid_for((long)N * (H / 2) * (W / 2));
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(nchw_to_s2d16_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, x, (bf16*)y, N, C, H, W);
+  else
+    hipLaunchKernelGGL(nchw_to_s2d16_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, x, (float*)y, N, C, H, W);
   return (int)hipGetLastError();
 }
 

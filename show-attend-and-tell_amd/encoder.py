@@ -13,7 +13,10 @@ activations:
     (sat_conv2d_nhwc): M = B*OH*OW, N = Cout, K = KH*KW*Cin;
   * MaxPool2d is a streaming NHWC kernel;
   * the image is converted once to NHWC with channels zero-padded 3 -> 8 so the
-    first conv loads 16-byte vectors;
+    first conv loads 16-byte vectors (VGG19); for ResNet152 it is converted to a
+    2x2 space-to-depth layout instead ([H/2, W/2, 16], 12 real channels) and the
+    7x7 / stride-2 / pad-3 stem runs as the equivalent 4x4 / stride-1 conv with
+    re-laid-out weights (K = 256 instead of 7*7*8 = 392, half the input bytes);
   * the final NHWC tensor already IS ``permute(0,2,3,1).view(B,-1,C)``
     (encoder.py:37-39): no transpose.
 
@@ -33,6 +36,25 @@ from . import ops
 
 VGG19_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M", 512, 512, 512, 512, "M"]
 IN_PAD = 8  # input channels padded 3 -> 8 (16-B bf16 vectors in the im2col loader)
+S2D_C = 16  # space-to-depth stem input channels (2*2*3 real, zero-padded)
+
+
+def stem_weight_s2d(w):
+    """[Cout, KH=7, KW=7, Cin<=4] (NHWC-ordered, folded) stride-2 / pad-3 stem weights -> the
+    [Cout, 4, 4, 16] weights of the same conv over the space-to-depth input: input row
+    ih = 2*oh - 3 + kh = 2*(oh - 2 + th) + sy with kh + 1 = 2*th + sy, so tap (th, tw) and
+    sub-pixel (sy, sx) of channel c land in s2d channel (sy*2 + sx)*Cin + c; the (kh + 1 = 0)
+    row / column of the 8x8 footprint carries zero weight."""
+    cout, kh_n, kw_n, cin = w.shape
+    assert kh_n == 7 and kw_n == 7 and 4 * cin <= S2D_C
+    out = torch.zeros(cout, 4, 4, S2D_C, dtype=w.dtype, device=w.device)
+    for kh in range(7):
+        th, sy = divmod(kh + 1, 2)
+        for kw in range(7):
+            tw, sx = divmod(kw + 1, 2)
+            c0 = (sy * 2 + sx) * cin
+            out[:, th, tw, c0:c0 + cin] = w[:, kh, kw, :]
+    return out
 
 
 class Bottleneck(nn.Module):
@@ -121,13 +143,13 @@ class Encoder(nn.Module):
         self._plan_key = None
         self.timing = None   # bench hook: list collecting (start, end) HIP events around every conv launch
 
-    def _conv(self, x, f, relu, residual=None):
+    def _conv(self, x, f, relu, residual=None, out_hw=None):
         w, b, s, p = f
         if self.timing is None:
-            return ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual)
+            return ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual, out_hw=out_hw)
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st.record()
-        y = ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual)
+        y = ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual, out_hw=out_hw)
         en.record()
         self.timing.append((st, en))
         return y
@@ -155,7 +177,9 @@ class Encoder(nn.Module):
         plan = []
         mods = list(self.net.children())
         if self.network == "resnet152":
-            plan.append(("conv", self._fold(mods[0], mods[1], IN_PAD), True, None))
+            w, b, _, _ = self._fold(mods[0], mods[1])
+            plan.append(("stem_s2d", (stem_weight_s2d(w.float()).to(self.compute_dtype).contiguous(), b, 1, 2),
+                         self._fold(mods[0], mods[1], IN_PAD)))
             plan.append(("pool", 3, 2, 1))
             for layer in mods[4:]:
                 for blk in layer:
@@ -184,8 +208,17 @@ class Encoder(nn.Module):
         L.require_device(x)
         dtype = dtype or self.compute_dtype
         plan = self.compiled_plan(x.device, dtype)
-        y = ops.nchw_to_nhwc(x, IN_PAD, dtype)
+        H, W = x.shape[2], x.shape[3]
+        if plan[0][0] == "stem_s2d" and H % 2 == 0 and W % 2 == 0:
+            y = ops.nchw_to_s2d(x, dtype)
+            y = self._conv(y, plan[0][1], True, out_hw=(H // 2, W // 2))
+        elif plan[0][0] == "stem_s2d":   # odd image sizes: the stem on the 8-channel layout
+            y = self._conv(ops.nchw_to_nhwc(x, IN_PAD, dtype), plan[0][2], True)
+        else:
+            y = ops.nchw_to_nhwc(x, IN_PAD, dtype)
         for step in plan:
+            if step[0] == "stem_s2d":
+                continue
             if step[0] == "conv":
                 y = self._conv(y, step[1], step[2])
             elif step[0] == "pool":

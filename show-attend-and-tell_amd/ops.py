@@ -83,14 +83,31 @@ def nchw_to_nhwc(x, c_pad, dtype):
     return y
 
 
-def conv2d_nhwc(x, w, bias, stride, pad, relu, residual=None, out=None):
-    """x [N,H,W,C] ; w [Cout,KH,KW,C] (same dtype) ; bias f32 [Cout]."""
+def nchw_to_s2d(x, dtype):
+    """[N,C,H,W] f32 (C <= 4, H, W even) -> space-to-depth [N,H/2,W/2,16] (dtype)."""
+    L.require_device(x)
+    x = x.contiguous() if not x.is_contiguous() else x
+    if x.dtype != torch.float32:
+        raise TypeError("images must be float32 (post-Normalize domain, train.py:27-32)")
+    N, C, H, W = x.shape
+    y = torch.empty(N, H // 2, W // 2, 16, device=x.device, dtype=dtype)
+    L.check(L.lib().sat_nchw_to_s2d(N, C, H, W, L.dtype_code(dtype), L.ptr(x), L.ptr(y), L.stream_of(y)),
+            "sat_nchw_to_s2d")
+    return y
+
+
+def conv2d_nhwc(x, w, bias, stride, pad, relu, residual=None, out=None, out_hw=None):
+    """x [N,H,W,C] ; w [Cout,KH,KW,C] (same dtype) ; bias f32 [Cout].  ``pad`` pads top/left;
+    ``out_hw`` (default: symmetric padding) fixes the output size."""
     L.require_device(x, w)
     N, H, W, C = x.shape
     Cout, KH, KW, Cw = w.shape
     assert Cw == C, (w.shape, x.shape)
-    OH = (H + 2 * pad - KH) // stride + 1
-    OW = (W + 2 * pad - KW) // stride + 1
+    if out_hw is None:
+        OH = (H + 2 * pad - KH) // stride + 1
+        OW = (W + 2 * pad - KW) // stride + 1
+    else:
+        OH, OW = out_hw
     y = out if out is not None else torch.empty(N, OH, OW, Cout, device=x.device, dtype=x.dtype)
     g = L.SatConvGeom(N, H, W, C, KH, KW, stride, pad, OH, OW)
     if residual is not None:

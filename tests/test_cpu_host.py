@@ -109,3 +109,25 @@ def test_cli_flags_mirror_reference():
     spec.loader.exec_module(g)
     with pytest.raises(SystemExit):
         g.main(["--img-path", "x.png", "--wandb-run", "a/b/c", "--wandb-model", "m"])
+
+
+def test_stem_space_to_depth_equivalence():
+    """The ResNet152 stem (7x7 / stride 2 / pad 3, encoder.py:13-17 conv1) equals the 4x4 /
+    stride-1 conv over the 2x2 space-to-depth input with stem_weight_s2d weights (top/left pad 2,
+    bottom/right pad 1), checked in fp64 with torch's CPU conv as the reference."""
+    import torch.nn.functional as F
+    from sat_amd.encoder import stem_weight_s2d
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 3, 20, 16, generator=g, dtype=torch.float64)
+    w = torch.randn(5, 3, 7, 7, generator=g, dtype=torch.float64)
+    ref = F.conv2d(x, w, stride=2, padding=3)
+    N, C, H, W = x.shape
+    xs = torch.zeros(N, 16, H // 2, W // 2, dtype=x.dtype)   # sat_nchw_to_s2d's channel order
+    for sy in range(2):
+        for sx in range(2):
+            c0 = (sy * 2 + sx) * C
+            xs[:, c0:c0 + C] = x[:, :, sy::2, sx::2]
+    ws = stem_weight_s2d(w.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+    out = F.conv2d(F.pad(xs, (2, 1, 2, 1)), ws)
+    assert out.shape == ref.shape
+    assert torch.allclose(out, ref, rtol=0, atol=1e-10)
