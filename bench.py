@@ -221,17 +221,17 @@ def main():
         # encoder does not read any decoder parameter), so the latency-bound decoder kernels and
         # the gradient exchange share the chip with the conv trunk.
         nbuf = 2 if overlap else 1
-        enc_pool, dec_pool = torch.cuda.graph_pool_handle(), torch.cuda.graph_pool_handle()
+        # one private memory pool per graph: no intermediate of one graph aliases another's
         g_enc = [torch.cuda.CUDAGraph() for _ in range(nbuf)]
         g_dec = [torch.cuda.CUDAGraph() for _ in range(nbuf)]
         feats_static, loss_static = [], []
         for k in range(nbuf):
-            with torch.cuda.graph(g_enc[k], pool=enc_pool):
+            with torch.cuda.graph(g_enc[k]):
                 with torch.no_grad():
                     feats_static.append(enc(imgs))
         for k in range(nbuf):
             opt.zero_grad(set_to_none=True)   # each capture overwrites the gradients (beta = 0)
-            with torch.cuda.graph(g_dec[k], pool=dec_pool):
+            with torch.cuda.graph(g_dec[k]):
                 preds, alphas = dec(feats_static[k], caps)
                 loss_k, _ = sat_amd.caption_loss(preds, alphas, caps)
                 loss_k.backward()

@@ -502,8 +502,7 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
       a.splitk = 2; a.kchunk = sat_cdiv(g.K, BK) * BK;   // split 1 has an empty K range and adds 0
     }
     if (g.beta == 0.f) {
-      if (g.ldc == g.N) { SAT_CHECK(hipMemsetAsync(g.C, 0, (size_t)g.M * g.N * 4, s)); }
-      else { SAT_CHECK(hipMemset2DAsync(g.C, (size_t)g.ldc * 4, 0, (size_t)g.N * 4, g.M, s)); }
+      SAT_CHECK((hipError_t)sat_zero_rows((float*)g.C, g.ldc, g.M, g.N, s));
     }
   }
   a.partial = partial ? 1 : 0;

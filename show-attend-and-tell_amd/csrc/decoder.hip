@@ -447,9 +447,9 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
 
   // ---------------- recurrent BPTT (reverse time loop) ----------------
   if (att) {
-    SAT_CHECK(hipMemsetAsync(w.dWs_acc, 0, (size_t)B * L * E * 4, s));
-    SAT_CHECK(hipMemsetAsync(w.dv_acc, 0, (size_t)B * E * 4, s));
-    SAT_CHECK(hipMemsetAsync(w.dbv_acc, 0, (size_t)B * 4, s));
+    SAT_CHECK((hipError_t)sat_zero_rows(w.dWs_acc, (long)B * L * E, 1, (long)B * L * E, s));
+    SAT_CHECK((hipError_t)sat_zero_rows(w.dv_acc, (long)B * E, 1, (long)B * E, s));
+    SAT_CHECK((hipError_t)sat_zero_rows(w.dbv_acc, B, 1, B, s));
   }
   for (int t = T1 - 1; t >= 0; --t) {
     LstmBwdArgs l{};
@@ -509,7 +509,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   SAT_CHECK((hipError_t)wgrad(4 * E, D, R, dg_t, HG, w.gated_t, D, G(lay->wih + E), E + D));
   if (!d.bert) {  // dense embedding gradient, scatter-added by fed token (decoder.py:87,133)
     SAT_CHECK((hipError_t)dgrad(R, E, 4 * E, dg_t, HG, c.W(lay->wih), E + D, w.demb, E, d.ado ? w.dcomb : nullptr, E));
-    if (!accumulate) SAT_CHECK(hipMemsetAsync(G(lay->embedding), 0, (size_t)V * E * 4, s));
+    if (!accumulate) SAT_CHECK((hipError_t)sat_zero_rows(G(lay->embedding), (long)V * E, 1, (long)V * E, s));
     SAT_CHECK((hipError_t)sat_embed_scatter_add(w.demb, w.tok, R, E, G(lay->embedding), s));
   }
   if (att) {

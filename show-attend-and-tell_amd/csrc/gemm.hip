@@ -13,6 +13,7 @@
 // fragments; the epilogue fuses bias, an addend matrix (residual / precomputed
 // gate terms), beta*C accumulation, activation and an optional second output.
 #include "sat_common.h"
+#include "sat_internal.h"
 
 #include <type_traits>
 
@@ -405,8 +406,7 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s) {
       k.kchunk = chunk;
       k.splitk = sat_cdiv(g.K, chunk);
       if (g.beta == 0.f) {
-        if (g.ldc == g.N) SAT_CHECK(hipMemsetAsync(g.C, 0, (size_t)g.M * g.N * 4, s));
-        else SAT_CHECK(hipMemset2DAsync(g.C, (size_t)g.ldc * 4, 0, (size_t)g.N * 4, g.M, s));
+        SAT_CHECK((hipError_t)sat_zero_rows((float*)g.C, g.ldc, g.M, g.N, s));
       }
     }
   }

@@ -183,6 +183,22 @@ __global__ void fill_kernel(float* p, long n, float v) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = v;
 }
 
+// Zero a [rows, cols] fp32 block with row stride ld.  Used instead of hipMemset(2D)Async: a
+// memset node inside a replayed hipGraph left every fourth dword of large buffers unwritten on
+// this stack when two graphs share the buffer (bench.py's two decoder graphs), so every
+// beta = 0 atomic accumulation target is cleared by a kernel node instead.
+__global__ void zero_rows_kernel(float* p, long ld, long rows, long cols) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  if (ld == cols && ((uintptr_t)p & 15) == 0) {
+    const long n = rows * cols, n4 = n >> 2;
+    float4* p4 = reinterpret_cast<float4*>(p);
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) p4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (long i = (n4 << 2) + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) p[i] = 0.f;
+    return;
+  }
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < rows * cols; i += stride) p[(i / cols) * ld + i % cols] = 0.f;
+}
+
 template <typename T>
 __global__ void broadcast_rows_kernel(const T* src, int B, int D, int T1, T* dst) {
   const long n = (long)B * T1 * D;
@@ -269,6 +285,13 @@ int sat_ado_combine(const float* fh, const float* fz, const void* emb, long n, i
 int sat_fill_const(float* p, long n, float v, hipStream_t s) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, n, v);
+  return (int)hipGetLastError();
+}
+int sat_zero_rows(float* p, long ld, long rows, long cols, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return 0;
+  const long n = rows * cols;
+  const long work = (ld == cols && ((uintptr_t)p & 15) == 0) ? (n + 3) / 4 : n;
+  hipLaunchKernelGGL(zero_rows_kernel, dim3(grid_for(work)), dim3(256), 0, s, p, ld, rows, cols);
   return (int)hipGetLastError();
 }
 int sat_broadcast_rows(const void* src, int B, int D, int T1, int dtype, void* dst, hipStream_t s) {

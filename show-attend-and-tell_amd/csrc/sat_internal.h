@@ -101,6 +101,7 @@ int sat_ado_bwd_split(const float* d_comb, const float* fh, const float* fz, lon
 int sat_ado_combine(const float* fh, const float* fz, const void* emb, long n, int dtype,
                     void* comb_t, hipStream_t s);
 int sat_fill_const(float* p, long n, float v, hipStream_t s);
+int sat_zero_rows(float* p, long ld, long rows, long cols, hipStream_t s);   // graph-safe memset
 int sat_broadcast_rows(const void* src, int B, int D, int T1, int dtype, void* dst, hipStream_t s);
 int sat_row_sum_accumulate(const float* X, int R, int N, float* out, hipStream_t s);
 int sat_tokens_from_captions(const int64_t* caps, int B, int T, int T1, int32_t* tok, hipStream_t s);
