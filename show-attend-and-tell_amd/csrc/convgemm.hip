@@ -24,7 +24,11 @@
 // same workgroups.  Variants that did not beat this kernel on the ResNet152 shapes: all fragment
 // reads issued before the DMA (sched_barrier-pinned), a persistent-tile variant with register
 // epilogue, non-temporal epilogue traffic, 16-wave and 4-wave (128x64 wave tile, in-wave
-// pipelined) 256x128 tiles.
+// pipelined) 256x128 tiles, residual rows requested before the main loop, a first-round start
+// offset for the second workgroup of each CU, and stream-K (2 x CUs workgroups sharing the
+// k-tile units, split tiles finished by the last arriver from sc1-published fp32 partials: the
+// 392-tile L3 shapes went 30 -> 46 us and 53 -> 68 us; publishing and re-reading 64 KB partials
+// per split costs more than the idle slots of the last round, tools/conv_trace.py).
 #include "sat_common.h"
 #include "sat_internal.h"
 
@@ -46,6 +50,7 @@ struct FArgs {
   int splitk, kchunk;      // atomic split-K (fp32 C, act NONE): blockIdx.z = split
   int xcd_remap;
   int partial; long split_stride;   // partial-output split-K: split s stores plain into C + s*split_stride
+  unsigned long* trace;    // diagnostics (tools/conv_trace.py): per-workgroup timestamps, or null
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -132,6 +137,8 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
   const int m0 = (tile / gridDim.x) * BM, n0 = (tile % gridDim.x) * BN;
   const int M = a.M, N = a.N;
   const int split = blockIdx.z;
+  unsigned long tr_t0 = 0, tr_t1 = 0;
+  if (a.trace) tr_t0 = __builtin_amdgcn_s_memrealtime();
   const int kbeg = split * a.kchunk;
   const int K = min(a.K, kbeg + a.kchunk);
 
@@ -294,6 +301,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
     compute(kt % NS);
   }
   __syncthreads();   // every wave done reading the ring before the epilogue reuses the LDS
+  if (a.trace) tr_t1 = __builtin_amdgcn_s_memrealtime();
 
   if (a.splitk > 1 && !a.partial) {   // atomic split-K: fp32 C, bias in split 0, act NONE (host-checked)
 #pragma unroll
@@ -393,12 +401,24 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
       }
     }
   }
+  if (a.trace) {
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned long t2 = __builtin_amdgcn_s_memrealtime();
+      const int lin = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+      unsigned long* rec = a.trace + (long)lin * 4;
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+      rec[0] = tr_t0; rec[1] = tr_t1; rec[2] = t2; rec[3] = ((unsigned long)xcc << 32) | hw;
+    }
+  }
 }
 
 __device__ __attribute__((aligned(16))) bf16 g_zero16[64];
 
 // experiment overrides (tools/bench_conv.py): 0 = automatic
 int g_force_stages = 0, g_force_tile = 0, g_xcd_remap = 1;
+unsigned long* g_trace = nullptr;
 
 // tile configurations (ids of sat_fast_gemm_set_config)
 enum { T_AUTO = 0, T128x128W8 = 1, T128x64W8 = 2, T128x128W4 = 3, T128x256W8 = 4, T256x128W8 = 5 };
@@ -518,6 +538,7 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
     a.stride = g.conv.stride; a.pad = g.conv.pad; a.OH = g.conv.OH; a.OW = g.conv.OW;
   }
   a.xcd_remap = g_xcd_remap;
+  a.trace = g_trace;
   dim3 grid(sat_cdiv(g.N, bn), sat_cdiv(g.M, bm), a.splitk);
   // skinny partial-split GEMMs run 2-4 k-tiles per block: a 3-deep ring puts the first two in
   // flight at once (their block counts leave LDS occupancy irrelevant)
@@ -528,6 +549,12 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   else launch_tile<false, false>(tcfg, ns, grid, s, a);
   *err = (int)hipGetLastError();
   return 1;
+}
+
+// diagnostics: per-workgroup [start, main loop done, end, hw id] records (4 x u64, 100 MHz clock)
+extern "C" int sat_fast_gemm_set_trace(void* buf) {
+  g_trace = (unsigned long*)buf;
+  return 0;
 }
 
 extern "C" int sat_fast_gemm_set_config(int stages, int tile, int xcd_remap) {

@@ -12,7 +12,8 @@ from sat_amd import ops  # noqa: E402
 
 SHAPES = {"L1_c3": (56, 64, 256, 1, 1, 0, 1), "L2_c3": (28, 128, 512, 1, 1, 0, 1), "L3_c1": (14, 1024, 256, 1, 1, 0, 0),
           "L3_c2": (14, 256, 256, 3, 1, 1, 0), "L3_c3": (14, 256, 1024, 1, 1, 0, 1), "L2_c2": (28, 128, 128, 3, 1, 1, 0),
-          "stem": (224, 8, 64, 7, 2, 3, 0)}
+          "stem": (224, 8, 64, 7, 2, 3, 0),
+          "L3_c2_16": (16, 256, 256, 3, 1, 1, 0), "L3_c1_16": (16, 1024, 256, 1, 1, 0, 0)}
 name = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 tile = int(sys.argv[3]) if len(sys.argv) > 3 else 0
