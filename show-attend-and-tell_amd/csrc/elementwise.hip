@@ -62,6 +62,37 @@ __global__ void nchw_to_s2d16_kernel(const float* __restrict__ x, T* __restrict_
   }
 }
 
+// RGB (C = 3) bf16 form of the above: one output pixel per thread, the two input columns of each
+// (channel, row) as one 8-byte load, the 16 output channels as two 16-byte stores.
+__global__ __launch_bounds__(256) void nchw3_to_s2d16_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y,
+                                                                  int N, int H, int W) {
+  const int H2 = H / 2, W2 = W / 2;
+  const long p = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (p >= (long)N * H2 * W2) return;
+  const long n = p / ((long)H2 * W2), r = p - n * H2 * W2;
+  const int by = (int)(r / W2), bx = (int)(r - (long)by * W2);
+  const float* src = x + n * 3 * H * W;
+  float2 v[2][3];
+#pragma unroll
+  for (int sy = 0; sy < 2; ++sy)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[sy][c] = *(const float2*)(src + ((long)c * H + 2 * by + sy) * W + 2 * bx);
+  uint4 u[2];
+  bf16* o = (bf16*)u;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) o[q] = (bf16)0.f;
+#pragma unroll
+  for (int sy = 0; sy < 2; ++sy)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      o[(sy * 2 + 0) * 3 + c] = (bf16)v[sy][c].x;
+      o[(sy * 2 + 1) * 3 + c] = (bf16)v[sy][c].y;
+    }
+  uint4* dst = (uint4*)(y + p * 16);
+  dst[0] = u[0];
+  dst[1] = u[1];
+}
+
 // ---- max-pool NHWC (floor mode), 8 channels per thread (16-B bf16 / 2x16-B f32 accesses) ----
 template <typename T>
 __global__ void maxpool_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W, int C, int k,
@@ -108,6 +139,52 @@ __global__ void maxpool_kernel(const T* __restrict__ x, T* __restrict__ y, int N
       *(uint4*)(dst + 4) = *(uint4*)(o + 4);
     }
   }
+}
+
+// bf16 k x k pool (the ResNet152 3x3/s2/p1 stem pool): one output pixel x 8 channels per thread,
+// every window tap requested before the first compare (clamped address + validity select), one
+// pass over the grid: the grid-stride form above issues its taps behind per-tap branches.
+template <int KS>
+__global__ __launch_bounds__(256) void maxpool_bf16_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N,
+                                                           int H, int W, int C, int stride, int pad, int OH,
+                                                           int OW) {
+  const int C8 = C / 8;
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= (long)N * OH * OW * C8) return;
+  const int c8 = (int)(i % C8);
+  long p = i / C8;
+  const int ow = (int)(p % OW); p /= OW;
+  const int oh = (int)(p % OH); const int n = (int)(p / OH);
+  uint4 v[KS * KS];
+  bool ok[KS * KS];
+#pragma unroll
+  for (int kh = 0; kh < KS; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < KS; ++kw) {
+      const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
+      const bool in = ih >= 0 && ih < H && iw >= 0 && iw < W;
+      const int ihc = in ? ih : 0, iwc = in ? iw : 0;
+      ok[kh * KS + kw] = in;
+      v[kh * KS + kw] = *(const uint4*)(x + (((long)n * H + ihc) * W + iwc) * C + c8 * 8);
+    }
+  float m[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < KS * KS; ++t) {
+    if (!ok[t]) continue;
+    const bf16* h = (const bf16*)&v[t];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float f = (float)h[e];
+      m[e] = (f > m[e] || f != f) ? f : m[e];   // NaN propagates like torch max_pool2d
+    }
+  }
+  uint4 u;
+  bf16* o = (bf16*)&u;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = (bf16)m[e];
+  *(uint4*)(y + i * 8) = u;
 }
 
 template <typename TI, typename TO>
@@ -383,7 +460,11 @@ extern "C" int sat_nchw_to_nhwc(int N, int C, int H, int W, int Cp, int dtype, c
 extern "C" int sat_nchw_to_s2d(int N, int C, int H, int W, int dtype, const float* x, void* y, void* stream) {
   SAT_REQUIRE(x && y && C > 0 && 4 * C <= 16 && H % 2 == 0 && W % 2 == 0);
   const int g = grid_for((long)N * (H / 2) * (W / 2));
-  if (dtype == SAT_BF16)
+  if (dtype == SAT_BF16 && C == 3 && ((uintptr_t)x & 7) == 0 && ((uintptr_t)y & 15) == 0) {
+    const long total = (long)N * (H / 2) * (W / 2);
+    hipLaunchKernelGGL(nchw3_to_s2d16_bf16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, x, (bf16*)y, N, H, W);
+  } else if (dtype == SAT_BF16)
     hipLaunchKernelGGL(nchw_to_s2d16_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, x, (bf16*)y, N, C, H, W);
   else
     hipLaunchKernelGGL(nchw_to_s2d16_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, x, (float*)y, N, C, H, W);
@@ -397,7 +478,10 @@ extern "C" int sat_maxpool2d_nhwc(int N, int H, int W, int C, int k, int stride,
   SAT_REQUIRE(C % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0);
   long total = (long)N * OH * OW * (C / 8);
   int g = grid_for(total);
-  if (dtype == SAT_BF16)
+  if (dtype == SAT_BF16 && k == 3) {
+    hipLaunchKernelGGL(maxpool_bf16_kernel<3>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16*)x, (bf16*)y, N, H, W, C, stride, pad, OH, OW);
+  } else if (dtype == SAT_BF16)
     hipLaunchKernelGGL(maxpool_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, (bf16*)y, N, H,
                        W, C, k, stride, pad, OH, OW);
   else

@@ -101,6 +101,37 @@ def test_maxpool(sat, k, stride, pad):
     assert torch.equal(y.permute(0, 3, 1, 2).cpu(), ref)
 
 
+@pytest.mark.parametrize("N,C,H,k,stride,pad", [(2, 64, 112, 3, 2, 1),   # ResNet152 stem pool (bf16 3x3 kernel)
+                                                (3, 16, 13, 3, 2, 1),     # odd size: clipped windows
+                                                (2, 32, 14, 2, 2, 0)])    # generic bf16 path
+def test_maxpool_bf16(sat, N, C, H, k, stride, pad):
+    """bf16 pooling is exact (max of representable values), NaN propagates like torch."""
+    from sat_amd import ops
+    g = torch.Generator().manual_seed(N * C + H)
+    x = torch.randn(N, C, H, H, generator=g).bfloat16()
+    x[0, 1, 2, 3] = float("nan")
+    ref = F.max_pool2d(x.float(), k, stride, pad)
+    y = ops.maxpool2d_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV), k, stride, pad)
+    y = y.permute(0, 3, 1, 2).float().cpu()
+    assert torch.equal(torch.isnan(y), torch.isnan(ref))
+    assert torch.equal(torch.nan_to_num(y), torch.nan_to_num(ref))
+
+
+@pytest.mark.parametrize("C,H,W", [(3, 224, 224), (3, 10, 6), (2, 8, 8)])
+def test_nchw_to_s2d_exact(sat, C, H, W):
+    """sat_nchw_to_s2d: channel (sy*2 + sx)*C + c of block (by, bx) holds x[n, c, 2by+sy, 2bx+sx]
+    rounded to bf16; channels 4C..15 are zero (bit-exact)."""
+    from sat_amd import ops
+    x = torch.randn(2, C, H, W, generator=torch.Generator().manual_seed(C * H + W))
+    y = ops.nchw_to_s2d(x.to(DEV), torch.bfloat16).cpu()
+    ref = torch.zeros(2, H // 2, W // 2, 16, dtype=torch.bfloat16)
+    for sy in range(2):
+        for sx in range(2):
+            for c in range(C):
+                ref[..., (sy * 2 + sx) * C + c] = x[:, c, sy::2, sx::2].bfloat16()
+    assert torch.equal(y, ref)
+
+
 # ---------------------------------------------------------------------------- decoder vs golden
 def build_decoder(sat, g, dtype=torch.float32):
     c = g["cfg"]
