@@ -51,6 +51,7 @@ struct FArgs {
   int xcd_remap;
   int partial; long split_stride;   // partial-output split-K: split s stores plain into C + s*split_stride
   unsigned long* trace;    // diagnostics (tools/conv_trace.py): per-workgroup timestamps, or null
+  int res_lds;             // fast_gemm_kernel<..., RL = true> epilogue (host-checked shape)
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -107,7 +108,10 @@ __device__ __forceinline__ void wait_vm_barrier() {
 }
 
 // Tile configurations: BM x BN block tile, WGM x WGN waves (wave tile BM/WGM x BN/WGN).
-template <int BM, int BN, int WGM, int WGN, bool AT, bool BT, int NS>
+// RL: bf16 residual + bf16 output epilogue through LDS (128x128 tiles, NS = 2, N % 128 == 0): the
+// residual tile is DMA'd into the free ring stage during the last k-tile, added in the MFMA
+// accumulator layout (ds_read_b64_tr_b16), and the finished bf16 tile is staged for 16-B row stores.
+template <int BM, int BN, int WGM, int WGN, bool AT, bool BT, int NS, bool RL = false>
 __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
   constexpr int NW = WGM * WGN;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
@@ -241,6 +245,23 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
     }
   };
 
+  // RL: the 128 x 128 bf16 residual tile into ring stage buf, 4 rows of 256 B per instruction,
+  // 16-B chunk ch of row r at slot ch ^ swz256(r) (the ds_read_b64_tr_b16 image of frag_tr)
+  auto stage_res = [&](int buf) {
+    if constexpr (RL) {
+      static_assert(BM == 128 && BN == 128 && NS == 2, "RL epilogue geometry");
+      if (!a.add1) return;
+#pragma unroll
+      for (int j = 0; j < 32 / NW; ++j) {
+        const int ins = w * (32 / NW) + j, r = ins * 4 + (lane >> 4);
+        const int ch = (lane & 15) ^ swz256(r);
+        const bool ok = m0 + r < M;
+        dma16(sel(ok, (const bf16*)a.add1 + (long)(m0 + r) * a.ld_add1 + n0 + 8 * ch, a.zero16),
+              smem + buf * STAGE + ins * 1024);
+      }
+    }
+  };
+
   f32x4 acc[MI][NJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -298,8 +319,45 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
       wait_vm_barrier<0>();
     }
     if (kt + NS - 1 < nk) stage((kt + NS - 1) % NS, kbeg + (kt + NS - 1) * BK);
+    else if (RL && kt == nk - 1) stage_res((kt + 1) % NS);
     compute(kt % NS);
   }
+  if constexpr (RL) {
+    wait_vm_barrier<0>();   // residual landed, every wave done with the ring
+    if (a.trace) tr_t1 = __builtin_amdgcn_s_memrealtime();
+    const char* rs = smem + (nk % NS) * STAGE;          // residual tile, swz256 rows of 256 B
+    char* os = smem + ((nk + NS - 1) % NS) * STAGE;     // finished bf16 tile
+    const int q = fr >> 2, p = fr & 3;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int cl = wn * WTN + j * 16;                 // block column base (tile-local)
+      const float bcol = a.bias ? a.bias[n0 + cl + fr] : 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int rb = wm * WTM + i * 16 + 4 * fh;      // this lane group's 4 rows
+        const int rq = rb + q, ch = (cl >> 3) + (p >> 1);
+        bf16x4 r4 = bf16x4{};
+        if (a.add1)
+          r4 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)(uintptr_t)(const void*)(rs + rq * 256 + 16 * (ch ^ swz256(rq)) + 8 * (p & 1)));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = apply_act(acc[i][j][r] + bcol + (float)r4[r], a.act);
+          const int row = rb + r, col = cl + fr;
+          *(bf16*)(os + row * 256 + 16 * ((col >> 3) ^ (((row >> 2) & 3) << 1)) + 2 * (col & 7)) = (bf16)v;
+        }
+      }
+    }
+    __syncthreads();
+    const int cc = tid & 15;
+#pragma unroll
+    for (int it = 0; it < BM / (NW * 4); ++it) {
+      const int rl = (tid >> 4) + it * NW * 4;
+      const int row = m0 + rl;
+      const uint4 u = *(const uint4*)(os + rl * 256 + 16 * (cc ^ (((rl >> 2) & 3) << 1)));
+      if (row < M) *(uint4*)((bf16*)a.C + (long)row * a.ldc + n0 + cc * 8) = u;
+    }
+  } else {
   __syncthreads();   // every wave done reading the ring before the epilogue reuses the LDS
   if (a.trace) tr_t1 = __builtin_amdgcn_s_memrealtime();
 
@@ -401,6 +459,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
       }
     }
   }
+  }   // !RL
   if (a.trace) {
     __syncthreads();
     if (tid == 0) {
@@ -417,7 +476,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
 __device__ __attribute__((aligned(16))) bf16 g_zero16[64];
 
 // experiment overrides (tools/bench_conv.py): 0 = automatic
-int g_force_stages = 0, g_force_tile = 0, g_xcd_remap = 1;
+int g_force_stages = 0, g_force_tile = 0, g_xcd_remap = 1, g_res_lds = 2;
 unsigned long* g_trace = nullptr;
 
 // tile configurations (ids of sat_fast_gemm_set_config)
@@ -427,6 +486,12 @@ inline int tile_bn(int t) { return t == T128x64W8 ? 64 : t == T128x256W8 ? 256 :
 
 template <int BM, int BN, int WGM, int WGN, bool AT, bool BT>
 void launch_ns(int ns, dim3 grid, hipStream_t s, const FArgs& a) {
+  if constexpr (BM == 128 && BN == 128 && WGM == 2 && WGN == 4 && !AT && !BT) {
+    if (ns == 2 && a.res_lds) {
+      hipLaunchKernelGGL((fast_gemm_kernel<128, 128, 2, 4, false, false, 2, true>), grid, dim3(512), 0, s, a);
+      return;
+    }
+  }
   if (ns == 3) hipLaunchKernelGGL((fast_gemm_kernel<BM, BN, WGM, WGN, AT, BT, 3>), grid, dim3(WGM * WGN * 64), 0, s, a);
   else hipLaunchKernelGGL((fast_gemm_kernel<BM, BN, WGM, WGN, AT, BT, 2>), grid, dim3(WGM * WGN * 64), 0, s, a);
 }
@@ -539,6 +604,10 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   }
   a.xcd_remap = g_xcd_remap;
   a.trace = g_trace;
+  a.res_lds = g_res_lds && tcfg == T128x128W8 && !at && !bt && a.splitk == 1 && !partial && a.c_bf16 &&
+              (!g.add1 || (a.add1_bf16 && g.ld_add1 % 8 == 0)) && g.N % 128 == 0 && g.ldc % 8 == 0 && al16(g.C) &&
+              (g.add1 || g_res_lds > 1) &&
+              (g_force_stages == 0 || g_force_stages == 2);
   dim3 grid(sat_cdiv(g.N, bn), sat_cdiv(g.M, bm), a.splitk);
   // skinny partial-split GEMMs run 2-4 k-tiles per block: a 3-deep ring puts the first two in
   // flight at once (their block counts leave LDS occupancy irrelevant)
@@ -549,6 +618,11 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   else launch_tile<false, false>(tcfg, ns, grid, s, a);
   *err = (int)hipGetLastError();
   return 1;
+}
+
+extern "C" int sat_fast_gemm_set_res_lds(int on) {
+  g_res_lds = on < 0 ? 0 : on;   // 1: residual epilogues, 2: also plain bf16 epilogues
+  return 0;
 }
 
 // diagnostics: per-workgroup [start, main loop done, end, hw id] records (4 x u64, 100 MHz clock)

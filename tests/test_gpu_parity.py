@@ -101,6 +101,39 @@ def test_maxpool(sat, k, stride, pad):
     assert torch.equal(y.permute(0, 3, 1, 2).cpu(), ref)
 
 
+@pytest.mark.parametrize("N,C,H,Cout,relu,resid", [(4, 256, 14, 1024, True, True),   # ResNet152 L3 c3 + identity
+                                                     (3, 64, 9, 256, True, True),      # M = 243: partial row tile
+                                                     (2, 128, 28, 512, False, True),   # no activation
+                                                     (4, 1024, 14, 256, True, False),  # L3 c1: plain epilogue
+                                                     (3, 72, 9, 128, False, False)])   # K tail, no bias act
+def test_bf16_lds_epilogue(sat, N, C, H, Cout, relu, resid):
+    """1x1 conv + bias (+ bf16 residual) (+ ReLU) through the bf16 LDS epilogue (residual DMA'd
+    during the last k-tile, added in the accumulator layout; the finished bf16 tile staged for
+    16-B row stores) vs torch fp32 and vs the staged-fp32 epilogue (sat_fast_gemm_set_res_lds(0))."""
+    from sat_amd import ops
+    lib = sat._lib.lib()
+    g = torch.Generator().manual_seed(N * Cout + C)
+    x = torch.randn(N, C, H, H, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, C, 1, 1, generator=g) / math.sqrt(C)).bfloat16().float()
+    b = torch.randn(Cout, generator=g)
+    res = torch.randn(N, Cout, H, H, generator=g).bfloat16().float() if resid else None
+    ref = F.conv2d(x, w, b) + (res if resid else 0.0)
+    ref = torch.relu(ref) if relu else ref
+    xd = x.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    wd = w.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    rd = res.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV) if resid else None
+    outs = []
+    try:
+        for mode in (2, 0):
+            lib.sat_fast_gemm_set_res_lds(mode)
+            y = ops.conv2d_nhwc(xd, wd, b.to(DEV), 1, 0, relu, residual=rd)
+            outs.append(y.float().permute(0, 3, 1, 2).cpu())
+    finally:
+        lib.sat_fast_gemm_set_res_lds(2)
+    assert rel(outs[0], ref) < 1e-2
+    assert torch.equal(outs[0], outs[1])   # same fp32 sums, same single rounding
+
+
 @pytest.mark.parametrize("N,C,H,k,stride,pad", [(2, 64, 112, 3, 2, 1),   # ResNet152 stem pool (bf16 3x3 kernel)
                                                 (3, 16, 13, 3, 2, 1),     # odd size: clipped windows
                                                 (2, 32, 14, 2, 2, 0)])    # generic bf16 path

@@ -33,6 +33,8 @@ for name, H, C, Co, k, s, p, r in SHAPES:
     for rnd in range(5):
         for cfg in CONFIGS:
             lib.sat_fast_gemm_set_config(*cfg[:3])
+            if len(cfg) > 3:
+                lib.sat_fast_gemm_set_res_lds(cfg[3])
             ops.conv2d_nhwc(x, w, b, s, p, True, residual=resid, out=y)
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             st.record()
@@ -41,8 +43,10 @@ for name, H, C, Co, k, s, p, r in SHAPES:
             en.record(); en.synchronize()
             times[cfg].append(st.elapsed_time(en) / 5)
     lib.sat_fast_gemm_set_config(0, 0, 1)
+    if any(len(c) > 3 for c in CONFIGS):
+        lib.sat_fast_gemm_set_res_lds(1)
     line = f"{name:6s} M={B*OH*OH:7d} N={Co:5d} K={k*k*C:5d} "
     for cfg in CONFIGS:
         ms = statistics.median(times[cfg])
-        line += f" {TNAME.get(cfg[1], 'auto')}/s{cfg[0]}/x{cfg[2]}:{ms*1e3:6.1f}us/{flops/ms/1e9:4.0f}TF"
+        line += f" {TNAME.get(cfg[1], 'auto')}/s{cfg[0]}/x{cfg[2]}{'/e%d' % cfg[3] if len(cfg) > 3 else ''}:{ms*1e3:6.1f}us/{flops/ms/1e9:4.0f}TF"
     print(line, flush=True)
