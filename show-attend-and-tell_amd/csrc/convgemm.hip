@@ -62,6 +62,13 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 // row r stored at slot ch ^ swz(r) (cdna_hip_programming.md T10, image (b)): conflict-free for
 // ds_read_b64_tr_b16 fragment reads.
 __device__ __forceinline__ int swz256(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+// bf16 LDS epilogue images (fast_gemm_kernel RL): residual tile for ds_read_b64_tr_b16 and the
+// finished output tile, rows of BN*2 bytes; both conflict-free for their access patterns
+template <int BN> __device__ __forceinline__ int res_swz(int r) {
+  if constexpr (BN == 128) return swz256(r);
+  else return ((r >> 1) & 3) << 1;   // 128-B rows: rows r and r+2 share banks
+}
+__device__ __forceinline__ int out_swz(int r) { return ((r >> 2) & 3) << 1; }
 
 // MFMA 16x16x32 operand fragment (8 consecutive k of one row x) from a k-major tile:
 // two transposing reads of 4 k-rows x 16 columns each.
@@ -108,7 +115,7 @@ __device__ __forceinline__ void wait_vm_barrier() {
 }
 
 // Tile configurations: BM x BN block tile, WGM x WGN waves (wave tile BM/WGM x BN/WGN).
-// RL: bf16 residual + bf16 output epilogue through LDS (128x128 tiles, NS = 2, N % 128 == 0): the
+// RL: bf16 residual + bf16 output epilogue through LDS (128x128 / 128x64 tiles, NS = 2, N % BN == 0): the
 // residual tile is DMA'd into the free ring stage during the last k-tile, added in the MFMA
 // accumulator layout (ds_read_b64_tr_b16), and the finished bf16 tile is staged for 16-B row stores.
 template <int BM, int BN, int WGM, int WGN, bool AT, bool BT, int NS, bool RL = false>
@@ -245,16 +252,17 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
     }
   };
 
-  // RL: the 128 x 128 bf16 residual tile into ring stage buf, 4 rows of 256 B per instruction,
-  // 16-B chunk ch of row r at slot ch ^ swz256(r) (the ds_read_b64_tr_b16 image of frag_tr)
+  // RL: the 128 x BN bf16 residual tile into ring stage buf (rows of BN*2 bytes, 1 KiB per
+  // instruction), 16-B chunk ch of row r at slot ch ^ res_swz<BN>(r)
   auto stage_res = [&](int buf) {
     if constexpr (RL) {
-      static_assert(BM == 128 && BN == 128 && NS == 2, "RL epilogue geometry");
+      static_assert(BM == 128 && (BN == 128 || BN == 64) && NS == 2, "RL epilogue geometry");
+      constexpr int CPR = BN / 8, RPI = 64 / CPR, NINS = BM / RPI;
       if (!a.add1) return;
 #pragma unroll
-      for (int j = 0; j < 32 / NW; ++j) {
-        const int ins = w * (32 / NW) + j, r = ins * 4 + (lane >> 4);
-        const int ch = (lane & 15) ^ swz256(r);
+      for (int j = 0; j < NINS / NW; ++j) {
+        const int ins = w * (NINS / NW) + j, r = ins * RPI + lane / CPR;
+        const int ch = (lane % CPR) ^ res_swz<BN>(r);
         const bool ok = m0 + r < M;
         dma16(sel(ok, (const bf16*)a.add1 + (long)(m0 + r) * a.ld_add1 + n0 + 8 * ch, a.zero16),
               smem + buf * STAGE + ins * 1024);
@@ -325,7 +333,8 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
   if constexpr (RL) {
     wait_vm_barrier<0>();   // residual landed, every wave done with the ring
     if (a.trace) tr_t1 = __builtin_amdgcn_s_memrealtime();
-    const char* rs = smem + (nk % NS) * STAGE;          // residual tile, swz256 rows of 256 B
+    constexpr int ROWB2 = BN * 2, CPR = BN / 8;
+    const char* rs = smem + (nk % NS) * STAGE;          // residual tile
     char* os = smem + ((nk + NS - 1) % NS) * STAGE;     // finished bf16 tile
     const int q = fr >> 2, p = fr & 3;
 #pragma unroll
@@ -339,22 +348,23 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
         bf16x4 r4 = bf16x4{};
         if (a.add1)
           r4 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-              (lds_bf16x4*)(uintptr_t)(const void*)(rs + rq * 256 + 16 * (ch ^ swz256(rq)) + 8 * (p & 1)));
+              (lds_bf16x4*)(uintptr_t)(const void*)(rs + rq * ROWB2 + 16 * (ch ^ res_swz<BN>(rq)) + 8 * (p & 1)));
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float v = apply_act(acc[i][j][r] + bcol + (float)r4[r], a.act);
           const int row = rb + r, col = cl + fr;
-          *(bf16*)(os + row * 256 + 16 * ((col >> 3) ^ (((row >> 2) & 3) << 1)) + 2 * (col & 7)) = (bf16)v;
+          *(bf16*)(os + row * ROWB2 + 16 * ((col >> 3) ^ out_swz(row)) + 2 * (col & 7)) = (bf16)v;
         }
       }
     }
     __syncthreads();
-    const int cc = tid & 15;
+    const int cc = tid % CPR;
+    constexpr int RPP = NW * 64 / CPR;
 #pragma unroll
-    for (int it = 0; it < BM / (NW * 4); ++it) {
-      const int rl = (tid >> 4) + it * NW * 4;
+    for (int it = 0; it < BM / RPP; ++it) {
+      const int rl = tid / CPR + it * RPP;
       const int row = m0 + rl;
-      const uint4 u = *(const uint4*)(os + rl * 256 + 16 * (cc ^ (((rl >> 2) & 3) << 1)));
+      const uint4 u = *(const uint4*)(os + rl * ROWB2 + 16 * (cc ^ out_swz(rl)));
       if (row < M) *(uint4*)((bf16*)a.C + (long)row * a.ldc + n0 + cc * 8) = u;
     }
   } else {
@@ -486,9 +496,9 @@ inline int tile_bn(int t) { return t == T128x64W8 ? 64 : t == T128x256W8 ? 256 :
 
 template <int BM, int BN, int WGM, int WGN, bool AT, bool BT>
 void launch_ns(int ns, dim3 grid, hipStream_t s, const FArgs& a) {
-  if constexpr (BM == 128 && BN == 128 && WGM == 2 && WGN == 4 && !AT && !BT) {
+  if constexpr (BM == 128 && (BN == 128 || BN == 64) && WGM == 2 && WGN == 4 && !AT && !BT) {
     if (ns == 2 && a.res_lds) {
-      hipLaunchKernelGGL((fast_gemm_kernel<128, 128, 2, 4, false, false, 2, true>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((fast_gemm_kernel<128, BN, 2, 4, false, false, 2, true>), grid, dim3(512), 0, s, a);
       return;
     }
   }
@@ -604,8 +614,9 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   }
   a.xcd_remap = g_xcd_remap;
   a.trace = g_trace;
-  a.res_lds = g_res_lds && tcfg == T128x128W8 && !at && !bt && a.splitk == 1 && !partial && a.c_bf16 &&
-              (!g.add1 || (a.add1_bf16 && g.ld_add1 % 8 == 0)) && g.N % 128 == 0 && g.ldc % 8 == 0 && al16(g.C) &&
+  a.res_lds = g_res_lds && (tcfg == T128x128W8 || tcfg == T128x64W8) && !at && !bt && a.splitk == 1 && !partial &&
+              a.c_bf16 && (!g.add1 || (a.add1_bf16 && g.ld_add1 % 8 == 0)) && g.N % bn == 0 && g.ldc % 8 == 0 &&
+              al16(g.C) &&
               (g.add1 || g_res_lds > 1) &&
               (g_force_stages == 0 || g_force_stages == 2);
   dim3 grid(sat_cdiv(g.N, bn), sat_cdiv(g.M, bm), a.splitk);

@@ -105,7 +105,9 @@ def test_maxpool(sat, k, stride, pad):
                                                      (3, 64, 9, 256, True, True),      # M = 243: partial row tile
                                                      (2, 128, 28, 512, False, True),   # no activation
                                                      (4, 1024, 14, 256, True, False),  # L3 c1: plain epilogue
-                                                     (3, 72, 9, 128, False, False)])   # K tail, no bias act
+                                                     (3, 72, 9, 128, False, False),    # K tail, no activation
+                                                     (8, 256, 56, 64, True, False),    # L1 c1: 128x64 tiles
+                                                     (3, 64, 13, 64, True, True)])     # 128x64 + residual, M tail
 def test_bf16_lds_epilogue(sat, N, C, H, Cout, relu, resid):
     """1x1 conv + bias (+ bf16 residual) (+ ReLU) through the bf16 LDS epilogue (residual DMA'd
     during the last k-tile, added in the accumulator layout; the finished bf16 tile staged for
