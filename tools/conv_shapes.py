@@ -2,7 +2,7 @@
 
     python tools/conv_shapes.py <run_kernel_trace.csv> [resnet152|vgg19] [B] [out.json]
 
-Takes the last complete encoder forward in the trace (``nchw_to_nhwc`` .. the decoder's first
+Takes the last complete encoder forward in the trace (``nchw_to_nhwc`` or ``*_s2d16`` .. the decoder's first
 ``mean_rows``), maps its ``fast_gemm_kernel`` dispatches in order onto bench.conv_launches()
 (the same class names and algorithmic bytes/FLOPs bench.py reports) and prints the average
 launch duration and achieved rate per class -- the numbers bench.py's roofline must agree with.
@@ -20,7 +20,7 @@ def encoder_dispatches(rows):
     groups, cur = [], None
     for r in rows:
         k = r["Kernel_Name"]
-        if "nchw_to_nhwc" in k:
+        if "nchw_to_nhwc" in k or "s2d16" in k:   # the input layout kernel opens a forward
             cur = []
             groups.append(cur)
         elif "mean_rows" in k:

@@ -4,8 +4,9 @@
 
 Counters per MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports half the bytes of a wide
 (16 B/lane) streaming read -> doubled here; WRITE_SIZE is exact for 16-B stores.  rocprofv3's
-derived FETCH_SIZE / WRITE_SIZE are in KiB.  The NCHW->NHWC conversion (a plain stream of known
-size: B*3*224*224*4 B read, B*224*224*8*2 B written) is reported beside them as the unit check.
+derived FETCH_SIZE / WRITE_SIZE are in KiB.  The input-layout conversion (a plain stream of known
+size: B*3*224*224*4 B read; B*112*112*16*2 B written by the ResNet152 space-to-depth kernel,
+B*224*224*8*2 by the VGG19 NHWC one) is reported beside them as the unit check.
 
 Dispatch mapping as tools/conv_shapes.py: last complete encoder forward in each pass, its
 fast_gemm_kernel dispatches in order onto bench.conv_launches().
@@ -39,7 +40,7 @@ def read_counter(d, name):
 def last_forward(rows, n_conv):
     groups, cur = [], None
     for did, k, v in rows:
-        if "nchw_to_nhwc" in k:
+        if "nchw_to_nhwc" in k or "s2d16" in k:   # the input layout kernel opens a forward
             cur = []
             groups.append(cur)
         elif "mean_rows" in k:
@@ -65,7 +66,7 @@ def main():
     write = last_forward(read_counter(wdir, "WRITE_SIZE"), n)
     unit = {}
     for tag, g, scale in (("fetch", fetch, 2.0), ("write", write, 1.0)):
-        layout = [v for k, v in g if "nchw_to_nhwc" in k]
+        layout = [v for k, v in g if "nchw_to_nhwc" in k or "s2d16" in k]
         unit[tag] = layout[0] * scale * 1024 if layout else None
         conv = [v * scale * 1024 for k, v in g if "fast_gemm" in k]
         for l, b in zip(launches, conv):
@@ -79,8 +80,11 @@ def main():
         c["ratio_to_algorithmic"] = round(c["hbm_bytes_per_launch"] / c["alg_bytes"], 3)
         tot += c["fetch"] + c["write"]
     out["hbm_bytes_encoder_convs"] = tot
-    out["unit_check_nchw_to_nhwc"] = {"fetch_bytes": unit["fetch"], "expected_read": B * 3 * 224 * 224 * 4,
-                                      "write_bytes": unit["write"], "expected_write": B * 224 * 224 * 8 * 2}
+    s2d = network == "resnet152"   # ResNet152: RGB -> 2x2 space-to-depth NHWC16 (stem as 4x4/s1 conv)
+    out["unit_check_input_layout"] = {"kernel": "nchw3_to_s2d16" if s2d else "nchw_to_nhwc",
+                                      "fetch_bytes": unit["fetch"], "expected_read": B * 3 * 224 * 224 * 4,
+                                      "write_bytes": unit["write"],
+                                      "expected_write": B * 112 * 112 * 16 * 2 if s2d else B * 224 * 224 * 8 * 2}
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 5:
         with open(sys.argv[5], "w") as f:
