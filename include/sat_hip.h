@@ -94,6 +94,14 @@ const char* sat_error_string(int code);
  * configuration (0 = auto, 1 = 128x128 / 8 waves, 2 = 128x64 / 8, 3 = 128x128 / 4, 4 = 128x256 / 8,
  * 5 = 256x128 / 8; k-major operands use 1 or 3), XCD-aware tile order (0 | 1, default 1). */
 int sat_fast_gemm_set_config(int stages, int tile, int xcd_remap);
+/* tuning hook (process-global): epilogue of 128-row tiles with bf16 output -- 0 = fp32 tile staged in
+ * LDS; 1 = bf16 LDS epilogue for residual launches (residual tile LDS-DMA'd during the last k-tile,
+ * added in the accumulator layout); 2 (default) = bf16 LDS epilogue for every eligible launch. */
+int sat_fast_gemm_set_res_lds(int mode);
+/* diagnostics (process-global): when buf is non-null every data-parallel launch of the bf16 GEMM
+ * writes, per workgroup (linear block id), 4 x u64 = [start, main loop done, end, XCC_ID << 32 |
+ * HW_ID] on the 100 MHz realtime clock into buf (tools/conv_trace.py); null disables. */
+int sat_fast_gemm_set_trace(void* buf);
 int sat_gemm(const SatGemmArgs* args, void* stream);
 /* elementwise cast between SAT_F32 and SAT_BF16 storage (n elements). */
 int sat_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, void* stream);

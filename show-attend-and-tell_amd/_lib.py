@@ -56,6 +56,8 @@ _SIGNATURES = [
     ("sat_abi_version", c_int, []),
     ("sat_error_string", ctypes.c_char_p, [c_int]),
     ("sat_fast_gemm_set_config", c_int, [c_int, c_int, c_int]),
+    ("sat_fast_gemm_set_res_lds", c_int, [c_int]),
+    ("sat_fast_gemm_set_trace", c_int, [c_void_p]),
     ("sat_decoder_set_splits", c_int, [c_int, c_int, c_int, c_int]),
     ("sat_gemm", c_int, [ctypes.POINTER(SatGemmArgs), c_void_p]),
     ("sat_cast", c_int, [c_void_p, c_int, c_void_p, c_int, c_int64, c_void_p]),
