@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
+#include <cstdlib>
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void gbl_void;
@@ -59,6 +60,51 @@ __global__ __launch_bounds__(NW * 64) void probe(const char* __restrict__ src, l
   if (threadIdx.x == 0 && smem[5] == 123) sink[0] = 1;
 }
 
+// Register staging for comparison: each wave loads its share of tile k+1 into VGPRs
+// (global_load_dwordx4), then after the barrier writes it to LDS (ds_write_b128).
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void probe_reg(const char* __restrict__ src, long span, int iters, int* sink) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int PER_WAVE = TILE / 1024 / NW;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long base = (long)blockIdx.x * 7919 * TILE;
+  uint4 r[PER_WAVE];
+  auto load = [&](int k) {
+    const long off = (base + (long)k * TILE) % span;
+#pragma unroll
+    for (int j = 0; j < PER_WAVE; ++j) r[j] = *(const uint4*)(src + off + (w * PER_WAVE + j) * 1024 + lane * 16);
+  };
+  load(0);
+  for (int k = 0; k < iters; ++k) {
+    char* dst = smem + (k & 1) * TILE;
+#pragma unroll
+    for (int j = 0; j < PER_WAVE; ++j) *(uint4*)(dst + (w * PER_WAVE + j) * 1024 + lane * 16) = r[j];
+    if (k + 1 < iters) load(k + 1);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && smem[5] == 123) sink[0] = 1;
+}
+
+template <int NW>
+void run_reg(const char* name, const char* src, long span, int cus, int wg_per_cu, int* sink) {
+  const int iters = 64, grid = cus * wg_per_cu, reps = 10;
+  const size_t lds = 2 * (size_t)TILE;
+  hipFuncSetAttribute((const void*)probe_reg<NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipEvent_t a, b;
+  hipEventCreate(&a); hipEventCreate(&b);
+  for (int q = 0; q < 3; ++q) hipLaunchKernelGGL(probe_reg<NW>, dim3(grid), dim3(NW * 64), lds, 0, src, span, iters, sink);
+  hipEventRecord(a);
+  for (int q = 0; q < reps; ++q) hipLaunchKernelGGL(probe_reg<NW>, dim3(grid), dim3(NW * 64), lds, 0, src, span, iters, sink);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, a, b);
+  const double bytes = (double)grid * iters * TILE * reps;
+  printf("%-34s wg/cu %d  %7.1f GB/s per CU  %6.2f TB/s chip  %.3f us per tile per wg\n", name, wg_per_cu,
+         bytes / (ms * 1e-3) / cus / 1e9, bytes / (ms * 1e-3) / 1e12, ms * 1e3 / reps / iters);
+  hipEventDestroy(a); hipEventDestroy(b);
+}
+
 template <int NW, int NS, bool BAR, int LW = NW>
 void run(const char* name, const char* src, long span, int cus, int wg_per_cu, int* sink) {
   const int iters = 64;
@@ -84,13 +130,15 @@ void run(const char* name, const char* src, long span, int cus, int wg_per_cu, i
 int main() {
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-  const long span = 8L << 20;   // 8 MiB working set: L2 / MALL resident
+  const long span = (getenv("SPAN_KB") ? atol(getenv("SPAN_KB")) : 8192) * 1024L;   // working set
   char* src = nullptr;
   int* sink = nullptr;
   hipMalloc(&src, span + TILE);
   hipMalloc(&sink, 4);
   hipMemset(src, 1, span + TILE);
   for (int wpc : {1, 2}) {
+    run_reg<8>("REG 8 waves, 1 tile ahead", src, span, cus, wpc, sink);
+    run_reg<4>("REG 4 waves, 1 tile ahead", src, span, cus, wpc, sink);
     run<8, 2, true, 4>("8 waves (4 load), 1 tile, barrier", src, span, cus, wpc, sink);
     run<8, 2, true, 2>("8 waves (2 load), 1 tile, barrier", src, span, cus, wpc, sink);
     run<4, 2, true, 2>("4 waves (2 load), 1 tile, barrier", src, span, cus, wpc, sink);
