@@ -181,6 +181,9 @@ def main():
     from sat_amd.data import synthetic_captions, synthetic_images
     from sat_amd.distributed import allreduce_grads
 
+    if not args.no_graph and not args.no_overlap:
+        # the decoder shares the chip with the next batch's encoder: fewer split-K workgroups
+        sat_amd.ops.set_decoder_split_target(64)
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()

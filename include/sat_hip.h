@@ -140,6 +140,9 @@ int sat_attention_forward(int B, int L, int D, int E, int dtype, const void* img
  * c: context part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic.  Must be set
  * before sat_decoder_workspace_bytes. */
 int sat_decoder_set_splits(int h, int c, int g, int dh);
+/* process-global: workgroups the automatic per-step split-K aims for (0 = default 192; 64 when the decoder
+ * shares the GPU with a concurrent encoder stream).  Set before the first workspace query. */
+int sat_decoder_set_split_target(int workgroups);
 size_t sat_decoder_workspace_bytes(const SatDecoderDims* d);
 /* preds [B,T-1,V] (dtype), alphas [B,T-1,L] fp32, tokens [B,T-1] int32 = token fed at each step. */
 int sat_decoder_forward(const SatDecoderDims* d, const SatDecoderLayout* lay, const float* params,

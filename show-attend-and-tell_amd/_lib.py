@@ -59,6 +59,7 @@ _SIGNATURES = [
     ("sat_fast_gemm_set_res_lds", c_int, [c_int]),
     ("sat_fast_gemm_set_trace", c_int, [c_void_p]),
     ("sat_decoder_set_splits", c_int, [c_int, c_int, c_int, c_int]),
+    ("sat_decoder_set_split_target", c_int, [c_int]),
     ("sat_gemm", c_int, [ctypes.POINTER(SatGemmArgs), c_void_p]),
     ("sat_cast", c_int, [c_void_p, c_int, c_void_p, c_int, c_int64, c_void_p]),
     ("sat_mean_rows_abi", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),

@@ -42,10 +42,16 @@ struct WS {
 // splits write and re-read fewer fp32 slabs: tools/bench_decoder_splits.py, B=128 bench shape
 // -1.3 % decoder time against ~1.5 waves); fp32 (parity) mode keeps a single split.
 struct Splits { int h, c, g, dh, i; };
+// Workgroups the split-K of one per-step GEMM aims for: 192 when the decoder has the chip to
+// itself; 64 when it shares it with the next batch's encoder (bench.py / train.py overlap): fewer,
+// longer workgroups cost the concurrent conv trunk less (overlapped step 8.23 -> 8.07 ms; alone the
+// decoder prefers 192: 10.24 vs 10.48 ms sequential).  sat_decoder_set_split_target.
+int g_split_target = 192;
+
 inline int pick_splits(int M, int N, int K, int dtype, bool kmajor_w) {
   if (dtype != SAT_BF16 || K % 64) return 1;
   const long tiles = (long)sat_cdiv(M, 128) * sat_cdiv(N, kmajor_w ? 128 : 64);
-  long want = (192 + tiles - 1) / tiles;
+  long want = (g_split_target + tiles - 1) / tiles;
   if (want > 32) want = 32;
   const int kt = K / 64;
   int best = 1;
@@ -251,6 +257,13 @@ int check_dims(const SatDecoderDims* d) {
 extern "C" int sat_decoder_set_splits(int h, int c, int g, int dh) {
   if (h < 0 || c < 0 || g < 0 || dh < 0 || h > 64 || c > 64 || g > 64 || dh > 64) return SAT_ERR_INVALID;
   g_force_splits = Splits{h, c, g, dh, 0};
+  return 0;
+}
+
+// workgroup target of the automatic per-step split-K (0 = default 192); set before any workspace query
+extern "C" int sat_decoder_set_split_target(int workgroups) {
+  if (workgroups < 0 || workgroups > 4096) return SAT_ERR_INVALID;
+  g_split_target = workgroups ? workgroups : 192;
   return 0;
 }
 

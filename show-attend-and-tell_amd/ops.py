@@ -128,6 +128,13 @@ def maxpool2d_nhwc(x, k, stride, pad=0):
     return y
 
 
+def set_decoder_split_target(workgroups):
+    """Workgroups the decoder's automatic per-step split-K aims for (0 = default 192).  64 suits a
+    decoder that shares the GPU with a concurrent encoder stream (bench.py / train.py overlap).
+    Process-global; call before the first decoder forward."""
+    L.check(L.lib().sat_decoder_set_split_target(int(workgroups)), "sat_decoder_set_split_target")
+
+
 def adam_step_(param, grad, exp_avg, exp_avg_sq, param_lp, beta1, beta2, eps, step_size, bc2_sqrt):
     L.check(L.lib().sat_adam_step(L.ptr(param), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), L.ptr(param_lp),
                                   param.numel(), beta1, beta2, eps, step_size, bc2_sqrt, L.stream_of(param)),

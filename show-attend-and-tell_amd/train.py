@@ -272,6 +272,8 @@ def main(argv=None):
             print(json.dumps(rec), flush=True)
 
     encoder, decoder, word_dict, dt = build(args, device)
+    if not args.no_overlap:   # the decoder shares the chip with the next batch's encoder
+        sat_amd.ops.set_decoder_split_target(64)
     opt = sat_amd.Adam(decoder.parameters(), lr=args.lr)
     sched = torch.optim.lr_scheduler.StepLR(opt, args.step_size)
     train_loader = loaders(args, "train", rank, world)

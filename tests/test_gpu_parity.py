@@ -360,6 +360,31 @@ def test_bench_shape_train_step_properties(sat):
     assert not torch.equal(before, dec.lstm.weight_ih.detach())
 
 
+def test_decoder_split_target(sat):
+    """The per-step split-K workgroup target (64 when the decoder shares the GPU with the encoder
+    stream) changes only the fp32 summation order of the bf16 path: loss and gradients agree."""
+    from sat_amd import ops
+    torch.manual_seed(0)
+    B, Lf, D, V, T = 128, 49, 2048, 10000, 27
+    dec = sat.Decoder(V, D, tf=True, ado=True, attention=True).to(DEV).eval()
+    feats = torch.randn(B, Lf, D, device=DEV).bfloat16()
+    caps = O.make_captions(B, T, V, 1).to(DEV)
+    out = []
+    try:
+        for target in (192, 64):
+            ops.set_decoder_split_target(target)
+            for p in dec.parameters():
+                p.grad = None
+            preds, alphas = dec(feats, caps)
+            loss, _ = sat.caption_loss(preds, alphas, caps)
+            loss.backward()
+            out.append((loss.item(), dec._grad_flat.clone()))
+    finally:
+        ops.set_decoder_split_target(0)
+    assert abs(out[0][0] - out[1][0]) < 1e-3 * abs(out[0][0])
+    assert ((out[0][1] - out[1][1]).norm() / out[0][1].norm()).item() < 2e-2
+
+
 def test_two_decoder_graphs_overwrite_gradients(sat):
     """bench.py's overlap schedule: two decoder hipGraphs over two feature buffers replayed in
     turn.  Every replay must overwrite the whole flat gradient buffer (beta = 0 targets are cleared
