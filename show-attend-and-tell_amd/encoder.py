@@ -204,10 +204,34 @@ class Encoder(nn.Module):
             self._plan_key = key
         return self._plan
 
-    def forward(self, x, dtype=None):
+    def stage_starts(self, device=None, dtype=None):
+        """Plan indices where each ResNet stage (layer1..layer4) starts; [] for VGG19."""
+        plan = self.compiled_plan(device or next(self.parameters()).device, dtype or self.compute_dtype)
+        starts, prev = [], None
+        for i, step in enumerate(plan):
+            if step[0] == "block":
+                cout = step[3][0].shape[0]   # c3's output channels: 256 / 512 / 1024 / 2048
+                if cout != prev:
+                    starts.append(i)
+                    prev = cout
+        return starts
+
+    def forward(self, x, dtype=None, steps=None):
+        """Images [B,3,H,W] -> features [B, L, D].  ``steps=(start, stop)`` runs a slice of the
+        plan (stage_starts()): start > 0 takes the NHWC activation the previous slice returned,
+        stop < len(plan) returns the NHWC activation instead of [B, L, D]."""
         L.require_device(x)
         dtype = dtype or self.compute_dtype
         plan = self.compiled_plan(x.device, dtype)
+        start, stop = steps if steps is not None else (0, len(plan))
+        if start > 0:
+            y = x
+            for step in plan[start:stop]:
+                y = self._run_step(y, step)
+            if stop < len(plan):
+                return y
+            B, H, W, C = y.shape
+            return y.view(B, H * W, C)
         H, W = x.shape[2], x.shape[3]
         if plan[0][0] == "stem_s2d" and H % 2 == 0 and W % 2 == 0:
             y = ops.nchw_to_s2d(x, dtype)
@@ -216,18 +240,22 @@ class Encoder(nn.Module):
             y = self._conv(ops.nchw_to_nhwc(x, IN_PAD, dtype), plan[0][2], True)
         else:
             y = ops.nchw_to_nhwc(x, IN_PAD, dtype)
-        for step in plan:
+        for step in plan[:stop]:
             if step[0] == "stem_s2d":
                 continue
-            if step[0] == "conv":
-                y = self._conv(y, step[1], step[2])
-            elif step[0] == "pool":
-                y = ops.maxpool2d_nhwc(y, step[1], step[2], step[3])
-            else:
-                _, c1, c2, c3, ds = step
-                out = self._conv(y, c1, True)
-                out = self._conv(out, c2, True)
-                idn = self._conv(y, ds, False) if ds is not None else y
-                y = self._conv(out, c3, True, residual=idn)
+            y = self._run_step(y, step)
+        if stop < len(plan):
+            return y
         B, H, W, C = y.shape
         return y.view(B, H * W, C)
+
+    def _run_step(self, y, step):
+        if step[0] == "conv":
+            return self._conv(y, step[1], step[2])
+        if step[0] == "pool":
+            return ops.maxpool2d_nhwc(y, step[1], step[2], step[3])
+        _, c1, c2, c3, ds = step
+        out = self._conv(y, c1, True)
+        out = self._conv(out, c2, True)
+        idn = self._conv(y, ds, False) if ds is not None else y
+        return self._conv(out, c3, True, residual=idn)

@@ -333,6 +333,23 @@ def test_encoder_matches_oracle(sat, network):
     assert rel(yb.float(), ref) < 5e-2   # bf16 trunk: documented looser bound
 
 
+def test_encoder_plan_slices(sat):
+    """Encoder.forward over two plan slices split at a stage start (bench.py --dec-after-stage)
+    equals the one-call forward bit for bit."""
+    torch.manual_seed(0)
+    enc = sat.Encoder("resnet152", dtype=torch.bfloat16).to(DEV).eval()
+    x = torch.randn(2, 3, 64, 64, device=DEV)
+    starts = enc.stage_starts()
+    assert len(starts) == 4 and starts == sorted(starts)
+    n = len(enc.compiled_plan(x.device, torch.bfloat16))
+    with torch.no_grad():
+        full = enc(x)
+        for s in starts[1:]:
+            mid = enc(x, steps=(0, s))
+            assert mid.dim() == 4
+            assert torch.equal(enc(mid, steps=(s, n)), full)
+
+
 # ---------------------------------------------------------------------------- full-size properties
 def test_bench_shape_train_step_properties(sat):
     """At the benchmark shape (B=128 per GPU, ResNet152 features, V=10000, T=27, bf16) the step
