@@ -142,9 +142,12 @@ class Encoder(nn.Module):
         self._plan = None
         self._plan_key = None
         self.timing = None   # bench hook: list collecting (start, end) HIP events around every conv launch
+        self.timing_args = None   # bench hook: list collecting every conv launch's arguments
 
     def _conv(self, x, f, relu, residual=None, out_hw=None):
         w, b, s, p = f
+        if self.timing_args is not None:
+            self.timing_args.append((x, w, b, s, p, relu, residual, out_hw))
         if self.timing is None:
             return ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual, out_hw=out_hw)
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
