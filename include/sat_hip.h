@@ -155,7 +155,7 @@ int sat_decoder_backward(const SatDecoderDims* d, const SatDecoderLayout* lay, c
                          const void* params_lp, const void* img_features, void* workspace,
                          size_t workspace_bytes, const void* preds, const float* alphas,
                          const void* d_preds, const float* d_alphas, float* grads, int accumulate,
-                         int phase, void* stream);
+                         int phase, void* stream);   /* phase 1 | 2 | 3, + 4: d_preds already ReLU-masked (ado) */
 
 /* --- beam-search captioning (decoder.py:160-269, Decoder.caption; generate_caption.py:86-88) ---
  * img_features: DEVICE [beam_size, L, D] (the reference expands one image to beam rows).
@@ -184,6 +184,12 @@ int sat_caption_loss_forward(int B, int T, int V, int L, int dtype, const void* 
                              int pad_id, int skip0, int skip1, int skip2, void* workspace,
                              float* out, void* stream);
 int sat_caption_loss_backward(int B, int T, int V, int L, int dtype, const void* preds,
+                              const int64_t* captions, float alpha_c, void* workspace,
+                              const float* grad_out, void* d_preds, float* d_alphas, void* stream);
+/* the same with the logits a ReLU's output (decoder.py:117-125 advanced deep output): the gradient
+ * leaves through that ReLU (zero where preds <= 0), so the decoder backward can skip its mask pass
+ * (sat_decoder_backward phase bit 4). */
+int sat_caption_loss_backward_relu(int B, int T, int V, int L, int dtype, const void* preds,
                               const int64_t* captions, float alpha_c, void* workspace,
                               const float* grad_out, void* d_preds, float* d_alphas, void* stream);
 

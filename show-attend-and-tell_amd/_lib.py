@@ -88,6 +88,8 @@ _SIGNATURES = [
                                          c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     ("sat_caption_loss_backward", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float,
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("sat_caption_loss_backward_relu", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("sat_adam_step", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
                               c_float, c_float, c_float, c_void_p]),
 ]

@@ -398,7 +398,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
                                     int phase, void* stream) {
   SAT_CHECK((hipError_t)check_dims(dp));
   SAT_REQUIRE(lay && params && img_features && workspace && preds && alphas && d_preds && d_alphas && grads);
-  SAT_REQUIRE(phase >= 1 && phase <= 3);
+  SAT_REQUIRE((phase & 3) != 0 && phase >= 1 && phase <= 7);   // bit 4: d_preds already ReLU-masked
   SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
   const SatDecoderDims& d = *dp;
   WS w;
@@ -439,10 +439,16 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
 
   if (phase & 1) {  // ---------------- output head (decoder.py:117-125,149-158) ----------------
     if (d.ado) {
-      SAT_CHECK((hipError_t)sat_relu_mask_mul(d_preds, preds, (long)R * V, d.dtype, w.dpre_t, s));
-      SAT_CHECK((hipError_t)wgrad(V, E, R, w.dpre_t, V, w.comb_t, E, G(lay->fout_w), E));
-      SAT_CHECK((hipError_t)colsum(w.dpre_t, d.dtype, V, R, V, G(lay->fout_b)));
-      SAT_CHECK((hipError_t)dgrad(R, E, V, w.dpre_t, V, c.W(lay->fout_w), E, w.dcomb, E));
+      // d logits through the ReLU of the advanced deep output; phase bit 4: the caller's d_preds is
+      // already masked (sat_caption_loss_backward_relu fused it)
+      const void* dpre = d_preds;
+      if (!(phase & 4)) {
+        SAT_CHECK((hipError_t)sat_relu_mask_mul(d_preds, preds, (long)R * V, d.dtype, w.dpre_t, s));
+        dpre = w.dpre_t;
+      }
+      SAT_CHECK((hipError_t)wgrad(V, E, R, dpre, V, w.comb_t, E, G(lay->fout_w), E));
+      SAT_CHECK((hipError_t)colsum(dpre, d.dtype, V, R, V, G(lay->fout_b)));
+      SAT_CHECK((hipError_t)dgrad(R, E, V, dpre, V, c.W(lay->fout_w), E, w.dcomb, E));
       SAT_CHECK((hipError_t)sat_ado_bwd_split(w.dcomb, w.fh, w.fz, (long)R * E, d.dtype, w.dfh_t, w.dfz_t, s));
       SAT_CHECK((hipError_t)wgrad(E, E, R, w.dfh_t, E, w.hd_t, E, G(lay->fh_w), E));
       SAT_CHECK((hipError_t)colsum(w.dfh_t, d.dtype, E, R, E, G(lay->fh_b)));

@@ -163,7 +163,12 @@ __global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* __restri
   }
 }
 
-template <typename TT>
+// dL/dlogit = g * (softmax - onehot) / (B*(T-2)) for scored rows, 0 for the unscored last step.
+// MASK: the logits are a ReLU's output (decoder.py:117-125 advanced deep output), and the
+// gradient leaves through that ReLU: zero where the logit is not positive (fused here so the
+// decoder skips its own mask pass over the [B*(T-1), V] gradient).  16-byte vectors when
+// V % (16 / sizeof(T)) == 0.
+template <typename TT, bool MASK>
 __global__ __launch_bounds__(256) void loss_bwd_kernel(const TT* __restrict__ preds, const int64_t* __restrict__ caps,
                                                        int B, int T, int V, int L, const float* __restrict__ stats,
                                                        const float* __restrict__ dreg, const float* __restrict__ grad_out,
@@ -174,17 +179,30 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const TT* __restrict__ pr
   const float g = grad_out ? grad_out[0] : 1.f;
   const TT* x = preds + (long)r * V;
   TT* dx = dpreds + (long)r * V;
-  if (t < T1 - 1) {
-    const int tgt = (int)caps[(long)b * T + t + 1];
-    const float lse = stats[(long)r * kStat];
-    const float scale = g / (float)(B * (T1 - 1));
-    for (int v = threadIdx.x; v < V; v += blockDim.x) {
-      float p = expf((float)x[v] - lse);
-      if (v == tgt) p -= 1.f;
-      dx[v] = (TT)(p * scale);
+  const bool scored = t < T1 - 1;
+  const int tgt = scored ? (int)caps[(long)b * T + t + 1] : -1;
+  const float lse = scored ? stats[(long)r * kStat] : 0.f;
+  const float scale = scored ? g / (float)(B * (T1 - 1)) : 0.f;
+  auto grad = [&](float xv, int v) {
+    float p = scored ? expf(xv - lse) : 0.f;
+    if (v == tgt) p -= 1.f;
+    float d = p * scale;
+    if (MASK && !(xv > 0.f)) d = 0.f;
+    return d;
+  };
+  constexpr int VEC = 16 / sizeof(TT);
+  if (V % VEC == 0) {
+    for (int c = threadIdx.x; c < V / VEC; c += blockDim.x) {
+      const uint4 u = *(const uint4*)(x + (long)c * VEC);
+      const TT* h = (const TT*)&u;
+      uint4 o;
+      TT* q = (TT*)&o;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) q[j] = (TT)grad((float)h[j], c * VEC + j);
+      *(uint4*)(dx + (long)c * VEC) = o;
     }
   } else {
-    for (int v = threadIdx.x; v < V; v += blockDim.x) dx[v] = (TT)0.0f;
+    for (int v = threadIdx.x; v < V; v += blockDim.x) dx[v] = (TT)grad((float)x[v], v);
   }
   for (int l = threadIdx.x; l < L; l += blockDim.x) dalphas[(long)r * L + l] = g * dreg[(long)b * L + l];
 }
@@ -217,20 +235,44 @@ extern "C" int sat_caption_loss_forward(int B, int T, int V, int L, int dtype, c
   return (int)hipGetLastError();
 }
 
-extern "C" int sat_caption_loss_backward(int B, int T, int V, int L, int dtype, const void* preds,
-                                         const int64_t* captions, float alpha_c, void* workspace,
-                                         const float* grad_out, void* d_preds, float* d_alphas, void* stream) {
+namespace {
+int loss_backward(int B, int T, int V, int L, int dtype, const void* preds, const int64_t* captions, void* workspace,
+                  const float* grad_out, void* d_preds, float* d_alphas, bool relu_mask, hipStream_t s) {
   SAT_REQUIRE(preds && captions && workspace && d_preds && d_alphas && B > 0 && T >= 3);
-  (void)alpha_c;
-  hipStream_t s = (hipStream_t)stream;
   const int R = B * (T - 1);
   const float* stats = (const float*)workspace;
   const float* dreg = stats + (size_t)R * kStat;
-  if (dtype == SAT_BF16)
-    hipLaunchKernelGGL(loss_bwd_kernel<bf16>, dim3(R), dim3(256), 0, s, (const bf16*)preds, captions, B, T, V, L, stats,
-                       dreg, grad_out, (bf16*)d_preds, d_alphas);
-  else
-    hipLaunchKernelGGL(loss_bwd_kernel<float>, dim3(R), dim3(256), 0, s, (const float*)preds, captions, B, T, V, L, stats,
-                       dreg, grad_out, (float*)d_preds, d_alphas);
+  if (dtype == SAT_BF16) {
+    if (relu_mask)
+      hipLaunchKernelGGL((loss_bwd_kernel<bf16, true>), dim3(R), dim3(256), 0, s, (const bf16*)preds, captions, B, T,
+                         V, L, stats, dreg, grad_out, (bf16*)d_preds, d_alphas);
+    else
+      hipLaunchKernelGGL((loss_bwd_kernel<bf16, false>), dim3(R), dim3(256), 0, s, (const bf16*)preds, captions, B,
+                         T, V, L, stats, dreg, grad_out, (bf16*)d_preds, d_alphas);
+  } else {
+    if (relu_mask)
+      hipLaunchKernelGGL((loss_bwd_kernel<float, true>), dim3(R), dim3(256), 0, s, (const float*)preds, captions, B,
+                         T, V, L, stats, dreg, grad_out, (float*)d_preds, d_alphas);
+    else
+      hipLaunchKernelGGL((loss_bwd_kernel<float, false>), dim3(R), dim3(256), 0, s, (const float*)preds, captions,
+                         B, T, V, L, stats, dreg, grad_out, (float*)d_preds, d_alphas);
+  }
   return (int)hipGetLastError();
+}
+}  // namespace
+
+extern "C" int sat_caption_loss_backward(int B, int T, int V, int L, int dtype, const void* preds,
+                                         const int64_t* captions, float alpha_c, void* workspace,
+                                         const float* grad_out, void* d_preds, float* d_alphas, void* stream) {
+  (void)alpha_c;
+  return loss_backward(B, T, V, L, dtype, preds, captions, workspace, grad_out, d_preds, d_alphas, false,
+                       (hipStream_t)stream);
+}
+
+extern "C" int sat_caption_loss_backward_relu(int B, int T, int V, int L, int dtype, const void* preds,
+                                              const int64_t* captions, float alpha_c, void* workspace,
+                                              const float* grad_out, void* d_preds, float* d_alphas, void* stream) {
+  (void)alpha_c;
+  return loss_backward(B, T, V, L, dtype, preds, captions, workspace, grad_out, d_preds, d_alphas, true,
+                       (hipStream_t)stream);
 }

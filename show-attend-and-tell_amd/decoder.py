@@ -255,7 +255,12 @@ class Decoder(nn.Module):
         if img_features.dtype == torch.bfloat16:
             self._ensure_lp()
         params = [p for n, p in self.named_parameters()]
-        return _DecoderFn.apply(img_features.contiguous(), captions.contiguous().long(), self, *params)
+        preds, alphas = _DecoderFn.apply(img_features.contiguous(), captions.contiguous().long(), self, *params)
+        if self.use_advanced_deep_output:
+            # the logits are a ReLU's output: sat_amd.caption_loss folds the ReLU's mask into its
+            # backward and tags the gradient, so the decoder's backward skips its own mask pass
+            preds._sat_relu_logits = True
+        return preds, alphas
 
     def caption(self, img_features, beam_size, max_step=50):
         """Beam search (decoder.py:160-269) as one C-ABI call (sat_decoder_beam_search).
@@ -371,11 +376,13 @@ class _DecoderFn(torch.autograd.Function):
             raise TypeError("sat_amd.Decoder.backward: grad dtype must match preds")
         accumulate = dec._attach_grads()
         lib = L.lib()
+        masked = 4 if getattr(d_preds, "_sat_relu_masked", False) else 0   # phase bit: d_preds already ReLU-masked
         for phase in (1, 2):
             L.check(lib.sat_decoder_backward(ctypes.byref(ctx.dims), ctypes.byref(ctx.lay), L.ptr(dec._flat),
                                              L.ptr(ctx.lp), L.ptr(feats), L.ptr(ctx.ws), ctx.ws_bytes, L.ptr(preds),
                                              L.ptr(alphas), L.ptr(d_preds), L.ptr(d_alphas),
-                                             L.ptr(dec._grad_flat), int(accumulate), phase, L.stream_of(preds)),
+                                             L.ptr(dec._grad_flat), int(accumulate), phase | masked,
+                                             L.stream_of(preds)),
                     "sat_decoder_backward")
             for hook in dec._grad_hooks:
                 hook(phase, dec)

@@ -39,6 +39,7 @@ class _CaptionLossFn(torch.autograd.Function):
                 "sat_caption_loss_forward")
         ctx.save_for_backward(preds_c, caps)
         ctx.ws, ctx.dims, ctx.alpha_c = ws, (B, T, V, Lf), float(alpha_c)
+        ctx.relu = bool(getattr(preds, "_sat_relu_logits", False))   # set by sat_amd.Decoder (ado)
         loss = out[0].clone()
         metrics = out[1:7].clone()
         ctx.mark_non_differentiable(metrics)
@@ -51,10 +52,13 @@ class _CaptionLossFn(torch.autograd.Function):
         d_preds = torch.empty_like(preds)
         d_alphas = torch.empty(B, T - 1, Lf, device=preds.device, dtype=torch.float32)
         g = (g_loss if g_loss is not None else torch.ones((), device=preds.device)).float().contiguous()
-        L.check(L.lib().sat_caption_loss_backward(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds), L.ptr(caps),
-                                                  ctx.alpha_c, L.ptr(ctx.ws), L.ptr(g), L.ptr(d_preds),
-                                                  L.ptr(d_alphas), L.stream_of(d_preds)),
+        # with ReLU'd logits the mask of that ReLU is applied here, and the gradient says so
+        fn = L.lib().sat_caption_loss_backward_relu if ctx.relu else L.lib().sat_caption_loss_backward
+        L.check(fn(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds), L.ptr(caps), ctx.alpha_c, L.ptr(ctx.ws),
+                   L.ptr(g), L.ptr(d_preds), L.ptr(d_alphas), L.stream_of(d_preds)),
                 "sat_caption_loss_backward")
+        if ctx.relu:
+            d_preds._sat_relu_masked = True
         ctx.ws = None
         return d_preds, d_alphas, None, None, None, None
 

@@ -377,6 +377,27 @@ def test_bench_shape_train_step_properties(sat):
     assert not torch.equal(before, dec.lstm.weight_ih.detach())
 
 
+def test_caption_loss_relu_fused_mask(sat):
+    """caption_loss on ReLU'd logits (tagged by sat_amd.Decoder in ado mode) returns the gradient
+    already multiplied by the ReLU mask (and says so); values equal mask * the plain gradient."""
+    torch.manual_seed(0)
+    B, T, V, Lf = 4, 7, 1000, 49
+    base = torch.relu(torch.randn(B, T - 1, V, device=DEV)).bfloat16()
+    alphas = torch.softmax(torch.randn(B, T - 1, Lf, device=DEV), -1)
+    caps = torch.randint(0, V, (B, T), device=DEV)
+    grads = []
+    for tag in (False, True):
+        preds = base.clone().requires_grad_(True)
+        if tag:
+            preds._sat_relu_logits = True
+        loss, _ = sat.caption_loss(preds, alphas, caps)
+        loss.backward()
+        grads.append(preds.grad.float())
+    mask = (base.float() > 0).float()
+    assert torch.equal(grads[1], grads[0] * mask)
+    assert (grads[0] * (1 - mask)).abs().sum() > 0   # the plain gradient is not masked
+
+
 def test_decoder_split_target(sat):
     """The per-step split-K workgroup target (64 when the decoder shares the GPU with the encoder
     stream) changes only the fp32 summation order of the bf16 path: loss and gradients agree."""
