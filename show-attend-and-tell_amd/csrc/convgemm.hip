@@ -5,7 +5,8 @@
 //   B: row-major [N][K] bf16 (conv weights [Cout][KH][KW][Cin], Linear weights [out][in]).
 //
 // Design (cdna_hip_programming.md sec. 5, "glds vs register staging"):
-//   * 256 threads = 4 waves, 2x2; block tile 128 x BN (BN = 128 or 64), BK = 64;
+//   * 512 threads = 8 waves, 2 (M) x 4 (N); block tile 128 x BN (BN = 128 or 64), BK = 64; two
+//     workgroups per CU (three for 128x64); 4-wave and 256-row tiles exist for experiments;
 //   * operands move HBM -> LDS with global_load_lds_dwordx4 (16 B per lane, no VGPR round
 //     trip), one 1 KiB wave-instruction = 8 LDS rows of 128 B, two-stage ring;
 //   * the LDS image is lane-linear, so the bank swizzle is applied to the SOURCE address:
@@ -15,20 +16,21 @@
 //     of being predicated, so every lane always issues its DMA;
 //   * im2col: when Cin % 64 == 0 a whole k-tile lies in one filter tap, so (kh, kw, ci0)
 //     are block-uniform scalars and each lane only adds its pixel's row offset;
-//   * v_mfma_f32_16x16x32_bf16, fp32 accumulation; the epilogue stages each wave's
-//     64 x BN/2 fp32 tile in LDS and writes 16-byte row segments (bias, residual add,
-//     activation and the bf16 conversion fused).
-// Measured limits (profiles/r1_s8_conv_ablation.txt, taken with a temporary ablation build): the
-// main loop is bound by the per-CU L2 -> LDS DMA rate and the LDS fragment traffic of 64x32 wave
-// tiles; the residual 1x1 convs by their epilogue traffic, which runs after the main loop of the
-// same workgroups.  Variants that did not beat this kernel on the ResNet152 shapes: all fragment
-// reads issued before the DMA (sched_barrier-pinned), a persistent-tile variant with register
-// epilogue, non-temporal epilogue traffic, 16-wave and 4-wave (128x64 wave tile, in-wave
-// pipelined) 256x128 tiles, residual rows requested before the main loop, a first-round start
-// offset for the second workgroup of each CU, and stream-K (2 x CUs workgroups sharing the
-// k-tile units, split tiles finished by the last arriver from sc1-published fp32 partials: the
-// 392-tile L3 shapes went 30 -> 46 us and 53 -> 68 us; publishing and re-reading 64 KB partials
-// per split costs more than the idle slots of the last round, tools/conv_trace.py).
+//   * v_mfma_f32_16x16x32_bf16, fp32 accumulation;
+//   * epilogue, bf16 output and N % BN == 0 (RL, the default for the conv trunk): the bf16
+//     residual tile is LDS-DMA'd into the ring stage the last k-tile leaves free, added in the
+//     MFMA accumulator layout via ds_read_b64_tr_b16 with bias and activation, rounded once to
+//     bf16 into the other stage, and stored as 16-byte row segments; otherwise the fp32 tile is
+//     staged in LDS and the same fusions run on 16-byte row segments.
+// Measured limits (profiles/r1_s8_conv_ablation.txt): a 128x128 k-tile takes ~1.27 us per
+// workgroup at two per CU, which is both the L2 -> LDS DMA rate of that configuration
+// (tools/dma_probe.hip, ~54 GB/s per CU) and its LDS-read + MFMA time.  Variants that did not
+// beat it on the ResNet152 shapes: fragment reads hoisted or fully prefetched, persistent tiles
+// with a register epilogue, non-temporal epilogue traffic, 16-wave and 4-wave (incl. interleaved)
+// tiles, 3- and 4-stage rings, half the waves issuing the DMA, residual rows requested before
+// the main loop, start offsets, round-filling M-tiles, a halo-tiled 3x3 kernel, and stream-K
+// (2 x CUs workgroups, last-arriver fixups from sc1-published fp32 partials: 30 -> 46 us and
+// 53 -> 68 us on the 392-tile L3 shapes).
 #include "sat_common.h"
 #include "sat_internal.h"
 
