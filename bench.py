@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--network", default="resnet152", choices=["resnet152", "vgg19"])
     ap.add_argument("--vocab", type=int, default=10000)
     ap.add_argument("--seq", type=int, default=27)
+    ap.add_argument("--no-tf", action="store_true",
+                    help="cfg4: no teacher forcing (greedy argmax feedback inside the time loop, decoder.py:131-133)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=2, help="images in the bounded CPU-baseline sample")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
@@ -181,7 +183,7 @@ def cpu_baseline(args):
         t0 = time.perf_counter()
         with torch.no_grad():
             feats = fwd(enc_p, x)
-        _, _, dec_p, _, _ = O.train_step(dec_p, feats, caps, tf=True, ado=True, attention=True, lr=1e-4,
+        _, _, dec_p, _, _ = O.train_step(dec_p, feats, caps, tf=not args.no_tf, ado=True, attention=True, lr=1e-4,
                                          training=True, adam_state={})
         t_total += time.perf_counter() - t0
         iters += 1
@@ -211,7 +213,7 @@ def main():
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
     torch.manual_seed(42)          # identical decoder init on every rank
-    dec = sat_amd.Decoder(args.vocab, D, tf=True, ado=True, attention=True).to(dev).train()
+    dec = sat_amd.Decoder(args.vocab, D, tf=not args.no_tf, ado=True, attention=True).to(dev).train()
     opt = sat_amd.Adam(dec.parameters(), lr=1e-4)
     g = torch.Generator().manual_seed(1000 + rank)
     B = args.batch
@@ -336,7 +338,7 @@ def main():
             "ms_per_step": round(1000 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic (224x224 N(0,1) images, random-token captions, random-init weights)",
-            "config": {"workload": f"COCO-shaped {args.network} encoder (bf16 fwd) + attention/tf/ado decoder train "
+            "config": {"workload": f"COCO-shaped {args.network} encoder (bf16 fwd) + attention/{'greedy' if args.no_tf else 'tf'}/ado decoder train "
                                    f"step, V={args.vocab}, T={args.seq}",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": args.seq,
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
