@@ -39,12 +39,20 @@ def parse():
     ap.add_argument("--seq", type=int, default=27)
     ap.add_argument("--no-tf", action="store_true",
                     help="cfg4: no teacher forcing (greedy argmax feedback inside the time loop, decoder.py:131-133)")
+    ap.add_argument("--bert", action="store_true",
+                    help="cfg5: frozen BERT word embeddings (V=30522, E=768, T=32), simple deep output (--ado off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=2, help="images in the bounded CPU-baseline sample")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode: run the next batch's encoder after, not beside, this batch's decoder")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.bert:   # generate_json_data_bert.py:47,69: [CLS] + 30 + [SEP]; BertConfig() vocabulary
+        args.vocab = 30522
+        if args.seq == 27:
+            args.seq = 32
+        args.no_cpu_baseline = True   # the oracle's CPU-baseline sample covers the plain-vocab decoder only
+    return args
 
 
 PEAK_HBM_ACHIEVABLE_GBS = 6300.0   # MI355X_MICROARCH.md §HBM (floor estimates only)
@@ -213,19 +221,21 @@ def main():
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
     torch.manual_seed(42)          # identical decoder init on every rank
-    dec = sat_amd.Decoder(args.vocab, D, tf=not args.no_tf, ado=True, attention=True).to(dev).train()
+    dec = sat_amd.Decoder(args.vocab, D, tf=not args.no_tf, ado=not args.bert, bert=args.bert,
+                          attention=True).to(dev).train()
+    pad_id, skip_ids = sat_amd.special_ids(args.bert)
     opt = sat_amd.Adam(dec.parameters(), lr=1e-4)
     g = torch.Generator().manual_seed(1000 + rank)
     B = args.batch
     imgs = synthetic_images(B, generator=g, device=dev)
-    caps = synthetic_captions(B, args.seq, args.vocab, generator=g, device=dev)
+    caps = synthetic_captions(B, args.seq, args.vocab, generator=g, bert=args.bert, device=dev)
     torch.cuda.synchronize()
 
     def fwd_bwd():
         with torch.no_grad():
             feats = enc(imgs)
         preds, alphas = dec(feats, caps)
-        loss, metrics = sat_amd.caption_loss(preds, alphas, caps)
+        loss, metrics = sat_amd.caption_loss(preds, alphas, caps, pad_id=pad_id, skip_ids=skip_ids)
         loss.backward()
         return loss
 
@@ -261,7 +271,7 @@ def main():
             opt.zero_grad(set_to_none=True)   # each capture overwrites the gradients (beta = 0)
             with torch.cuda.graph(g_dec[k]):
                 preds, alphas = dec(feats_static[k], caps)
-                loss_k, _ = sat_amd.caption_loss(preds, alphas, caps)
+                loss_k, _ = sat_amd.caption_loss(preds, alphas, caps, pad_id=pad_id, skip_ids=skip_ids)
                 loss_k.backward()
             loss_static.append(loss_k)
         torch.cuda.synchronize()
@@ -338,7 +348,7 @@ def main():
             "ms_per_step": round(1000 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic (224x224 N(0,1) images, random-token captions, random-init weights)",
-            "config": {"workload": f"COCO-shaped {args.network} encoder (bf16 fwd) + attention/{'greedy' if args.no_tf else 'tf'}/ado decoder train "
+            "config": {"workload": f"{'Flickr8k' if args.bert else 'COCO'}-shaped {args.network} encoder (bf16 fwd) + attention/{'greedy' if args.no_tf else 'tf'}/{'bert' if args.bert else 'ado'} decoder train "
                                    f"step, V={args.vocab}, T={args.seq}",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": args.seq,
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
