@@ -102,6 +102,12 @@ int sat_fast_gemm_set_res_lds(int mode);
  * writes, per workgroup (linear block id), 4 x u64 = [start, main loop done, end, XCC_ID << 32 |
  * HW_ID] on the 100 MHz realtime clock into buf (tools/conv_trace.py); null disables. */
 int sat_fast_gemm_set_trace(void* buf);
+/* tuning hook (process-global) for the 256x128 pipelined conv / GEMM kernel (convpipe.hip): 0 = off,
+ * 1 = automatic (default: long-K problems that fill the chip), 2 = every eligible problem. */
+int sat_conv_pipe_set_mode(int mode);
+/* experiment hook (process-global, tools/pipe_ab.py): waves per workgroup of the pipelined kernel
+ * (8 | 4) and diagnostic ablation bits (conv + ReLU launches only; 0 = off). */
+int sat_conv_pipe_set_experiment(int waves, int ablate);
 int sat_gemm(const SatGemmArgs* args, void* stream);
 /* elementwise cast between SAT_F32 and SAT_BF16 storage (n elements). */
 int sat_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, void* stream);

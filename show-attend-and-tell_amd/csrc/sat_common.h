@@ -83,3 +83,5 @@ struct SatGemm {
 int sat_gemm_launch(const SatGemm& g, hipStream_t s);
 // bf16 NT fast path (convgemm.hip); returns 1 when it launched (error code in *err).
 int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err);
+// 256x128 pipelined bf16 conv / NT GEMM (convpipe.hip); returns 1 when it launched.
+int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err);

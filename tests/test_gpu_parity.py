@@ -490,6 +490,69 @@ def test_fast_conv_path(sat, N, C, H, Cout, k, stride, pad):
     assert ((y - ref_r).abs() <= 1e-2 * ref_r.abs() + 2e-2).all()
 
 
+@pytest.mark.parametrize("N,C,H,Cout,k,stride,pad,relu,resid", [
+    (2, 256, 14, 256, 3, 1, 1, True, False),     # L3 c2 shape class, M = 392: partial second row tile
+    (2, 1024, 14, 256, 1, 1, 0, True, False),    # L3 c1: 1x1, 16 k-tiles
+    (1, 128, 28, 128, 3, 2, 1, True, False),     # stride-2 3x3 (first block of a stage)
+    (3, 64, 9, 64, 3, 1, 1, False, False),       # N = 64: half-empty column tile, no activation
+    (2, 512, 7, 2048, 1, 1, 0, True, True),      # L4 c3 + residual
+    (2, 64, 8, 200, 1, 1, 0, True, True),        # N tail (200 % 128), residual, single k-tile
+    (2, 128, 10, 128, 1, 1, 0, False, True)])    # two k-tiles (no steady-state iteration)
+def test_conv_pipe_kernel(sat, N, C, H, Cout, k, stride, pad, relu, resid):
+    """convpipe.hip (256x128 tiles, 3-stage LDS-DMA ring, counted vmcnt) forced on every eligible
+    shape: bit-identical to the 128-row kernel (same fp32 MFMA sums, same single rounding) and
+    within bf16 output rounding of torch fp32."""
+    from sat_amd import ops
+    lib = sat._lib.lib()
+    g = torch.Generator().manual_seed(N * C + Cout + k + stride)
+    x = torch.randn(N, C, H, H, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, C, k, k, generator=g) / math.sqrt(C * k * k)).bfloat16().float()
+    b = torch.randn(Cout, generator=g)
+    ref = F.conv2d(x, w, b, stride=stride, padding=pad)
+    res = torch.randn_like(ref).bfloat16().float() if resid else None
+    ref = ref + res if resid else ref
+    ref = torch.relu(ref) if relu else ref
+    xd = x.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    wd = w.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    rd = res.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV) if resid else None
+    outs = []
+    try:
+        for mode in (2, 0):
+            assert lib.sat_conv_pipe_set_mode(mode) == 0
+            y = ops.conv2d_nhwc(xd, wd, b.to(DEV), stride, pad, relu, residual=rd)
+            outs.append(y.float().permute(0, 3, 1, 2).cpu())
+    finally:
+        lib.sat_conv_pipe_set_mode(1)
+    assert rel(outs[0], ref) < 1e-2
+    assert ((outs[0] - ref).abs() <= 1e-2 * ref.abs() + 2e-2).all()
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("M,N,K", [(3328, 10000, 512), (6272, 512, 2048), (300, 136, 192)])
+def test_conv_pipe_gemm(sat, M, N, K):
+    """Plain NT GEMM through the pipelined kernel (bf16 out, bias, bf16 residual, ReLU) vs the
+    128-row kernel (bit-identical) and torch fp32."""
+    from sat_amd import ops
+    lib = sat._lib.lib()
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    Bm = torch.randn(N, K, generator=g).bfloat16()
+    bias = torch.randn(N, generator=g)
+    add1 = torch.randn(M, N, generator=g).bfloat16()
+    ref = torch.relu(A.float() @ Bm.float().T + bias + add1.float())
+    outs = []
+    try:
+        for mode in (2, 0):
+            assert lib.sat_conv_pipe_set_mode(mode) == 0
+            C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            ops.gemm(A.to(DEV), Bm.to(DEV), C, bias=bias.to(DEV), add1=add1.to(DEV), act=sat._lib.ACT_RELU)
+            outs.append(C.float().cpu())
+    finally:
+        lib.sat_conv_pipe_set_mode(1)
+    assert rel(outs[0], ref) < 8e-3
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("M,N,K,out", [(3000, 1000, 520, torch.float32), (4096, 64, 512, torch.bfloat16),
                                        (2500, 1003, 256, torch.float32), (3328, 10000, 512, torch.bfloat16)])
 def test_fast_gemm_path(sat, M, N, K, out):
