@@ -31,7 +31,7 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=128, help="images per GPU")
     ap.add_argument("--network", default="resnet152", choices=["resnet152", "vgg19"])
@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode: run the next batch's encoder after, not beside, this batch's decoder")
+    ap.add_argument("--fp32-steps", type=int, default=3,
+                    help="timed steps of the fp32 leg (the reference's precision, the exact-parity path; 0 = skip)")
+    ap.add_argument("--no-diagnostics", action="store_true",
+                    help="skip the per-kernel roofline measurements after the timed region")
     args = ap.parse_args()
     if args.bert:   # generate_json_data_bert.py:47,69: [CLS] + 30 + [SEP]; BertConfig() vocabulary
         args.vocab = 30522
@@ -200,6 +204,64 @@ def cpu_baseline(args):
                       f"V={args.vocab}, T={args.seq}) through oracle/sat_oracle.py on host CPU"}
 
 
+def decoder_step_roofline(dec, enc, imgs, caps, reps=20):
+    """The per-time-step decoder kernels (fused attention + LSTM step and the skinny per-step
+    GEMMs) timed live: each group of the middle step re-issued `reps` times between HIP events on
+    the launch stream (sat_decoder_step_bench); achieved = algorithmic bytes / time vs 8 TB/s."""
+    from sat_amd.diagnostics import FUSED, decoder_step_kernels
+    with torch.no_grad():
+        feats = enc(imgs)
+    times, by = decoder_step_kernels(dec, feats, caps, reps=reps)
+    groups = {}
+    for g, us in times.items():
+        if us <= 0 or by[g] <= 0:
+            continue
+        groups[g] = {"us": round(us, 2), "mb": round(by[g] / 1e6, 2), "gbs": round(by[g] / (us * 1e-6) / 1e9, 1),
+                     "frac": round(by[g] / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+    f_by = sum(by[g] for g in FUSED if g in groups)
+    f_us = sum(times[g] for g in FUSED if g in groups)
+    a_by = sum(by[g] for g in groups)
+    a_us = sum(times[g] for g in groups)
+    return {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "timing": f"each group of step (T-1)/2 re-issued "
+            f"{reps}x back to back between HIP events", "groups": groups,
+            "fused_attention_lstm": {"kernels": list(FUSED), "us_per_step": round(f_us, 2),
+                                     "achieved": round(f_by / (f_us * 1e-6) / 1e9, 1),
+                                     "frac": round(f_by / (f_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)},
+            "all_step_kernels": {"us_per_step": round(a_us, 2), "achieved": round(a_by / (a_us * 1e-6) / 1e9, 1),
+                                 "frac": round(a_by / (a_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
+def fp32_step(args, enc, dec, imgs, caps, pad_id, skip_ids, world):
+    """The same train step at the reference's precision (fp32 encoder and decoder: the exact-parity
+    path), eager, on this rank's batch; reported beside the bf16 line."""
+    import sat_amd
+    enc32 = sat_amd.Encoder(args.network, dtype=torch.float32).to(imgs.device).eval()
+    enc32.load_state_dict(enc.state_dict())
+    opt = sat_amd.Adam(dec.parameters(), lr=1e-4)
+
+    def step():
+        with torch.no_grad():
+            feats = enc32(imgs)
+        opt.zero_grad()
+        preds, alphas = dec(feats, caps)
+        loss, _ = sat_amd.caption_loss(preds, alphas, caps, pad_id=pad_id, skip_ids=skip_ids)
+        loss.backward()
+        opt.step()
+        return loss
+
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.fp32_steps):
+        loss = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value": round(imgs.shape[0] * args.fp32_steps / el, 2), "unit": "images/s", "dtype": "fp32",
+            "steps": args.fp32_steps, "ms_per_step": round(1000 * el / args.fp32_steps, 2),
+            "per_gpu_batch": imgs.shape[0], "loss": round(loss.item(), 4),
+            "note": "exact-parity path (fp32 MFMA), eager, rank 0 only; not the headline value"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -212,7 +274,7 @@ def main():
     torch.cuda.set_device(dev)
     import sat_amd
     from sat_amd.data import synthetic_captions, synthetic_images
-    from sat_amd.distributed import allreduce_grads
+    from sat_amd.distributed import GradAllReduce, allreduce_bucket_async, allreduce_grads
 
     if not args.no_graph and not args.no_overlap:
         # the decoder shares the chip with the next batch's encoder: fewer split-K workgroups
@@ -239,14 +301,18 @@ def main():
         loss.backward()
         return loss
 
+    # eager DP: bucket all-reduces launched from inside the decoder's backward (phase hooks)
+    grad_ar = GradAllReduce(dec) if world > 1 else None
     # eager warm-up (builds the encoder plan, caches, allocator pools)
     for _ in range(args.warmup):
         opt.zero_grad()
         loss = fwd_bwd()
         if world > 1:
-            allreduce_grads(dec)
+            grad_ar.wait()
         opt.step()
     torch.cuda.synchronize()
+    if grad_ar is not None and not args.no_graph:
+        dec._grad_hooks.remove(grad_ar._on_phase)   # graph mode issues the bucket all-reduces itself
 
     use_graph = not args.no_graph
     overlap = use_graph and not args.no_overlap
@@ -261,19 +327,24 @@ def main():
         nbuf = 2 if overlap else 1
         # one private memory pool per graph: no intermediate of one graph aliases another's
         g_enc = [torch.cuda.CUDAGraph() for _ in range(nbuf)]
-        g_dec = [torch.cuda.CUDAGraph() for _ in range(nbuf)]
+        g_dec = [torch.cuda.CUDAGraph() for _ in range(nbuf)]   # fwd + loss + backward phase 1 (output head)
+        g_rec = [torch.cuda.CUDAGraph() for _ in range(nbuf)]   # backward phase 2 (BPTT + remaining wgrads)
         feats_static, loss_static = [], []
         for k in range(nbuf):
             with torch.cuda.graph(g_enc[k]):
                 with torch.no_grad():
                     feats_static.append(enc(imgs))
+        dec.defer_recurrent_backward(True)
         for k in range(nbuf):
             opt.zero_grad(set_to_none=True)   # each capture overwrites the gradients (beta = 0)
             with torch.cuda.graph(g_dec[k]):
                 preds, alphas = dec(feats_static[k], caps)
                 loss_k, _ = sat_amd.caption_loss(preds, alphas, caps, pad_id=pad_id, skip_ids=skip_ids)
                 loss_k.backward()
+            with torch.cuda.graph(g_rec[k]):
+                dec.finish_backward()
             loss_static.append(loss_k)
+        dec.defer_recurrent_backward(False)
         torch.cuda.synchronize()
 
     enc_events = []
@@ -303,6 +374,11 @@ def main():
                 k = i % len(g_enc)
                 s_main.wait_event(ev_enc[k])
                 g_dec[k].replay()
+                # DP: the output-head bucket is final after phase 1 -> its all-reduce runs on RCCL's
+                # stream beside the BPTT graph; the rest follows phase 2
+                w1 = allreduce_bucket_async(dec, 1) if world > 1 else None
+                g_rec[k].replay()
+                w2 = allreduce_bucket_async(dec, 2) if world > 1 else None
                 ev_dec[k].record(s_main)
                 loss = loss_static[k]
                 if i + 1 < n:
@@ -310,11 +386,14 @@ def main():
                         replay_encoder((i + 1) % 2, i >= 1)
                     else:
                         replay_encoder(0, False)
+                if world > 1:
+                    w1.wait()
+                    w2.wait()
             else:
                 opt.zero_grad()
                 loss = fwd_bwd()
-            if world > 1:
-                allreduce_grads(dec)
+                if world > 1:
+                    grad_ar.wait()
             opt.step()
         return loss
 
@@ -337,9 +416,26 @@ def main():
     launches = conv_launches(args.network, B)
     enc_ms = sum(s.elapsed_time(e) for s, e in enc_events) if use_graph else None
     loss_v = loss.item()
-    roof, trunk = trunk_roofline(enc, imgs, launches) if rank == 0 else (None, None)
-    if rank == 0:
+    diag = rank == 0 and not args.no_diagnostics
+    roof, trunk = trunk_roofline(enc, imgs, launches) if diag else (None, None)
+    step_kernels = decoder_step_roofline(dec, enc, imgs, caps) if diag else None
+    fp32_leg = fp32_step(args, enc, dec, imgs, caps, pad_id, skip_ids, world) if world == 1 and args.fp32_steps > 0 \
+        else None
+    if roof is not None:
         roof["traffic"], roof["traffic_source"] = pmc_traffic(args.network, roof["cls"])
+        # the whole step's algorithmic FLOPs (encoder fwd + decoder fwd/bwd with W.a
+        # hoisted) per image x images / step time, against the dense bf16 MFMA peak
+        from sat_amd.diagnostics import decoder_flops
+        D = 2048 if args.network == "resnet152" else 512
+        Lf = 49 if args.network == "resnet152" else 196
+        E = 768 if args.bert else 512
+        enc_f = sum(l["flops"] for l in launches) / B
+        dec_f = decoder_flops(Lf, D, E, args.vocab, args.seq, ado=not args.bert, attention=True)
+        step_tf = (enc_f + dec_f) * B * world * args.steps / elapsed / 1e12
+        roof["step"] = {"encoder_gflop_per_img": round(enc_f / 1e9, 3), "decoder_gflop_per_img": round(dec_f / 1e9, 3),
+                        "achieved": round(step_tf, 1), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(step_tf / BF16_DENSE_PEAK_TFLOPS, 4)}
+        roof["decoder_step_kernels"] = step_kernels
         out = {
             "metric": "train images/sec on COCO batch=128 at 1/2/4/8 MI355X",
             "value": round(B * world * args.steps / elapsed, 2),
@@ -354,9 +450,11 @@ def main():
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
                        "encoder_decoder_overlap": overlap},
             "roofline": roof,
-            "encoder_trunk": dict(trunk, graph_ms_per_step=(round(enc_ms / args.steps, 3) if enc_ms else None)),
+            "encoder_trunk": dict(trunk or {}, graph_ms_per_step=(round(enc_ms / args.steps, 3) if enc_ms else None)),
             "loss": round(loss_v, 4),
         }
+        if fp32_leg is not None:
+            out["fp32"] = fp32_leg
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)

@@ -146,6 +146,14 @@ int sat_attention_forward(int B, int L, int D, int E, int dtype, const void* img
  * c: context part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic.  Must be set
  * before sat_decoder_workspace_bytes. */
 int sat_decoder_set_splits(int h, int c, int g, int dh);
+/* diagnostics (bench.py): after sat_decoder_forward + sat_decoder_backward filled `workspace`, re-issue
+ * each per-step kernel group of step (T-1)/2 `reps` times back to back between HIP events on `stream`;
+ * us_out[8] = average us per launch: h GEMM, attention fwd, context GEMM, LSTM fwd, LSTM bwd, d(gated
+ * context) GEMM, attention bwd, dh GEMM (0 for groups the configuration does not run).  Overwrites the
+ * workspace's running BPTT sums (call after the gradients are consumed). */
+int sat_decoder_step_bench(const SatDecoderDims* dims, const SatDecoderLayout* layout, const float* params,
+                           const void* params_lp, const void* img_features, void* workspace, size_t workspace_bytes,
+                           float* alphas, const float* d_alphas, int reps, float* us_out, void* stream);
 /* process-global: workgroups the automatic per-step split-K aims for (0 = default 192; 64 when the decoder
  * shares the GPU with a concurrent encoder stream).  Set before the first workspace query. */
 int sat_decoder_set_split_target(int workgroups);

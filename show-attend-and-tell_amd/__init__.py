@@ -9,7 +9,7 @@ from . import _lib
 from .attention import Attention
 from .decoder import Decoder
 from .encoder import Encoder
-from .loss import caption_loss, special_ids, StepMetrics
+from .loss import caption_loss, special_ids, StepMetrics, RunningMeters
 from .optim import Adam
 
-__all__ = ["Attention", "Decoder", "Encoder", "caption_loss", "special_ids", "StepMetrics", "Adam"]
+__all__ = ["Attention", "Decoder", "Encoder", "caption_loss", "special_ids", "StepMetrics", "RunningMeters", "Adam"]

@@ -81,6 +81,9 @@ _SIGNATURES = [
     ("sat_decoder_backward", c_int, [ctypes.POINTER(SatDecoderDims), ctypes.POINTER(SatDecoderLayout), c_void_p,
                                      c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    ("sat_decoder_step_bench", c_int, [ctypes.POINTER(SatDecoderDims), ctypes.POINTER(SatDecoderLayout), c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_int, c_void_p,
+                                       c_void_p]),
     ("sat_decoder_beam_workspace_bytes", c_size_t, [ctypes.POINTER(SatDecoderDims), c_int]),
     ("sat_decoder_beam_search", c_int, [ctypes.POINTER(SatDecoderDims), ctypes.POINTER(SatDecoderLayout), c_void_p,
                                         c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p, c_void_p,

@@ -12,8 +12,11 @@
 //
 // Backward, two launches per step: (1) grid (B, NS): dL/dcontext, the gate
 // gradient and per-slice partial dL/dalpha; (2) grid B: softmax backward,
-// recomputed tanh, dL/d(U h), and running sums of dL/dWs, dL/dv, dL/dv.bias
-// over the time loop (weight gradients are formed once after the loop).
+// recomputed tanh, dL/d(U h), running sums of dL/dv, dL/dv.bias, and the step's
+// dL/d(score) rows de[b,t,:] (B*L floats).  dL/dWs is NOT accumulated per step (that
+// read-modify-write of a B*L*E fp32 buffer was 8 of the step's 10 bytes per element):
+// one launch after the time loop (attn_dws_kernel) forms sum_t de_t v (1 - tanh^2)
+// reading Ws once; weight gradients are formed once after the loop.
 #include "sat_common.h"
 #include "sat_internal.h"
 
@@ -37,14 +40,14 @@ __device__ __forceinline__ void load4(const T* p, float* o) {
   }
 }
 
-// tanh: exact libm in the fp32 parity path; exp-based (v_exp_f32 + v_rcp_f32, ~1e-6 rel) in bf16 mode.
+// tanh: exact libm in the fp32 parity path; exp-based (v_exp_f32 + v_rcp_f32, ~1e-6 abs) in bf16 mode.
 template <typename T>
 __device__ __forceinline__ float tanh_t(float x) {
   if constexpr (sizeof(T) == 4) {
     return tanhf(x);
   } else {
     const float e = __expf(2.f * x);
-    return 1.f - 2.f * __frcp_rn(e + 1.f);
+    return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);   // v_rcp_f32 (1 ulp); __frcp_rn expands to a full division
   }
 }
 
@@ -329,19 +332,15 @@ __global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int 
   const float* alpha = a.alpha + (long)b * a.alpha_ld;
   const float* uh = a.uh + (long)b * a.uh_ld;
   const T* Ws = (const T*)a.Ws + (long)b * L * E;
-  float* dWs = a.dWs_acc + (long)b * L * E;
   // loop invariants and the first batch of slots: requested before the softmax backward
   float uu[BEV], vw[BEV];
   load_e4<float>(uh + e, eok, uu);
   load_e4<float>(a.v_w + e, eok, vw);
   float xw[BFU][BEV];
-  float4 acc[BFU];
 #pragma unroll
   for (int u = 0; u < BFU; ++u) {
     const int l = w + BNW * u;
-    const bool ok = l < L && eok;
-    load_e4<T>(Ws + (long)l * E + e, ok, xw[u]);
-    acc[u] = ok ? *(const float4*)(dWs + (long)l * E + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    load_e4<T>(Ws + (long)l * E + e, l < L && eok, xw[u]);
   }
   // dL/dalpha and sum_l alpha*dalpha
   float loc = 0.f;
@@ -359,7 +358,11 @@ __global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int 
 #pragma unroll
   for (int i = 0; i < BNW; i += 2) sad += s_tmp[i] + s_tmp[i + 1];
   __syncthreads();
-  for (int l = tid; l < L; l += BNW * 64) s_de[l] = alpha[l] * (s_de[l] - sad);
+  for (int l = tid; l < L; l += BNW * 64) {
+    const float de = alpha[l] * (s_de[l] - sad);
+    s_de[l] = de;
+    if (eslice == 0) a.de_out[(long)b * a.de_ld + l] = de;
+  }
   __syncthreads();
   // recompute tanh, accumulate
   float duh[BEV], dv[BEV];
@@ -371,9 +374,7 @@ __global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int 
 #pragma unroll
       for (int u = 0; u < BFU; ++u) {
         const int l = l0 + BNW * u;
-        const bool ok = l < L && eok;
-        load_e4<T>(Ws + (long)l * E + e, ok, xw[u]);
-        acc[u] = ok ? *(const float4*)(dWs + (long)l * E + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+        load_e4<T>(Ws + (long)l * E + e, l < L && eok, xw[u]);
       }
     }
 #pragma unroll
@@ -383,16 +384,13 @@ __global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int 
       const float de = s_de[l];
       dbv += de;
       if (!eok) continue;
-      float* ac = (float*)&acc[u];
 #pragma unroll
       for (int j = 0; j < BEV; ++j) {
         const float t = tanh_t<T>(xw[u][j] + uu[j]);
         const float datt = de * vw[j] * (1.f - t * t);
         duh[j] += datt;
         dv[j] += de * t;
-        ac[j] += datt;
       }
-      *(float4*)(dWs + (long)l * E + e) = acc[u];
     }
   }
   // fold the waves (fixed order): dU_h, then dv
@@ -424,6 +422,77 @@ __global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int 
 #pragma unroll
     for (int i = 0; i < BNW; i += 2) v += s_tmp[i] + s_tmp[i + 1];
     a.dbv_acc[b] += v;
+  }
+}
+
+// After the time loop: dWs[b,l,e] = sum over t = T1-1 .. 0 of de[b,t,l] v[e] (1 - tanh^2(Ws[b,l,e] +
+// uh[b,t,e])) -- the per-element expression and summation order of the per-step accumulation it
+// replaces, so the fp32 path is bit-identical to it.  A wave owns DWS_LG rows l of one batch row b
+// and a 256-wide e-chunk (lane: 4 consecutive e): each uh[b,t,e..e+3] load feeds DWS_LG x 4 tanh and
+// the next step's uh is requested before the current step's arithmetic; the wave's de[b,:,l0..]
+// block is staged in LDS once (a scalar load per step would wait on the scalar cache every step).
+// Ws is read once.  VALU-bound: B*L*E*(T-1) tanh.
+constexpr int DWS_LG = 4, DWS_WAVES = 4, DWS_TMAX = 128;   // T - 1 <= 128 caption steps
+template <typename T>
+__global__ __launch_bounds__(DWS_WAVES * 64) void attn_dws_kernel(const T* Ws, const float* uh_all,
+                                                                 const float* de_all, const float* v_w, int B, int L,
+                                                                 int E, int T1, int n_ech, int n_lg, float* out_f32,
+                                                                 T* out_t) {
+  __shared__ float s_de[DWS_WAVES][DWS_TMAX * DWS_LG];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * DWS_WAVES + wv;
+  const bool wok = wid < B * n_ech * n_lg;
+  const int lg = wid % n_lg, ec = (wid / n_lg) % n_ech, b = wok ? wid / (n_lg * n_ech) : 0;
+  const int l0 = lg * DWS_LG, e = ec * 256 + lane * 4;
+  // stage de[b, t, l0 + r] -> s_de[wv][t * DWS_LG + r]
+  for (int i = lane; i < T1 * DWS_LG; i += 64) {
+    const int t = i / DWS_LG, r = i - t * DWS_LG;
+    s_de[wv][i] = (wok && l0 + r < L) ? de_all[((long)b * T1 + t) * L + l0 + r] : 0.f;
+  }
+  __syncthreads();
+  if (!wok) return;   // wave-uniform; no barriers below
+  const bool eok = e < E;
+  float xw[DWS_LG][4], acc[DWS_LG][4], vw[4];
+  load_e4<float>(v_w + e, eok, vw);
+#pragma unroll
+  for (int r = 0; r < DWS_LG; ++r) {
+    load_e4<T>(Ws + ((long)b * L + l0 + r) * E + e, eok && l0 + r < L, xw[r]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[r][j] = 0.f;
+  }
+  const float* uh = uh_all + (long)b * T1 * E + e;
+  float un[4];
+  load_e4<float>(uh + (long)(T1 - 1) * E, eok, un);
+  for (int t = T1 - 1; t >= 0; --t) {
+    float uu[4] = {un[0], un[1], un[2], un[3]};
+    if (t > 0) load_e4<float>(uh + (long)(t - 1) * E, eok, un);
+    const float4 d4 = *(const float4*)&s_de[wv][t * DWS_LG];
+    const float d[DWS_LG] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+    for (int r = 0; r < DWS_LG; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float th = tanh_t<T>(xw[r][j] + uu[j]);
+        acc[r][j] += d[r] * vw[j] * (1.f - th * th);
+      }
+  }
+  if (!eok) return;
+#pragma unroll
+  for (int r = 0; r < DWS_LG; ++r) {
+    if (l0 + r >= L) break;
+    const long o = ((long)b * L + l0 + r) * E + e;
+    *(float4*)(out_f32 + o) = make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+    if (out_t) {
+      if constexpr (sizeof(T) == 2) {
+        uint2 u;
+        bf16* h = (bf16*)&u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) h[j] = (bf16)acc[r][j];
+        *(uint2*)(out_t + o) = u;
+      } else {
+        *(float4*)(out_t + o) = make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+      }
+    }
   }
 }
 
@@ -466,6 +535,21 @@ int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(attn_bwd1_kernel<float>, dim3(a.B, NS), dim3(ANW * 64), 0, s, a);
     hipLaunchKernelGGL(attn_bwd2_kernel<float>, dim3(a.B, sat_cdiv(a.E, BSLICE)), dim3(BNW * 64), 0, s, a, NS);
   }
+  return (int)hipGetLastError();
+}
+
+int sat_attention_dws_launch(const void* Ws, const float* uh_all, const float* de_all, const float* v_w, int B,
+                             int L, int E, int T1, int dtype, float* out_f32, void* out_t, hipStream_t s) {
+  SAT_REQUIRE(E % 4 == 0 && E <= 1024 && L > 0 && B > 0 && T1 > 0 && T1 <= DWS_TMAX);
+  static_assert(DWS_LG == 4, "s_de rows are read as one float4 per step");
+  const int n_ech = sat_cdiv(E, 256), n_lg = sat_cdiv(L, DWS_LG);
+  const dim3 grid(sat_cdiv((long)B * n_ech * n_lg, DWS_WAVES));
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(attn_dws_kernel<bf16>, grid, dim3(DWS_WAVES * 64), 0, s, (const bf16*)Ws, uh_all, de_all, v_w, B, L, E, T1,
+                       n_ech, n_lg, out_f32, (bf16*)out_t);
+  else
+    hipLaunchKernelGGL(attn_dws_kernel<float>, grid, dim3(DWS_WAVES * 64), 0, s, (const float*)Ws, uh_all, de_all, v_w, B, L, E,
+                       T1, n_ech, n_lg, out_f32, (float*)out_t);
   return (int)hipGetLastError();
 }
 

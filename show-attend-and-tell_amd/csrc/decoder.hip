@@ -33,7 +33,7 @@ struct WS {
   // backward
   void *dpre_t, *dfh_t, *dfz_t, *dhg_t, *dWs_t, *dpre0_t;
   float *dcomb, *dhd, *dctx_head, *dhg, *dgated, *dh_rec, *dc, *dWs_acc, *dv_acc, *dbv_acc, *part, *demb, *dpre0,
-      *colsum;
+      *colsum, *de_all;
 };
 
 // split counts of the per-step skinny GEMMs (M = B rows).  bf16: the LDS-DMA kernel (128 x 64
@@ -126,6 +126,7 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   c.take(w->dh_rec, sp.dh * B * E * f); c.take(w->dc, B * E * f);
   c.take(w->dWs_acc, B * L * E * f); c.take(w->dWs_t, B * L * E * ts);
   c.take(w->dv_acc, B * E * f); c.take(w->dbv_acc, B * f);
+  c.take(w->de_all, R * L * f);
   c.take(w->part, sat_attention_part_floats(d.B, d.L, d.D, d.dtype) * f);
   c.take(w->demb, R * E * f);
   c.take(w->dpre0, B * 2 * E * f); c.take(w->dpre0_t, B * 2 * E * ts);
@@ -242,6 +243,148 @@ int head_forward(const Ctx& c, const WS& w, int rows, int t, bool per_step, void
   return 0;
 }
 
+// ---- per-step kernels (shared by the time loops and sat_decoder_step_bench) ----
+struct StepIO {
+  const void* feats;          // img_features [B,L,D] (dtype)
+  float* alphas;              // [B,T-1,L]
+  const float* d_alphas;      // [B,T-1,L] (backward)
+};
+
+// h GEMM: [U h + b_U | f_beta h + b | W_hh h + b_hh] (one N = E+D+4E product; W_hh only without attention)
+int fwd_hgemm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) {
+  const SatDecoderDims& d = c.d;
+  const int B = d.B, D = d.D, E = d.E;
+  const long T1 = c.T1, HG = c.HG;
+  const void* h_t = c.at(w.h_in_t, (long)t * E);
+  if (d.attention)
+    return linear(c, B, (int)HG, E, h_t, T1 * E, c.W(c.lay.hcat_w), E, c.F(c.lay.hcat_b), w.hg, HG, SAT_F32,
+                  SAT_ACT_NONE, s, nullptr, 0, SAT_F32, nullptr, 0, SAT_F32, sp.h, (long)B * HG);
+  return linear(c, B, 4 * E, E, h_t, T1 * E, c.W(c.lay.hcat_w + (long)(E + D) * E), E, c.F(c.lay.hcat_b + E + D),
+                w.hg + E + D, HG, SAT_F32, SAT_ACT_NONE, s, nullptr, 0, SAT_F32, nullptr, 0, SAT_F32, sp.h,
+                (long)B * HG);
+}
+
+int fwd_attn(const Ctx& c, const WS& w, const Splits& sp, const StepIO& io, int t, hipStream_t s) {
+  const SatDecoderDims& d = c.d;
+  const int B = d.B, L = d.L, D = d.D, E = d.E;
+  const long T1 = c.T1, HG = c.HG;
+  AttnFwdArgs a{};
+  a.B = B; a.L = L; a.D = D; a.E = E; a.dtype = d.dtype;
+  a.Ws = w.Ws; a.uh = w.hg; a.uh_ld = HG; a.v_w = c.F(c.lay.v_w); a.v_b = c.F(c.lay.v_b); a.a = io.feats;
+  a.gate_pre = w.hg + E; a.gate_ld = HG;
+  a.hg_splits = sp.h; a.hg_split_stride = (long)B * HG;
+  a.alpha = io.alphas + (long)t * L; a.alpha_ld = T1 * L;
+  a.ctx = w.ctx_all + (long)t * D; a.ctx_ld = T1 * D;
+  a.ctx_t = c.at(w.ctx_t, (long)t * D); a.ctx_t_ld = T1 * D;
+  a.gate = w.gate_all + (long)t * D; a.gate_out_ld = T1 * D;
+  a.gated = c.at(w.gated_t, (long)t * D); a.gated_ld = T1 * D;
+  a.uh_save = w.uh_all + (long)t * E; a.uh_save_ld = T1 * E;
+  return sat_attention_fwd_launch(a, s);
+}
+
+// context half of the LSTM input GEMM: gated context . W_ih[:, E:]^T
+int fwd_cgemm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) {
+  const SatDecoderDims& d = c.d;
+  const int B = d.B, D = d.D, E = d.E;
+  return linear(c, B, 4 * E, D, c.at(w.gated_t, (long)t * D), c.T1 * D, c.W(c.lay.wih + E), E + D, nullptr, w.gctx,
+                4 * E, SAT_F32, SAT_ACT_NONE, s, nullptr, 0, SAT_F32, nullptr, 0, SAT_F32, sp.c, (long)B * 4 * E);
+}
+
+int fwd_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) {
+  const SatDecoderDims& d = c.d;
+  const int B = d.B, D = d.D, E = d.E;
+  const long T1 = c.T1, HG = c.HG;
+  const bool att = d.attention != 0;
+  LstmFwdArgs l{};
+  l.B = B; l.E = E; l.dtype = d.dtype;
+  l.hpart = w.hg + E + D; l.hpart_ld = HG;
+  l.xpart = w.xg + (long)t * 4 * E; l.xpart_ld = T1 * 4 * E;
+  l.cpart = att ? w.gctx : w.gctx_const; l.cpart_ld = 4 * E;
+  l.h_splits = sp.h; l.h_split_stride = (long)B * HG;
+  l.c_splits = att ? sp.c : 1; l.c_split_stride = (long)B * 4 * E;
+  l.c_prev = w.c_in + (long)t * E; l.c_prev_ld = T1 * E;
+  l.gates = w.gates_all + (long)t * 4 * E; l.gates_ld = T1 * 4 * E;
+  l.c_out = w.c_out + (long)t * E; l.c_out_ld = T1 * E;
+  l.c_next_in = t + 1 < T1 ? w.c_in + (long)(t + 1) * E : nullptr; l.c_next_in_ld = T1 * E;
+  l.h_out = w.h_out + (long)t * E; l.h_out_ld = T1 * E;
+  l.h_next_in_t = t + 1 < T1 ? c.at(w.h_in_t, (long)(t + 1) * E) : nullptr; l.h_next_in_t_ld = T1 * E;
+  return sat_lstm_fwd_launch(l, s);
+}
+
+int bwd_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) {
+  const SatDecoderDims& d = c.d;
+  const int B = d.B, D = d.D, E = d.E;
+  const long T1 = c.T1, HG = c.HG;
+  LstmBwdArgs l{};
+  l.B = B; l.E = E; l.dtype = d.dtype;
+  l.gates = w.gates_all + (long)t * 4 * E; l.gates_ld = T1 * 4 * E;
+  l.c_prev = w.c_in + (long)t * E; l.c_prev_ld = T1 * E;
+  l.c_new = w.c_out + (long)t * E; l.c_new_ld = T1 * E;
+  l.dh_rec = t == T1 - 1 ? nullptr : w.dh_rec; l.dh_rec_ld = E;
+  l.dh_splits = sp.dh; l.dh_split_stride = (long)B * E;
+  l.dh_head = w.dhd + (long)t * E; l.dh_head_ld = T1 * E;
+  l.mask = d.training ? w.dmask + (long)t * E : nullptr; l.mask_ld = T1 * E;
+  l.dc = w.dc; l.dc_zero = t == T1 - 1;
+  l.d_gates = w.dhg + (long)t * HG + E + D; l.d_gates_ld = T1 * HG;
+  l.d_gates_t = c.at(w.dhg_t, (long)t * HG + E + D); l.d_gates_t_ld = T1 * HG;
+  return sat_lstm_bwd_launch(l, s);
+}
+
+// input gradient: Y[M,N] = X[M,K] W[K,N]   (W stored [K][N] row-major = torch weight [out,in])
+int dgrad_launch(const Ctx& c, int M, int N, int K, const void* X, long ldx, const void* Wt, long ldw, float* out,
+                 long ldo, hipStream_t s, const float* add1 = nullptr, long ld_add1 = 0, int splits = 0,
+                 long split_stride = 0) {
+  SatGemm g;
+  g.partial_splits = splits; g.split_stride = split_stride;
+  g.M = M; g.N = N; g.K = K; g.dtype = c.d.dtype;
+  g.A = X; g.lda = ldx; g.B = Wt; g.ldb = ldw; g.transB = 1;
+  g.C = out; g.ldc = ldo; g.c_dtype = SAT_F32;
+  g.add1 = add1; g.ld_add1 = ld_add1; g.add1_dtype = SAT_F32;
+  return sat_gemm_launch(g, s);
+}
+
+// dL/d(gated context) = d gates . W_ih[:, E:]
+int bwd_ggemm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) {
+  const SatDecoderDims& d = c.d;
+  const int B = d.B, D = d.D, E = d.E;
+  return dgrad_launch(c, B, D, 4 * E, c.at(w.dhg_t, (long)t * c.HG + E + D), c.T1 * c.HG, c.W(c.lay.wih + E), E + D,
+                      w.dgated, D, s, nullptr, 0, sp.g, (long)B * D);
+}
+
+int bwd_attn(const Ctx& c, const WS& w, const Splits& sp, const StepIO& io, int t, hipStream_t s) {
+  const SatDecoderDims& d = c.d;
+  const int B = d.B, L = d.L, D = d.D, E = d.E;
+  const long T1 = c.T1, HG = c.HG;
+  AttnBwdArgs a{};
+  a.B = B; a.L = L; a.D = D; a.E = E; a.dtype = d.dtype;
+  a.Ws = w.Ws; a.a = io.feats;
+  a.uh = w.uh_all + (long)t * E; a.uh_ld = T1 * E;
+  a.v_w = c.F(c.lay.v_w);
+  a.alpha = io.alphas + (long)t * L; a.alpha_ld = T1 * L;
+  a.d_alpha_ext = io.d_alphas + (long)t * L; a.d_alpha_ext_ld = T1 * L;
+  a.d_gated = w.dgated; a.d_gated_ld = D;
+  a.gate = w.gate_all + (long)t * D; a.gate_ld = T1 * D;
+  a.ctx = w.ctx_all + (long)t * D; a.ctx_ld = T1 * D;
+  a.d_ctx_ext = d.ado ? w.dctx_head + (long)t * D : nullptr; a.d_ctx_ext_ld = T1 * D;
+  a.d_uh = w.dhg + (long)t * HG; a.d_uh_ld = T1 * HG; a.d_uh_t = c.at(w.dhg_t, (long)t * HG);
+  a.d_gpre = w.dhg + (long)t * HG + E; a.d_gpre_ld = T1 * HG; a.d_gpre_t = c.at(w.dhg_t, (long)t * HG + E);
+  a.de_out = w.de_all + (long)t * L; a.de_ld = T1 * L; a.dv_acc = w.dv_acc; a.dbv_acc = w.dbv_acc; a.part = w.part;
+  a.dg_splits = sp.g; a.dg_split_stride = (long)B * D;
+  return sat_attention_bwd_launch(a, s);
+}
+
+// recurrent dL/dh = [dU_h | d(f_beta h) | d gates] . [U ; f_beta ; W_hh]   (W_hh only without attention)
+int bwd_dhgemm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) {
+  const SatDecoderDims& d = c.d;
+  const int B = d.B, D = d.D, E = d.E;
+  const long T1 = c.T1, HG = c.HG;
+  if (d.attention)
+    return dgrad_launch(c, B, E, (int)HG, c.at(w.dhg_t, (long)t * HG), T1 * HG, c.W(c.lay.hcat_w), E, w.dh_rec, E, s,
+                        nullptr, 0, sp.dh, (long)B * E);
+  return dgrad_launch(c, B, E, 4 * E, c.at(w.dhg_t, (long)t * HG + E + D), T1 * HG,
+                      c.W(c.lay.hcat_w + (long)(E + D) * E), E, w.dh_rec, E, s, nullptr, 0, sp.dh, (long)B * E);
+}
+
 int check_dims(const SatDecoderDims* d) {
   if (!d) return SAT_ERR_INVALID;
   if (d->B <= 0 || d->L <= 0 || d->D <= 0 || d->E <= 0 || d->V <= 0 || d->T < 3) return SAT_ERR_INVALID;
@@ -291,6 +434,7 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
   const long HG = c.HG;
   const bool att = d.attention != 0;
   const Splits sp = splits_for(d);
+  const StepIO io{img_features, alphas, nullptr};
 
   // fed tokens + embeddings
   if (d.tf) {
@@ -337,46 +481,12 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
     if (!d.tf)
       SAT_CHECK((hipError_t)linear(c, B, 4 * E, E, c.at(w.emb_t, (long)t * E), (long)T1 * E, c.W(lay->wih), E + D,
                                    c.F(lay->bih), w.xg + (long)t * 4 * E, (long)T1 * 4 * E, SAT_F32, SAT_ACT_NONE, s));
-    const void* h_t = c.at(w.h_in_t, (long)t * E);
+    SAT_CHECK((hipError_t)fwd_hgemm(c, w, sp, t, s));
     if (att) {
-      // [U h + b_U | f_beta h + b | W_hh h + b_hh] in one GEMM
-      SAT_CHECK((hipError_t)linear(c, B, (int)HG, E, h_t, (long)T1 * E, c.W(lay->hcat_w), E, c.F(lay->hcat_b), w.hg,
-                                   HG, SAT_F32, SAT_ACT_NONE, s, nullptr, 0, SAT_F32, nullptr, 0, SAT_F32, sp.h,
-                                   (long)B * HG));
-      AttnFwdArgs a{};
-      a.B = B; a.L = L; a.D = D; a.E = E; a.dtype = d.dtype;
-      a.Ws = w.Ws; a.uh = w.hg; a.uh_ld = HG; a.v_w = c.F(lay->v_w); a.v_b = c.F(lay->v_b); a.a = img_features;
-      a.gate_pre = w.hg + E; a.gate_ld = HG;
-      a.hg_splits = sp.h; a.hg_split_stride = (long)B * HG;
-      a.alpha = alphas + (long)t * L; a.alpha_ld = (long)T1 * L;
-      a.ctx = w.ctx_all + (long)t * D; a.ctx_ld = (long)T1 * D;
-      a.ctx_t = c.at(w.ctx_t, (long)t * D); a.ctx_t_ld = (long)T1 * D;
-      a.gate = w.gate_all + (long)t * D; a.gate_out_ld = (long)T1 * D;
-      a.gated = c.at(w.gated_t, (long)t * D); a.gated_ld = (long)T1 * D;
-      a.uh_save = w.uh_all + (long)t * E; a.uh_save_ld = (long)T1 * E;
-      SAT_CHECK((hipError_t)sat_attention_fwd_launch(a, s));
-      SAT_CHECK((hipError_t)linear(c, B, 4 * E, D, c.at(w.gated_t, (long)t * D), (long)T1 * D, c.W(lay->wih + E),
-                                   E + D, nullptr, w.gctx, 4 * E, SAT_F32, SAT_ACT_NONE, s, nullptr, 0, SAT_F32,
-                                   nullptr, 0, SAT_F32, sp.c, (long)B * 4 * E));
-    } else {
-      SAT_CHECK((hipError_t)linear(c, B, 4 * E, E, h_t, (long)T1 * E, c.W(lay->hcat_w + (long)(E + D) * E), E,
-                                   c.F(lay->hcat_b + E + D), w.hg + E + D, HG, SAT_F32, SAT_ACT_NONE, s, nullptr, 0,
-                                   SAT_F32, nullptr, 0, SAT_F32, sp.h, (long)B * HG));
+      SAT_CHECK((hipError_t)fwd_attn(c, w, sp, io, t, s));
+      SAT_CHECK((hipError_t)fwd_cgemm(c, w, sp, t, s));
     }
-    LstmFwdArgs l{};
-    l.B = B; l.E = E; l.dtype = d.dtype;
-    l.hpart = w.hg + E + D; l.hpart_ld = HG;
-    l.xpart = w.xg + (long)t * 4 * E; l.xpart_ld = (long)T1 * 4 * E;
-    l.cpart = att ? w.gctx : w.gctx_const; l.cpart_ld = 4 * E;
-    l.h_splits = sp.h; l.h_split_stride = (long)B * HG;
-    l.c_splits = att ? sp.c : 1; l.c_split_stride = (long)B * 4 * E;
-    l.c_prev = w.c_in + (long)t * E; l.c_prev_ld = (long)T1 * E;
-    l.gates = w.gates_all + (long)t * 4 * E; l.gates_ld = (long)T1 * 4 * E;
-    l.c_out = w.c_out + (long)t * E; l.c_out_ld = (long)T1 * E;
-    l.c_next_in = t + 1 < T1 ? w.c_in + (long)(t + 1) * E : nullptr; l.c_next_in_ld = (long)T1 * E;
-    l.h_out = w.h_out + (long)t * E; l.h_out_ld = (long)T1 * E;
-    l.h_next_in_t = t + 1 < T1 ? c.at(w.h_in_t, (long)(t + 1) * E) : nullptr; l.h_next_in_t_ld = (long)T1 * E;
-    SAT_CHECK((hipError_t)sat_lstm_fwd_launch(l, s));
+    SAT_CHECK((hipError_t)fwd_lstm(c, w, sp, t, s));
     if (!d.tf) {
       SAT_CHECK((hipError_t)head_forward(c, w, B, t, true, preds, dropout_mask, s));
       if (t + 1 < T1)   // greedy feedback: argmax -> next token + its embedding (decoder.py:131-133)
@@ -422,16 +532,9 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
     g.C = out; g.ldc = ldo; g.c_dtype = SAT_F32; g.beta = beta;
     return sat_gemm_launch(g, s);
   };
-  // input gradient: Y[M,N] = X[M,K] W[K,N]   (W stored [K][N] row-major = torch weight [out,in])
   auto dgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Wt, long ldw, float* out, long ldo,
-                   const float* add1 = nullptr, long ld_add1 = 0, int splits = 0, long split_stride = 0) {
-    SatGemm g;
-    g.partial_splits = splits; g.split_stride = split_stride;
-    g.M = M; g.N = N; g.K = K; g.dtype = d.dtype;
-    g.A = X; g.lda = ldx; g.B = Wt; g.ldb = ldw; g.transB = 1;
-    g.C = out; g.ldc = ldo; g.c_dtype = SAT_F32;
-    g.add1 = add1; g.ld_add1 = ld_add1; g.add1_dtype = SAT_F32;
-    return sat_gemm_launch(g, s);
+                   const float* add1 = nullptr, long ld_add1 = 0) {
+    return dgrad_launch(c, M, N, K, X, ldx, Wt, ldw, out, ldo, s, add1, ld_add1);
   };
   auto colsum = [&](const void* X, int dt, long ld, int rows, int N, float* out, float* out2 = nullptr) {
     return sat_colsum(X, dt, ld, rows, N, out, accumulate, out2, w.colsum, s);
@@ -466,51 +569,17 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
 
   // ---------------- recurrent BPTT (reverse time loop) ----------------
   if (att) {
-    SAT_CHECK((hipError_t)sat_zero_rows(w.dWs_acc, (long)B * L * E, 1, (long)B * L * E, s));
     SAT_CHECK((hipError_t)sat_zero_rows(w.dv_acc, (long)B * E, 1, (long)B * E, s));
     SAT_CHECK((hipError_t)sat_zero_rows(w.dbv_acc, B, 1, B, s));
   }
+  const StepIO io{img_features, const_cast<float*>(alphas), d_alphas};
   for (int t = T1 - 1; t >= 0; --t) {
-    LstmBwdArgs l{};
-    l.B = B; l.E = E; l.dtype = d.dtype;
-    l.gates = w.gates_all + (long)t * 4 * E; l.gates_ld = (long)T1 * 4 * E;
-    l.c_prev = w.c_in + (long)t * E; l.c_prev_ld = (long)T1 * E;
-    l.c_new = w.c_out + (long)t * E; l.c_new_ld = (long)T1 * E;
-    l.dh_rec = t == T1 - 1 ? nullptr : w.dh_rec; l.dh_rec_ld = E;
-    l.dh_splits = sp.dh; l.dh_split_stride = (long)B * E;
-    l.dh_head = w.dhd + (long)t * E; l.dh_head_ld = (long)T1 * E;
-    l.mask = d.training ? w.dmask + (long)t * E : nullptr; l.mask_ld = (long)T1 * E;
-    l.dc = w.dc; l.dc_zero = t == T1 - 1;
-    l.d_gates = w.dhg + (long)t * HG + E + D; l.d_gates_ld = (long)T1 * HG;
-    l.d_gates_t = c.at(w.dhg_t, (long)t * HG + E + D); l.d_gates_t_ld = (long)T1 * HG;
-    SAT_CHECK((hipError_t)sat_lstm_bwd_launch(l, s));
-    const void* dgates_t = c.at(w.dhg_t, (long)t * HG + E + D);
+    SAT_CHECK((hipError_t)bwd_lstm(c, w, sp, t, s));
     if (att) {
-      SAT_CHECK((hipError_t)dgrad(B, D, 4 * E, dgates_t, (long)T1 * HG, c.W(lay->wih + E), E + D, w.dgated, D,
-                                  nullptr, 0, sp.g, (long)B * D));
-      AttnBwdArgs a{};
-      a.B = B; a.L = L; a.D = D; a.E = E; a.dtype = d.dtype;
-      a.Ws = w.Ws; a.a = img_features;
-      a.uh = w.uh_all + (long)t * E; a.uh_ld = (long)T1 * E;
-      a.v_w = c.F(lay->v_w);
-      a.alpha = alphas + (long)t * L; a.alpha_ld = (long)T1 * L;
-      a.d_alpha_ext = d_alphas + (long)t * L; a.d_alpha_ext_ld = (long)T1 * L;
-      a.d_gated = w.dgated; a.d_gated_ld = D;
-      a.gate = w.gate_all + (long)t * D; a.gate_ld = (long)T1 * D;
-      a.ctx = w.ctx_all + (long)t * D; a.ctx_ld = (long)T1 * D;
-      a.d_ctx_ext = d.ado ? w.dctx_head + (long)t * D : nullptr; a.d_ctx_ext_ld = (long)T1 * D;
-      a.d_uh = w.dhg + (long)t * HG; a.d_uh_ld = (long)T1 * HG; a.d_uh_t = c.at(w.dhg_t, (long)t * HG);
-      a.d_gpre = w.dhg + (long)t * HG + E; a.d_gpre_ld = (long)T1 * HG; a.d_gpre_t = c.at(w.dhg_t, (long)t * HG + E);
-      a.dWs_acc = w.dWs_acc; a.dv_acc = w.dv_acc; a.dbv_acc = w.dbv_acc; a.part = w.part;
-      a.dg_splits = sp.g; a.dg_split_stride = (long)B * D;
-      SAT_CHECK((hipError_t)sat_attention_bwd_launch(a, s));
-      // dh = [dU_h | d(f_beta h) | d gates] . [U ; f_beta ; W_hh]
-      SAT_CHECK((hipError_t)dgrad(B, E, (int)HG, c.at(w.dhg_t, (long)t * HG), (long)T1 * HG, c.W(lay->hcat_w), E,
-                                  w.dh_rec, E, nullptr, 0, sp.dh, (long)B * E));
-    } else {
-      SAT_CHECK((hipError_t)dgrad(B, E, 4 * E, dgates_t, (long)T1 * HG, c.W(lay->hcat_w + (long)(E + D) * E), E,
-                                  w.dh_rec, E, nullptr, 0, sp.dh, (long)B * E));
+      SAT_CHECK((hipError_t)bwd_ggemm(c, w, sp, t, s));
+      SAT_CHECK((hipError_t)bwd_attn(c, w, sp, io, t, s));
     }
+    SAT_CHECK((hipError_t)bwd_dhgemm(c, w, sp, t, s));
   }
 
   // ---------------- weight gradients, batched over all B*(T-1) rows ----------------
@@ -532,7 +601,8 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
     SAT_CHECK((hipError_t)sat_embed_scatter_add(w.demb, w.tok, R, E, G(lay->embedding), s));
   }
   if (att) {
-    SAT_CHECK((hipError_t)sat_cast_launch(w.dWs_acc, SAT_F32, w.dWs_t, d.dtype, (long)B * L * E, s));
+    SAT_CHECK((hipError_t)sat_attention_dws_launch(w.Ws, w.uh_all, w.de_all, c.F(lay->v_w), B, L, E, T1, d.dtype,
+                                                   w.dWs_acc, w.dWs_t, s));
     SAT_CHECK((hipError_t)wgrad(E, D, B * L, w.dWs_t, E, img_features, D, G(lay->attW_w), D));
     SAT_CHECK((hipError_t)colsum(w.dWs_acc, SAT_F32, E, B * L, E, G(lay->attW_b)));
     SAT_CHECK((hipError_t)colsum(w.dv_acc, SAT_F32, E, B, E, G(lay->v_w)));
@@ -544,4 +614,57 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   SAT_CHECK((hipError_t)wgrad(2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D));
   SAT_CHECK((hipError_t)colsum(w.dpre0, SAT_F32, 2 * E, B, 2 * E, G(lay->init_b)));
   return 0;
+}
+
+// Diagnostics (bench.py roofline of the per-step decoder kernels): after a forward + backward on the
+// same arguments have filled the workspace, re-issue each per-step kernel group of step t = (T-1)/2
+// `reps` times back to back between two HIP events on `stream`, and return the average microseconds
+// per launch group in us_out[0..7]: h GEMM, attention forward, context GEMM, LSTM forward, LSTM
+// backward, d(gated context) GEMM, attention backward (2 kernels), dh GEMM.  The re-issued backward
+// groups overwrite the workspace's running dc / dv sums: call it only after the gradients are read.
+extern "C" int sat_decoder_step_bench(const SatDecoderDims* dp, const SatDecoderLayout* lay, const float* params,
+                                      const void* params_lp, const void* img_features, void* workspace,
+                                      size_t workspace_bytes, float* alphas, const float* d_alphas, int reps,
+                                      float* us_out, void* stream) {
+  SAT_CHECK((hipError_t)check_dims(dp));
+  SAT_REQUIRE(lay && params && img_features && workspace && alphas && d_alphas && us_out && reps > 0);
+  SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
+  const SatDecoderDims& d = *dp;
+  WS w;
+  SAT_REQUIRE(carve(d, nullptr, &w) <= workspace_bytes);
+  carve(d, (char*)workspace, &w);
+  hipStream_t s = (hipStream_t)stream;
+  Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D};
+  const Splits sp = splits_for(d);
+  const StepIO io{img_features, alphas, d_alphas};
+  const int t = (d.T - 1) / 2;
+  hipEvent_t e0, e1;
+  SAT_CHECK(hipEventCreate(&e0));
+  SAT_CHECK(hipEventCreate(&e1));
+  int rc = 0;
+  for (int k = 0; k < 8 && rc == 0; ++k) {
+    us_out[k] = 0.f;
+    if (!d.attention && (k == 1 || k == 2 || k == 5 || k == 6)) continue;
+    for (int r = -1; r < reps && rc == 0; ++r) {   // r = -1: warm-up launch
+      if (r == 0) rc = (int)hipEventRecord(e0, s);
+      switch (k) {
+        case 0: rc = fwd_hgemm(c, w, sp, t, s); break;
+        case 1: rc = fwd_attn(c, w, sp, io, t, s); break;
+        case 2: rc = fwd_cgemm(c, w, sp, t, s); break;
+        case 3: rc = fwd_lstm(c, w, sp, t, s); break;
+        case 4: rc = bwd_lstm(c, w, sp, t, s); break;
+        case 5: rc = bwd_ggemm(c, w, sp, t, s); break;
+        case 6: rc = bwd_attn(c, w, sp, io, t, s); break;
+        default: rc = bwd_dhgemm(c, w, sp, t, s); break;
+      }
+    }
+    if (rc == 0) rc = (int)hipEventRecord(e1, s);
+    if (rc == 0) rc = (int)hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (rc == 0) rc = (int)hipEventElapsedTime(&ms, e0, e1);
+    us_out[k] = ms * 1000.f / reps;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return rc;
 }

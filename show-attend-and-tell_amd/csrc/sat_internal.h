@@ -46,13 +46,17 @@ struct AttnBwdArgs {
   void* d_uh_t;                         // out dtype copy (same ld), nullable
   float* d_gpre; long d_gpre_ld;        // out fp32 dL/d(f_beta h + b)
   void* d_gpre_t;                       // out dtype copy, nullable
-  float* dWs_acc;                       // [B,L,E] += dL/dWs
+  float* de_out; long de_ld;            // out: this step's dL/d(score) rows, row b at de_out + b*de_ld
   float* dv_acc;                        // [B,E]  += dL/dv (per row b)
   float* dbv_acc;                       // [B]    += dL/dv.bias
   float* part;                          // scratch [B, NS, L]
   int dg_splits; long dg_split_stride;  // d_gated = sum of dg_splits partial slabs (0|1 = plain)
 };
 int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s);
+// dL/dWs[b,l,:] = sum_t de[b,t,l] v (1 - tanh^2(Ws[b,l,:] + uh[b,t,:])), summed t = T1-1 .. 0 (the
+// BPTT order), after the time loop: fp32 rows (out_f32) and a dtype copy (out_t).
+int sat_attention_dws_launch(const void* Ws, const float* uh_all, const float* de_all, const float* v_w, int B,
+                             int L, int E, int T1, int dtype, float* out_f32, void* out_t, hipStream_t s);
 
 // ---- LSTMCell pointwise (decoder.py:115, nn.LSTMCell gate order i,f,g,o) ----
 struct LstmFwdArgs {

@@ -104,6 +104,8 @@ class Decoder(nn.Module):
         self.dropout_mask = None       # test hook: uint8 keep-mask [B, T-1, E] used in training mode
         self._seed_host = None
         self._seed_dev = None
+        self._defer_phase2 = False     # see defer_recurrent_backward()
+        self._pending_bwd = None
         self.last_tokens = None        # int32 [B, T-1]: token fed at each step of the last forward
 
     # ------------------------------------------------------------------ layout
@@ -223,6 +225,28 @@ class Decoder(nn.Module):
             return self._grad_flat[o["deep_output.weight"]:end("deep_output.bias")]
         stop = o["embedding.weight"] if self.use_bert else self._grad_flat.numel()
         return self._grad_flat[o["init_h.weight"]:stop]
+
+    def defer_recurrent_backward(self, on=True):
+        """Split the backward in two: autograd's backward then runs only phase 1 (the output head,
+        whose gradient bucket is final before BPTT starts) and finish_backward() runs phase 2 (the
+        recurrent BPTT + the remaining weight gradients).  Data parallelism launches the head
+        bucket's all-reduce in between, so it overlaps BPTT -- also across two captured hipGraphs
+        (bench.py), where no Python hook can run between the phases."""
+        self._defer_phase2 = bool(on)
+
+    def finish_backward(self):
+        """Phase 2 of a backward whose recurrent part was deferred (no-op if none is pending)."""
+        if self._pending_bwd is None:
+            return
+        dims, lay, lp, feats, ws, ws_bytes, preds, alphas, d_preds, d_alphas, accumulate, masked = self._pending_bwd
+        lib = L.lib()
+        L.check(lib.sat_decoder_backward(ctypes.byref(dims), ctypes.byref(lay), L.ptr(self._flat), L.ptr(lp),
+                                         L.ptr(feats), L.ptr(ws), ws_bytes, L.ptr(preds), L.ptr(alphas),
+                                         L.ptr(d_preds), L.ptr(d_alphas), L.ptr(self._grad_flat), int(accumulate),
+                                         2 | masked, L.stream_of(preds)), "sat_decoder_backward")
+        self._pending_bwd = None
+        for hook in self._grad_hooks:
+            hook(2, self)
 
     # ----------------------------------------------------------------- forward
     def _dims(self, feats, captions):
@@ -377,7 +401,8 @@ class _DecoderFn(torch.autograd.Function):
         accumulate = dec._attach_grads()
         lib = L.lib()
         masked = 4 if getattr(d_preds, "_sat_relu_masked", False) else 0   # phase bit: d_preds already ReLU-masked
-        for phase in (1, 2):
+        phases = (1,) if dec._defer_phase2 else (1, 2)
+        for phase in phases:
             L.check(lib.sat_decoder_backward(ctypes.byref(ctx.dims), ctypes.byref(ctx.lay), L.ptr(dec._flat),
                                              L.ptr(ctx.lp), L.ptr(feats), L.ptr(ctx.ws), ctx.ws_bytes, L.ptr(preds),
                                              L.ptr(alphas), L.ptr(d_preds), L.ptr(d_alphas),
@@ -386,6 +411,9 @@ class _DecoderFn(torch.autograd.Function):
                     "sat_decoder_backward")
             for hook in dec._grad_hooks:
                 hook(phase, dec)
+        if dec._defer_phase2:   # phase 2 runs in dec.finish_backward()
+            dec._pending_bwd = (ctx.dims, ctx.lay, ctx.lp, feats, ctx.ws, ctx.ws_bytes, preds, alphas, d_preds,
+                                d_alphas, accumulate, masked)
         ctx.ws = None
         n_params = len(ctx.needs_input_grad) - 3
         return (None, None, None) + (None,) * n_params

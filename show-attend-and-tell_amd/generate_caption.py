@@ -11,6 +11,10 @@ Same flags as the reference (generate_caption.py:153-160) plus:
   --bert-vocab    a local bert-base-uncased vocab.txt (offline BertTokenizer); without it BERT
                   ids print as the [CLS]/[SEP]/[PAD]/tokN stub
   --plot          write the attention visualisation (:111-150) to this PNG (matplotlib)
+  --encoder-weights  the trunk's state_dict (weights_only); default: the encoder_weights entry
+                  train.py wrote into model_config.json.  The reference relies on torchvision's
+                  pretrained weights being the same everywhere; this build has none offline, so the
+                  trunk must be the one the decoder was trained on
 W&B restore (--wandb-run/--wandb-model) needs network access and is not supported here.
 """
 import argparse
@@ -38,8 +42,10 @@ def load_image(path):
     return torch.from_numpy(x.transpose(2, 0, 1).copy()).unsqueeze(0)
 
 
-def load_model(model_path, model_config_path=None, dtype=torch.float32, device="cuda", bert_vocab=None):
-    """generate_caption.py:24-75: config -> Encoder/Decoder, checkpoint loaded (strict, then lax)."""
+def load_model(model_path, model_config_path=None, dtype=torch.float32, device="cuda", bert_vocab=None,
+               encoder_weights=None):
+    """generate_caption.py:24-75: config -> Encoder/Decoder, checkpoint loaded (strict, then lax); the
+    encoder trunk from ``encoder_weights`` or the config's ``encoder_weights`` entry (train.py)."""
     if model_path is None:
         raise ValueError("Model path must be provided (W&B restore is not available offline)")
     model_config_path = model_config_path or os.path.join(os.path.dirname(model_path) or ".", "model_config.json")
@@ -57,6 +63,15 @@ def load_model(model_path, model_config_path=None, dtype=torch.float32, device="
         word_dict = json.load(open(os.path.join(cfg["data"], "word_dict.json")))
         vocab = len(word_dict)
     encoder = sat_amd.Encoder(cfg["network"], dtype=dtype)
+    enc_w = encoder_weights or cfg.get("encoder_weights")
+    if enc_w and not os.path.isabs(enc_w) and not os.path.exists(enc_w):
+        enc_w = os.path.join(os.path.dirname(model_config_path) or ".", os.path.basename(enc_w))
+    if enc_w:
+        encoder.load_state_dict(torch.load(enc_w, map_location="cpu", weights_only=True))
+    else:
+        print("WARNING: no encoder weights (neither --encoder-weights nor model_config.json's encoder_weights): "
+              "the trunk is randomly initialised and its features do not match the ones the decoder was trained "
+              "on", file=sys.stderr, flush=True)
     decoder = sat_amd.Decoder(vocab, encoder.dim, ado=cfg["ado"], bert=cfg["bert"], attention=cfg["attention"],
                               bert_embedding_weight=sd.get("embedding.weight") if cfg["bert"] else None,
                               tokenizer=tokenizer)
@@ -138,11 +153,13 @@ def main(argv=None):
     p.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
     p.add_argument("--bert-vocab", type=str, default=None)
     p.add_argument("--plot", type=str, default=None)
+    p.add_argument("--encoder-weights", type=str, default=None)
     args = p.parse_args(argv)
     if args.wandb_run or args.wandb_model:
         p.error("W&B restore needs network access; pass --model/--model-config")
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    encoder, decoder, cfg, word_dict = load_model(args.model, args.model_config, dt, bert_vocab=args.bert_vocab)
+    encoder, decoder, cfg, word_dict = load_model(args.model, args.model_config, dt, bert_vocab=args.bert_vocab,
+                                                  encoder_weights=args.encoder_weights)
     sentence, alpha = caption_image(load_image(args.img_path), encoder, decoder, args.beam_size)
     tokens = sentence_tokens(sentence, decoder, word_dict)
     print(json.dumps({"caption": " ".join(tokens), "ids": sentence, "score": decoder.last_caption_score}))

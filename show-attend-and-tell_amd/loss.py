@@ -87,3 +87,32 @@ class StepMetrics:
         acc5 = c5 * 100.0 / nonpad if nonpad > 0 else 0
         return dict(loss=float(self.loss.detach().cpu()), ce=ce, att_reg=reg, acc1=acc1, acc5=acc5,
                     caption_length=int(cap_len))
+
+
+class RunningMeters:
+    """The reference's three AverageMeters (utils.py:4-19; train.py:179-181: loss, top-1, top-5, each
+    weighted by the step's caption length) accumulated ON THE DEVICE every step: update() issues
+    four tiny elementwise ops and never synchronises; read() is the one host copy per log line."""
+
+    def __init__(self, device):
+        self.acc = torch.zeros(4, device=device, dtype=torch.float64)   # sum loss*n, acc1*n, acc5*n, n
+        self.last = None
+
+    def update(self, loss, metrics):
+        # metrics = [CE, att_reg, n_top1, n_top5, n_nonpad, caption_length] (float32 device tensor)
+        m = metrics.detach().double()
+        n = m[5]
+        nonpad = m[4].clamp_min(1.0)
+        has = (m[4] > 0).double()
+        step = torch.stack([loss.detach().double() * n, m[2] * 100.0 / nonpad * has * n,
+                            m[3] * 100.0 / nonpad * has * n, n])
+        self.acc += step
+        self.last = (loss, metrics)
+
+    def read(self):
+        """dict(loss, top1, top5 running averages, loss_val = the last step's loss, count)."""
+        s = self.acc.cpu().tolist()
+        n = s[3]
+        out = dict(loss=s[0] / n if n else 0.0, top1=s[1] / n if n else 0.0, top5=s[2] / n if n else 0.0, count=n)
+        out["loss_val"] = float(self.last[0].detach().cpu()) if self.last is not None else 0.0
+        return out

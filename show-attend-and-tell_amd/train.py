@@ -11,6 +11,12 @@ so it cannot be disabled, as in train.py:450), plus:
   --max-steps     cap batches per epoch (smoke runs)
   --no-overlap    encode each batch just before its decoder step (default: the frozen encoder of
                   batch i+1 runs on a side stream beside batch i's decoder step)
+  --encoder-weights  torchvision-layout state_dict of the trunk (weights_only load); without it the
+                  trunk is randomly initialised under --seed (no pretrained weights offline).  Either
+                  way the trunk actually used is saved as <out>/encoder_<network>.pth and recorded in
+                  model_config.json, so generate_caption.py runs the same encoder
+  --bert-embeddings  a local [30522, 768] bert-base-uncased word-embedding table (a tensor, or a
+                  state_dict holding embeddings.word_embeddings.weight / embedding.weight)
 Multi-GPU: ``python -m torch.distributed.run --nproc-per-node N show-attend-and-tell_amd/train.py ...``
 (RCCL data parallel; the batch size is per GPU).  W&B logging is not part of this build; the
 reference's scalar names are printed / written as JSON lines instead.
@@ -129,7 +135,28 @@ def parse(argv=None):
     p.add_argument("--out", type=str, default="model")
     p.add_argument("--no-overlap", action="store_true",
                    help="encode each batch right before its decoder step instead of one batch ahead on a side stream")
+    p.add_argument("--encoder-weights", type=str, default=None,
+                   help="torchvision-layout encoder state_dict (weights_only); default: random init under --seed")
+    p.add_argument("--bert-embeddings", type=str, default=None,
+                   help="local bert-base-uncased word-embedding table [30522, 768] (weights_only)")
     return p.parse_args(argv)
+
+
+def load_bert_embeddings(path):
+    """The frozen BERT word-embedding table the reference takes from BertModel.from_pretrained
+    (decoder.py:21-36), from a local file: a tensor or a state_dict holding it."""
+    obj = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(obj, dict):
+        for k in ("embeddings.word_embeddings.weight", "bert.embeddings.word_embeddings.weight",
+                  "word_embeddings.weight", "embedding.weight", "weight"):
+            if k in obj:
+                obj = obj[k]
+                break
+        else:
+            raise ValueError(f"{path}: no word-embedding table among keys {sorted(obj)[:8]}")
+    if obj.dim() != 2 or obj.shape[1] != sat_amd.Decoder.BERT_HIDDEN:
+        raise ValueError(f"{path}: expected a [V, 768] table, got {tuple(obj.shape)}")
+    return obj.float()
 
 
 def build(args, device):
@@ -145,22 +172,58 @@ def build(args, device):
         word_dict = json.load(open(os.path.join(args.data, "word_dict.json")))
         vocab = len(word_dict)
     encoder = sat_amd.Encoder(args.network, dtype=dt)
-    decoder = sat_amd.Decoder(vocab, encoder.dim, tf=args.tf, ado=args.ado, bert=args.bert, attention=args.attention)
+    if args.encoder_weights:
+        encoder.load_state_dict(torch.load(args.encoder_weights, map_location="cpu", weights_only=True))
+    bert_w = None
+    if args.bert:
+        if args.bert_embeddings:
+            bert_w = load_bert_embeddings(args.bert_embeddings)
+            vocab = bert_w.shape[0]
+        elif not args.model:
+            print("WARNING: --bert without --bert-embeddings or --model: the frozen word-embedding table is "
+                  "randomly initialised, not bert-base-uncased's (decoder.py:21-36); this is not the reference's "
+                  "BERT configuration", file=sys.stderr, flush=True)
+    decoder = sat_amd.Decoder(vocab, encoder.dim, tf=args.tf, ado=args.ado, bert=args.bert, attention=args.attention,
+                              bert_embedding_weight=bert_w)
     if args.model:   # train.py:65-67 (reference checkpoints load unchanged)
         decoder.load_state_dict(torch.load(args.model, map_location="cpu", weights_only=True))
     return encoder.to(device).eval(), decoder.to(device), word_dict, dt
+
+
+SPLIT_SEED = {"train": 0, "val": 1, "test": 2}   # fixed per-split offsets (str hash() is randomised per process)
+
+
+class ShardSampler(torch.utils.data.Sampler):
+    """Rank r's items r, r+N, r+2N, ... of an evaluation split: every item exactly once across ranks
+    (DistributedSampler pads with repeats), so gathered BLEU / meters cover the whole split."""
+
+    def __init__(self, n, rank, world):
+        self.idx = list(range(rank, n, world))
+
+    def __iter__(self):
+        return iter(self.idx)
+
+    def __len__(self):
+        return len(self.idx)
 
 
 def loaders(args, split, rank, world):
     if args.synthetic:
         ds = SyntheticDataset(args.synthetic if split == "train" else max(args.batch_size, args.synthetic // 8),
                               args.vocab if not args.bert else sat_amd.Decoder.BERT_VOCAB,
-                              32 if args.bert else args.seq, args.bert, seed=args.seed + hash(split) % 1000)
+                              32 if args.bert else args.seq, args.bert, seed=args.seed * 10 + SPLIT_SEED[split])
     else:
         ds = JsonCaptionDataset(args.data, split, args.fraction, args.bert)
-    sampler = torch.utils.data.distributed.DistributedSampler(ds, world, rank, shuffle=True) if world > 1 else None
-    return torch.utils.data.DataLoader(ds, batch_size=args.batch_size, shuffle=sampler is None, sampler=sampler,
-                                       num_workers=4 if not args.synthetic else 0, pin_memory=True, drop_last=True)
+    train = split == "train"
+    if world > 1:
+        sampler = torch.utils.data.distributed.DistributedSampler(ds, world, rank, shuffle=True, seed=args.seed) \
+            if train else ShardSampler(len(ds), rank, world)
+    else:
+        sampler = None
+    # train.py:76-88: the reference shuffles train only and keeps every validation / test batch
+    return torch.utils.data.DataLoader(ds, batch_size=args.batch_size, shuffle=train and sampler is None,
+                                       sampler=sampler, num_workers=4 if not args.synthetic else 0, pin_memory=True,
+                                       drop_last=train)
 
 
 def encoded_batches(loader, encoder, device, dt, max_steps, overlap):
@@ -198,28 +261,29 @@ def encoded_batches(loader, encoder, device, dt, max_steps, overlap):
         yield pending
 
 
-def train_epoch(epoch, encoder, decoder, opt, loader, args, device, dt, world, log):
-    """train.py:119-192"""
+def train_epoch(epoch, encoder, decoder, opt, loader, args, device, dt, world, log, grad_ar=None):
+    """train.py:119-192.  ``grad_ar``: a sat_amd.distributed.GradAllReduce for DP (N > 1)."""
     encoder.eval()
     decoder.train()
     pad, skip = sat_amd.special_ids(args.bert)
-    losses, top1, top5 = AverageMeter(), AverageMeter(), AverageMeter()
+    # the reference updates its meters every batch (train.py:179-181) with 4 host syncs per step; here
+    # they accumulate on the device and are read once per log line
+    meters = sat_amd.RunningMeters(device)
     for batch_idx, feats, captions in encoded_batches(loader, encoder, device, dt, args.max_steps,
                                                       not args.no_overlap):
         opt.zero_grad()
         preds, alphas = decoder(feats, captions)
         loss, metrics = sat_amd.caption_loss(preds, alphas, captions, args.alpha_c, pad, skip)
-        loss.backward()
-        if world > 1:
-            sat_dist.allreduce_grads(decoder)
+        loss.backward()   # with DP the head bucket's all-reduce starts inside it, beside BPTT
+        if grad_ar is not None:
+            grad_ar.wait()
         opt.step()
-        if batch_idx % args.log_interval == 0:   # one host read per logged step (reference: 4 per step)
-            m = sat_amd.StepMetrics(loss, metrics).values()
-            n = m["caption_length"]
-            losses.update(m["loss"], n); top1.update(m["acc1"], n); top5.update(m["acc5"], n)
-            log(dict(epoch=epoch, batch=batch_idx, train_loss=losses.avg, train_top1_acc=top1.avg,
-                     train_top5_acc=top5.avg, train_loss_raw=losses.val))
-    return losses.avg
+        meters.update(loss, metrics)
+        if batch_idx % args.log_interval == 0:   # train.py:183-192
+            m = meters.read()
+            log(dict(epoch=epoch, batch=batch_idx, train_loss=m["loss"], train_top1_acc=m["top1"],
+                     train_top5_acc=m["top5"], train_loss_raw=m["loss_val"], train_tokens=m["count"]))
+    return meters.read()["loss"] if meters.last is not None else 0.0
 
 
 def evaluate(epoch, encoder, decoder, loader, args, device, dt, word_dict, mode, log):
@@ -250,8 +314,19 @@ def evaluate(epoch, encoder, decoder, loader, args, device, dt, word_dict, mode,
                 dec = lambda c: [str(t) for t in c if t not in (0, 3)][:c.index(1) if 1 in c else None]  # noqa: E731
             refs += [[dec(c) for c in cs] for cs in all_caps.tolist()]
             hyps += [dec(c) for c in ids]
+    sums = [losses.sum, top1.sum, top5.sum, losses.count]
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        # every rank evaluated a disjoint shard (ShardSampler): gather hypotheses, references and the
+        # meters' sums so the logged BLEU-1..4 and averages cover the whole split
+        parts = [None] * dist.get_world_size()
+        dist.all_gather_object(parts, (refs, hyps, sums))
+        refs = [r for p in parts for r in p[0]]
+        hyps = [h for p in parts for h in p[1]]
+        sums = [sum(p[2][i] for p in parts) for i in range(4)]
+    n = sums[3]
+    avg = [v / n if n else 0.0 for v in sums[:3]]
     b1, b2, b3, b4 = bleu_mod.bleu_1_to_4(refs, hyps)
-    log({"epoch": epoch, f"{mode}_loss": losses.avg, f"{mode}_top1_acc": top1.avg, f"{mode}_top5_acc": top5.avg,
+    log({"epoch": epoch, f"{mode}_loss": avg[0], f"{mode}_top1_acc": avg[1], f"{mode}_top5_acc": avg[2],
          f"{mode}_bleu1": b1, f"{mode}_bleu2": b2, f"{mode}_bleu3": b3, f"{mode}_bleu4": b4})
     return b4
 
@@ -275,18 +350,25 @@ def main(argv=None):
     if not args.no_overlap:   # the decoder shares the chip with the next batch's encoder
         sat_amd.ops.set_decoder_split_target(64)
     opt = sat_amd.Adam(decoder.parameters(), lr=args.lr)
+    grad_ar = sat_dist.GradAllReduce(decoder) if world > 1 else None
     sched = torch.optim.lr_scheduler.StepLR(opt, args.step_size)
     train_loader = loaders(args, "train", rank, world)
     val_loader = loaders(args, "val", rank, world)
     os.makedirs(args.out, exist_ok=True)
+    enc_path = os.path.join(args.out, f"encoder_{args.network}.pth")
+    if rank == 0:   # the trunk this run uses, so generate_caption.py encodes with the same weights
+        torch.save({k: v.detach().cpu() for k, v in encoder.state_dict().items()}, enc_path)
     for epoch in range(1, args.epochs + 1):
         t0 = time.time()
-        train_epoch(epoch, encoder, decoder, opt, train_loader, args, device, dt, world, log)
+        if isinstance(getattr(train_loader, "sampler", None), torch.utils.data.distributed.DistributedSampler):
+            train_loader.sampler.set_epoch(epoch)
+        train_epoch(epoch, encoder, decoder, opt, train_loader, args, device, dt, world, log, grad_ar)
         evaluate(epoch, encoder, decoder, val_loader, args, device, dt, word_dict, "val", log)
         sched.step()
         if rank == 0:   # train.py:103-110
             torch.save(decoder.state_dict(), os.path.join(args.out, f"model_{args.network}_{epoch}.pth"))
             cfg = dict(vars(args))
+            cfg["encoder_weights"] = os.path.abspath(enc_path)
             if args.synthetic and word_dict:   # generate_caption.py reads <data>/word_dict.json
                 cfg["data"] = args.out
                 with open(os.path.join(args.out, "word_dict.json"), "w") as f:

@@ -47,3 +47,28 @@ def test_bert_synthetic_captions_layout():
     assert (caps[:, 0] == 101).all() and (caps[:, -1] == 102).all()
     body = caps[:, 1:-1]
     assert ((body == 0) | ((body >= 1000) & (body < 30522))).all()
+
+
+@pytest.mark.parametrize("args,gflop", [((49, 2048, 512, 10000, 27, True), 2.53),    # ResNet152 / V10k, ado
+                                        ((196, 512, 512, 2600, 27, True), 1.20),     # VGG19 / Flickr8k
+                                        ((196, 512, 768, 30522, 27, False), 5.30)])  # BERT, simple head
+def test_decoder_flops_match_survey(args, gflop):
+    """decoder fwd+bwd GFLOP/img with W.a hoisted (the whole-step roofline's decoder part)."""
+    from sat_amd.diagnostics import decoder_flops
+    assert abs(decoder_flops(*args[:5], ado=args[5]) / 1e9 - gflop) < 0.01
+
+
+def test_step_group_bytes_bench_shape():
+    """Per-step algorithmic bytes of the fused attention step at the bench shape (the
+    attention forward streams Ws and the annotation vectors once: ~38 MB at B=128, L=49, D=2048, bf16)."""
+    from sat_amd.diagnostics import step_group_bytes, GROUPS
+    by = step_group_bytes(128, 49, 2048, 512, 27, 2)
+    assert set(by) == set(GROUPS)
+    assert 35e6 < by["attn_fwd"] < 40e6
+    assert all(v > 0 for v in by.values())
+    assert step_group_bytes(128, 49, 2048, 512, 27, 2, attention=False)["attn_fwd"] == 0
+
+
+def test_bench_defaults_time_enough_steps(monkeypatch):
+    a = _parse(monkeypatch)
+    assert a.steps >= 200 and a.fp32_steps > 0

@@ -71,3 +71,90 @@ def test_gloo_world_size_2():
         results = mgr.dict()
         mp.spawn(_worker, args=(world, init_file, results), nprocs=world, join=True)
         assert dict(results) == {0: (True, True, True), 1: (True, True, True)}
+
+
+# ---------------------------------------------------------------------------- real bucket slicing
+COMBOS = [dict(ado=a, attention=t, bert=b) for a in (True, False) for t in (True, False) for b in (False, True)]
+
+
+def _dec(c, V=30, D=16):
+    import sat_amd
+    torch.manual_seed(0)
+    if c["bert"]:
+        return sat_amd.Decoder(V, D, ado=c["ado"], attention=c["attention"], bert=True,
+                               bert_embedding_weight=torch.randn(V, 768))
+    return sat_amd.Decoder(V, D, ado=c["ado"], attention=c["attention"])
+
+
+@pytest.mark.parametrize("c", COMBOS, ids=[f"ado{int(c['ado'])}-att{int(c['attention'])}-bert{int(c['bert'])}"
+                                            for c in COMBOS])
+def test_grad_buckets_cover_active_params(c):
+    """Decoder.grad_bucket(1) (output head) and (2) (the rest) are disjoint slices of the flat
+    gradient buffer; every active parameter lies in exactly one; the frozen BERT
+    table lies in none; inactive params inside bucket 2 only ever carry zero gradients."""
+    dec = _dec(c)
+    dec._build_flat(torch.device("cpu"))
+    base = dec._grad_flat.data_ptr()
+    spans = []
+    for ph in (1, 2):
+        b = dec.grad_bucket(ph)
+        o = (b.data_ptr() - base) // 4
+        spans.append((o, o + b.numel()))
+    assert spans[0][1] <= spans[1][0] or spans[1][1] <= spans[0][0]
+    params = dict(dec.named_parameters())
+    active = set(dec.active_param_names())
+    for n, p in params.items():
+        lo, hi = dec._offsets[n], dec._offsets[n] + p.numel()
+        inside = [lo >= s and hi <= e for s, e in spans]
+        overlap = [lo < e and hi > s for s, e in spans]
+        if n in active:
+            assert sum(inside) == 1, (n, spans, lo, hi)
+        elif n == "embedding.weight" and c["bert"]:
+            assert not any(overlap), n
+        else:   # all-reducing zeros is a no-op
+            assert n.startswith(("attention.", "f_beta.", "deep_output.")), n
+
+
+def _bucket_worker(rank, world, init_file, results):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    import sat_amd.distributed as D
+    torch.set_num_threads(1)
+    ok = True
+    for c in COMBOS:
+        dec = _dec(c)
+        dec._build_flat(torch.device("cpu"))
+        g = dec._grad_flat
+        g.copy_(torch.arange(g.numel(), dtype=torch.float32) * (rank + 1))
+        r = D.GradAllReduce(dec)
+        for phase in (1, 2):        # what _DecoderFn.backward / finish_backward fire
+            for hook in dec._grad_hooks:
+                hook(phase, dec)
+        r.wait()
+        mean = torch.arange(g.numel(), dtype=torch.float32) * 1.5
+        covered = torch.zeros(g.numel(), dtype=torch.bool)
+        for ph in (1, 2):
+            b = dec.grad_bucket(ph)
+            o = (b.data_ptr() - g.data_ptr()) // 4
+            covered[o:o + b.numel()] = True
+        own = torch.arange(g.numel(), dtype=torch.float32) * (rank + 1)
+        ok &= torch.allclose(g[covered], mean[covered]) and torch.equal(g[~covered], own[~covered])
+        # the hipGraph path's helper (bench.py) on the same slices
+        g.copy_(own)
+        hs = [D.allreduce_bucket_async(dec, ph) for ph in (1, 2)]
+        for h in hs:
+            h.wait()
+        ok &= torch.allclose(g[covered], mean[covered])
+    results[rank] = ok
+    dist.destroy_process_group()
+
+
+def test_gloo_real_bucket_slicing():
+    """GradAllReduce / allreduce_bucket_async over the REAL Decoder bucket slicing (all ado x
+    attention x bert layouts), world size 2: bucket elements become the rank mean, the rest stays."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        init_file = os.path.join(d, "init")
+        mgr = mp.Manager()
+        results = mgr.dict()
+        mp.spawn(_bucket_worker, args=(world, init_file, results), nprocs=world, join=True)
+        assert dict(results) == {0: True, 1: True}
