@@ -1,0 +1,303 @@
+// Weight-stationary streaming kernel for short-K 1x1 convolutions (gfx950 / MI355X).
+//
+//   C[M,N] = act(A[M,K] . B[N,K]^T + bias[N] (+ res[M,N]))       bf16 in/out, fp32 accumulate
+//   A row m = the NHWC input pixel of output pixel m (stride 1: row m; stride s: (n, oh*s, ow*s)),
+//   K = Cin in {64, 128, 256, 512}, B = conv weights [Cout][Cin].
+//
+// These are the ResNet152 bottleneck c3 (+ identity / projection residual) and downsample convs
+// and the K <= 512 c1 convs: 2-13 GFLOP each against 60-460 MB of activations, so they are
+// bound by HBM (output + residual + input bytes), not by MFMA.  The 128-row tile kernel
+// (convgemm.hip) pays, per 128 x 128 tile, a full A + B staging round trip, a K-loop of 1-8
+// k-tiles, and an epilogue that nothing overlaps; at K = 256 that ran at 2.9 TB/s (L3 c3).
+// Here instead:
+//   * one persistent workgroup per CU (8 waves) owns a 128-column slice of N; each wave holds its
+//     16 columns of B for ALL of K in registers (loaded once: K/32 x 16 B per lane), so the only
+//     operand streamed per item is an MT x K tile of A (LDS-DMA, double-buffered);
+//   * the workgroup walks M-tiles (items) of its slice; the 8 slices of one M-tile sequence are
+//     placed on one XCD (blocks b, b+8, ... share an L2), so each A tile is fetched from HBM once
+//     and re-served from L2 to the other slices;
+//   * C^T = B . A^T on v_mfma_f32_16x16x32_bf16 (B fragments as the first operand): a lane then
+//     holds 4 consecutive output COLUMNS of one row, so the epilogue (bias, fp32 residual add,
+//     activation, one bf16 rounding -- the same arithmetic as the other conv kernels) needs no
+//     LDS transpose: 8-byte residual loads and 8-byte stores, 32 contiguous bytes per row per wave;
+//   * pipeline per item: barrier -> LDS-DMA of the next item's A tile and residual tile into the
+//     other stage -> fragment reads + MFMAs -> epilogue (residual from LDS) -> 8-B stores, with a
+//     counted vmcnt (never 0 in the loop) so stores stay in flight across the next barrier; every
+//     global read in the loop is a DMA, so the compiler inserts no vmcnt waits of its own;
+//   * LDS image lane-linear (DMA), swizzle on the source: 16-B chunk c of row r at slot
+//     c ^ (r & 15) (rows >= 256 B) or c ^ ((r >> 1) & 7) (128-B rows) -> conflict-free
+//     ds_read_b128 fragment reads (verified for every lane group).
+#include "sat_common.h"
+#include "sat_internal.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void s_lds_void;
+
+constexpr int S_NW = 8, S_BN = 16 * S_NW;    // 8 waves x 16 columns
+constexpr unsigned S_OOB = 0x80000000u;
+
+struct SArgs {
+  int M, N, K;
+  const bf16* A; const bf16* B; bf16* C;
+  const float* bias;
+  const bf16* res;
+  int H, W, Cin, stride, OH, OW;     // input geometry (1x1 conv, pad 0)
+  int slices, per_slice, items;      // N / 128, workgroups per slice, M-tiles
+  int xcd_group;                     // 1: slice = (b / 8) % slices (one M-tile sequence per XCD)
+  unsigned a_bytes;
+};
+
+template <int N>
+__device__ __forceinline__ void s_wait_barrier() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 32) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+
+// KT = K / 32 k-steps, MB = 16-row m-blocks per item (MT = 16 * MB rows)
+template <int KT, int MB, bool RES, int ACT, bool STRIDED>
+__global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
+  constexpr int K = KT * 32, MT = MB * 16, ROWB = K * 2;
+  constexpr int TILE = MT * ROWB;                  // A tile bytes
+  constexpr int RTILE = RES ? MT * S_BN * 2 : 0;   // residual tile bytes (128 bf16 columns per row)
+  constexpr int STG = TILE + RTILE;                // one LDS stage
+  static_assert(2 * STG <= 160 * 1024, "two stages must fit in LDS");
+  constexpr int DMA_A = TILE / (S_NW * 64 * 16);   // 16-B DMAs per lane per item
+  constexpr int DMA_R = RTILE / (S_NW * 64 * 16);
+  static_assert(DMA_A * S_NW * 64 * 16 == TILE && DMA_R * S_NW * 64 * 16 == RTILE, "whole 8 KiB rounds");
+  constexpr int ST = MB;                           // 8-B stores per lane per item
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.x;
+  int slice, grp;
+  if (a.xcd_group) {
+    slice = (b / 8) % a.slices;
+    grp = (b % 8) + 8 * (b / (8 * a.slices));
+  } else {
+    slice = b % a.slices;
+    grp = b / a.slices;
+  }
+  const int ns = slice * S_BN;            // the workgroup's 128 columns
+  const int n0 = ns + w * 16;             // this wave's 16 columns
+  const int fr = lane & 15, fh = lane >> 4;
+
+  // B fragments for all of K (registers for the whole kernel): lane (fh, fr) holds B[n0 + fr][32 ks + 8 fh ..]
+  bf16x8 bq[KT];
+  {
+    const bf16* bp = a.B + (long)(n0 + fr) * K + 8 * fh;
+#pragma unroll
+    for (int ks = 0; ks < KT; ++ks) bq[ks] = *(const bf16x8*)(bp + 32 * ks);
+  }
+  float bias4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bias4[j] = a.bias ? a.bias[n0 + 4 * fh + j] : 0.f;
+
+  const unsigned c_bytes = (unsigned)((long)a.M * a.N * 2);
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, (int)a.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc((void*)a.C, (short)0, (int)c_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rR =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(RES ? a.res : a.C), (short)0, (int)c_bytes, 0x00020000);
+
+  // Every global read of the loop is an LDS-DMA (A tile and residual tile of the next item), so the
+  // only vmcnt waits are the counted ones below; rows >= M read zeros through out-of-range buffer
+  // offsets and their stores are dropped the same way, so every lane issues every instruction.
+  auto stage = [&](int it, int buf) {
+    const int m0 = it * MT;
+    char* st = smem + buf * STG;
+#pragma unroll
+    for (int d = 0; d < DMA_A; ++d) {
+      const int byte = (d * S_NW + w) * 1024 + lane * 16;   // LDS offset of this lane's 16 B
+      const int r = byte / ROWB, pc = (byte % ROWB) / 16;
+      int c;
+      if constexpr (ROWB >= 256) c = (pc & ~15) | ((pc & 15) ^ (r & 15));
+      else c = pc ^ ((r >> 1) & 7);
+      const int m = m0 + r;
+      unsigned off = S_OOB;
+      if (m < a.M) {
+        long pix = m;
+        if constexpr (STRIDED) {
+          const int ohw = a.OH * a.OW;
+          const int n = m / ohw, rem = m - n * ohw;
+          const int oh = rem / a.OW, ow = rem - oh * a.OW;
+          pix = ((long)n * a.H + oh * a.stride) * a.W + ow * a.stride;
+        }
+        off = (unsigned)((pix * K + 8 * c) * 2);
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (s_lds_void*)(st + (d * S_NW + w) * 1024), 16, (int)off, 0, 0, 0);
+    }
+    if constexpr (RES) {   // residual rows of 256 B (this slice's 128 columns), chunk c at slot c ^ (r & 15)
+#pragma unroll
+      for (int d = 0; d < DMA_R; ++d) {
+        const int byte = (d * S_NW + w) * 1024 + lane * 16;
+        const int r = byte / 256, c = ((byte % 256) / 16) ^ (r & 15);
+        const int m = m0 + r;
+        const unsigned off = m < a.M ? (unsigned)(((long)m * a.N + ns + 8 * c) * 2) : S_OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rR, (s_lds_void*)(st + TILE + (d * S_NW + w) * 1024), 16, (int)off,
+                                                 0, 0, 0);
+      }
+    }
+  };
+
+  // A fragment: row mb*16 + fr, logical chunk 4 ks + fh
+  auto afrag = [&](const char* base, int mb, int ks) {
+    const int r = mb * 16 + fr, c = ks * 4 + fh;
+    int pc;
+    if constexpr (ROWB >= 256) pc = (c & ~15) | ((c & 15) ^ (r & 15));
+    else pc = c ^ ((r >> 1) & 7);
+    return *(const bf16x8*)(base + r * ROWB + 16 * pc);
+  };
+  typedef unsigned __attribute__((ext_vector_type(2))) u32x2;
+
+  int it = grp;
+  if (it >= a.items) return;   // workgroup-uniform: no barrier is reached by part of a group
+  stage(it, 0);
+  int buf = 0;
+  bool first = true;
+  while (true) {
+    const int nxt = it + a.per_slice;
+    // this wave's DMAs of item `it` landed (only the previous item's stores are younger); after the
+    // barrier every wave's have, and every wave finished reading the other stage
+    if (first) s_wait_barrier<0>();
+    else s_wait_barrier<ST>();
+    first = false;
+    if (nxt < a.items) stage(nxt, buf ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const char* base = smem + buf * STG;
+    f32x4 acc[MB];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 af[2][MB];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) af[0][mb] = afrag(base, mb, 0);
+#pragma unroll
+    for (int ks = 0; ks < KT; ++ks) {
+      if (ks + 1 < KT) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) af[(ks + 1) & 1][mb] = afrag(base, mb, ks + 1);
+      }
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+        acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks], af[ks & 1][mb], acc[mb], 0, 0, 0);
+    }
+    // epilogue: lane holds C[m0 + mb*16 + fr][n0 + 4 fh + j], j = 0..3
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int r = mb * 16 + fr, m = it * MT + r;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = acc[mb][j] + bias4[j];
+      if constexpr (RES) {
+        const int c = (w * 2 + (fh >> 1)) ^ (r & 15);   // 16-B chunk of this lane's 8 B
+        const u32x2 rv = *(const u32x2*)(base + TILE + r * 256 + 16 * c + 8 * (fh & 1));
+        const bf16* h = (const bf16*)&rv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] += (float)h[j];
+      }
+      u32x2 o;
+      bf16* ob = (bf16*)&o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ob[j] = (bf16)apply_act(v[j], ACT);
+      const unsigned off = m < a.M ? (unsigned)(((long)m * a.N + n0 + 4 * fh) * 2) : S_OOB;
+      __builtin_amdgcn_raw_buffer_store_b64(o, rC, (int)off, 0, 0);
+    }
+    if (nxt >= a.items) break;
+    it = nxt;
+    buf ^= 1;
+  }
+}
+
+int g_stream_mode = 1;   // 0 off, 1 auto, 2 every eligible problem (A/B)
+int g_stream_cus = 0;    // CU count (queried once)
+
+template <int KT, int MB, bool RES, bool STRIDED>
+void launch_s(int act, dim3 grid, hipStream_t s, const SArgs& a) {
+  if (act == SAT_ACT_RELU)
+    hipLaunchKernelGGL((conv1x1_stream_kernel<KT, MB, RES, SAT_ACT_RELU, STRIDED>), grid, dim3(S_NW * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv1x1_stream_kernel<KT, MB, RES, SAT_ACT_NONE, STRIDED>), grid, dim3(S_NW * 64), 0, s, a);
+}
+template <int KT, int MB>
+void launch_kt(bool res, bool strided, int act, dim3 grid, hipStream_t s, const SArgs& a) {
+  if (res) {
+    if (strided) launch_s<KT, MB, true, true>(act, grid, s, a);
+    else launch_s<KT, MB, true, false>(act, grid, s, a);
+  } else {
+    if (strided) launch_s<KT, MB, false, true>(act, grid, s, a);
+    else launch_s<KT, MB, false, false>(act, grid, s, a);
+  }
+}
+
+inline bool sal16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+// Returns 1 if the 1x1 conv was launched by the streaming kernel (error code in *err), 0 otherwise.
+int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err) {
+  *err = 0;
+  if (g_stream_mode == 0) return 0;
+  const SatConvGeom& cv = g.conv;
+  if (cv.C <= 0 || cv.KH != 1 || cv.KW != 1 || cv.pad != 0) return 0;
+  if (g.dtype != SAT_BF16 || g.c_dtype != SAT_BF16 || g.batch != 1 || g.aux || g.transB) return 0;
+  if (g.beta != 0.f || g.alpha != 1.f || g.partial_splits > 1) return 0;
+  if (g.act != SAT_ACT_NONE && g.act != SAT_ACT_RELU) return 0;
+  const int K = g.K;
+  if (!(K == 64 || K == 128 || K == 256 || K == 512) || g.ldb != K) return 0;
+  if (g.N % S_BN || g.ldc != g.N) return 0;
+  if (g.add1 && (g.add1_dtype != SAT_BF16 || g.ld_add1 != g.N || !sal16(g.add1))) return 0;
+  if (!sal16(g.A) || !sal16(g.B) || !sal16(g.C) || (g.bias && ((uintptr_t)g.bias & 15))) return 0;
+  const long a_bytes = 2L * cv.N * cv.H * cv.W * cv.C;
+  if (a_bytes >= (1L << 31) || (long)g.M * g.N >= (1L << 31)) return 0;
+  const bool strided = cv.stride != 1 || cv.OH != cv.H || cv.OW != cv.W;
+  if (g_stream_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      return 0;
+    g_stream_cus = n;
+  }
+  // rows per item: MT = 64 (K <= 256: A tiles of 8 / 16 / 32 KiB) or 32 (K = 512: 32 KiB)
+  const int MB = K == 512 ? 2 : 4;
+  const int MT = MB * 16;
+  const int slices = g.N / S_BN;
+  const int items = sat_cdiv(g.M, MT);
+  if (g_stream_mode == 1) {
+    // HBM-bound shapes only: enough items per workgroup to pipeline (>= ~3)
+    if ((long)items * slices < 2L * g_stream_cus) return 0;
+  }
+  // K <= 128: two workgroups per CU fit (<= 64 KiB of LDS and <= 128 VGPRs each) and hide each
+  // other's barrier / epilogue latency; K = 256 / 512 kernels need ~160 VGPRs: one per CU
+  const int wpc = K <= 128 ? 2 : 1;
+  int per_slice = g_stream_cus * wpc / slices;
+  if (per_slice < 1) per_slice = 1;
+  if (per_slice > items) per_slice = items;
+  SArgs a{};
+  a.M = g.M; a.N = g.N; a.K = K;
+  a.A = (const bf16*)g.A; a.B = (const bf16*)g.B; a.C = (bf16*)g.C;
+  a.bias = g.bias; a.res = (const bf16*)g.add1;
+  a.H = cv.H; a.W = cv.W; a.Cin = cv.C; a.stride = cv.stride; a.OH = cv.OH; a.OW = cv.OW;
+  a.slices = slices; a.per_slice = per_slice; a.items = items;
+  a.xcd_group = (per_slice * slices) % (8 * slices) == 0 && per_slice % 8 == 0;
+  a.a_bytes = (unsigned)a_bytes;
+  const dim3 grid(per_slice * slices);
+  const bool res = g.add1 != nullptr;
+  switch (K) {
+    case 64: launch_kt<2, 4>(res, strided, g.act, grid, s, a); break;
+    case 128: launch_kt<4, 4>(res, strided, g.act, grid, s, a); break;
+    case 256: launch_kt<8, 4>(res, strided, g.act, grid, s, a); break;
+    default: launch_kt<16, 2>(res, strided, g.act, grid, s, a); break;
+  }
+  *err = (int)hipGetLastError();
+  return 1;
+}
+
+extern "C" int sat_conv_stream_set_mode(int mode) {
+  if (mode < 0 || mode > 2) return SAT_ERR_INVALID;
+  g_stream_mode = mode;
+  return 0;
+}

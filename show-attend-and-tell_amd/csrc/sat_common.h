@@ -85,3 +85,5 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s);
 int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err);
 // 256x128 pipelined bf16 conv / NT GEMM (convpipe.hip); returns 1 when it launched.
 int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err);
+// weight-stationary streaming kernel for K <= 512 1x1 convs (convstream.hip); returns 1 when it launched.
+int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err);

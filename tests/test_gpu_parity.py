@@ -589,6 +589,43 @@ def test_conv_pipe_kernel(sat, N, C, H, Cout, k, stride, pad, relu, resid):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("N,C,H,Cout,stride,relu,resid", [
+    (2, 256, 14, 1024, 1, True, True),     # L3 c3 + identity: K = 256, 8 slices, M tail (392 rows)
+    (3, 64, 16, 256, 1, True, True),       # L1 c3: K = 64 (128-byte LDS rows)
+    (2, 128, 20, 512, 1, False, True),     # L2 c3 shape class, no activation
+    (2, 512, 7, 2048, 1, True, True),      # L4 c3: K = 512, 64-row items
+    (1, 512, 28, 1024, 2, False, False),   # strided 1x1 downsample (projection shortcut)
+    (2, 1024, 14, 256, 1, True, False),    # c1-like K = 1024: not eligible -> other kernels
+    (5, 256, 9, 128, 1, True, False)])     # one slice, many partial items
+def test_conv_stream_kernel(sat, N, C, H, Cout, stride, relu, resid):
+    """convstream.hip (weight-stationary, B in registers, A streamed by LDS-DMA, C^T on MFMA) forced on
+    every eligible 1x1 shape vs the other conv kernels (same fp32 sums -> bit-identical) and torch fp32."""
+    from sat_amd import ops
+    lib = sat._lib.lib()
+    g = torch.Generator().manual_seed(N * C + Cout + stride)
+    x = torch.randn(N, C, H, H, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, C, 1, 1, generator=g) / math.sqrt(C)).bfloat16().float()
+    b = torch.randn(Cout, generator=g)
+    ref = F.conv2d(x, w, b, stride=stride)
+    res = torch.randn_like(ref).bfloat16().float() if resid else None
+    ref = ref + res if resid else ref
+    ref = torch.relu(ref) if relu else ref
+    xd = x.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    wd = w.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    rd = res.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV) if resid else None
+    outs = []
+    try:
+        for mode in (2, 0):
+            assert lib.sat_conv_stream_set_mode(mode) == 0
+            y = ops.conv2d_nhwc(xd, wd, b.to(DEV), stride, 0, relu, residual=rd)
+            outs.append(y.float().permute(0, 3, 1, 2).cpu())
+    finally:
+        lib.sat_conv_stream_set_mode(1)
+    assert rel(outs[0], ref) < 1e-2
+    assert ((outs[0] - ref).abs() <= 1e-2 * ref.abs() + 2e-2).all()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("M,N,K", [(3328, 10000, 512), (6272, 512, 2048), (300, 136, 192)])
 def test_conv_pipe_gemm(sat, M, N, K):
     """Plain NT GEMM through the pipelined kernel (bf16 out, bias, bf16 residual, ReLU) vs the

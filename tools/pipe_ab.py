@@ -1,5 +1,5 @@
-"""A/B the 256x128 pipelined conv kernel (convpipe.hip, sat_conv_pipe_set_mode(2)) against the
-128-row LDS-DMA kernel (convgemm.hip, mode 0) on the ResNet152 / VGG19 conv shapes at B=128.
+"""A/B the 256x128 pipelined conv kernel (convpipe.hip) and the 1x1 streaming kernel (convstream.hip),
+both forced on (mode 2), against the 128-row LDS-DMA kernel (convgemm.hip, both mode 0) on the ResNet152 / VGG19 conv shapes at B=128.
 Interleaved rounds in one process (cdna_hip_programming.md 5.4 rule 24); median of rounds.
 Also checks that both kernels give bit-identical outputs (same fp32 sums, same rounding)."""
 import os
@@ -21,7 +21,10 @@ SHAPES = [("L3_c2", 14, 256, 256, 3, 1, 1, 0), ("L3_c1", 14, 1024, 256, 1, 1, 0,
           ("L4_c3", 7, 512, 2048, 1, 1, 0, 1), ("L1_c2", 56, 64, 64, 3, 1, 1, 0),
           ("L3_c2s2", 28, 256, 256, 3, 2, 1, 0), ("L4_c1a", 14, 1024, 512, 1, 1, 0, 0),
           ("vgg_c512", 28, 512, 512, 3, 1, 1, 0), ("vgg_c256", 56, 256, 256, 3, 1, 1, 0),
-          ("vgg_c14", 14, 512, 512, 3, 1, 1, 0), ("vgg_c128", 112, 128, 128, 3, 1, 1, 0)]
+          ("vgg_c14", 14, 512, 512, 3, 1, 1, 0), ("vgg_c128", 112, 128, 128, 3, 1, 1, 0),
+          ("L1_c3", 56, 64, 256, 1, 1, 0, 1), ("L1_ds", 56, 64, 256, 1, 1, 0, 0), ("L1_c1", 56, 256, 64, 1, 1, 0, 0),
+          ("L2_dss2", 56, 256, 512, 1, 2, 0, 0), ("L3_dss2", 28, 512, 1024, 1, 2, 0, 0),
+          ("L4_dss2", 14, 1024, 2048, 1, 2, 0, 0), ("L2_c1a", 56, 256, 128, 1, 1, 0, 0)]
 ONLY = os.environ.get("SHAPES")
 if ONLY:
     SHAPES = [t for t in SHAPES if t[0] in ONLY.split(",")]
@@ -36,6 +39,7 @@ for name, H, C, Co, k, s, p, r in (SHAPES if not os.environ.get("EXP") else []):
     outs = {}
     for mode in (0, 2):
         lib.sat_conv_pipe_set_mode(mode)
+        lib.sat_conv_stream_set_mode(mode)
         outs[mode] = ops.conv2d_nhwc(x, w, b, s, p, True, residual=resid)
     same = torch.equal(outs[0], outs[2])
     maxdiff = (outs[0].float() - outs[2].float()).abs().max().item()
@@ -45,6 +49,7 @@ for name, H, C, Co, k, s, p, r in (SHAPES if not os.environ.get("EXP") else []):
     for rnd in range(5):
         for mode in (0, 2):
             lib.sat_conv_pipe_set_mode(mode)
+            lib.sat_conv_stream_set_mode(mode)
             ops.conv2d_nhwc(x, w, b, s, p, True, residual=resid, out=y)
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             st.record()
@@ -54,6 +59,7 @@ for name, H, C, Co, k, s, p, r in (SHAPES if not os.environ.get("EXP") else []):
             en.synchronize()
             times[mode].append(st.elapsed_time(en) / REPS)
     lib.sat_conv_pipe_set_mode(1)
+    lib.sat_conv_stream_set_mode(1)
     t0, t2 = statistics.median(times[0]), statistics.median(times[2])
     print(f"{name:9s} M={B*OH*OH:7d} N={Co:5d} K={k*k*C:5d}  old {t0*1e3:7.1f}us {flops/t0/1e9:5.0f}TF  "
           f"pipe {t2*1e3:7.1f}us {flops/t2/1e9:5.0f}TF  x{t0/t2:4.2f}  bitequal={same} maxdiff={maxdiff:.3g}",
