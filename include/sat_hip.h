@@ -111,6 +111,9 @@ int sat_conv_pipe_set_experiment(int waves, int ablate);
 /* tuning hook (process-global) for the weight-stationary streaming kernel of K <= 512 1x1 convs
  * (convstream.hip): 0 = off, 1 = automatic (default), 2 = every eligible problem. */
 int sat_conv_stream_set_mode(int mode);
+/* tuning hook (process-global) for the 3x3 / stride-1 halo kernel (convhalo.hip): 0 = off (default),
+ * 1 = automatic, 2 = every eligible problem. */
+int sat_conv_halo_set_mode(int mode);
 int sat_gemm(const SatGemmArgs* args, void* stream);
 /* elementwise cast between SAT_F32 and SAT_BF16 storage (n elements). */
 int sat_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, void* stream);

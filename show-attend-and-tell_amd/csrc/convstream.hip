@@ -2,7 +2,8 @@
 //
 //   C[M,N] = act(A[M,K] . B[N,K]^T + bias[N] (+ res[M,N]))       bf16 in/out, fp32 accumulate
 //   A row m = the NHWC input pixel of output pixel m (stride 1: row m; stride s: (n, oh*s, ow*s)),
-//   K = Cin in {64, 128, 256, 512}, B = conv weights [Cout][Cin].
+//   K = Cin in {64, 128, 256, 512}, B = conv weights [Cout][Cin].  (K = 1024 with 128 VGPRs of B per
+//   lane measured slower than convpipe.hip on L3 c1: 27.1 vs 23 us, profiles/r2_s10_stream_k1024.txt.)
 //
 // These are the ResNet152 bottleneck c3 (+ identity / projection residual) and downsample convs
 // and the K <= 512 c1 convs: 2-13 GFLOP each against 60-460 MB of activations, so they are
@@ -20,10 +21,11 @@
 //     holds 4 consecutive output COLUMNS of one row, so the epilogue (bias, fp32 residual add,
 //     activation, one bf16 rounding -- the same arithmetic as the other conv kernels) needs no
 //     LDS transpose: 8-byte residual loads and 8-byte stores, 32 contiguous bytes per row per wave;
-//   * pipeline per item: barrier -> LDS-DMA of the next item's A tile and residual tile into the
-//     other stage -> fragment reads + MFMAs -> epilogue (residual from LDS) -> 8-B stores, with a
-//     counted vmcnt (never 0 in the loop) so stores stay in flight across the next barrier; every
-//     global read in the loop is a DMA, so the compiler inserts no vmcnt waits of its own;
+//   * pipeline per item: barrier -> LDS-DMA of item i+2's A tile and residual tile into the free
+//     stage of a 3-stage ring (item i+1 is landing) -> fragment reads + MFMAs -> epilogue (residual
+//     from LDS) -> 8-B stores, with a counted vmcnt (never 0 in the loop) so the next item's DMAs
+//     and the last two items' stores stay in flight across the barrier; every global read in the
+//     loop is a DMA, so the compiler inserts no vmcnt waits of its own;
 //   * LDS image lane-linear (DMA), swizzle on the source: 16-B chunk c of row r at slot
 //     c ^ (r & 15) (rows >= 256 B) or c ^ ((r >> 1) & 7) (128-B rows) -> conflict-free
 //     ds_read_b128 fragment reads (verified for every lane group).
@@ -46,32 +48,44 @@ struct SArgs {
   int slices, per_slice, items;      // N / 128, workgroups per slice, M-tiles
   int xcd_group;                     // 1: slice = (b / 8) % slices (one M-tile sequence per XCD)
   unsigned a_bytes;
+  int abl;                           // diagnostics (tools/pipe_ab.py): 1 no MFMA, 2 no stores, 4 no A DMA
 };
 
 template <int N>
-__device__ __forceinline__ void s_wait_barrier() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if constexpr (N == 32) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else static_assert(N < 0, "unsupported vmcnt");
+__device__ __forceinline__ void s_wait_barrier_n() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+// s_waitcnt vmcnt(n) + s_barrier for a workgroup-uniform runtime n (the literal comes from a switch)
+__device__ __forceinline__ void s_wait_barrier(int n) {
+  switch (n) {
+#define SW_CASE(k) case k: s_wait_barrier_n<k>(); break;
+    SW_CASE(1) SW_CASE(2) SW_CASE(3) SW_CASE(4) SW_CASE(5) SW_CASE(6) SW_CASE(7) SW_CASE(8) SW_CASE(9) SW_CASE(10)
+    SW_CASE(11) SW_CASE(12) SW_CASE(13) SW_CASE(14) SW_CASE(15) SW_CASE(16) SW_CASE(17) SW_CASE(18) SW_CASE(19)
+    SW_CASE(20) SW_CASE(21) SW_CASE(22) SW_CASE(23) SW_CASE(24)
+#undef SW_CASE
+    default: s_wait_barrier_n<0>(); break;
+  }
 }
 
-// KT = K / 32 k-steps, MB = 16-row m-blocks per item (MT = 16 * MB rows)
-template <int KT, int MB, bool RES, int ACT, bool STRIDED>
+// KT = K / 32 k-steps, MB = 16-row m-blocks per item (MT = 16 * MB rows), NB = 16-column n-blocks
+// per wave (the workgroup's slice is 128 * NB columns)
+template <int KT, int MB, int NB, bool RES, int ACT, bool STRIDED>
 __global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
   constexpr int K = KT * 32, MT = MB * 16, ROWB = K * 2;
-  constexpr int TILE = MT * ROWB;                  // A tile bytes
-  constexpr int RTILE = RES ? MT * S_BN * 2 : 0;   // residual tile bytes (128 bf16 columns per row)
-  constexpr int STG = TILE + RTILE;                // one LDS stage
-  static_assert(2 * STG <= 160 * 1024, "two stages must fit in LDS");
-  constexpr int DMA_A = TILE / (S_NW * 64 * 16);   // 16-B DMAs per lane per item
+  constexpr int SN = S_BN * NB, RROWB = SN * 2;            // slice columns, residual row bytes
+  constexpr int TILE = MT * ROWB;                           // A tile bytes
+  constexpr int RTILE = MT * RROWB;                          // residual-in / output-out tile bytes
+  constexpr int STG = TILE + RTILE;                         // one LDS stage
+  constexpr int NSTG = 3;                                   // items i, i+1 (landing), i+2 (issued)
+  static_assert(NSTG * STG <= 160 * 1024, "the ring must fit in LDS");
+  constexpr int DMA_A = TILE / (S_NW * 64 * 16);            // 16-B DMAs per lane per item
   constexpr int DMA_R = RTILE / (S_NW * 64 * 16);
   static_assert(DMA_A * S_NW * 64 * 16 == TILE && DMA_R * S_NW * 64 * 16 == RTILE, "whole 8 KiB rounds");
-  constexpr int ST = MB;                           // 8-B stores per lane per item
-  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  constexpr int ST = RTILE / (S_NW * 64 * 16);              // 16-B row-segment stores per lane per item
+  constexpr int DMA_N = DMA_A + (RES ? DMA_R : 0);
+  constexpr int CPR = RROWB / 16;                           // 16-B chunks per output row
+  __shared__ __attribute__((aligned(16))) char smem[NSTG * STG];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -84,20 +98,24 @@ __global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
     slice = b % a.slices;
     grp = b / a.slices;
   }
-  const int ns = slice * S_BN;            // the workgroup's 128 columns
-  const int n0 = ns + w * 16;             // this wave's 16 columns
+  const int ns = slice * SN;                 // the workgroup's columns
+  const int wc = w * 16 * NB;                // this wave's first column within the slice
   const int fr = lane & 15, fh = lane >> 4;
 
-  // B fragments for all of K (registers for the whole kernel): lane (fh, fr) holds B[n0 + fr][32 ks + 8 fh ..]
-  bf16x8 bq[KT];
-  {
-    const bf16* bp = a.B + (long)(n0 + fr) * K + 8 * fh;
+  // B fragments for all of K (registers for the whole kernel): lane (fh, fr) of n-block nb holds
+  // B[ns + wc + nb*16 + fr][32 ks + 8 fh ..]
+  bf16x8 bq[KT][NB];
 #pragma unroll
-    for (int ks = 0; ks < KT; ++ks) bq[ks] = *(const bf16x8*)(bp + 32 * ks);
+  for (int nb = 0; nb < NB; ++nb) {
+    const bf16* bp = a.B + (long)(ns + wc + nb * 16 + fr) * K + 8 * fh;
+#pragma unroll
+    for (int ks = 0; ks < KT; ++ks) bq[ks][nb] = *(const bf16x8*)(bp + 32 * ks);
   }
-  float bias4[4];
+  float bias4[NB][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) bias4[j] = a.bias ? a.bias[n0 + 4 * fh + j] : 0.f;
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bias4[nb][j] = a.bias ? a.bias[ns + wc + nb * 16 + 4 * fh + j] : 0.f;
 
   const unsigned c_bytes = (unsigned)((long)a.M * a.N * 2);
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, (int)a.a_bytes, 0x00020000);
@@ -130,13 +148,14 @@ __global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
         }
         off = (unsigned)((pix * K + 8 * c) * 2);
       }
+      if (a.abl & 4) off = S_OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (s_lds_void*)(st + (d * S_NW + w) * 1024), 16, (int)off, 0, 0, 0);
     }
-    if constexpr (RES) {   // residual rows of 256 B (this slice's 128 columns), chunk c at slot c ^ (r & 15)
+    if constexpr (RES) {   // residual rows of this slice's columns, 16-B chunk c at slot c ^ (r & 15) in 256-B groups
 #pragma unroll
       for (int d = 0; d < DMA_R; ++d) {
         const int byte = (d * S_NW + w) * 1024 + lane * 16;
-        const int r = byte / 256, c = ((byte % 256) / 16) ^ (r & 15);
+        const int r = byte / RROWB, pc = (byte % RROWB) / 16, c = (pc & ~15) | ((pc & 15) ^ (r & 15));
         const int m = m0 + r;
         const unsigned off = m < a.M ? (unsigned)(((long)m * a.N + ns + 8 * c) * 2) : S_OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rR, (s_lds_void*)(st + TILE + (d * S_NW + w) * 1024), 16, (int)off,
@@ -157,22 +176,25 @@ __global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
 
   int it = grp;
   if (it >= a.items) return;   // workgroup-uniform: no barrier is reached by part of a group
+  const int step = a.per_slice;
   stage(it, 0);
+  if (it + step < a.items) stage(it + step, 1);
   int buf = 0;
-  bool first = true;
-  while (true) {
-    const int nxt = it + a.per_slice;
-    // this wave's DMAs of item `it` landed (only the previous item's stores are younger); after the
-    // barrier every wave's have, and every wave finished reading the other stage
-    if (first) s_wait_barrier<0>();
-    else s_wait_barrier<ST>();
-    first = false;
-    if (nxt < a.items) stage(nxt, buf ^ 1);
+  for (int k = 0;; ++k) {
+    const int nxt2 = it + 2 * step;
+    // wait for this wave's DMAs of item `it`; younger: the next item's DMAs (if any) and the
+    // stores of the previous one or two items -- they stay in flight across the barrier.  After it
+    // every wave's DMAs of `it` have landed and every wave finished reading stage (k+2) % 3.
+    const int younger = (it + step < a.items ? DMA_N : 0) + (k >= 1 ? ST : 0) + (k >= 2 ? ST : 0);
+    s_wait_barrier(younger);
+    if (nxt2 < a.items) stage(nxt2, buf == 0 ? 2 : buf - 1);
     __builtin_amdgcn_sched_barrier(0);
     const char* base = smem + buf * STG;
-    f32x4 acc[MB];
+    f32x4 acc[MB][NB];
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
     bf16x8 af[2][MB];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) af[0][mb] = afrag(base, mb, 0);
@@ -182,55 +204,82 @@ __global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) af[(ks + 1) & 1][mb] = afrag(base, mb, ks + 1);
       }
+      if (a.abl & 1) {
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
-        acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks], af[ks & 1][mb], acc[mb], 0, 0, 0);
+        for (int mb = 0; mb < MB; ++mb) asm volatile("" ::"v"(af[ks & 1][mb]));
+      } else {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks][nb], af[ks & 1][mb], acc[mb][nb], 0, 0, 0);
+      }
     }
-    // epilogue: lane holds C[m0 + mb*16 + fr][n0 + 4 fh + j], j = 0..3
+    // epilogue: lane holds C[m0 + mb*16 + fr][ns + wc + nb*16 + 4 fh + j], j = 0..3.  bias, the residual
+    // (from the stage's R/O tile), activation, one bf16 rounding; the 8 result bytes go back to the
+    // same R/O slot they came from, and after a workgroup barrier the tile leaves as whole rows
+    // (16 B per lane, 256 / 512 contiguous bytes per row) instead of 8-B pieces of 16 rows.
+    char* ro = (char*)base + TILE;
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
-      const int r = mb * 16 + fr, m = it * MT + r;
-      float v[4];
+      const int r = mb * 16 + fr;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = acc[mb][j] + bias4[j];
-      if constexpr (RES) {
-        const int c = (w * 2 + (fh >> 1)) ^ (r & 15);   // 16-B chunk of this lane's 8 B
-        const u32x2 rv = *(const u32x2*)(base + TILE + r * 256 + 16 * c + 8 * (fh & 1));
-        const bf16* h = (const bf16*)&rv;
+      for (int nb = 0; nb < NB; ++nb) {
+        const int lc = (wc + nb * 16 + 4 * fh) / 8;                     // logical 16-B chunk of these 8 B
+        const int pc = (lc & ~15) | ((lc & 15) ^ (r & 15));
+        u32x2* slot = (u32x2*)(ro + r * RROWB + 16 * pc + 8 * (fh & 1));
+        float v[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] += (float)h[j];
+        for (int j = 0; j < 4; ++j) v[j] = acc[mb][nb][j] + bias4[nb][j];
+        if constexpr (RES) {
+          const u32x2 rv = *slot;
+          const bf16* h = (const bf16*)&rv;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] += (float)h[j];
+        }
+        u32x2 o;
+        bf16* ob = (bf16*)&o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ob[j] = (bf16)apply_act(v[j], ACT);
+        *slot = o;
       }
-      u32x2 o;
-      bf16* ob = (bf16*)&o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) ob[j] = (bf16)apply_act(v[j], ACT);
-      const unsigned off = m < a.M ? (unsigned)(((long)m * a.N + n0 + 4 * fh) * 2) : S_OOB;
-      __builtin_amdgcn_raw_buffer_store_b64(o, rC, (int)off, 0, 0);
     }
-    if (nxt >= a.items) break;
-    it = nxt;
-    buf ^= 1;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // LDS only: DMAs and stores stay in flight
+#pragma unroll
+    for (int p = 0; p < ST; ++p) {
+      const int t = p * S_NW * 64 + tid, r = t / CPR, lc = t % CPR;
+      const int pc = (lc & ~15) | ((lc & 15) ^ (r & 15));
+      const uint4 u = *(const uint4*)(ro + r * RROWB + 16 * pc);
+      const int m = it * MT + r;
+      const unsigned off = (m < a.M && !(a.abl & 2)) ? (unsigned)(((long)m * a.N + ns + 8 * lc) * 2) : S_OOB;
+      typedef unsigned __attribute__((ext_vector_type(4))) u32x4;
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rC, (int)off, 0, 0);
+    }
+    it += step;
+    if (it >= a.items) break;
+    buf = buf == 2 ? 0 : buf + 1;
   }
 }
 
 int g_stream_mode = 1;   // 0 off, 1 auto, 2 every eligible problem (A/B)
+int g_stream_abl = 0;    // diagnostics: SArgs::abl
 int g_stream_cus = 0;    // CU count (queried once)
 
-template <int KT, int MB, bool RES, bool STRIDED>
+template <int KT, int MB, int NB, bool RES, bool STRIDED>
 void launch_s(int act, dim3 grid, hipStream_t s, const SArgs& a) {
   if (act == SAT_ACT_RELU)
-    hipLaunchKernelGGL((conv1x1_stream_kernel<KT, MB, RES, SAT_ACT_RELU, STRIDED>), grid, dim3(S_NW * 64), 0, s, a);
+    hipLaunchKernelGGL((conv1x1_stream_kernel<KT, MB, NB, RES, SAT_ACT_RELU, STRIDED>), grid, dim3(S_NW * 64), 0, s, a);
   else
-    hipLaunchKernelGGL((conv1x1_stream_kernel<KT, MB, RES, SAT_ACT_NONE, STRIDED>), grid, dim3(S_NW * 64), 0, s, a);
+    hipLaunchKernelGGL((conv1x1_stream_kernel<KT, MB, NB, RES, SAT_ACT_NONE, STRIDED>), grid, dim3(S_NW * 64), 0, s, a);
 }
-template <int KT, int MB>
+template <int KT, int MB, int NB>
 void launch_kt(bool res, bool strided, int act, dim3 grid, hipStream_t s, const SArgs& a) {
   if (res) {
-    if (strided) launch_s<KT, MB, true, true>(act, grid, s, a);
-    else launch_s<KT, MB, true, false>(act, grid, s, a);
+    if (strided) launch_s<KT, MB, NB, true, true>(act, grid, s, a);
+    else launch_s<KT, MB, NB, true, false>(act, grid, s, a);
   } else {
-    if (strided) launch_s<KT, MB, false, true>(act, grid, s, a);
-    else launch_s<KT, MB, false, false>(act, grid, s, a);
+    if (strided) launch_s<KT, MB, NB, false, true>(act, grid, s, a);
+    else launch_s<KT, MB, NB, false, false>(act, grid, s, a);
   }
 }
 
@@ -261,18 +310,20 @@ int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err) {
       return 0;
     g_stream_cus = n;
   }
-  // rows per item: MT = 64 (K <= 256: A tiles of 8 / 16 / 32 KiB) or 32 (K = 512: 32 KiB)
-  const int MB = K == 512 ? 2 : 4;
+  // NB = 2 (256-column slices; each A fragment read feeds two MFMAs) when N allows it, 32-row items;
+  // NB = 1 (128-column slices) otherwise, 64-row items (32 at K = 512)
+  const int NB = g.N % (2 * S_BN) == 0 ? 2 : 1;
+  const int MB = NB == 2 ? (K == 64 ? 4 : 2) : (K >= 512 ? 2 : 4);
   const int MT = MB * 16;
-  const int slices = g.N / S_BN;
+  const int slices = g.N / (S_BN * NB);
   const int items = sat_cdiv(g.M, MT);
   if (g_stream_mode == 1) {
     // HBM-bound shapes only: enough items per workgroup to pipeline (>= ~3)
     if ((long)items * slices < 2L * g_stream_cus) return 0;
   }
-  // K <= 128: two workgroups per CU fit (<= 64 KiB of LDS and <= 128 VGPRs each) and hide each
-  // other's barrier / epilogue latency; K = 256 / 512 kernels need ~160 VGPRs: one per CU
-  const int wpc = K <= 128 ? 2 : 1;
+  // K = 64 with 128-column slices: two workgroups per CU fit (3 x 24 KiB of LDS, <= 128 VGPRs each)
+  // and hide each other's barrier / epilogue latency; the other rings take 72-144 KiB: one per CU
+  const int wpc = (K <= 64 && NB == 1) ? 2 : 1;
   int per_slice = g_stream_cus * wpc / slices;
   if (per_slice < 1) per_slice = 1;
   if (per_slice > items) per_slice = items;
@@ -284,20 +335,31 @@ int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err) {
   a.slices = slices; a.per_slice = per_slice; a.items = items;
   a.xcd_group = (per_slice * slices) % (8 * slices) == 0 && per_slice % 8 == 0;
   a.a_bytes = (unsigned)a_bytes;
+  a.abl = g_stream_abl;
   const dim3 grid(per_slice * slices);
   const bool res = g.add1 != nullptr;
-  switch (K) {
-    case 64: launch_kt<2, 4>(res, strided, g.act, grid, s, a); break;
-    case 128: launch_kt<4, 4>(res, strided, g.act, grid, s, a); break;
-    case 256: launch_kt<8, 4>(res, strided, g.act, grid, s, a); break;
-    default: launch_kt<16, 2>(res, strided, g.act, grid, s, a); break;
+  if (NB == 2) {
+    switch (K) {
+      case 64: launch_kt<2, 4, 2>(res, strided, g.act, grid, s, a); break;
+      case 128: launch_kt<4, 2, 2>(res, strided, g.act, grid, s, a); break;
+      case 256: launch_kt<8, 2, 2>(res, strided, g.act, grid, s, a); break;
+      default: launch_kt<16, 2, 2>(res, strided, g.act, grid, s, a); break;
+    }
+  } else {
+    switch (K) {
+      case 64: launch_kt<2, 4, 1>(res, strided, g.act, grid, s, a); break;
+      case 128: launch_kt<4, 4, 1>(res, strided, g.act, grid, s, a); break;
+      case 256: launch_kt<8, 4, 1>(res, strided, g.act, grid, s, a); break;
+      default: launch_kt<16, 2, 1>(res, strided, g.act, grid, s, a); break;
+    }
   }
   *err = (int)hipGetLastError();
   return 1;
 }
 
 extern "C" int sat_conv_stream_set_mode(int mode) {
-  if (mode < 0 || mode > 2) return SAT_ERR_INVALID;
-  g_stream_mode = mode;
+  if (mode < 0 || mode > 2 + 4 * 7) return SAT_ERR_INVALID;
+  g_stream_mode = mode & 3;
+  g_stream_abl = mode >> 2;   // diagnostics: ablation bits in mode bits 2-4 (tools/pipe_ab.py)
   return 0;
 }

@@ -87,3 +87,5 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err);
 int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err);
 // weight-stationary streaming kernel for K <= 512 1x1 convs (convstream.hip); returns 1 when it launched.
 int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err);
+// 3x3 / stride 1 convs with a per-channel-chunk input halo (convhalo.hip); returns 1 when it launched.
+int sat_conv_halo_try(const SatGemm& g, hipStream_t s, int* err);

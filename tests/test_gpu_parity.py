@@ -626,6 +626,44 @@ def test_conv_stream_kernel(sat, N, C, H, Cout, stride, relu, resid):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("N,C,H,Cout,relu,resid", [
+    (2, 256, 14, 256, True, False),    # L3 c2: 4 chunks x 9 taps, M tail (392 rows)
+    (1, 128, 28, 128, True, False),    # L2 c2: halo rows span image rows and the image end
+    (2, 64, 56, 64, True, False),      # L1 c2: W = 56 (384 halo rows), N = 64 half tile
+    (3, 512, 7, 512, False, True),     # L4 c2 shape class, residual, no activation, 3 images per tile
+    (1, 64, 5, 200, True, False),      # tiny image, N tail, single chunk
+    (2, 256, 14, 136, True, True)])    # N tail + residual
+def test_conv_halo_kernel(sat, N, C, H, Cout, relu, resid):
+    """convhalo.hip (input halo per 64-channel chunk, taps as row shifts with border masks) forced on
+    every eligible 3x3 shape vs torch fp32 (chunk-major k order: fp32-summation-order close to the
+    other kernels, not bit-identical)."""
+    from sat_amd import ops
+    lib = sat._lib.lib()
+    g = torch.Generator().manual_seed(N * C + Cout + H)
+    x = torch.randn(N, C, H, H, generator=g).bfloat16().float()
+    w = (torch.randn(Cout, C, 3, 3, generator=g) / math.sqrt(C * 9)).bfloat16().float()
+    b = torch.randn(Cout, generator=g)
+    ref = F.conv2d(x, w, b, padding=1)
+    res = torch.randn_like(ref).bfloat16().float() if resid else None
+    ref = ref + res if resid else ref
+    ref = torch.relu(ref) if relu else ref
+    xd = x.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    wd = w.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
+    rd = res.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV) if resid else None
+    outs = []
+    try:
+        for mode in (2, 0):
+            assert lib.sat_conv_halo_set_mode(mode) == 0
+            y = ops.conv2d_nhwc(xd, wd, b.to(DEV), 1, 1, relu, residual=rd)
+            outs.append(y.float().permute(0, 3, 1, 2).cpu())
+    finally:
+        lib.sat_conv_halo_set_mode(1)
+    assert rel(outs[0], ref) < 1e-2
+    assert ((outs[0] - ref).abs() <= 1e-2 * ref.abs() + 2e-2).all()
+    # vs the implicit-GEMM kernels: same products, k summed chunk-major -> one bf16 ulp at most
+    assert ((outs[0] - outs[1]).abs() <= 2 ** -7 * outs[1].abs() + 1e-4).all()
+
+
 @pytest.mark.parametrize("M,N,K", [(3328, 10000, 512), (6272, 512, 2048), (300, 136, 192)])
 def test_conv_pipe_gemm(sat, M, N, K):
     """Plain NT GEMM through the pipelined kernel (bf16 out, bias, bf16 residual, ReLU) vs the

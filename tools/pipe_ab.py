@@ -30,7 +30,7 @@ if ONLY:
     SHAPES = [t for t in SHAPES if t[0] in ONLY.split(",")]
 lib = sat_amd._lib.lib()
 torch.manual_seed(0)
-for name, H, C, Co, k, s, p, r in (SHAPES if not os.environ.get("EXP") else []):
+for name, H, C, Co, k, s, p, r in (SHAPES if not (os.environ.get("EXP") or os.environ.get("SABL")) else []):
     x = torch.randn(B, H, H, C, device="cuda").bfloat16()
     w = (torch.randn(Co, k, k, C, device="cuda") / (k * k * C) ** 0.5).bfloat16()
     b = torch.randn(Co, device="cuda")
@@ -40,6 +40,7 @@ for name, H, C, Co, k, s, p, r in (SHAPES if not os.environ.get("EXP") else []):
     for mode in (0, 2):
         lib.sat_conv_pipe_set_mode(mode)
         lib.sat_conv_stream_set_mode(mode)
+        lib.sat_conv_halo_set_mode(mode)
         outs[mode] = ops.conv2d_nhwc(x, w, b, s, p, True, residual=resid)
     same = torch.equal(outs[0], outs[2])
     maxdiff = (outs[0].float() - outs[2].float()).abs().max().item()
@@ -50,6 +51,7 @@ for name, H, C, Co, k, s, p, r in (SHAPES if not os.environ.get("EXP") else []):
         for mode in (0, 2):
             lib.sat_conv_pipe_set_mode(mode)
             lib.sat_conv_stream_set_mode(mode)
+            lib.sat_conv_halo_set_mode(mode)
             ops.conv2d_nhwc(x, w, b, s, p, True, residual=resid, out=y)
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             st.record()
@@ -60,6 +62,7 @@ for name, H, C, Co, k, s, p, r in (SHAPES if not os.environ.get("EXP") else []):
             times[mode].append(st.elapsed_time(en) / REPS)
     lib.sat_conv_pipe_set_mode(1)
     lib.sat_conv_stream_set_mode(1)
+    lib.sat_conv_halo_set_mode(1)
     t0, t2 = statistics.median(times[0]), statistics.median(times[2])
     print(f"{name:9s} M={B*OH*OH:7d} N={Co:5d} K={k*k*C:5d}  old {t0*1e3:7.1f}us {flops/t0/1e9:5.0f}TF  "
           f"pipe {t2*1e3:7.1f}us {flops/t2/1e9:5.0f}TF  x{t0/t2:4.2f}  bitequal={same} maxdiff={maxdiff:.3g}",
@@ -67,7 +70,7 @@ for name, H, C, Co, k, s, p, r in (SHAPES if not os.environ.get("EXP") else []):
 
 # ---- plain NT GEMMs (decoder shapes): C bf16 = relu(A B^T + bias)
 GEMMS = [(3328, 10000, 512), (6272, 512, 2048), (3328, 2048, 512), (6272, 768, 512), (4096, 30522, 768)]
-for M, N, K in (GEMMS if not os.environ.get("EXP") and not ONLY else []):
+for M, N, K in (GEMMS if not (os.environ.get("EXP") or os.environ.get("SABL")) and not ONLY else []):
     A = torch.randn(M, K, device="cuda").bfloat16()
     Wt = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
     bias = torch.randn(N, device="cuda")
@@ -91,6 +94,32 @@ for M, N, K in (GEMMS if not os.environ.get("EXP") and not ONLY else []):
     fl = 2.0 * M * N * K
     print(f"gemm {M}x{N}x{K}  old {t0*1e3:7.1f}us {fl/t0/1e9:5.0f}TF  pipe {t2*1e3:7.1f}us {fl/t2/1e9:5.0f}TF  "
           f"x{t0/t2:4.2f} bitequal={torch.equal(outs[0], outs[2])}", flush=True)
+
+# ---- streaming-kernel ablation: SABL="0;1;2;4;3" (mode bits 2-4 of sat_conv_stream_set_mode)
+SABL = os.environ.get("SABL")
+if SABL:
+    abls = [int(v) for v in SABL.split(";")]
+    for name, H, C, Co, k, s, p, r in SHAPES:
+        x = torch.randn(B, H, H, C, device="cuda").bfloat16()
+        w = (torch.randn(Co, k, k, C, device="cuda") / (k * k * C) ** 0.5).bfloat16()
+        b = torch.randn(Co, device="cuda")
+        OH = (H + 2 * p - k) // s + 1
+        resid = torch.randn(B, OH, OH, Co, device="cuda").bfloat16() if r else None
+        y = torch.empty(B, OH, OH, Co, device="cuda", dtype=torch.bfloat16)
+        times = {c: [] for c in abls}
+        for rnd in range(5):
+            for c in abls:
+                lib.sat_conv_stream_set_mode(2 + 4 * c)
+                ops.conv2d_nhwc(x, w, b, s, p, True, residual=resid, out=y)
+                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                st.record()
+                for _ in range(REPS):
+                    ops.conv2d_nhwc(x, w, b, s, p, True, residual=resid, out=y)
+                en.record()
+                en.synchronize()
+                times[c].append(st.elapsed_time(en) / REPS)
+        lib.sat_conv_stream_set_mode(1)
+        print(f"{name:9s}" + "".join(f"  abl{c}: {statistics.median(times[c])*1e3:6.1f}us" for c in abls), flush=True)
 
 # ---- experiment configs: EXP="8,0;4,0;8,1;8,2;8,4" (waves, ablation bits) on SHAPES, pipe forced
 EXP = os.environ.get("EXP")
