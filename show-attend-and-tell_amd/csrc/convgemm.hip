@@ -40,6 +40,7 @@ constexpr int BK = 64, ROWB = BK * 2;   // 128-byte LDS rows
 
 struct FArgs {
   int M, N, K;
+  int a_mlim;              // k-major A: chunks of 8 m's are loaded while m + 8 <= a_mlim (SatGemm::a_tail)
   const bf16* A; long lda;
   const bf16* B; long ldb;
   void* C; long ldc; int c_bf16;
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
         const int r = (w * A_INSTR + j) * 4 + trow;       // k-row of the tile
         const int ch = tslot ^ swz256(r);
         const int k = k0 + r, m = m0 + 8 * ch;
-        const bool ok = k < K && m + 8 <= M;
+        const bool ok = k < K && m + 8 <= a.a_mlim;
         dma16(sel(ok, a.A + (long)k * a.lda + m, a.zero16), sa + (w * A_INSTR + j) * 1024);
       }
     } else if (a.amode == 1) {   // block-uniform filter tap
@@ -536,9 +537,10 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   const bool conv = g.conv.C > 0;
   const bool at = g.transA != 0, bt = g.transB != 0;
   if (conv && at) return 0;
-  if (at && (g.M % 8 || g.lda % 8)) return 0;
+  if (at && ((g.M % 8 && !g.a_tail) || g.lda % 8)) return 0;
   if (bt && (g.N % 8 || g.ldb % 8)) return 0;
-  if (!at && (g.K % 8 || (!conv && g.lda % 8))) return 0;
+  // a K tail needs B guarded per k row (k-major B) and A readable to the next 8
+  if (!at && ((g.K % 8 && !(g.a_tail && bt && !conv)) || (!conv && g.lda % 8))) return 0;
   if (!bt && (g.K % 8 || g.ldb % 8)) return 0;
   if (g.bias && !al16(g.bias)) return 0;
   if (g.add1 && !al16(g.add1)) return 0;
@@ -584,6 +586,7 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   }
   FArgs a{};
   a.M = g.M; a.N = g.N; a.K = g.K;
+  a.a_mlim = at && g.a_tail ? sat_cdiv(g.M, 8) * 8 : g.M;
   a.A = (const bf16*)g.A; a.lda = g.lda; a.B = (const bf16*)g.B; a.ldb = g.ldb;
   a.C = g.C; a.ldc = g.ldc; a.c_bf16 = g.c_dtype == SAT_BF16;
   a.bias = g.bias;

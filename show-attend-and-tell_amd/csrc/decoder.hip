@@ -90,6 +90,11 @@ struct Carver {
   }
 };
 
+// row stride of the workspace copy of d logits: bf16 vocabularies that are not a multiple of 8
+// (BERT's 30522) are padded with zero columns so the two vocab GEMMs of the head backward stay on
+// the 16-B LDS-DMA kernel (SatGemm::a_tail) instead of the register-staged fallback (~4 ms / step)
+inline int head_ld(const SatDecoderDims& d) { return d.dtype == SAT_BF16 && d.V % 8 ? (d.V + 7) / 8 * 8 : d.V; }
+
 size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   const size_t B = d.B, L = d.L, D = d.D, E = d.E, V = d.V, T1 = d.T - 1, R = B * T1;
   const size_t HG = 5 * E + D;
@@ -116,7 +121,7 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   c.take(w->hd_t, R * E * ts);
   c.take(w->fh, R * E * f); c.take(w->fz, R * E * f); c.take(w->comb_t, R * E * ts);
   // backward
-  c.take(w->dpre_t, R * V * ts);
+  c.take(w->dpre_t, R * head_ld(d) * ts);
   c.take(w->dcomb, R * E * f);
   c.take(w->dfh_t, R * E * ts); c.take(w->dfz_t, R * E * ts);
   c.take(w->dhd, R * E * f);
@@ -333,8 +338,9 @@ int bwd_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) 
 // input gradient: Y[M,N] = X[M,K] W[K,N]   (W stored [K][N] row-major = torch weight [out,in])
 int dgrad_launch(const Ctx& c, int M, int N, int K, const void* X, long ldx, const void* Wt, long ldw, float* out,
                  long ldo, hipStream_t s, const float* add1 = nullptr, long ld_add1 = 0, int splits = 0,
-                 long split_stride = 0) {
+                 long split_stride = 0, int a_tail = 0) {
   SatGemm g;
+  g.a_tail = a_tail;
   g.partial_splits = splits; g.split_stride = split_stride;
   g.M = M; g.N = N; g.K = K; g.dtype = c.d.dtype;
   g.A = X; g.lda = ldx; g.B = Wt; g.ldb = ldw; g.transB = 1;
@@ -518,14 +524,17 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D};
   const int B = d.B, L = d.L, D = d.D, E = d.E, V = d.V, T1 = d.T - 1;
   const int R = (int)c.R;
+  const int VP = head_ld(d);
   const long HG = c.HG;
   const bool att = d.attention != 0;
   const float beta = accumulate ? 1.f : 0.f;
   const Splits sp = splits_for(d);
   auto G = [&](int64_t off) { return grads + off; };
   // weight gradient: G[M,N] (+)= X[K,M]^T Y[K,N]   (X m-contig, Y n-contig)
-  auto wgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo) {
+  auto wgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo,
+                   int a_tail = 0) {
     SatGemm g;
+    g.a_tail = a_tail;
     g.M = M; g.N = N; g.K = K; g.dtype = d.dtype;
     g.A = X; g.lda = ldx; g.transA = 1;
     g.B = Y; g.ldb = ldy; g.transB = 1;
@@ -545,13 +554,18 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
       // d logits through the ReLU of the advanced deep output; phase bit 4: the caller's d_preds is
       // already masked (sat_caption_loss_backward_relu fused it)
       const void* dpre = d_preds;
-      if (!(phase & 4)) {
+      long ldp = V;
+      if (VP != V) {
+        SAT_CHECK((hipError_t)sat_pad_rows(d_preds, (phase & 4) ? nullptr : preds, R, V, VP, d.dtype, w.dpre_t, s));
+        dpre = w.dpre_t; ldp = VP;
+      } else if (!(phase & 4)) {
         SAT_CHECK((hipError_t)sat_relu_mask_mul(d_preds, preds, (long)R * V, d.dtype, w.dpre_t, s));
         dpre = w.dpre_t;
       }
-      SAT_CHECK((hipError_t)wgrad(V, E, R, dpre, V, w.comb_t, E, G(lay->fout_w), E));
-      SAT_CHECK((hipError_t)colsum(dpre, d.dtype, V, R, V, G(lay->fout_b)));
-      SAT_CHECK((hipError_t)dgrad(R, E, V, dpre, V, c.W(lay->fout_w), E, w.dcomb, E));
+      SAT_CHECK((hipError_t)wgrad(V, E, R, dpre, ldp, w.comb_t, E, G(lay->fout_w), E, VP != V));
+      SAT_CHECK((hipError_t)colsum(dpre, d.dtype, ldp, R, V, G(lay->fout_b)));
+      SAT_CHECK((hipError_t)dgrad_launch(c, R, E, V, dpre, ldp, c.W(lay->fout_w), E, w.dcomb, E, s, nullptr, 0, 0, 0,
+                                         VP != V));
       SAT_CHECK((hipError_t)sat_ado_bwd_split(w.dcomb, w.fh, w.fz, (long)R * E, d.dtype, w.dfh_t, w.dfz_t, s));
       SAT_CHECK((hipError_t)wgrad(E, E, R, w.dfh_t, E, w.hd_t, E, G(lay->fh_w), E));
       SAT_CHECK((hipError_t)colsum(w.dfh_t, d.dtype, E, R, E, G(lay->fh_b)));
@@ -560,9 +574,16 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
       SAT_CHECK((hipError_t)dgrad(R, E, E, w.dfh_t, E, c.W(lay->fh_w), E, w.dhd, E));
       if (att) SAT_CHECK((hipError_t)dgrad(R, D, E, w.dfz_t, E, c.W(lay->fz_w), D, w.dctx_head, D));
     } else {
-      SAT_CHECK((hipError_t)wgrad(V, E, R, d_preds, V, w.hd_t, E, G(lay->do_w), E));
+      const void* dpre = d_preds;
+      long ldp = V;
+      if (VP != V) {
+        SAT_CHECK((hipError_t)sat_pad_rows(d_preds, nullptr, R, V, VP, d.dtype, w.dpre_t, s));
+        dpre = w.dpre_t; ldp = VP;
+      }
+      SAT_CHECK((hipError_t)wgrad(V, E, R, dpre, ldp, w.hd_t, E, G(lay->do_w), E, VP != V));
       SAT_CHECK((hipError_t)colsum(d_preds, d.dtype, V, R, V, G(lay->do_b)));
-      SAT_CHECK((hipError_t)dgrad(R, E, V, d_preds, V, c.W(lay->do_w), E, w.dhd, E));
+      SAT_CHECK((hipError_t)dgrad_launch(c, R, E, V, dpre, ldp, c.W(lay->do_w), E, w.dhd, E, s, nullptr, 0, 0, 0,
+                                         VP != V));
     }
   }
   if (!(phase & 2)) return 0;

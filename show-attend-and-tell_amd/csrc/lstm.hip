@@ -154,6 +154,39 @@ __global__ void relu_mask_kernel(const T* d, const T* ref, long n, T* out) {
     out[i] = (float)ref[i] > 0.f ? d[i] : (T)0.0f;
 }
 
+// rows of cols elements (ld cols) -> rows of ld_out elements, zero past cols; optional ReLU mask
+// from ref (same layout as d).  bf16 pairs when cols is even (4-B aligned rows).
+template <bool MASK>
+__global__ void pad_rows_bf16x2_kernel(const bf16* d, const bf16* ref, int rows, int cols, int ld_out, bf16* out) {
+  const int c = 2 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (c >= ld_out) return;
+  for (long r = blockIdx.y; r < rows; r += gridDim.y) {
+  unsigned v = 0u;   // two bf16: low half = column c
+  if (c < cols) {
+    v = *(const unsigned*)(d + r * cols + c);
+    if constexpr (MASK) {
+      const unsigned m = *(const unsigned*)(ref + r * cols + c);
+      if (!(__uint_as_float(m << 16) > 0.f)) v &= 0xffff0000u;
+      if (!(__uint_as_float(m & 0xffff0000u) > 0.f)) v &= 0x0000ffffu;
+    }
+  }
+  *(unsigned*)(out + r * ld_out + c) = v;
+  }
+}
+template <typename T>
+__global__ void pad_rows_kernel(const T* d, const T* ref, int rows, int cols, int ld_out, T* out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ld_out) return;
+  for (long r = blockIdx.y; r < rows; r += gridDim.y) {
+  T v = (T)0.0f;
+  if (c < cols) {
+    v = d[r * cols + c];
+    if (ref && !((float)ref[r * cols + c] > 0.f)) v = (T)0.0f;
+  }
+  out[r * ld_out + c] = v;
+  }
+}
+
 template <typename T>
 __global__ void ado_split_kernel(const float* dcomb, const float* fh, const float* fz, long n, T* dfh, T* dfz) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -266,6 +299,21 @@ int sat_relu_mask_mul(const void* d, const void* ref, long n, int dtype, void* o
   dim3 g(grid_for(n));
   if (dtype == SAT_BF16) hipLaunchKernelGGL(relu_mask_kernel<bf16>, g, dim3(256), 0, s, (const bf16*)d, (const bf16*)ref, n, (bf16*)out_t);
   else hipLaunchKernelGGL(relu_mask_kernel<float>, g, dim3(256), 0, s, (const float*)d, (const float*)ref, n, (float*)out_t);
+  return (int)hipGetLastError();
+}
+int sat_pad_rows(const void* d, const void* ref, int rows, int cols, int ld_out, int dtype, void* out,
+                 hipStream_t s) {
+  if (rows <= 0 || ld_out < cols) return (int)hipErrorInvalidValue;
+  const int gy = rows < 32768 ? rows : 32768;
+  if (dtype == SAT_BF16 && cols % 2 == 0 && ld_out % 2 == 0) {
+    const dim3 g(sat_cdiv(ld_out / 2, 256), gy);
+    if (ref) hipLaunchKernelGGL(pad_rows_bf16x2_kernel<true>, g, dim3(256), 0, s, (const bf16*)d, (const bf16*)ref, rows, cols, ld_out, (bf16*)out);
+    else hipLaunchKernelGGL(pad_rows_bf16x2_kernel<false>, g, dim3(256), 0, s, (const bf16*)d, nullptr, rows, cols, ld_out, (bf16*)out);
+  } else {
+    const dim3 g(sat_cdiv(ld_out, 256), gy);
+    if (dtype == SAT_BF16) hipLaunchKernelGGL(pad_rows_kernel<bf16>, g, dim3(256), 0, s, (const bf16*)d, (const bf16*)ref, rows, cols, ld_out, (bf16*)out);
+    else hipLaunchKernelGGL(pad_rows_kernel<float>, g, dim3(256), 0, s, (const float*)d, (const float*)ref, rows, cols, ld_out, (float*)out);
+  }
   return (int)hipGetLastError();
 }
 int sat_ado_bwd_split(const float* d_comb, const float* fh, const float* fz, long n, int dtype, void* d_fh_t,

@@ -78,6 +78,9 @@ struct SatGemm {
   // partial-output split-K: split s writes its fp32 partial product to C + s*split_stride
   // (bias/add1 in split 0 only, act must be NONE); the consumer sums the slabs.
   int partial_splits = 0; long split_stride = 0;
+  // A's contiguous dimension (M when transA, else K) is readable -- zero-padded -- up to the next
+  // multiple of 8, so the 16-B DMA paths may take M % 8 / K % 8 != 0 (the decoder's padded d logits)
+  int a_tail = 0;
 };
 
 int sat_gemm_launch(const SatGemm& g, hipStream_t s);

@@ -100,6 +100,9 @@ int sat_dropout_apply(const float* h, long h_ld, int B, int T1, int E, int train
                       const uint64_t* seed_ptr, int t_offset, void* out_t, long out_ld, int dtype, hipStream_t s);
 int sat_bump_seed(uint64_t* p, hipStream_t s);
 int sat_relu_mask_mul(const void* d, const void* ref, long n, int dtype, void* out_t, hipStream_t s);
+// [rows][cols] -> [rows][ld_out] zero-padded past cols, ReLU-masked by ref when ref != null
+int sat_pad_rows(const void* d, const void* ref, int rows, int cols, int ld_out, int dtype, void* out,
+                 hipStream_t s);
 int sat_ado_bwd_split(const float* d_comb, const float* fh, const float* fz, long n, int dtype, void* d_fh_t,
                       void* d_fz_t, hipStream_t s);
 int sat_ado_combine(const float* fh, const float* fz, const void* emb, long n, int dtype,

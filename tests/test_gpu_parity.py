@@ -484,6 +484,42 @@ def test_decoder_split_target(sat):
     assert ((out[0][1] - out[1][1]).norm() / out[0][1].norm()).item() < 2e-2
 
 
+@pytest.mark.parametrize("ado", [False, True])
+@pytest.mark.parametrize("loss_kind", ["caption", "ce", "tail"])
+def test_decoder_odd_vocab_bf16_head(sat, ado, loss_kind):
+    """A vocabulary that is not a multiple of 8 (BERT's 30522): the bf16 head backward copies d logits
+    into zero-padded rows so both vocab GEMMs run on the 16-B LDS-DMA kernel (SatGemm::a_tail).  Its
+    gradients must agree with the same step in fp32 mode within the bf16 gradient bound (5e-2 rel):
+    caption_loss (ReLU mask fused into the loss backward), a generic autograd consumer (the decoder
+    applies the mask while padding), and a loss on the last 3 logits only -- the columns inside the
+    final partial 8-chunk -- so a dropped or garbage tail shows up as an O(1) error everywhere."""
+    torch.manual_seed(0)
+    B, Lf, D, V, T = 32, 49, 512, 1003, 12
+    dec = sat.Decoder(V, D, tf=True, ado=ado, attention=True).to(DEV).eval()
+    feats = torch.randn(B, Lf, D, device=DEV)
+    caps = O.make_captions(B, T, V, 1).to(DEV)
+    coef = torch.randn(B, T - 1, 3, device=DEV)
+    out = {}
+    for dt in (torch.float32, torch.bfloat16):
+        for p in dec.parameters():
+            p.grad = None
+        preds, alphas = dec(feats.to(dt), caps)
+        if loss_kind == "caption":
+            loss, _ = sat.caption_loss(preds, alphas, caps)
+        elif loss_kind == "ce":
+            loss = torch.nn.functional.cross_entropy(preds.float().reshape(-1, V), caps[:, 1:].reshape(-1))
+        else:
+            loss = (preds.float()[..., V - 3:] * coef).sum()
+        loss.backward()
+        out[dt] = {n: p.grad.float().clone() for n, p in dec.named_parameters() if p.grad is not None}
+    head = ["f_out.weight", "f_out.bias", "f_h.weight", "f_z.weight"] if ado else ["deep_output.weight", "deep_output.bias"]
+    for n in head + ["lstm.weight_ih", "embedding.weight"]:
+        a, b = out[torch.bfloat16][n], out[torch.float32][n]
+        assert torch.isfinite(a).all(), n
+        assert b.norm() > 0, n
+        assert ((a - b).norm() / b.norm()).item() < 5e-2, n
+
+
 def test_two_decoder_graphs_overwrite_gradients(sat):
     """bench.py's overlap schedule: two decoder hipGraphs over two feature buffers replayed in
     turn.  Every replay must overwrite the whole flat gradient buffer (beta = 0 targets are cleared
