@@ -213,6 +213,18 @@ int sat_caption_loss_backward_relu(int B, int T, int V, int L, int dtype, const 
                               const int64_t* captions, float alpha_c, void* workspace,
                               const float* grad_out, void* d_preds, float* d_alphas, void* stream);
 
+/* --- streaming image input (train.py:27-32 transform, dataset.py:9-12 decode on the host) ------
+ * Decoded uint8 RGB images of any size, packed HWC (image b at pixels + offsets[b], sizes[b] =
+ * {H, W}; offsets / sizes are device arrays) -> Resize((OH, OW)) with Pillow's 8-bit BILINEAR
+ * resampler (bit-identical bytes) -> ToTensor -> Normalize(mean, std) (host float[3] each) -> the
+ * encoder's input layout.  max_h / max_w bound the sizes (downscale <= sat_images_max_downscale()). */
+enum { SAT_IMG_NCHW = 0, SAT_IMG_NHWC = 1, SAT_IMG_S2D16 = 2 };
+size_t sat_images_workspace_bytes(int B, int OH, int OW);
+int sat_images_max_downscale(void);
+int sat_images_to_input(const uint8_t* pixels, const int64_t* offsets, const int32_t* sizes, int B, int max_h,
+                        int max_w, int OH, int OW, const float* mean, const float* std, int layout, int c_pad,
+                        int dtype, void* out, void* workspace, size_t workspace_bytes, void* stream);
+
 /* --- optimiser (torch.optim.Adam single-tensor step, train.py:71,164) ---- */
 int sat_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                   void* param_lp, int64_t n, float beta1, float beta2, float eps,

@@ -7,9 +7,11 @@ C ABI in include/sat_hip.h (libsat_hip.so, loaded with ctypes).
 """
 from . import _lib
 from .attention import Attention
+from .data import PackedImages, collate_packed
 from .decoder import Decoder
 from .encoder import Encoder
 from .loss import caption_loss, special_ids, StepMetrics, RunningMeters
 from .optim import Adam
 
-__all__ = ["Attention", "Decoder", "Encoder", "caption_loss", "special_ids", "StepMetrics", "RunningMeters", "Adam"]
+__all__ = ["Attention", "Decoder", "Encoder", "caption_loss", "special_ids", "StepMetrics", "RunningMeters", "Adam",
+           "PackedImages", "collate_packed"]

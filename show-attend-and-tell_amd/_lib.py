@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SAT_HIP_LIB_TUNING") or os.path.join(_HERE, "libsat_hip.so")   # override: A/B builds only
 
 SAT_F32, SAT_BF16 = 0, 1
+IMG_NCHW, IMG_NHWC, IMG_S2D16 = 0, 1, 2
 ACT_NONE, ACT_RELU, ACT_TANH, ACT_SIGMOID = 0, 1, 2, 3
 
 c_int, c_int64, c_float, c_void_p, c_size_t, c_uint64 = (ctypes.c_int, ctypes.c_int64, ctypes.c_float,
@@ -97,6 +98,11 @@ _SIGNATURES = [
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("sat_caption_loss_backward_relu", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float,
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("sat_images_workspace_bytes", c_size_t, [c_int, c_int, c_int]),
+    ("sat_images_max_downscale", c_int, []),
+    ("sat_images_to_input", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                    ctypes.POINTER(c_float), ctypes.POINTER(c_float), c_int, c_int, c_int, c_void_p,
+                                    c_void_p, c_size_t, c_void_p]),
     ("sat_adam_step", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
                               c_float, c_float, c_float, c_void_p]),
 ]

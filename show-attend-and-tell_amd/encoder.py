@@ -33,6 +33,7 @@ import torch.nn as nn
 
 from . import _lib as L
 from . import ops
+from .data import PackedImages
 
 VGG19_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M", 512, 512, 512, 512, "M"]
 IN_PAD = 8  # input channels padded 3 -> 8 (16-B bf16 vectors in the im2col loader)
@@ -223,10 +224,20 @@ class Encoder(nn.Module):
         """Images [B,3,H,W] -> features [B, L, D].  ``steps=(start, stop)`` runs a slice of the
         plan (stage_starts()): start > 0 takes the NHWC activation the previous slice returned,
         stop < len(plan) returns the NHWC activation instead of [B, L, D]."""
-        L.require_device(x)
+        packed = isinstance(x, PackedImages)
+        L.require_device(x.pixels if packed else x)
         dtype = dtype or self.compute_dtype
-        plan = self.compiled_plan(x.device, dtype)
+        plan = self.compiled_plan((x.pixels if packed else x).device, dtype)
         start, stop = steps if steps is not None else (0, len(plan))
+        if packed:   # decoded uint8 images: resize + normalize straight into the first layer's layout
+            if start > 0:
+                raise ValueError("Encoder: packed images enter at plan step 0")
+            if plan[0][0] == "stem_s2d":
+                y = ops.images_to_input(x, L.IMG_S2D16, dtype)
+                y = self._conv(y, plan[0][1], True, out_hw=(y.shape[1], y.shape[2]))
+            else:
+                y = ops.images_to_input(x, L.IMG_NHWC, dtype, c_pad=IN_PAD)
+            return self._run_plan(y, plan, stop)
         if start > 0:
             y = x
             for step in plan[start:stop]:
@@ -243,6 +254,9 @@ class Encoder(nn.Module):
             y = self._conv(ops.nchw_to_nhwc(x, IN_PAD, dtype), plan[0][2], True)
         else:
             y = ops.nchw_to_nhwc(x, IN_PAD, dtype)
+        return self._run_plan(y, plan, stop)
+
+    def _run_plan(self, y, plan, stop):
         for step in plan[:stop]:
             if step[0] == "stem_s2d":
                 continue

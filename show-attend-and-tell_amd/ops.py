@@ -96,6 +96,46 @@ def nchw_to_s2d(x, dtype):
     return y
 
 
+# Normalize(mean, std) of the reference's transform (train.py:27-32), as float32
+IMAGE_MEAN = (0.485, 0.456, 0.406)
+IMAGE_STD = (0.229, 0.224, 0.225)
+
+
+def images_to_input(packed, layout=L.IMG_NCHW, dtype=torch.float32, c_pad=8, size=(224, 224),
+                    mean=IMAGE_MEAN, std=IMAGE_STD):
+    """Decoded uint8 images (a device-resident ``data.PackedImages``) -> the reference's
+    Resize(size) + ToTensor + Normalize(mean, std), bit-identical to PIL + torch, written straight
+    into ``layout``: IMG_NCHW [B,3,H,W] f32, IMG_NHWC [B,H,W,c_pad] (dtype) or IMG_S2D16
+    [B,H/2,W/2,16] (dtype)."""
+    L.require_device(packed.pixels, packed.offsets, packed.sizes)
+    lib = L.lib()
+    B = packed.count
+    OH, OW = size
+    mx = lib.sat_images_max_downscale()
+    if packed.max_h > mx * OH or packed.max_w > mx * OW:
+        raise ValueError(f"images_to_input: {packed.max_h}x{packed.max_w} exceeds the {mx}x downscale limit "
+                         f"to {OH}x{OW}")
+    dev = packed.pixels.device
+    if layout == L.IMG_NCHW:
+        if dtype != torch.float32:
+            raise TypeError("images_to_input: the NCHW layout is the reference's float32 tensor")
+        out = torch.empty(B, 3, OH, OW, device=dev, dtype=torch.float32)
+    elif layout == L.IMG_NHWC:
+        out = torch.empty(B, OH, OW, c_pad, device=dev, dtype=dtype)
+    elif layout == L.IMG_S2D16:
+        out = torch.empty(B, OH // 2, OW // 2, 16, device=dev, dtype=dtype)
+    else:
+        raise ValueError(f"images_to_input: unknown layout {layout}")
+    ws_bytes = lib.sat_images_workspace_bytes(B, OH, OW)
+    ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
+    m = (ctypes.c_float * 3)(*mean)
+    sd = (ctypes.c_float * 3)(*std)
+    L.check(lib.sat_images_to_input(L.ptr(packed.pixels), L.ptr(packed.offsets), L.ptr(packed.sizes), B,
+                                    packed.max_h, packed.max_w, OH, OW, m, sd, layout, c_pad, L.dtype_code(dtype),
+                                    L.ptr(out), L.ptr(ws), ws_bytes, L.stream_of(out)), "sat_images_to_input")
+    return out
+
+
 def conv2d_nhwc(x, w, bias, stride, pad, relu, residual=None, out=None, out_hw=None):
     """x [N,H,W,C] ; w [Cout,KH,KW,C] (same dtype) ; bias f32 [Cout].  ``pad`` pads top/left;
     ``out_hw`` (default: symmetric padding) fixes the output size."""

@@ -15,6 +15,10 @@ so it cannot be disabled, as in train.py:450), plus:
                   trunk is randomly initialised under --seed (no pretrained weights offline).  Either
                   way the trunk actually used is saved as <out>/encoder_<network>.pth and recorded in
                   model_config.json, so generate_caption.py runs the same encoder
+  --host-preprocess  resize + normalize on the DataLoader workers (default: workers only decode, the
+                  uint8 images travel at native size and sat_images_to_input resamples them on the GPU,
+                  bit-identical to PIL's bilinear resize + torchvision's ToTensor / Normalize)
+  --workers       decode workers per rank (default 8)
   --bert-embeddings  a local [30522, 768] bert-base-uncased word-embedding table (a tensor, or a
                   state_dict holding embeddings.word_embeddings.weight / embedding.weight)
 Multi-GPU: ``python -m torch.distributed.run --nproc-per-node N show-attend-and-tell_amd/train.py ...``
@@ -63,7 +67,8 @@ class JsonCaptionDataset(torch.utils.data.Dataset):
     """The reference's on-disk layout (generate_json_data.py:51-63, dataset.py:15-52), loaded
     lazily per item (the reference decodes every image eagerly into RAM, which does not fit COCO)."""
 
-    def __init__(self, data_path, split_type="train", fraction=1.0, bert=False):
+    def __init__(self, data_path, split_type="train", fraction=1.0, bert=False, decode_only=False):
+        self.decode_only = decode_only   # uint8 HWC at native size; resize + normalize run on the GPU
         self.paths = json.load(open(os.path.join(data_path, f"{split_type}_img_paths.json")))
         name = f"{split_type}_captions_bert.json" if bert else f"{split_type}_captions.json"
         self.captions = json.load(open(os.path.join(data_path, name)))
@@ -80,11 +85,14 @@ class JsonCaptionDataset(torch.utils.data.Dataset):
 
     def __getitem__(self, i):
         from PIL import Image
-        with open(self.paths[i], "rb") as f:
-            img = Image.open(f).convert("RGB").resize((224, 224), Image.BILINEAR)
+        with open(self.paths[i], "rb") as f:   # dataset.py:9-12
+            img = Image.open(f).convert("RGB")
+        caps = torch.tensor(self.captions[i]), torch.tensor(self.all_captions[i])
+        if self.decode_only:
+            return (np.asarray(img, dtype=np.uint8),) + caps
+        img = img.resize((224, 224), Image.BILINEAR)   # host transform (train.py:27-32), --host-preprocess
         x = (np.asarray(img, dtype=np.float32) / 255.0 - MEAN) / STD
-        return torch.from_numpy(x.transpose(2, 0, 1).copy()), torch.tensor(self.captions[i]), \
-            torch.tensor(self.all_captions[i])
+        return (torch.from_numpy(x.transpose(2, 0, 1).copy()),) + caps
 
 
 class SyntheticDataset(torch.utils.data.Dataset):
@@ -137,6 +145,10 @@ def parse(argv=None):
                    help="encode each batch right before its decoder step instead of one batch ahead on a side stream")
     p.add_argument("--encoder-weights", type=str, default=None,
                    help="torchvision-layout encoder state_dict (weights_only); default: random init under --seed")
+    p.add_argument("--host-preprocess", action="store_true",
+                   help="resize + normalize on the host workers (default: workers only decode; the GPU resamples "
+                        "the uint8 images bit-identically to PIL and normalizes into the encoder's input layout)")
+    p.add_argument("--workers", type=int, default=8, help="DataLoader decode workers per rank")
     p.add_argument("--bert-embeddings", type=str, default=None,
                    help="local bert-base-uncased word-embedding table [30522, 768] (weights_only)")
     return p.parse_args(argv)
@@ -213,8 +225,9 @@ def loaders(args, split, rank, world):
                               args.vocab if not args.bert else sat_amd.Decoder.BERT_VOCAB,
                               32 if args.bert else args.seq, args.bert, seed=args.seed * 10 + SPLIT_SEED[split])
     else:
-        ds = JsonCaptionDataset(args.data, split, args.fraction, args.bert)
+        ds = JsonCaptionDataset(args.data, split, args.fraction, args.bert, decode_only=not args.host_preprocess)
     train = split == "train"
+    packed = not args.synthetic and not args.host_preprocess
     if world > 1:
         sampler = torch.utils.data.distributed.DistributedSampler(ds, world, rank, shuffle=True, seed=args.seed) \
             if train else ShardSampler(len(ds), rank, world)
@@ -222,8 +235,9 @@ def loaders(args, split, rank, world):
         sampler = None
     # train.py:76-88: the reference shuffles train only and keeps every validation / test batch
     return torch.utils.data.DataLoader(ds, batch_size=args.batch_size, shuffle=train and sampler is None,
-                                       sampler=sampler, num_workers=4 if not args.synthetic else 0, pin_memory=True,
-                                       drop_last=train)
+                                       sampler=sampler, num_workers=args.workers if not args.synthetic else 0,
+                                       pin_memory=True, drop_last=train,
+                                       collate_fn=sat_amd.collate_packed if packed else None)
 
 
 def encoded_batches(loader, encoder, device, dt, max_steps, overlap):
@@ -237,7 +251,7 @@ def encoded_batches(loader, encoder, device, dt, max_steps, overlap):
 
     def encode(imgs, captions):
         with torch.cuda.stream(side), torch.no_grad():
-            imgs = imgs.to(device, non_blocking=True)
+            imgs = imgs.to(device, non_blocking=True)   # a Tensor, or PackedImages (uint8, native size)
             captions = captions.to(device, non_blocking=True)
             feats = encoder(imgs, dtype=dt)
             ev = torch.cuda.Event()
@@ -299,7 +313,7 @@ def evaluate(epoch, encoder, decoder, loader, args, device, dt, word_dict, mode,
         for batch_idx, (imgs, captions, all_caps) in enumerate(loader):
             if args.max_steps and batch_idx >= args.max_steps:
                 break
-            imgs, captions = imgs.to(device), captions.to(device)
+            imgs, captions = imgs.to(device), captions.to(device)   # Tensor or PackedImages
             preds, alphas = decoder(encoder(imgs, dtype=dt), captions)
             loss, metrics = sat_amd.caption_loss(preds, alphas, captions, args.alpha_c, pad, skip)
             m = sat_amd.StepMetrics(loss, metrics).values()

@@ -997,3 +997,88 @@ def test_bleu4_parity_teacher_forced(sat):
                    ((1, 0, 0, 0), (0.5, 0.5, 0, 0), (0.33, 0.33, 0.33, 0), (0.25, 0.25, 0.25, 0.25)))
     assert ours == theirs
     assert 0.0 < ours[3] < 1.0
+
+
+# ---------------------------------------------------------------------------- streaming image input (f4)
+def _image_batch(seed=0):
+    from tests.karpathy_fixture import SIZES
+    rng = np.random.default_rng(seed)
+    sizes = SIZES + [(1000, 231), (7, 3000), (225, 223)]
+    return [rng.integers(0, 256, (h, w, 3), dtype=np.uint8) for h, w in sizes]
+
+
+def test_images_to_input_bit_exact(sat):
+    """sat_images_to_input == Pillow BILINEAR resize + ToTensor + Normalize (oracle/pil_resize.py, itself
+    pinned bit-exact against PIL by tests/test_cpu_images.py), bit for bit, in every output layout."""
+    from oracle import pil_resize as PR
+    from sat_amd import ops, _lib as Lb
+    imgs = _image_batch()
+    ref = torch.from_numpy(np.stack([PR.transform(a) for a in imgs]))            # [B,3,224,224] f32
+    packed = sat.PackedImages.from_arrays(imgs).to(DEV)
+    got = ops.images_to_input(packed, Lb.IMG_NCHW, torch.float32)
+    assert torch.equal(got.cpu(), ref)
+    refd = ref.to(DEV)
+    for dt in (torch.float32, torch.bfloat16):
+        s2d = ops.images_to_input(packed, Lb.IMG_S2D16, dt)
+        assert torch.equal(s2d, ops.nchw_to_s2d(refd, dt))
+        nhwc = ops.images_to_input(packed, Lb.IMG_NHWC, dt, c_pad=8)
+        assert torch.equal(nhwc, ops.nchw_to_nhwc(refd, 8, dt))
+
+
+def test_images_to_input_rejects_oversized(sat):
+    from sat_amd import ops, _lib as Lb
+    packed = sat.PackedImages.from_arrays([np.zeros((16 * 224, 300, 3), np.uint8)]).to(DEV)
+    with pytest.raises(ValueError):
+        ops.images_to_input(packed, Lb.IMG_NCHW, torch.float32)
+
+
+@pytest.mark.parametrize("network", ["vgg19", "resnet152"])
+def test_encoder_packed_images_equal_tensor_input(sat, network):
+    """Encoder(PackedImages) (resize + normalize fused into the first layer's layout) returns exactly
+    the features of Encoder(the reference's transformed NCHW tensor)."""
+    from oracle import pil_resize as PR
+    imgs = _image_batch(1)[:3]
+    torch.manual_seed(0)
+    enc = sat.Encoder(network, dtype=torch.bfloat16).to(DEV).eval()
+    x = torch.from_numpy(np.stack([PR.transform(a) for a in imgs])).to(DEV)
+    with torch.no_grad():
+        a = enc(x)
+        b = enc(sat.PackedImages.from_arrays(imgs).to(DEV))
+    assert torch.equal(a, b)
+
+
+def test_cli_karpathy_fixture_streaming(sat, tmp_path, capsys):
+    """train.py on a Karpathy-layout fixture (PNG files + JSON): the default streaming path (workers
+    decode, the GPU resizes) logs exactly the losses of --host-preprocess (PIL resize on the host)."""
+    import json as _json
+    from sat_amd import train as T
+    from tests.karpathy_fixture import make_fixture
+    make_fixture(str(tmp_path / "data"))
+    from sat_amd import ops
+    logs = {}
+    for mode in ("stream", "host"):
+        argv = ["--data", str(tmp_path / "data"), "--epochs", "1", "--batch-size", "4", "--network", "vgg19",
+                "--tf", "--ado", "--attention", "--out", str(tmp_path / mode), "--workers", "0", "--log-interval", "1",
+                "--dtype", "fp32"]
+        if mode == "host":
+            argv.append("--host-preprocess")
+        capsys.readouterr()
+        try:
+            T.main(argv)
+        finally:
+            ops.set_decoder_split_target(0)   # main() sets the overlap split target process-wide
+        out = capsys.readouterr().out
+        logs[mode] = [_json.loads(l) for l in out.splitlines() if l.startswith("{")]
+    a = [r for r in logs["stream"] if "epoch_seconds" not in r]
+    b = [r for r in logs["host"] if "epoch_seconds" not in r]
+    assert any("train_loss" in r for r in a) and any("test_bleu4" in r for r in a)
+    assert [sorted(r) for r in a] == [sorted(r) for r in b]
+    # the first batch sees identical features and weights: bit-equal; later ones may differ by the
+    # fp32 summation order of atomically accumulated weight gradients
+    assert a[0]["train_loss"] == b[0]["train_loss"]
+    for ra, rb in zip(a, b):
+        for k, v in ra.items():
+            if isinstance(v, float):
+                assert abs(v - rb[k]) <= 1e-3 * max(1.0, abs(rb[k])), (k, v, rb[k])
+            else:
+                assert v == rb[k], k
