@@ -134,6 +134,21 @@ int sat_nchw_to_s2d(int N, int C, int H, int W, int dtype, const float* x, void*
  * covers Conv2d+ReLU (VGG19) and Conv2d+BatchNorm(eval, folded)+[residual]+ReLU (ResNet152). */
 int sat_conv2d_nhwc(const SatConvGeom* g, int Cout, int dtype, const void* x, const void* w,
                     const float* bias, const void* residual, int relu, void* y, void* stream);
+/* Weight re-layout for register-direct MFMA fragment loads (once per weight version):
+ * src [N][K] bf16 row-major -> dst [N/16][K/32][64][8], lane l = 16*(k8 % 4) + (n % 16) of block
+ * (n / 16, k / 32) holding src[n][32*(k/32) + 8*(l >> 4) .. +8].  N % 16 == 0, K % 32 == 0. */
+int sat_mfma_frag_layout(int N, int K, const void* src, void* dst, void* stream);
+/* 1 if sat_bottleneck_fused runs this geometry (today: bf16, 14x14, Cin 1024, Cmid 256 -- the 35
+ * identity blocks of ResNet152 layer3), else 0. */
+int sat_bottleneck_fused_supported(int H, int W, int Cin, int Cmid, int dtype);
+/* One torchvision Bottleneck with identity residual and stride 1, eval-BN folded (encoder.py:13-17,
+ * 33-36 through torchvision): y = relu(c3(relu(c2(relu(c1(x))))) + x) in ONE launch; c1/c2 outputs
+ * stay on chip.  x, y NHWC [N,H,W,Cin] (x != y); w1f/w2f/w3f: sat_mfma_frag_layout of the folded
+ * [Cmid][Cin], [Cmid][3*3*Cmid] (tap-major) and [Cin][Cmid] weights; b1/b2/b3 folded fp32 biases.
+ * Bit-identical to the three sat_conv2d_nhwc launches it replaces. */
+int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int dtype, const void* x, const void* w1f,
+                         const float* b1, const void* w2f, const float* b2, const void* w3f, const float* b3,
+                         void* y, void* stream);
 /* MaxPool2d (floor mode, -inf padding) on NHWC. */
 int sat_maxpool2d_nhwc(int N, int H, int W, int C, int k, int stride, int pad, int dtype,
                        const void* x, void* y, int OH, int OW, void* stream);

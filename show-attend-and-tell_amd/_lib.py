@@ -72,6 +72,10 @@ _SIGNATURES = [
     ("sat_nchw_to_s2d", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     ("sat_conv2d_nhwc", c_int, [ctypes.POINTER(SatConvGeom), c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_int, c_void_p, c_void_p]),
+    ("sat_mfma_frag_layout", c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    ("sat_bottleneck_fused_supported", c_int, [c_int, c_int, c_int, c_int, c_int]),
+    ("sat_bottleneck_fused", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("sat_maxpool2d_nhwc", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                    c_int, c_int, c_void_p]),
     ("sat_attention_forward", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,

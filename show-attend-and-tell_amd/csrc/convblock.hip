@@ -1,0 +1,341 @@
+// Fused ResNet bottleneck block (identity residual, stride 1) for gfx950 / MI355X.
+//
+//   y = relu(c3(relu(c2(relu(c1(x))))) + x)        c1 1x1 Cin->Cmid, c2 3x3/pad 1 Cmid->Cmid,
+//                                                  c3 1x1 Cmid->Cin, eval-BN folded into each conv
+// (torchvision Bottleneck.forward as the reference's encoder runs it, encoder.py:13-17,33-36.)
+//
+// Why: ResNet152's layer3 has 35 such blocks at 14 x 14 x 1024 (mid 256).  As three conv launches
+// each (convpipe.hip / convstream.hip) a block took ~90 us in the trunk graph: two intermediate
+// activations went through HBM, every launch paid its own prologue / epilogue / launch gap, and the
+// 196 tiles of 256 x 128 left 60 of 256 CUs idle.  Here one launch runs the whole block:
+//   * one workgroup per half image (RO = 7 output rows = 98 pixels): 256 workgroups for B = 128;
+//     c1 is computed for the 8 image rows c2 needs (its one-row halo), c1 and c2 outputs never
+//     leave LDS (X1: c1 rows + a zero row, X2: c2 rows, both bf16 in 64-channel planes of 128-B
+//     rows, 16-B chunk c of row r at slot c ^ (r & 7): conflict-free ds_read_b128 for every 3x3
+//     row shift, as in convhalo.hip);
+//   * 8 waves, each owning 32 output channels of the current 256-wide phase (n-blocks 2w, 2w+1) and
+//     all 7 16-row m-blocks; MFMA v_mfma_f32_16x16x32_bf16 computes C^T = W . X^T, so a lane holds
+//     4 consecutive channels of one pixel: epilogues write 8-byte pieces (X1 / X2 / global) without
+//     a transpose;
+//   * weights never touch LDS: they are pre-permuted once (sat_mfma_frag_layout) so that every
+//     16-B-per-lane fragment load of a wave is 1 KiB contiguous, and each wave streams its own
+//     n-blocks straight into VGPRs two k-tiles ahead (three register buffers); the compiler's own
+//     vmcnt tracking orders them;
+//   * c1's input rows are the only LDS-DMA stream (3-stage ring aliasing X2, counted vmcnt + one raw
+//     barrier per k-tile); c2 reads its A operand from X1 with a per-lane row shift per filter tap
+//     (taps in the image padding read the zero row), c3 from X2: neither needs a barrier per k-tile;
+//   * the whole 68-k-tile schedule (c1 16, c2 36, c3 4 x 4) is unrolled at compile time, so register
+//     buffers are static and the weight prefetch runs across phase boundaries.
+// Arithmetic: each conv sums its K in the same order as the unfused kernels (k-tiles ascending, c2
+// tap-major), adds the folded bias in fp32, applies ReLU and rounds to bf16 once; c3 adds the residual
+// in fp32 before the ReLU -- bit-identical to the three-launch path (tests/test_gpu_parity.py).
+#include "sat_common.h"
+#include "sat_internal.h"
+
+#include <utility>
+
+namespace {
+
+typedef __attribute__((address_space(3))) void k_lds_void;
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr unsigned K_OOB = 0x80000000u;
+
+// compile-time loop: f(std::integral_constant<int, T>) for T = 0 .. N-1 (register arrays indexed by
+// T stay static, every wait count is a literal)
+template <typename F, int... Ts>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Ts...>) {
+  (f(std::integral_constant<int, Ts>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+struct KArgs {
+  const bf16* x;      // [N][IH][IW][CIN]
+  const bf16* w1;     // fragment layout of [CMID][CIN]
+  const bf16* w2;     // fragment layout of [CMID][9][CMID]
+  const bf16* w3;     // fragment layout of [CIN][CMID]
+  const float* b1; const float* b2; const float* b3;
+  bf16* y;            // [N][IH][IW][CIN]
+  unsigned x_bytes;
+};
+
+template <int N>
+__device__ __forceinline__ void k_wait_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void k_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// IW: image width = height, RO: output image rows per workgroup (IW % RO == 0, IW / RO == 2),
+// CIN: block input/output channels, CMID: bottleneck width (256: one 256-wide phase per conv)
+template <int IW, int RO, int CIN, int CMID>
+__global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
+  static_assert(IW / RO == 2 && IW % RO == 0, "two workgroups per image");
+  static_assert(CMID == 256 && CIN % 256 == 0 && CIN % 64 == 0, "256-wide phases");
+  constexpr int IH = IW;
+  constexpr int PO = RO * IW;                    // output pixels per workgroup (98)
+  constexpr int R1 = RO + 1;                     // c1 image rows (one halo row)
+  constexpr int P1 = R1 * IW;                    // c1 pixels (112)
+  constexpr int MB1 = (P1 + 15) / 16, MB2 = (PO + 15) / 16;
+  static_assert(MB1 == 7 && MB2 == 7, "7 m-blocks per phase");
+  constexpr int MB = 7;
+  constexpr int ROWB = 128;                      // 64 channels per LDS row
+  constexpr int X1ROWS = P1 + 1;                 // + zero row
+  constexpr int X1PL = X1ROWS * ROWB;            // X1 plane bytes
+  constexpr int X2PL = MB2 * 16 * ROWB;          // X2 plane bytes
+  constexpr int NPL = CMID / 64;
+  constexpr int X1 = 0, X2 = NPL * X1PL;         // LDS regions
+  constexpr int RING = X2;                       // c1 input ring aliases X2
+  constexpr int STG = 128 * ROWB;                // 128 rows x 64 channels per stage
+  static_assert(3 * STG <= NPL * X2PL, "ring fits in X2");
+  constexpr int LDS = X2 + NPL * X2PL;
+  constexpr int KT1 = CIN / 64, KT2 = 9 * CMID / 64, NCK = CIN / 256, KT3C = CMID / 64;
+  constexpr int NT = KT1 + KT2 + NCK * KT3C;
+  constexpr int KS1 = CIN / 32, KS2 = 9 * CMID / 32, KS3 = CMID / 32;
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fh = lane >> 4;
+  const int img = blockIdx.x >> 1, half = blockIdx.x & 1;
+  const int y0 = half * RO;                      // first output image row
+  const int ws = half ? IH - R1 : 0;             // first c1 image row
+  const long pix_img = (long)img * IH * IW;
+
+  // ---- zero row of every X1 plane (taps in the padding read it) ----
+  if (tid < NPL * 8) *(uint4*)(smem + X1 + (tid >> 3) * X1PL + P1 * ROWB + (tid & 7) * 16) = make_uint4(0, 0, 0, 0);
+
+  // ---- c1 input ring: k-tile t = channels 64t.., 128 rows (rows >= P1 read zeros) ----
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, (int)a.x_bytes, 0x00020000);
+  unsigned dsrc[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int d = w * 2 + u, r = d * 8 + (lane >> 3), c = (lane & 7) ^ (lane >> 3);
+    dsrc[u] = r < P1 ? (unsigned)(((pix_img + (long)ws * IW + r) * CIN + 8 * c) * 2) : K_OOB;
+  }
+  auto dma_a = [&](int t) {
+    char* st = smem + RING + (t % 3) * STG;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (k_lds_void*)(st + (w * 2 + u) * 1024), 16,
+                                               dsrc[u] == K_OOB ? (int)K_OOB : (int)(dsrc[u] + t * 128), 0, 0, 0);
+  };
+
+  // ---- weight fragments: tile T of the 68-tile schedule, this wave's n-blocks, both 32-k halves ----
+  bf16x8 bq[3][2][2];
+  auto load_b = [&](int T, bf16x8 (&dst)[2][2]) {
+    const bf16* base;
+    int nb0, ks0, KS;
+    if (T < KT1) { base = a.w1; nb0 = 0; ks0 = 2 * T; KS = KS1; }
+    else if (T < KT1 + KT2) { base = a.w2; nb0 = 0; ks0 = 2 * (T - KT1); KS = KS2; }
+    else { const int t = T - KT1 - KT2; base = a.w3; nb0 = (t / KT3C) * 16; ks0 = 2 * (t % KT3C); KS = KS3; }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        dst[ks][j] = *(const bf16x8*)(base + ((long)((nb0 + w * 2 + j) * KS + ks0 + ks) * 64 + lane) * 8);
+  };
+
+  // ---- A fragment offsets: row i*16 + fr of a 128-B-row image = i * 2048 (immediate) + per-lane part ----
+  int offu[2];   // unshifted rows (c1 ring, X2)
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) offu[ks] = fr * ROWB + 16 * ((ks * 4 + fh) ^ (fr & 7));
+  // c2: output pixel p = i*16 + fr reads X1 row p + (y0 - ws) * IW + dh * IW + dw under tap (dh, dw),
+  // or the zero row P1 where the tap falls into the image padding (or p >= PO)
+  int offs[MB][2];
+  auto tap_offsets = [&](int tap) {
+    const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int p = i * 16 + fr, py = p / IW, pxx = p - py * IW;
+      const bool ok = p < PO && (unsigned)(y0 + py + dh) < (unsigned)IH && (unsigned)(pxx + dw) < (unsigned)IW;
+      const int q = ok ? p + (y0 - ws + dh) * IW + dw : P1;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) offs[i][ks] = q * ROWB + 16 * ((ks * 4 + fh) ^ (q & 7));
+    }
+  };
+
+  f32x4 acc[MB][2];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  // fragments + MFMAs of one 64-deep k-tile; A row block i at base + i * 16 * ROWB + offu (unshifted)
+  // or base + offs[i] (c2's shifted rows)
+  auto mma = [&](const bf16x8 (&af)[2][MB], const bf16x8 (&b)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto tile_u = [&](const char* base, const bf16x8 (&b)[2][2]) {
+    bf16x8 af[2][MB];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < MB; ++i) af[ks][i] = *(const bf16x8*)(base + i * 16 * ROWB + offu[ks]);
+    mma(af, b);
+  };
+  auto tile_s = [&](const char* base, const bf16x8 (&b)[2][2]) {
+    bf16x8 af[2][MB];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < MB; ++i) af[ks][i] = *(const bf16x8*)(base + offs[i][ks]);
+    mma(af, b);
+  };
+  // epilogue into an LDS plane image: lane holds channels w*32 + j*16 + 4fh .. +3 of pixel i*16 + fr
+  // bias values of the lane's channels, loaded well before their epilogue (a load issued at the
+  // epilogue would be younger than the weight prefetches and drain them)
+  auto load_bias = [&](const float* bias, int ch0, float4 (&bv)[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + ch0 + w * 32 + j * 16 + 4 * fh);
+  };
+  auto store_planes = [&](int region, int plane_bytes, const float4 (&bias)[2]) {
+    const int plane = w >> 1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float4 bv = bias[j];
+      const int c = (w & 1) * 4 + j * 2 + (fh >> 1);
+#pragma unroll
+      for (int i = 0; i < MB; ++i) {
+        const int r = i * 16 + fr;
+        u32x2 o;
+        bf16* ob = (bf16*)&o;
+        ob[0] = (bf16)fmaxf(acc[i][j][0] + bv.x, 0.f);
+        ob[1] = (bf16)fmaxf(acc[i][j][1] + bv.y, 0.f);
+        ob[2] = (bf16)fmaxf(acc[i][j][2] + bv.z, 0.f);
+        ob[3] = (bf16)fmaxf(acc[i][j][3] + bv.w, 0.f);
+        *(u32x2*)(smem + region + plane * plane_bytes + r * ROWB + 16 * (c ^ (r & 7)) + 8 * (fh & 1)) = o;
+      }
+    }
+  };
+
+  // ---- prologue ----
+  float4 bias_a[2], bias_b[2];
+  load_bias(a.b1, 0, bias_a);
+  dma_a(0);
+  load_b(0, bq[0]);
+  dma_a(1);
+  load_b(1, bq[1]);
+  zero_acc();
+  u32x2 resv[MB][2];
+
+  static_for<NT>([&](auto Tc) {
+    constexpr int T = decltype(Tc)::value;
+    if constexpr (T < KT1) {
+      // this wave's DMAs of input tile T have landed; younger: B(T), [A(T+1)], B(T+1)
+      if constexpr (T + 1 < KT1) k_wait_barrier<10>();
+      else k_wait_barrier<8>();
+      if constexpr (T + 2 < KT1) dma_a(T + 2);
+    }
+    if constexpr (T + 2 < NT) load_b(T + 2, bq[(T + 2) % 3]);
+    if constexpr (T < KT1) {
+      tile_u(smem + RING + (T % 3) * STG, bq[T % 3]);
+      if constexpr (T == KT1 - 1) {   // c1 epilogue -> X1 (the ring is read for the last time above)
+        store_planes(X1, X1PL, bias_a);
+        zero_acc();
+        k_lds_barrier();
+      }
+    } else if constexpr (T < KT1 + KT2) {
+      constexpr int t = T - KT1, tap = t / (CMID / 64), pl = t % (CMID / 64);
+      if constexpr (t == 0) load_bias(a.b2, 0, bias_b);
+      if constexpr (pl == 0) tap_offsets(tap);
+      tile_s(smem + X1 + pl * X1PL, bq[T % 3]);
+      if constexpr (t == KT2 - 1) {   // c2 epilogue -> X2
+        store_planes(X2, X2PL, bias_b);
+        zero_acc();
+        k_lds_barrier();
+      }
+    } else {
+      constexpr int t = T - KT1 - KT2, ck = t / KT3C, kt = t % KT3C;
+      if constexpr (kt == 0) {   // residual rows + bias of this 256-channel chunk, needed by its epilogue
+        load_bias(a.b3, ck * 256, bias_a);
+#pragma unroll
+        for (int i = 0; i < MB; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {   // rows past PO load a valid row (never stored): no branch
+            const int p = min(i * 16 + fr, PO - 1), ch = ck * 256 + w * 32 + j * 16 + 4 * fh;
+            resv[i][j] = *(const u32x2*)(a.x + (pix_img + (long)y0 * IW + p) * CIN + ch);
+          }
+      }
+      tile_u(smem + X2 + kt * X2PL, bq[T % 3]);
+      if constexpr (kt == KT3C - 1) {   // c3 epilogue: bias, fp32 residual add, ReLU, one rounding, 8-B stores
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int ch = ck * 256 + w * 32 + j * 16 + 4 * fh;
+          const float4 bv = bias_a[j];
+#pragma unroll
+          for (int i = 0; i < MB; ++i) {
+            const int p = i * 16 + fr;
+            const bf16* rh = (const bf16*)&resv[i][j];
+            float v[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
+            u32x2 o;
+            bf16* ob = (bf16*)&o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ob[e] = (bf16)fmaxf(v[e] + (float)rh[e], 0.f);
+            if (p < PO) *(u32x2*)(a.y + (pix_img + (long)y0 * IW + p) * CIN + ch) = o;
+          }
+        }
+        zero_acc();
+      }
+    }
+  });
+}
+
+// [N][K] bf16 -> [N/16][K/32][64 lanes][8]: lane l = (fh << 4) | fr holds row 16 nb + fr, k 32 ks + 8 fh ..
+__global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst, int N, int K) {
+  const long n8 = (long)N * K / 8;
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
+    const long e = v * 8;                      // destination element
+    const int lane = (int)((e / 8) % 64);
+    const long blk = e / 512;                  // (nb, ks)
+    const int KS = K / 32;
+    const int nb = (int)(blk / KS), ks = (int)(blk % KS);
+    const int row = nb * 16 + (lane & 15), k = ks * 32 + (lane >> 4) * 8;
+    *(uint4*)(dst + e) = *(const uint4*)(src + (long)row * K + k);
+  }
+}
+
+}  // namespace
+
+extern "C" int sat_mfma_frag_layout(int N, int K, const void* src, void* dst, void* stream) {
+  SAT_REQUIRE(src && dst && N > 0 && K > 0 && N % 16 == 0 && K % 32 == 0);
+  SAT_REQUIRE(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0);
+  const long n8 = (long)N * K / 8;
+  const int g = (int)((n8 + 255) / 256 < 4096 ? (n8 + 255) / 256 : 4096);
+  hipLaunchKernelGGL(frag_layout_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16*)src, (bf16*)dst, N, K);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sat_bottleneck_fused_supported(int H, int W, int Cin, int Cmid, int dtype) {
+  return dtype == SAT_BF16 && H == 14 && W == 14 && Cin == 1024 && Cmid == 256;
+}
+
+extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int dtype, const void* x, const void* w1f,
+                                    const float* b1, const void* w2f, const float* b2, const void* w3f,
+                                    const float* b3, void* y, void* stream) {
+  SAT_REQUIRE(N > 0 && x && w1f && w2f && w3f && b1 && b2 && b3 && y && x != y);
+  SAT_REQUIRE(sat_bottleneck_fused_supported(H, W, Cin, Cmid, dtype));
+  auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
+  SAT_REQUIRE(al(x, 16) && al(y, 16) && al(w1f, 16) && al(w2f, 16) && al(w3f, 16) && al(b1, 16) && al(b2, 16) &&
+              al(b3, 16));
+  const long x_bytes = 2L * N * H * W * Cin;
+  SAT_REQUIRE(x_bytes < (1L << 31));
+  KArgs a{};
+  a.x = (const bf16*)x; a.y = (bf16*)y;
+  a.w1 = (const bf16*)w1f; a.w2 = (const bf16*)w2f; a.w3 = (const bf16*)w3f;
+  a.b1 = b1; a.b2 = b2; a.b3 = b3;
+  a.x_bytes = (unsigned)x_bytes;
+  hipLaunchKernelGGL((bottleneck_kernel<14, 7, 1024, 256>), dim3(2 * N), dim3(512), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}

@@ -144,6 +144,9 @@ class Encoder(nn.Module):
         self._plan_key = None
         self.timing = None   # bench hook: list collecting (start, end) HIP events around every conv launch
         self.timing_args = None   # bench hook: list collecting every conv launch's arguments
+        # identity-residual bottlenecks the fused kernel supports run as ONE launch
+        # (sat_bottleneck_fused, csrc/convblock.hip); False = three conv launches (A/B, tests)
+        self.fuse_blocks = True
 
     def _conv(self, x, f, relu, residual=None, out_hw=None):
         w, b, s, p = f
@@ -189,7 +192,7 @@ class Encoder(nn.Module):
                 for blk in layer:
                     ds = self._fold(blk.downsample[0], blk.downsample[1]) if blk.downsample is not None else None
                     plan.append(("block", self._fold(blk.conv1, blk.bn1), self._fold(blk.conv2, blk.bn2),
-                                 self._fold(blk.conv3, blk.bn3), ds))
+                                 self._fold(blk.conv3, blk.bn3), ds, self._fused_weights(plan, blk, ds)))
         else:
             first = True
             for i, m in enumerate(mods):
@@ -200,6 +203,23 @@ class Encoder(nn.Module):
                 elif isinstance(m, nn.MaxPool2d):
                     plan.append(("pool", m.kernel_size, m.stride, m.padding))
         self._plan = plan
+
+    def _fused_weights(self, plan, blk, ds):
+        """Fragment-layout weights of an identity-residual bottleneck the fused kernel runs, else None."""
+        if ds is not None or blk.conv2.stride[0] != 1 or self.compute_dtype != torch.bfloat16 \
+                or not blk.conv1.weight.is_cuda:
+            return None
+        # spatial size at this block: the trunk halves it at each stride-2 step (224 input assumed
+        # by the plan; forward checks the activation's real size before taking the fused path)
+        cin, cmid = blk.conv1.in_channels, blk.conv1.out_channels
+        hw = {256: 56, 512: 28, 1024: 14, 2048: 7}.get(cin)
+        if hw is None or not ops.bottleneck_fused_supported(hw, hw, cin, cmid, self.compute_dtype):
+            return None
+        frags = []
+        for conv, bn in ((blk.conv1, blk.bn1), (blk.conv2, blk.bn2), (blk.conv3, blk.bn3)):
+            w, b, _, _ = self._fold(conv, bn)
+            frags.append((ops.mfma_frag_layout(w.reshape(w.shape[0], -1)), b))
+        return tuple(frags)
 
     def compiled_plan(self, device, dtype):
         key = self._state_key(device, dtype)
@@ -271,7 +291,10 @@ class Encoder(nn.Module):
             return self._conv(y, step[1], step[2])
         if step[0] == "pool":
             return ops.maxpool2d_nhwc(y, step[1], step[2], step[3])
-        _, c1, c2, c3, ds = step
+        _, c1, c2, c3, ds, fused = step
+        if (fused is not None and self.fuse_blocks and self.timing is None and self.timing_args is None
+                and ops.bottleneck_fused_supported(y.shape[1], y.shape[2], y.shape[3], c1[0].shape[0], y.dtype)):
+            return ops.bottleneck_fused(y, *fused)
         out = self._conv(y, c1, True)
         out = self._conv(out, c2, True)
         idn = self._conv(y, ds, False) if ds is not None else y

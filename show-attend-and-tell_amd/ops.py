@@ -157,6 +157,33 @@ def conv2d_nhwc(x, w, bias, stride, pad, relu, residual=None, out=None, out_hw=N
     return y
 
 
+def mfma_frag_layout(w2d):
+    """[N, K] bf16 -> the register-direct MFMA fragment layout sat_bottleneck_fused streams."""
+    L.require_device(w2d)
+    N, K = w2d.shape
+    src = w2d.contiguous()
+    dst = torch.empty_like(src)
+    L.check(L.lib().sat_mfma_frag_layout(N, K, L.ptr(src), L.ptr(dst), L.stream_of(dst)), "sat_mfma_frag_layout")
+    return dst
+
+
+def bottleneck_fused_supported(H, W, Cin, Cmid, dtype):
+    return bool(L.lib().sat_bottleneck_fused_supported(H, W, Cin, Cmid, L.dtype_code(dtype)))
+
+
+def bottleneck_fused(x, f1, f2, f3, out=None):
+    """One identity-residual stride-1 bottleneck in one launch.  x NHWC [N,H,W,Cin]; f1/f2/f3 =
+    (fragment-layout weight, fp32 bias) of the folded c1 / c2 / c3 (Encoder plan)."""
+    L.require_device(x)
+    N, H, W, C = x.shape
+    Cmid = f1[1].shape[0]
+    y = out if out is not None else torch.empty_like(x)
+    L.check(L.lib().sat_bottleneck_fused(N, H, W, C, Cmid, L.dtype_code(x.dtype), L.ptr(x), L.ptr(f1[0]),
+                                         L.ptr(f1[1]), L.ptr(f2[0]), L.ptr(f2[1]), L.ptr(f3[0]), L.ptr(f3[1]),
+                                         L.ptr(y), L.stream_of(y)), "sat_bottleneck_fused")
+    return y
+
+
 def maxpool2d_nhwc(x, k, stride, pad=0):
     L.require_device(x)
     N, H, W, C = x.shape

@@ -1082,3 +1082,64 @@ def test_cli_karpathy_fixture_streaming(sat, tmp_path, capsys):
                 assert abs(v - rb[k]) <= 1e-3 * max(1.0, abs(rb[k])), (k, v, rb[k])
             else:
                 assert v == rb[k], k
+
+
+# ---------------------------------------------------------------------------- fused bottleneck block
+def test_mfma_frag_layout_exact(sat):
+    """sat_mfma_frag_layout: [N][K] -> [N/16][K/32][lane][8], lane = 16 * (k-chunk) + row."""
+    from sat_amd import ops
+    g = torch.Generator().manual_seed(3)
+    w = torch.randn(48, 96, generator=g).bfloat16()
+    ref = w.view(3, 16, 3, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(48, 96)
+    assert torch.equal(ops.mfma_frag_layout(w.to(DEV)).cpu(), ref)
+
+
+def _bottleneck_operands(N, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(N, 14, 14, 1024, generator=g).relu().bfloat16()   # a block input is post-ReLU
+
+    def conv(cout, cin, k):
+        w = (torch.randn(cout, k, k, cin, generator=g) * math.sqrt(2.0 / (k * k * cin))).bfloat16()
+        return w.to(DEV), (0.1 * torch.randn(cout, generator=g)).to(DEV)
+    return x.to(DEV), (conv(256, 1024, 1), conv(256, 256, 3), conv(1024, 256, 1))
+
+
+@pytest.mark.parametrize("N", [1, 3])
+def test_bottleneck_fused_bit_identical(sat, N):
+    """csrc/convblock.hip runs a ResNet152 layer3 identity bottleneck (14x14, 1024 -> 256 -> 1024) as one
+    launch: bit-identical to the three conv launches it replaces (same fp32 sums, bias, ReLU and
+    residual order, one bf16 rounding per conv) and close to torch fp32 on the same bf16 operands."""
+    from sat_amd import ops
+    xd, ((w1, b1), (w2, b2), (w3, b3)) = _bottleneck_operands(N, 10 + N)
+    y1 = ops.conv2d_nhwc(xd, w1, b1, 1, 0, True)
+    y2 = ops.conv2d_nhwc(y1, w2, b2, 1, 1, True)
+    ref = ops.conv2d_nhwc(y2, w3, b3, 1, 0, True, residual=xd)
+    frags = [(ops.mfma_frag_layout(w.reshape(w.shape[0], -1)), b) for w, b in ((w1, b1), (w2, b2), (w3, b3))]
+    y = ops.bottleneck_fused(xd, *frags)
+    torch.cuda.synchronize()
+    d = (y.float() - ref.float()).abs().max().item()
+    assert torch.equal(y, ref), f"max |fused - unfused| = {d}"
+    # torch fp32 of the same operands (intermediates rounded to bf16 as both kernels do)
+    nchw = lambda t: t.float().permute(0, 3, 1, 2).cpu()   # noqa: E731
+    wt = lambda w: w.float().permute(0, 3, 1, 2).cpu()      # noqa: E731
+    t1 = torch.relu(F.conv2d(nchw(xd), wt(w1), b1.cpu())).bfloat16().float()
+    t2 = torch.relu(F.conv2d(t1, wt(w2), b2.cpu(), padding=1)).bfloat16().float()
+    t3 = torch.relu(F.conv2d(t2, wt(w3), b3.cpu()) + nchw(xd))
+    assert rel(nchw(y), t3) < 2e-2
+
+
+def test_encoder_fused_blocks_equal_unfused(sat):
+    """ResNet152 trunk at 224 x 224: the fused layer3 blocks change no output bit."""
+    torch.manual_seed(0)
+    p = O.make_resnet152_params(4)
+    enc = sat.Encoder("resnet152", dtype=torch.bfloat16)
+    enc.load_state_dict(p, strict=True)
+    enc = enc.to(DEV).eval()
+    x = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(6)).to(DEV)
+    plan = enc.compiled_plan(x.device, torch.bfloat16)
+    assert sum(1 for s in plan if s[0] == "block" and s[5] is not None) == 35
+    with torch.no_grad():
+        y_f = enc(x)
+        enc.fuse_blocks = False
+        y_u = enc(x)
+    assert torch.equal(y_f, y_u)
