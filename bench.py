@@ -46,6 +46,19 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode: run the next batch's encoder after, not beside, this batch's decoder")
+    ap.add_argument("--enc-split", choices=["none", "layer2", "layer3", "layer4"], default="layer3",
+                    help="graph + overlap (ResNet152): the encoder runs as two graphs split at this stage; the "
+                         "decoder of batch i runs beside batch i+1's first part only, the second part (the fused, "
+                         "chip-filling layer3 blocks) starts when that decoder is done")
+    ap.add_argument("--split-target", type=int, default=64,
+                    help="graph + overlap: workgroups the decoder's per-step split-K GEMMs aim for")
+    ap.add_argument("--no-fuse-blocks", action="store_true",
+                    help="run the layer3 identity bottlenecks as three conv launches (A/B of csrc/convblock.hip)")
+    ap.add_argument("--fuse-every", type=int, default=1,
+                    help="fuse every n-th layer3 identity bottleneck only (the rest: three conv launches)")
+    ap.add_argument("--stream-priority", choices=["decoder-high", "equal"], default="decoder-high",
+                    help="graph + overlap: the decoder / all-reduce / Adam stream gets the higher HIP stream "
+                         "priority, so its short per-step kernels are dispatched first when CUs free up")
     ap.add_argument("--fp32-steps", type=int, default=3,
                     help="timed steps of the fp32 leg (the reference's precision, the exact-parity path; 0 = skip)")
     ap.add_argument("--no-diagnostics", action="store_true",
@@ -62,18 +75,27 @@ def parse():
 PEAK_HBM_ACHIEVABLE_GBS = 6300.0   # MI355X_MICROARCH.md §HBM (floor estimates only)
 
 
-def conv_launches(network, B, H=224):
+def conv_launches(network, B, H=224, fused=True):
     """Every conv launch of one encoder forward, in launch order (encoder.py forward: per
-    bottleneck c1, c2, downsample, c3), with its algorithmic work: FLOPs = 2*M*N*K (real Cin=3
-    for the first conv) and bytes = input activation read once + weights + output (+ residual),
-    bf16.  ``bound`` is the roofline that is larger at 2.5 PFLOP/s / 6.3 TB/s."""
+    bottleneck c1, c2, downsample, c3, or ONE fused launch for the identity blocks the fused
+    bottleneck kernel runs), with its algorithmic work: FLOPs = 2*M*N*K (real Cin=3 for the first
+    conv) and bytes = input activation read once + weights + output (+ residual), bf16; a fused
+    block reads its input once (the residual is the same tensor), writes its output once and reads
+    its three weights.  ``bound`` is the roofline that is larger at 2.5 PFLOP/s / 6.3 TB/s."""
     out = []
+
+    def bound_of(f, by):
+        return "mfma" if f / (BF16_DENSE_PEAK_TFLOPS * 1e12) > by / (PEAK_HBM_ACHIEVABLE_GBS * 1e9) else "hbm"
 
     def add(name, M, N, K, in_elems, res=False, real_k=None):
         f = 2.0 * M * N * (real_k or K)
         by = 2.0 * (in_elems + N * K + M * N * (2 if res else 1))
-        bound = "mfma" if f / (BF16_DENSE_PEAK_TFLOPS * 1e12) > by / (PEAK_HBM_ACHIEVABLE_GBS * 1e9) else "hbm"
-        out.append(dict(cls=f"{name} {M}x{N}x{K}", flops=f, bytes=by, bound=bound))
+        out.append(dict(cls=f"{name} {M}x{N}x{K}", flops=f, bytes=by, bound=bound_of(f, by)))
+
+    def add_block(name, M, cin, pl):
+        f = 2.0 * M * (cin * pl + 9 * pl * pl + pl * cin)
+        by = 2.0 * (2 * M * cin + 2 * cin * pl + 9 * pl * pl)
+        out.append(dict(cls=f"{name} {M}x{cin}x{pl}", flops=f, bytes=by, bound=bound_of(f, by), fused=True))
 
     if network == "resnet152":
         h = H // 2   # stem: 4x4 conv over the 2x2 space-to-depth input (16 channels, 12 real)
@@ -84,6 +106,10 @@ def conv_launches(network, B, H=224):
             for bi in range(n):
                 s = (1 if li == 0 else 2) if bi == 0 else 1
                 oh = h // s
+                if fused and bi > 0 and (h, cin, pl) == (14, 1024, 256) \
+                        and (fused is True or (bi - 1) % int(fused) == 0):   # sat_bottleneck_fused_supported
+                    add_block(f"L{li + 1}block(fused)", B * h * h, cin, pl)
+                    continue
                 add(f"L{li + 1}c1", B * h * h, pl, cin, B * h * h * cin)
                 add(f"L{li + 1}c2{'s2' if s == 2 else ''}", B * oh * oh, pl, 9 * pl, B * h * h * pl)
                 if bi == 0:
@@ -122,7 +148,8 @@ def trunk_roofline(enc, imgs, launches, reps=3):
             dur[i] += st.elapsed_time(en) / reps   # ms
     cls = {}
     for l, d in zip(launches, dur):
-        c = cls.setdefault(l["cls"], dict(n=0, ms=0.0, flops=l["flops"], bytes=l["bytes"], bound=l["bound"]))
+        c = cls.setdefault(l["cls"], dict(n=0, ms=0.0, flops=l["flops"], bytes=l["bytes"], bound=l["bound"],
+                                          fused=l.get("fused", False)))
         c["n"] += 1
         c["ms"] += d
     name, dom = max(cls.items(), key=lambda kv: kv[1]["ms"])
@@ -133,16 +160,21 @@ def trunk_roofline(enc, imgs, launches, reps=3):
     idx = [i for i, l in enumerate(launches) if l["cls"] == name]
     last = conv_args[(reps - 1) * n:]
     b2b = 5
+    def launch(a):
+        if a[0] == "fused":
+            ops.bottleneck_fused(a[1], *a[2])
+        else:
+            x, w, b, s, p, relu, res, hw = a
+            ops.conv2d_nhwc(x, w, b, s, p, relu, residual=res, out_hw=hw)
+
     with torch.no_grad():
         for i in idx[:2]:   # warm
-            x, w, b, s, p, relu, res, hw = last[i]
-            ops.conv2d_nhwc(x, w, b, s, p, relu, residual=res, out_hw=hw)
+            launch(last[i])
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st.record()
         for i in idx:
-            x, w, b, s, p, relu, res, hw = last[i]
             for _ in range(b2b):
-                ops.conv2d_nhwc(x, w, b, s, p, relu, residual=res, out_hw=hw)
+                launch(last[i])
         en.record()
     en.synchronize()
     avg_s = st.elapsed_time(en) / (len(idx) * b2b) * 1e-3
@@ -153,7 +185,8 @@ def trunk_roofline(enc, imgs, launches, reps=3):
     floor_us = sum(max(l["flops"] / (BF16_DENSE_PEAK_TFLOPS * 1e12), l["bytes"] / (PEAK_HBM_ACHIEVABLE_GBS * 1e9))
                    for l in launches) * 1e6
     trunk_us = sum(dur) * 1e3
-    return dict(kernel=f"fast_gemm_kernel, conv class {name} ({dom['n']} launches/forward)", cls=name,
+    kname = "bottleneck_kernel (csrc/convblock.hip), fused block" if dom.get("fused") else "conv kernels, conv class"
+    return dict(kernel=f"{kname} {name} ({dom['n']} launches/forward)", cls=name,
                 bound=dom["bound"], achieved=round(achieved, 2), peak=peak, unit=unit,
                 frac=round(achieved / peak, 4), avg_launch_us=round(avg_s * 1e6, 2),
                 avg_launch_us_event_pairs=round(avg_event_us, 2),
@@ -278,10 +311,11 @@ def main():
 
     if not args.no_graph and not args.no_overlap:
         # the decoder shares the chip with the next batch's encoder: fewer split-K workgroups
-        sat_amd.ops.set_decoder_split_target(64)
+        sat_amd.ops.set_decoder_split_target(args.split_target)
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
+    enc.fuse_blocks = False if args.no_fuse_blocks else (True if args.fuse_every == 1 else args.fuse_every)
     torch.manual_seed(42)          # identical decoder init on every rank
     dec = sat_amd.Decoder(args.vocab, D, tf=not args.no_tf, ado=not args.bert, bert=args.bert,
                           attention=True).to(dev).train()
@@ -316,6 +350,7 @@ def main():
 
     use_graph = not args.no_graph
     overlap = use_graph and not args.no_overlap
+    g_encA = None
     if use_graph:
         # hipGraphs: the encoder trunk (so its kernels can be bracketed with events) and decoder
         # fwd + loss + BPTT.  Adam and the RCCL all-reduce run eagerly after replay (Adam's bias
@@ -325,15 +360,29 @@ def main():
         # encoder does not read any decoder parameter), so the latency-bound decoder kernels and
         # the gradient exchange share the chip with the conv trunk.
         nbuf = 2 if overlap else 1
+        # encoder part A (plan[:split], beside the previous batch's decoder) and part B (plan[split:])
+        split = 0
+        if overlap and args.network == "resnet152" and args.enc_split != "none":
+            split = enc.stage_starts()[{"layer2": 1, "layer3": 2, "layer4": 3}[args.enc_split]]
+        g_encA = [torch.cuda.CUDAGraph() for _ in range(nbuf)] if split else None
         # one private memory pool per graph: no intermediate of one graph aliases another's
         g_enc = [torch.cuda.CUDAGraph() for _ in range(nbuf)]
         g_dec = [torch.cuda.CUDAGraph() for _ in range(nbuf)]   # fwd + loss + backward phase 1 (output head)
         g_rec = [torch.cuda.CUDAGraph() for _ in range(nbuf)]   # backward phase 2 (BPTT + remaining wgrads)
         feats_static, loss_static = [], []
+        n_plan = len(enc.compiled_plan(imgs.device, torch.bfloat16))
         for k in range(nbuf):
-            with torch.cuda.graph(g_enc[k]):
-                with torch.no_grad():
-                    feats_static.append(enc(imgs))
+            if split:
+                with torch.cuda.graph(g_encA[k]):
+                    with torch.no_grad():
+                        mid = enc(imgs, steps=(0, split))
+                with torch.cuda.graph(g_enc[k]):
+                    with torch.no_grad():
+                        feats_static.append(enc(mid, steps=(split, n_plan)))
+            else:
+                with torch.cuda.graph(g_enc[k]):
+                    with torch.no_grad():
+                        feats_static.append(enc(imgs))
         dec.defer_recurrent_backward(True)
         for k in range(nbuf):
             opt.zero_grad(set_to_none=True)   # each capture overwrites the gradients (beta = 0)
@@ -348,15 +397,33 @@ def main():
         torch.cuda.synchronize()
 
     enc_events = []
-    s_main = torch.cuda.current_stream()
-    s_enc = torch.cuda.Stream() if overlap else s_main
+    if overlap and args.stream_priority == "decoder-high":
+        lo, hi = torch.cuda.Stream.priority_range()
+        s_main = torch.cuda.Stream(priority=hi)
+        s_enc = torch.cuda.Stream(priority=lo)
+        s_main.wait_stream(torch.cuda.current_stream())
+        torch.cuda.set_stream(s_main)
+    else:
+        s_main = torch.cuda.current_stream()
+        s_enc = torch.cuda.Stream() if overlap else s_main
     ev_enc = [torch.cuda.Event() for _ in range(2)]
     ev_dec = [torch.cuda.Event() for _ in range(2)]
 
-    def replay_encoder(k, wait_dec):
+    def replay_encoder(k, wait_dec, dec_ev=None):
+        """Batch k's encoder on s_enc.  wait_dec: feature buffer k was last read by the decoder two
+        batches ago.  Split encoder: part A right away (beside the running decoder), part B after
+        dec_ev (that decoder's end), so the chip-filling fused blocks do not starve it."""
         with torch.cuda.stream(s_enc):
-            if wait_dec:   # feature buffer k was last read by the decoder two batches ago
+            if wait_dec:
                 s_enc.wait_event(ev_dec[k])
+            if g_encA is not None:   # encoder time = the two parts' own spans (not the wait between)
+                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                st.record(s_enc)
+                g_encA[k].replay()
+                en.record(s_enc)
+                enc_events.append((st, en))
+                if dec_ev is not None:
+                    s_enc.wait_event(dec_ev)
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             st.record(s_enc)
             g_enc[k].replay()
@@ -383,7 +450,7 @@ def main():
                 loss = loss_static[k]
                 if i + 1 < n:
                     if overlap:
-                        replay_encoder((i + 1) % 2, i >= 1)
+                        replay_encoder((i + 1) % 2, i >= 1, ev_dec[k])
                     else:
                         replay_encoder(0, False)
                 if world > 1:
@@ -413,7 +480,7 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    launches = conv_launches(args.network, B)
+    launches = conv_launches(args.network, B, fused=enc.fuse_blocks)
     enc_ms = sum(s.elapsed_time(e) for s, e in enc_events) if use_graph else None
     loss_v = loss.item()
     diag = rank == 0 and not args.no_diagnostics
@@ -423,6 +490,7 @@ def main():
         else None
     if roof is not None:
         roof["traffic"], roof["traffic_source"] = pmc_traffic(args.network, roof["cls"])
+    if rank == 0:
         # the whole step's algorithmic FLOPs (encoder fwd + decoder fwd/bwd with W.a
         # hoisted) per image x images / step time, against the dense bf16 MFMA peak
         from sat_amd.diagnostics import decoder_flops
@@ -432,10 +500,12 @@ def main():
         enc_f = sum(l["flops"] for l in launches) / B
         dec_f = decoder_flops(Lf, D, E, args.vocab, args.seq, ado=not args.bert, attention=True)
         step_tf = (enc_f + dec_f) * B * world * args.steps / elapsed / 1e12
-        roof["step"] = {"encoder_gflop_per_img": round(enc_f / 1e9, 3), "decoder_gflop_per_img": round(dec_f / 1e9, 3),
-                        "achieved": round(step_tf, 1), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(step_tf / BF16_DENSE_PEAK_TFLOPS, 4)}
-        roof["decoder_step_kernels"] = step_kernels
+        if roof is not None:
+            roof["step"] = {"encoder_gflop_per_img": round(enc_f / 1e9, 3),
+                            "decoder_gflop_per_img": round(dec_f / 1e9, 3), "achieved": round(step_tf, 1),
+                            "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
+                            "frac": round(step_tf / BF16_DENSE_PEAK_TFLOPS, 4)}
+            roof["decoder_step_kernels"] = step_kernels
         out = {
             "metric": "train images/sec on COCO batch=128 at 1/2/4/8 MI355X",
             "value": round(B * world * args.steps / elapsed, 2),
@@ -450,7 +520,8 @@ def main():
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
                        "encoder_decoder_overlap": overlap},
             "roofline": roof,
-            "encoder_trunk": dict(trunk or {}, graph_ms_per_step=(round(enc_ms / args.steps, 3) if enc_ms else None)),
+            "encoder_trunk": dict(trunk or {}, graph_ms_per_step=(round(enc_ms / args.steps, 3) if enc_ms else None),
+                                  split_at=args.enc_split if g_encA is not None else None),
             "loss": round(loss_v, 4),
         }
         if fp32_leg is not None:

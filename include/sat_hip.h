@@ -138,6 +138,10 @@ int sat_conv2d_nhwc(const SatConvGeom* g, int Cout, int dtype, const void* x, co
  * src [N][K] bf16 row-major -> dst [N/16][K/32][64][8], lane l = 16*(k8 % 4) + (n % 16) of block
  * (n / 16, k / 32) holding src[n][32*(k/32) + 8*(l >> 4) .. +8].  N % 16 == 0, K % 32 == 0. */
 int sat_mfma_frag_layout(int N, int K, const void* src, void* dst, void* stream);
+/* experiment hook (process-global, tools/block_ab.py) of the fused bottleneck kernel: weight prefetch
+ * distance in k-tiles (2 | 3) and diagnostic ablation bits (1 no MFMA, 2 no weight streaming, 4 no
+ * LDS fragment reads; 0 = off). */
+int sat_bottleneck_set_experiment(int pf, int abl);
 /* 1 if sat_bottleneck_fused runs this geometry (today: bf16, 14x14, Cin 1024, Cmid 256 -- the 35
  * identity blocks of ResNet152 layer3), else 0. */
 int sat_bottleneck_fused_supported(int H, int W, int Cin, int Cmid, int dtype);

@@ -73,6 +73,7 @@ _SIGNATURES = [
     ("sat_conv2d_nhwc", c_int, [ctypes.POINTER(SatConvGeom), c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                 c_int, c_void_p, c_void_p]),
     ("sat_mfma_frag_layout", c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    ("sat_bottleneck_set_experiment", c_int, [c_int, c_int]),
     ("sat_bottleneck_fused_supported", c_int, [c_int, c_int, c_int, c_int, c_int]),
     ("sat_bottleneck_fused", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

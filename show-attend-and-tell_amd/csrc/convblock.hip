@@ -69,9 +69,36 @@ __device__ __forceinline__ void k_wait_barrier() {
 }
 __device__ __forceinline__ void k_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// vmem instructions one wave issues after its input DMAs A(T) (2 instructions) and before the wait
+// of c1 k-tile T: the issue order is A0 B0 A1 B1 B2 .. B(PF-1) (B = 4 weight loads), then per k-tile
+// it, after its wait: A(it+2) (it+2 < KT1), B(it+PF) (it+PF < NT, when weights stream)
+constexpr int younger_than_a(int T, int KT1, int NT, int PF, bool stream) {
+  int n = 0;
+  bool after = false;
+  auto ev_a = [&](int idx) {
+    if (after) n += 2;
+    if (idx == T) after = true;
+  };
+  auto ev_b = [&]() {
+    if (after) n += 4;
+  };
+  ev_a(0); ev_b(); ev_a(1); ev_b();
+  for (int e = 2; e < PF; ++e) ev_b();
+  for (int it = 0; it < T; ++it) {
+    if (it + 2 < KT1) ev_a(it + 2);
+    if (stream && it + PF < NT) ev_b();
+  }
+  return n;
+}
+
 // IW: image width = height, RO: output image rows per workgroup (IW % RO == 0, IW / RO == 2),
-// CIN: block input/output channels, CMID: bottleneck width (256: one 256-wide phase per conv)
-template <int IW, int RO, int CIN, int CMID>
+// CIN: block input/output channels, CMID: bottleneck width (256: one 256-wide phase per conv);
+// PF: weight prefetch distance in k-tiles; ABL (diagnostics, tools/block_ab.py): bit 0 no MFMA,
+// bit 1 no weight streaming (the prologue's fragments reused), bit 2 no A fragment reads; bit 3
+// non-temporal input / residual loads, bit 4 non-temporal output stores (both measured slower:
+// 65.6 -> 77.9 / 101.8 us, profiles/r2_s25_block_nt.txt); bit 5 per-workgroup rotation of the waves'
+// n-blocks, bit 6 k-major fragment layout
+template <int IW, int RO, int CIN, int CMID, int PF, int ABL>
 __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
   static_assert(IW / RO == 2 && IW % RO == 0, "two workgroups per image");
   static_assert(CMID == 256 && CIN % 256 == 0 && CIN % 64 == 0, "256-wide phases");
@@ -100,6 +127,9 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fh = lane >> 4;
+  // the wave's 32 output channels of each phase: n-blocks 2wn, 2wn+1 (wn rotated per workgroup in the
+  // bit-5 experiment so the workgroups of one XCD do not request the same weight lines together)
+  const int wn = (ABL & 32) ? __builtin_amdgcn_readfirstlane((w + (blockIdx.x >> 3)) & 7) : w;
   const int img = blockIdx.x >> 1, half = blockIdx.x & 1;
   const int y0 = half * RO;                      // first output image row
   const int ws = half ? IH - R1 : 0;             // first c1 image row
@@ -121,22 +151,25 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (k_lds_void*)(st + (w * 2 + u) * 1024), 16,
-                                               dsrc[u] == K_OOB ? (int)K_OOB : (int)(dsrc[u] + t * 128), 0, 0, 0);
+                                               dsrc[u] == K_OOB ? (int)K_OOB : (int)(dsrc[u] + t * 128), 0, 0,
+                                               (ABL & 8) ? 2 : 0);
   };
 
   // ---- weight fragments: tile T of the 68-tile schedule, this wave's n-blocks, both 32-k halves ----
-  bf16x8 bq[3][2][2];
+  bf16x8 bq[PF + 1][2][2];
   auto load_b = [&](int T, bf16x8 (&dst)[2][2]) {
     const bf16* base;
-    int nb0, ks0, KS;
-    if (T < KT1) { base = a.w1; nb0 = 0; ks0 = 2 * T; KS = KS1; }
-    else if (T < KT1 + KT2) { base = a.w2; nb0 = 0; ks0 = 2 * (T - KT1); KS = KS2; }
-    else { const int t = T - KT1 - KT2; base = a.w3; nb0 = (t / KT3C) * 16; ks0 = 2 * (t % KT3C); KS = KS3; }
+    int nb0, ks0, KS, NBW;
+    if (T < KT1) { base = a.w1; nb0 = 0; ks0 = 2 * T; KS = KS1; NBW = CMID / 16; }
+    else if (T < KT1 + KT2) { base = a.w2; nb0 = 0; ks0 = 2 * (T - KT1); KS = KS2; NBW = CMID / 16; }
+    else { const int t = T - KT1 - KT2; base = a.w3; nb0 = (t / KT3C) * 16; ks0 = 2 * (t % KT3C); KS = KS3; NBW = CIN / 16; }
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-        dst[ks][j] = *(const bf16x8*)(base + ((long)((nb0 + w * 2 + j) * KS + ks0 + ks) * 64 + lane) * 8);
+        dst[ks][j] = (ABL & 64)   // k-major fragment layout: block (nb, ks) at ks * NB + nb
+                         ? *(const bf16x8*)(base + ((long)((ks0 + ks) * NBW + nb0 + wn * 2 + j) * 64 + lane) * 8)
+                         : *(const bf16x8*)(base + ((long)((nb0 + wn * 2 + j) * KS + ks0 + ks) * 64 + lane) * 8);
   };
 
   // ---- A fragment offsets: row i*16 + fr of a 128-B-row image = i * 2048 (immediate) + per-lane part ----
@@ -168,6 +201,16 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
   // fragments + MFMAs of one 64-deep k-tile; A row block i at base + i * 16 * ROWB + offu (unshifted)
   // or base + offs[i] (c2's shifted rows)
   auto mma = [&](const bf16x8 (&af)[2][MB], const bf16x8 (&b)[2][2]) {
+    if constexpr (ABL & 1) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < MB; ++i) asm volatile("" ::"v"(af[ks][i]));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(b[ks][j]));
+      }
+      return;
+    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -182,7 +225,8 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < MB; ++i) af[ks][i] = *(const bf16x8*)(base + i * 16 * ROWB + offu[ks]);
+      for (int i = 0; i < MB; ++i)
+        af[ks][i] = (ABL & 4) ? b[ks][i & 1] : *(const bf16x8*)(base + i * 16 * ROWB + offu[ks]);
     mma(af, b);
   };
   auto tile_s = [&](const char* base, const bf16x8 (&b)[2][2]) {
@@ -190,7 +234,7 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < MB; ++i) af[ks][i] = *(const bf16x8*)(base + offs[i][ks]);
+      for (int i = 0; i < MB; ++i) af[ks][i] = (ABL & 4) ? b[ks][i & 1] : *(const bf16x8*)(base + offs[i][ks]);
     mma(af, b);
   };
   // epilogue into an LDS plane image: lane holds channels w*32 + j*16 + 4fh .. +3 of pixel i*16 + fr
@@ -198,14 +242,14 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
   // epilogue would be younger than the weight prefetches and drain them)
   auto load_bias = [&](const float* bias, int ch0, float4 (&bv)[2]) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + ch0 + w * 32 + j * 16 + 4 * fh);
+    for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + ch0 + wn * 32 + j * 16 + 4 * fh);
   };
   auto store_planes = [&](int region, int plane_bytes, const float4 (&bias)[2]) {
-    const int plane = w >> 1;
+    const int plane = wn >> 1;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const float4 bv = bias[j];
-      const int c = (w & 1) * 4 + j * 2 + (fh >> 1);
+      const int c = (wn & 1) * 4 + j * 2 + (fh >> 1);
 #pragma unroll
       for (int i = 0; i < MB; ++i) {
         const int r = i * 16 + fr;
@@ -227,6 +271,7 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
   load_b(0, bq[0]);
   dma_a(1);
   load_b(1, bq[1]);
+  static_for<PF - 2>([&](auto e) { load_b(2 + decltype(e)::value, bq[2 + decltype(e)::value]); });
   zero_acc();
   u32x2 resv[MB][2];
 
@@ -234,13 +279,13 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
     constexpr int T = decltype(Tc)::value;
     if constexpr (T < KT1) {
       // this wave's DMAs of input tile T have landed; younger: B(T), [A(T+1)], B(T+1)
-      if constexpr (T + 1 < KT1) k_wait_barrier<10>();
-      else k_wait_barrier<8>();
+      k_wait_barrier<younger_than_a(T, KT1, NT, PF, !(ABL & 2))>();
       if constexpr (T + 2 < KT1) dma_a(T + 2);
     }
-    if constexpr (T + 2 < NT) load_b(T + 2, bq[(T + 2) % 3]);
+    if constexpr (T + PF < NT && !(ABL & 2)) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
+    constexpr int BQ = (ABL & 2) ? 0 : T % (PF + 1);
     if constexpr (T < KT1) {
-      tile_u(smem + RING + (T % 3) * STG, bq[T % 3]);
+      tile_u(smem + RING + (T % 3) * STG, bq[BQ]);
       if constexpr (T == KT1 - 1) {   // c1 epilogue -> X1 (the ring is read for the last time above)
         store_planes(X1, X1PL, bias_a);
         zero_acc();
@@ -250,7 +295,7 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
       constexpr int t = T - KT1, tap = t / (CMID / 64), pl = t % (CMID / 64);
       if constexpr (t == 0) load_bias(a.b2, 0, bias_b);
       if constexpr (pl == 0) tap_offsets(tap);
-      tile_s(smem + X1 + pl * X1PL, bq[T % 3]);
+      tile_s(smem + X1 + pl * X1PL, bq[BQ]);
       if constexpr (t == KT2 - 1) {   // c2 epilogue -> X2
         store_planes(X2, X2PL, bias_b);
         zero_acc();
@@ -264,15 +309,17 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
         for (int i = 0; i < MB; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {   // rows past PO load a valid row (never stored): no branch
-            const int p = min(i * 16 + fr, PO - 1), ch = ck * 256 + w * 32 + j * 16 + 4 * fh;
-            resv[i][j] = *(const u32x2*)(a.x + (pix_img + (long)y0 * IW + p) * CIN + ch);
+            const int p = min(i * 16 + fr, PO - 1), ch = ck * 256 + wn * 32 + j * 16 + 4 * fh;
+            const u32x2* rp = (const u32x2*)(a.x + (pix_img + (long)y0 * IW + p) * CIN + ch);
+            if constexpr (ABL & 8) resv[i][j] = __builtin_nontemporal_load(rp);
+            else resv[i][j] = *rp;
           }
       }
-      tile_u(smem + X2 + kt * X2PL, bq[T % 3]);
+      tile_u(smem + X2 + kt * X2PL, bq[BQ]);
       if constexpr (kt == KT3C - 1) {   // c3 epilogue: bias, fp32 residual add, ReLU, one rounding, 8-B stores
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const int ch = ck * 256 + w * 32 + j * 16 + 4 * fh;
+          const int ch = ck * 256 + wn * 32 + j * 16 + 4 * fh;
           const float4 bv = bias_a[j];
 #pragma unroll
           for (int i = 0; i < MB; ++i) {
@@ -283,7 +330,12 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
             bf16* ob = (bf16*)&o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) ob[e] = (bf16)fmaxf(v[e] + (float)rh[e], 0.f);
-            if (p < PO) *(u32x2*)(a.y + (pix_img + (long)y0 * IW + p) * CIN + ch) = o;
+            u32x2* yp = (u32x2*)(a.y + (pix_img + (long)y0 * IW + p) * CIN + ch);
+            if constexpr (ABL & 16) {
+              if (p < PO) __builtin_nontemporal_store(o, yp);
+            } else {
+              if (p < PO) *yp = o;
+            }
           }
         }
         zero_acc();
@@ -293,14 +345,15 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
 }
 
 // [N][K] bf16 -> [N/16][K/32][64 lanes][8]: lane l = (fh << 4) | fr holds row 16 nb + fr, k 32 ks + 8 fh ..
-__global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst, int N, int K) {
+__global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst, int N, int K, int kmajor) {
   const long n8 = (long)N * K / 8;
   for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
     const long e = v * 8;                      // destination element
     const int lane = (int)((e / 8) % 64);
     const long blk = e / 512;                  // (nb, ks)
     const int KS = K / 32;
-    const int nb = (int)(blk / KS), ks = (int)(blk % KS);
+    const int NB = N / 16;
+    const int nb = kmajor ? (int)(blk % NB) : (int)(blk / KS), ks = kmajor ? (int)(blk / NB) : (int)(blk % KS);
     const int row = nb * 16 + (lane & 15), k = ks * 32 + (lane >> 4) * 8;
     *(uint4*)(dst + e) = *(const uint4*)(src + (long)row * K + k);
   }
@@ -308,13 +361,54 @@ __global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restric
 
 }  // namespace
 
+static int g_frag_kmajor = 0;   // experiment: k-major fragment layout (ABL bit 6)
+
 extern "C" int sat_mfma_frag_layout(int N, int K, const void* src, void* dst, void* stream) {
   SAT_REQUIRE(src && dst && N > 0 && K > 0 && N % 16 == 0 && K % 32 == 0);
   SAT_REQUIRE(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0);
   const long n8 = (long)N * K / 8;
   const int g = (int)((n8 + 255) / 256 < 4096 ? (n8 + 255) / 256 : 4096);
-  hipLaunchKernelGGL(frag_layout_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16*)src, (bf16*)dst, N, K);
+  hipLaunchKernelGGL(frag_layout_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16*)src, (bf16*)dst, N, K,
+                     g_frag_kmajor);
   return (int)hipGetLastError();
+}
+
+namespace {
+
+int g_block_pf = 2;    // weight prefetch distance (k-tiles)
+int g_block_abl = 0;   // diagnostics: ABL bits
+
+template <int PF, int ABL>
+void launch_block(dim3 grid, hipStream_t s, const KArgs& a) {
+  hipLaunchKernelGGL((bottleneck_kernel<14, 7, 1024, 256, PF, ABL>), grid, dim3(512), 0, s, a);
+}
+template <int PF>
+void launch_block_abl(int abl, dim3 grid, hipStream_t s, const KArgs& a) {
+  switch (abl) {
+    case 1: launch_block<PF, 1>(grid, s, a); break;
+    case 2: launch_block<PF, 2>(grid, s, a); break;
+    case 4: launch_block<PF, 4>(grid, s, a); break;
+    case 6: launch_block<PF, 6>(grid, s, a); break;
+    case 32: launch_block<PF, 32>(grid, s, a); break;
+    case 64: launch_block<PF, 64>(grid, s, a); break;
+    case 96: launch_block<PF, 96>(grid, s, a); break;
+    case 33: launch_block<PF, 33>(grid, s, a); break;
+    case 97: launch_block<PF, 97>(grid, s, a); break;
+    default: launch_block<PF, 0>(grid, s, a); break;
+  }
+}
+
+}  // namespace
+
+// experiment hook (tools/block_ab.py): weight prefetch distance (2; 3 measured no faster:
+// profiles/r2_s24_block_ablation.txt) and ablation bits (0 = off)
+extern "C" int sat_bottleneck_set_experiment(int pf, int abl) {
+  if (pf != 2 || (abl != 0 && abl != 1 && abl != 2 && abl != 4 && abl != 6 && abl != 32 && abl != 64 && abl != 96 &&
+                  abl != 33 && abl != 97)) return SAT_ERR_INVALID;
+  g_block_pf = pf;
+  g_block_abl = abl;
+  g_frag_kmajor = (abl & 64) ? 1 : 0;
+  return 0;
 }
 
 extern "C" int sat_bottleneck_fused_supported(int H, int W, int Cin, int Cmid, int dtype) {
@@ -336,6 +430,6 @@ extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int 
   a.w1 = (const bf16*)w1f; a.w2 = (const bf16*)w2f; a.w3 = (const bf16*)w3f;
   a.b1 = b1; a.b2 = b2; a.b3 = b3;
   a.x_bytes = (unsigned)x_bytes;
-  hipLaunchKernelGGL((bottleneck_kernel<14, 7, 1024, 256>), dim3(2 * N), dim3(512), 0, (hipStream_t)stream, a);
+  launch_block_abl<2>(g_block_abl, dim3(2 * N), (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }

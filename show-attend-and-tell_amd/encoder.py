@@ -144,8 +144,11 @@ class Encoder(nn.Module):
         self._plan_key = None
         self.timing = None   # bench hook: list collecting (start, end) HIP events around every conv launch
         self.timing_args = None   # bench hook: list collecting every conv launch's arguments
+        # (a fused bottleneck launch is recorded as ("fused", x, frags))
         # identity-residual bottlenecks the fused kernel supports run as ONE launch
-        # (sat_bottleneck_fused, csrc/convblock.hip); False = three conv launches (A/B, tests)
+        # (sat_bottleneck_fused, csrc/convblock.hip); False = three conv launches (A/B, tests);
+        # an int n fuses every n-th eligible block only (the unfused ones leave CUs to a decoder
+        # running beside the encoder: bench.py --fuse-every)
         self.fuse_blocks = True
 
     def _conv(self, x, f, relu, residual=None, out_hw=None):
@@ -276,6 +279,13 @@ class Encoder(nn.Module):
             y = ops.nchw_to_nhwc(x, IN_PAD, dtype)
         return self._run_plan(y, plan, stop)
 
+    def _fuse_this(self, plan, step):
+        f = self.fuse_blocks
+        if f is True or f is False:
+            return f
+        elig = [s for s in plan if s[0] == "block" and s[5] is not None]
+        return next(i for i, s in enumerate(elig) if s is step) % int(f) == 0
+
     def _run_plan(self, y, plan, stop):
         for step in plan[:stop]:
             if step[0] == "stem_s2d":
@@ -292,9 +302,18 @@ class Encoder(nn.Module):
         if step[0] == "pool":
             return ops.maxpool2d_nhwc(y, step[1], step[2], step[3])
         _, c1, c2, c3, ds, fused = step
-        if (fused is not None and self.fuse_blocks and self.timing is None and self.timing_args is None
+        if (fused is not None and self.fuse_blocks is not False and self._fuse_this(self._plan, step)
                 and ops.bottleneck_fused_supported(y.shape[1], y.shape[2], y.shape[3], c1[0].shape[0], y.dtype)):
-            return ops.bottleneck_fused(y, *fused)
+            if self.timing_args is not None:
+                self.timing_args.append(("fused", y, fused))
+            if self.timing is None:
+                return ops.bottleneck_fused(y, *fused)
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st.record()
+            out = ops.bottleneck_fused(y, *fused)
+            en.record()
+            self.timing.append((st, en))
+            return out
         out = self._conv(y, c1, True)
         out = self._conv(out, c2, True)
         idn = self._conv(y, ds, False) if ds is not None else y

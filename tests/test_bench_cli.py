@@ -34,10 +34,16 @@ def test_no_tf_mode(monkeypatch):
     assert a.no_tf and a.vocab == 10000 and a.seq == 27
 
 
-@pytest.mark.parametrize("network,n", [("resnet152", 155), ("vgg19", 16)])
-def test_conv_launch_inventory(network, n):
-    launches = bench.conv_launches(network, 1)
+@pytest.mark.parametrize("network,fused,n", [("resnet152", False, 155), ("resnet152", True, 155 - 2 * 35),
+                                             ("vgg19", True, 16)])
+def test_conv_launch_inventory(network, fused, n):
+    launches = bench.conv_launches(network, 1, fused=fused)
     assert len(launches) == n
+    blocks = [l for l in launches if l.get("fused")]
+    assert len(blocks) == (35 if fused and network == "resnet152" else 0)
+    if blocks:   # one layer3 block = c1 + c2 + c3 of the unfused inventory
+        un = {l["cls"].split()[0]: l["flops"] for l in bench.conv_launches(network, 1, fused=False)}
+        assert abs(blocks[0]["flops"] - (un["L3c1"] + un["L3c2"] + un["L3c3+res"])) < 1
 
 
 def test_bert_synthetic_captions_layout():

@@ -16,6 +16,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import conv_launches, BF16_DENSE_PEAK_TFLOPS, HBM_PEAK_GBS  # noqa: E402
 
 
+CONV_KERNELS = ("fast_gemm_kernel", "conv_pipe_kernel", "conv1x1_stream_kernel", "conv3x3_halo_kernel",
+                "bottleneck_kernel")
+
+
+def is_conv_kernel(name):
+    """A dispatch of one of the conv kernels bench.conv_launches() enumerates (one per launch)."""
+    return any(k in name for k in CONV_KERNELS)
+
+
 def encoder_dispatches(rows):
     groups, cur = [], None
     for r in rows:
@@ -37,10 +46,10 @@ def main():
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     launches = conv_launches(network, B)
-    groups = [g for g in encoder_dispatches(rows) if sum("fast_gemm" in r["Kernel_Name"] for r in g) == len(launches)]
+    groups = [g for g in encoder_dispatches(rows) if sum(is_conv_kernel(r["Kernel_Name"]) for r in g) == len(launches)]
     if not groups:
         raise SystemExit("no complete encoder forward in the trace")
-    conv = [r for r in groups[-1] if "fast_gemm" in r["Kernel_Name"]]
+    conv = [r for r in groups[-1] if is_conv_kernel(r["Kernel_Name"])]
     cls = {}
     for r, l in zip(conv, launches):
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3   # us

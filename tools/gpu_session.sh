@@ -23,7 +23,8 @@ for s in $STEPS; do
            rc=$?; grep -E "^FAILED" "$OUT/tests.log" | head -30; [ $rc -le 1 ] || exit $rc ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     conv)  run conv 300 python tools/bench_conv.py || exit $? ;;
-    bench) run bench 400 python bench.py --steps 20 --warmup 5 || exit $? ;;
+    bench) run bench 400 python bench.py || exit $? ;;
+    benchno) run benchno 300 python bench.py --steps 50 --no-overlap --no-cpu-baseline --fp32-steps 0 || exit $? ;;
     benchq) run benchq 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline || exit $? ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
                python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-graph || exit $? ;;

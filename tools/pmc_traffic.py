@@ -21,6 +21,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import conv_launches  # noqa: E402
 
 
+CONV_KERNELS = ("fast_gemm_kernel", "conv_pipe_kernel", "conv1x1_stream_kernel", "conv3x3_halo_kernel",
+                "bottleneck_kernel")
+
+
+def is_conv_kernel(name):
+    """A dispatch of one of the conv kernels bench.conv_launches() enumerates (one per launch)."""
+    return any(k in name for k in CONV_KERNELS)
+
+
 def read_counter(d, name):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -47,7 +56,7 @@ def last_forward(rows, n_conv):
             cur = None
         if cur is not None:
             cur.append((k, v))
-    groups = [g for g in groups if sum("fast_gemm" in k for k, _ in g) == n_conv]
+    groups = [g for g in groups if sum(is_conv_kernel(k) for k, _ in g) == n_conv]
     if not groups:
         raise SystemExit("no complete encoder forward")
     return groups[-1]
@@ -68,7 +77,7 @@ def main():
     for tag, g, scale in (("fetch", fetch, 2.0), ("write", write, 1.0)):
         layout = [v for k, v in g if "nchw_to_nhwc" in k or "s2d16" in k]
         unit[tag] = layout[0] * scale * 1024 if layout else None
-        conv = [v * scale * 1024 for k, v in g if "fast_gemm" in k]
+        conv = [v * scale * 1024 for k, v in g if is_conv_kernel(k)]
         for l, b in zip(launches, conv):
             c = out["classes"].setdefault(l["cls"], {"n": 0, "fetch": 0.0, "write": 0.0, "alg_bytes": l["bytes"]})
             if tag == "fetch":

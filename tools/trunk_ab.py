@@ -15,7 +15,7 @@ lib = sat_amd._lib.lib()
 torch.manual_seed(0)
 enc = sat_amd.Encoder(net, dtype=torch.bfloat16).cuda().eval()
 imgs = torch.randn(B, 3, 224, 224, device="cuda")
-launches = bench.conv_launches(net, B)
+launches = bench.conv_launches(net, B, fused=enc.fuse_blocks)
 MODES = [(1, 1, 1), (1, 1, 0), (0, 1, 1), (0, 0, 0)]   # (stream, pipe, halo)
 res = {}
 for rnd in range(2):
