@@ -166,6 +166,10 @@ int sat_attention_forward(int B, int L, int D, int E, int dtype, const void* img
                           const float* v_w, const float* v_b, float* ws_scratch,
                           float* context, float* alpha, void* stream);
 
+/* tuning hook (process-global): the attention backward of a decoder step as ONE launch per step
+ * (1, default: a workgroup per batch row) or the two-launch form (0, A/B). */
+int sat_attention_set_bwd_mode(int fused);
+
 /* --- decoder (decoder.py:69-158) ----------------------------------------- */
 /* tuning hook (process-global): split-K counts of the per-step bf16 decoder GEMMs -- h: [U; f_beta; W_hh] h,
  * c: context part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic.  Must be set

@@ -425,6 +425,218 @@ __global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int 
   }
 }
 
+// One launch for the whole attention backward of a step (replaces attn_bwd1 + attn_bwd2): one
+// 16-wave workgroup per batch row b.  The two-launch form existed only because dL/dalpha needs a
+// reduction over D and the softmax / tanh backward needs all of it; with the whole row in one
+// workgroup that reduction stays in LDS.  Everything the row needs from memory -- the first batch
+// of annotation rows a[b, l, :], the first rows of Ws[b], U h + b and v -- is requested at kernel
+// entry (issue order = order of first use), so a step is one dependent memory round trip plus
+// the LDS phases:
+//   A  thread per column d: dL/dcontext = dL/dgated * gate (+ head term) into LDS, the gate
+//      gradient written on the way;
+//   B  wave per slot l, lanes over d: dL/dalpha_l = <dL/dcontext, a[b,l,:]> (+ the loss term);
+//   C  softmax backward: de_l = alpha_l (dL/dalpha_l - sum_k alpha_k dL/dalpha_k);
+//   D  wave per slot l, lanes over e: tanh recomputed, dL/d(U h) and dL/dv (+ dL/dv.bias) folded
+//      over the waves in a fixed order.
+
+// DCH / ECH: 16-B chunks per lane covering D / E; FBW waves, FBU slots per wave per batch (FBW * FBU
+// >= L keeps a row's annotation rows in one batch of loads: 16 x 4 at D <= 1024 elements per 16 B,
+// 8 x 7 (256 VGPRs per lane) at ResNet152's D = 2048)
+template <typename T, int DCH, int ECH, int FBW, int FBU>
+__global__ __launch_bounds__(FBW * 64) void attn_bwd_fused_kernel(AttnBwdArgs a) {
+  constexpr int VN = V16<T>::N;
+  __shared__ float s_dctx[64 * VN * DCH];
+  __shared__ float s_de[kMaxL];
+  __shared__ float s_red[FBW][64 * VN * ECH];
+  __shared__ float s_tmp[FBW];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int L = a.L, D = a.D, E = a.E;
+  const T* ab = (const T*)a.a + (long)b * L * D + lane * VN;
+  const T* Ws = (const T*)a.Ws + (long)b * L * E + lane * VN;
+  // ---- requests in order of first use ----
+  float dcol[(64 * VN * DCH + FBW * 64 - 1) / (FBW * 64)][4];   // dg, g, cx, dx of this thread's columns
+  constexpr int CPT = (64 * VN * DCH + FBW * 64 - 1) / (FBW * 64);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int d = k * FBW * 64 + tid;
+    float dg = 0.f, g = 0.f, cx = 0.f, dx = 0.f;
+    if (d < D) {
+      dg = sum_parts(a.d_gated, (long)b * a.d_gated_ld + d, a.dg_splits, a.dg_split_stride);
+      g = a.gate[(long)b * a.gate_ld + d];
+      cx = a.ctx[(long)b * a.ctx_ld + d];
+      if (a.d_ctx_ext) dx = a.d_ctx_ext[(long)b * a.d_ctx_ext_ld + d];
+    }
+    dcol[k][0] = dg; dcol[k][1] = g; dcol[k][2] = cx; dcol[k][3] = dx;
+  }
+  uint4 xa[FBU][DCH];
+#pragma unroll
+  for (int u = 0; u < FBU; ++u)
+#pragma unroll
+    for (int c = 0; c < DCH; ++c) {
+      const int l = w + FBW * u, d = c * 64 * VN + lane * VN;
+      xa[u][c] = ld16(ab + (long)l * D + c * 64 * VN, l < L && d < D);
+    }
+  uint4 xw[FBU][ECH];
+#pragma unroll
+  for (int u = 0; u < FBU; ++u)
+#pragma unroll
+    for (int c = 0; c < ECH; ++c) {
+      const int l = w + FBW * u, e = c * 64 * VN + lane * VN;
+      xw[u][c] = ld16(Ws + (long)l * E + c * 64 * VN, l < L && e < E);
+    }
+  float uu[ECH][VN], vw[ECH][VN];
+#pragma unroll
+  for (int c = 0; c < ECH; ++c) {
+    const int e = c * 64 * VN + lane * VN;
+#pragma unroll
+    for (int j = 0; j < VN; j += 4) {
+      float4 u4 = make_float4(0.f, 0.f, 0.f, 0.f), v4 = u4;
+      if (e < E) {
+        u4 = *(const float4*)(a.uh + (long)b * a.uh_ld + e + j);
+        v4 = *(const float4*)(a.v_w + e + j);
+      }
+      uu[c][j] = u4.x; uu[c][j + 1] = u4.y; uu[c][j + 2] = u4.z; uu[c][j + 3] = u4.w;
+      vw[c][j] = v4.x; vw[c][j + 1] = v4.y; vw[c][j + 2] = v4.z; vw[c][j + 3] = v4.w;
+    }
+  }
+  // ---- A: dL/dcontext and the gate gradient (thread per column) ----
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int d = k * FBW * 64 + tid;
+    if (d < 64 * VN * DCH) {
+      float dctx = 0.f;
+      if (d < D) {
+        const float dg = dcol[k][0], g = dcol[k][1], cx = dcol[k][2], dx = dcol[k][3];
+        dctx = dg * g + dx;
+        const float dgp = dg * cx * g * (1.f - g);
+        a.d_gpre[(long)b * a.d_gpre_ld + d] = dgp;
+        if (a.d_gpre_t) ((T*)a.d_gpre_t)[(long)b * a.d_gpre_ld + d] = (T)dgp;
+      }
+      s_dctx[d] = dctx;
+    }
+  }
+  lds_barrier();   // the annotation / Ws rows stay in flight
+  float dctx[DCH][VN];
+#pragma unroll
+  for (int c = 0; c < DCH; ++c)
+#pragma unroll
+    for (int j = 0; j < VN; ++j) dctx[c][j] = s_dctx[c * 64 * VN + lane * VN + j];
+  // ---- B: dL/dalpha per slot ----
+  for (int l0 = w; l0 < L; l0 += FBW * FBU) {
+    if (l0 != w) {
+#pragma unroll
+      for (int u = 0; u < FBU; ++u)
+#pragma unroll
+        for (int c = 0; c < DCH; ++c) {
+          const int l = l0 + FBW * u, d = c * 64 * VN + lane * VN;
+          xa[u][c] = ld16(ab + (long)l * D + c * 64 * VN, l < L && d < D);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < FBU; ++u) {
+      const int l = l0 + FBW * u;
+      if (l >= L) break;   // wave-uniform
+      float p = 0.f;
+#pragma unroll
+      for (int c = 0; c < DCH; ++c) {
+        const T* h = (const T*)&xa[u][c];
+#pragma unroll
+        for (int j = 0; j < VN; ++j) p += dctx[c][j] * (float)h[j];
+      }
+      p = wave_sum(p);
+      if (lane == 0) s_de[l] = p + (a.d_alpha_ext ? a.d_alpha_ext[(long)b * a.d_alpha_ext_ld + l] : 0.f);
+    }
+  }
+  __syncthreads();
+  // ---- C: softmax backward ----
+  const float* alpha = a.alpha + (long)b * a.alpha_ld;
+  float loc = 0.f;
+  for (int l = tid; l < L; l += FBW * 64) loc += alpha[l] * s_de[l];
+  loc = wave_sum(loc);
+  if (lane == 0) s_tmp[w] = loc;
+  __syncthreads();
+  float sad = 0.f;
+#pragma unroll
+  for (int i = 0; i < FBW; i += 2) sad += s_tmp[i] + s_tmp[i + 1];
+  __syncthreads();
+  for (int l = tid; l < L; l += FBW * 64) {
+    const float de = alpha[l] * (s_de[l] - sad);
+    s_de[l] = de;
+    a.de_out[(long)b * a.de_ld + l] = de;
+  }
+  __syncthreads();
+  // ---- D: tanh backward over E ----
+  float duh[ECH][VN], dv[ECH][VN];
+#pragma unroll
+  for (int c = 0; c < ECH; ++c)
+#pragma unroll
+    for (int j = 0; j < VN; ++j) duh[c][j] = dv[c][j] = 0.f;
+  float dbv = 0.f;
+  for (int l0 = w; l0 < L; l0 += FBW * FBU) {
+    if (l0 != w) {
+#pragma unroll
+      for (int u = 0; u < FBU; ++u)
+#pragma unroll
+        for (int c = 0; c < ECH; ++c) {
+          const int l = l0 + FBW * u, e = c * 64 * VN + lane * VN;
+          xw[u][c] = ld16(Ws + (long)l * E + c * 64 * VN, l < L && e < E);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < FBU; ++u) {
+      const int l = l0 + FBW * u;
+      if (l >= L) break;   // wave-uniform
+      const float de = s_de[l];
+      dbv += de;
+#pragma unroll
+      for (int c = 0; c < ECH; ++c) {
+        const T* h = (const T*)&xw[u][c];
+#pragma unroll
+        for (int j = 0; j < VN; ++j) {
+          const float t = tanh_t<T>((float)h[j] + uu[c][j]);
+          duh[c][j] += de * vw[c][j] * (1.f - t * t);
+          dv[c][j] += de * t;
+        }
+      }
+    }
+  }
+  // fold the waves in a fixed order: dL/d(U h), then dL/dv
+  constexpr int EC = 64 * VN * ECH;
+#pragma unroll
+  for (int c = 0; c < ECH; ++c)
+#pragma unroll
+    for (int j = 0; j < VN; ++j) s_red[w][c * 64 * VN + lane * VN + j] = duh[c][j];
+  __syncthreads();
+  for (int e = tid; e < EC && e < E; e += FBW * 64) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < FBW; i += 2) v += s_red[i][e] + s_red[i + 1][e];
+    a.d_uh[(long)b * a.d_uh_ld + e] = v;
+    if (a.d_uh_t) ((T*)a.d_uh_t)[(long)b * a.d_uh_ld + e] = (T)v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < ECH; ++c)
+#pragma unroll
+    for (int j = 0; j < VN; ++j) s_red[w][c * 64 * VN + lane * VN + j] = dv[c][j];
+  dbv = wave_sum(dbv);
+  if (lane == 0) s_tmp[w] = dbv;
+  __syncthreads();
+  for (int e = tid; e < EC && e < E; e += FBW * 64) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < FBW; i += 2) v += s_red[i][e] + s_red[i + 1][e];
+    a.dv_acc[(long)b * E + e] += v;
+  }
+  if (tid == 0) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < FBW; i += 2) v += s_tmp[i] + s_tmp[i + 1];
+    a.dbv_acc[b] += v;
+  }
+}
+
 // After the time loop: dWs[b,l,e] = sum over t = T1-1 .. 0 of de[b,t,l] v[e] (1 - tanh^2(Ws[b,l,e] +
 // uh[b,t,e])) -- the per-element expression and summation order of the per-step accumulation it
 // replaces, so the fp32 path is bit-identical to it.  A wave owns DWS_LG rows l of one batch row b
@@ -523,10 +735,53 @@ int sat_attention_fwd_launch(const AttnFwdArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+namespace {
+
+int g_attn_bwd_fused = 1;   // 1: attn_bwd_fused_kernel where it applies, 0: the two-launch form (A/B)
+
+template <typename T, int DCH>
+bool launch_bwd_fused_e(int ech, hipStream_t s, const AttnBwdArgs& a) {
+  constexpr int NW = DCH >= 4 ? 8 : 16, NU = DCH >= 4 ? 7 : 4;
+  if (ech == 1) {
+    hipLaunchKernelGGL((attn_bwd_fused_kernel<T, DCH, 1, NW, NU>), dim3(a.B), dim3(NW * 64), 0, s, a);
+    return true;
+  }
+  if constexpr (sizeof(T) == 4 || DCH == 1) {   // bf16 with DCH >= 2 and ECH = 2 spills: two-launch form
+    if (ech == 2) {
+      hipLaunchKernelGGL((attn_bwd_fused_kernel<T, DCH, 2, NW, NU>), dim3(a.B), dim3(NW * 64), 0, s, a);
+      return true;
+    }
+  }
+  return false;
+}
+template <typename T>
+bool launch_bwd_fused(const AttnBwdArgs& a, hipStream_t s) {
+  constexpr int VN = V16<T>::N;
+  const int dch = sat_cdiv(a.D, 64 * VN), ech = sat_cdiv(a.E, 64 * VN);
+  switch (dch) {
+    case 1: return launch_bwd_fused_e<T, 1>(ech, s, a);
+    case 2: return launch_bwd_fused_e<T, 2>(ech, s, a);
+    case 4: return launch_bwd_fused_e<T, 4>(ech, s, a);
+    default: return false;
+  }
+}
+
+}  // namespace
+
+extern "C" int sat_attention_set_bwd_mode(int fused) {
+  if (fused != 0 && fused != 1) return SAT_ERR_INVALID;
+  g_attn_bwd_fused = fused;
+  return 0;
+}
+
 int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s) {
   const int VD = a.dtype == SAT_BF16 ? 8 : 4;
   SAT_REQUIRE(a.L <= kMaxL && a.E % VD == 0 && a.E <= 1024);
   SAT_REQUIRE(a.D % VD == 0);
+  if (g_attn_bwd_fused && (a.uh_ld % 4) == 0 && (a.E % 4) == 0) {
+    const bool ok = a.dtype == SAT_BF16 ? launch_bwd_fused<bf16>(a, s) : launch_bwd_fused<float>(a, s);
+    if (ok) return (int)hipGetLastError();
+  }
   const int NS = sat_cdiv(a.D, 64 * VD);
   if (a.dtype == SAT_BF16) {
     hipLaunchKernelGGL(attn_bwd1_kernel<bf16>, dim3(a.B, NS), dim3(ANW * 64), 0, s, a);

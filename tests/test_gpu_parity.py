@@ -1143,3 +1143,40 @@ def test_encoder_fused_blocks_equal_unfused(sat):
         enc.fuse_blocks = False
         y_u = enc(x)
     assert torch.equal(y_f, y_u)
+
+
+@pytest.mark.parametrize("dtype,D,bert", [(torch.bfloat16, 2048, False), (torch.float32, 512, False),
+                                          (torch.bfloat16, 512, True)])
+def test_attention_backward_one_launch_matches_two(sat, dtype, D, bert):
+    """attn_bwd_fused_kernel (one workgroup per batch row, the whole step's attention backward in one
+    launch) against the two-launch form it replaces: every decoder gradient at the same inputs, fp32
+    within summation-order noise, bf16 within its rounding (E = 768 with BERT embeddings)."""
+    lib = sat._lib.lib()
+    B, Lf, T = 32, 49, 9
+    V = 30522 if bert else 500
+    pad_id, skip_ids = sat.special_ids(bert)
+    grads = []
+    try:
+        for mode in (1, 0):
+            assert lib.sat_attention_set_bwd_mode(mode) == 0
+            torch.manual_seed(0)
+            dec = sat.Decoder(V, D, tf=True, ado=not bert, bert=bert, attention=True).to(DEV).eval()
+            if dtype == torch.bfloat16:
+                dec.train()
+            g = torch.Generator().manual_seed(3)
+            feats = torch.randn(B, Lf, D, generator=g).to(DEV).to(dtype)
+            caps = O.make_captions(B, T, V, 1, bert=bert).to(DEV)
+            preds, alphas = dec(feats, caps)
+            loss, _ = sat.caption_loss(preds, alphas, caps, pad_id=pad_id, skip_ids=skip_ids)
+            loss.backward()
+            torch.cuda.synchronize()
+            grads.append({n: p.grad.detach().float().cpu().clone() for n, p in dec.named_parameters()
+                          if p.grad is not None})
+    finally:
+        lib.sat_attention_set_bwd_mode(1)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert set(grads[0]) == set(grads[1]) and grads[0]
+    for n, g1 in grads[0].items():
+        g0 = grads[1][n]
+        err = ((g1 - g0).abs().max() / g0.abs().max().clamp_min(1e-12)).item()
+        assert err < tol, (n, err)
