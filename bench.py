@@ -54,6 +54,8 @@ def parse():
                     help="graph + overlap: workgroups the decoder's per-step split-K GEMMs aim for")
     ap.add_argument("--no-fuse-blocks", action="store_true",
                     help="run the layer3 identity bottlenecks as three conv launches (A/B of csrc/convblock.hip)")
+    ap.add_argument("--block-variant", choices=["default", "share"], default="default",
+                    help="fused bottleneck kernel: 'share' = the co-residency variant (57 KB LDS, <= 168 VGPRs)")
     ap.add_argument("--fuse-every", type=int, default=1,
                     help="fuse every n-th layer3 identity bottleneck only (the rest: three conv launches)")
     ap.add_argument("--stream-priority", choices=["decoder-high", "equal"], default="decoder-high",
@@ -316,6 +318,8 @@ def main():
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
     enc.fuse_blocks = False if args.no_fuse_blocks else (True if args.fuse_every == 1 else args.fuse_every)
+    if args.block_variant == "share":
+        assert sat_amd._lib.lib().sat_bottleneck_set_experiment(2, 128) == 0
     torch.manual_seed(42)          # identical decoder init on every rank
     dec = sat_amd.Decoder(args.vocab, D, tf=not args.no_tf, ado=not args.bert, bert=args.bert,
                           attention=True).to(dev).train()
@@ -383,15 +387,22 @@ def main():
                 with torch.cuda.graph(g_enc[k]):
                     with torch.no_grad():
                         feats_static.append(enc(imgs))
-        dec.defer_recurrent_backward(True)
+        # N > 1: backward phase 1 (output head) and phase 2 (BPTT) as two graphs, the head bucket's
+        # all-reduce issued between them; N = 1: one graph, the head's weight gradients on the
+        # decoder's side stream beside the BPTT loop (sat_decoder_backward phase bit 8)
+        split_bwd = world > 1
+        dec.defer_recurrent_backward(split_bwd)
         for k in range(nbuf):
             opt.zero_grad(set_to_none=True)   # each capture overwrites the gradients (beta = 0)
             with torch.cuda.graph(g_dec[k]):
                 preds, alphas = dec(feats_static[k], caps)
                 loss_k, _ = sat_amd.caption_loss(preds, alphas, caps, pad_id=pad_id, skip_ids=skip_ids)
                 loss_k.backward()
-            with torch.cuda.graph(g_rec[k]):
-                dec.finish_backward()
+            if split_bwd:
+                with torch.cuda.graph(g_rec[k]):
+                    dec.finish_backward()
+            else:
+                g_rec[k] = None
             loss_static.append(loss_k)
         dec.defer_recurrent_backward(False)
         torch.cuda.synchronize()
@@ -444,7 +455,8 @@ def main():
                 # DP: the output-head bucket is final after phase 1 -> its all-reduce runs on RCCL's
                 # stream beside the BPTT graph; the rest follows phase 2
                 w1 = allreduce_bucket_async(dec, 1) if world > 1 else None
-                g_rec[k].replay()
+                if g_rec[k] is not None:
+                    g_rec[k].replay()
                 w2 = allreduce_bucket_async(dec, 2) if world > 1 else None
                 ev_dec[k].record(s_main)
                 loss = loss_static[k]

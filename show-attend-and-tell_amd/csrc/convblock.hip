@@ -97,9 +97,10 @@ constexpr int younger_than_a(int T, int KT1, int NT, int PF, bool stream) {
 // bit 1 no weight streaming (the prologue's fragments reused), bit 2 no A fragment reads; bit 3
 // non-temporal input / residual loads, bit 4 non-temporal output stores (both measured slower:
 // 65.6 -> 77.9 / 101.8 us, profiles/r2_s25_block_nt.txt); bit 5 per-workgroup rotation of the waves'
-// n-blocks, bit 6 k-major fragment layout
+// n-blocks, bit 6 k-major fragment layout; bit 7 the co-residency variant (one LDS activation image,
+// <= 168 VGPRs: bottleneck_kernel_share)
 template <int IW, int RO, int CIN, int CMID, int PF, int ABL>
-__global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
+__device__ __forceinline__ void bottleneck_body(const KArgs& a) {
   static_assert(IW / RO == 2 && IW % RO == 0, "two workgroups per image");
   static_assert(CMID == 256 && CIN % 256 == 0 && CIN % 64 == 0, "256-wide phases");
   constexpr int IH = IW;
@@ -114,11 +115,18 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
   constexpr int X1PL = X1ROWS * ROWB;            // X1 plane bytes
   constexpr int X2PL = MB2 * 16 * ROWB;          // X2 plane bytes
   constexpr int NPL = CMID / 64;
-  constexpr int X1 = 0, X2 = NPL * X1PL;         // LDS regions
-  constexpr int RING = X2;                       // c1 input ring aliases X2
+  // SHARE (ABL bit 7, the co-residency variant): one activation image -- c2's output overwrites c1's
+  // after a barrier, and c1's input ring lives there too before c1's epilogue: 57 KB of LDS instead
+  // of 113 KB, so decoder workgroups can share the CU
+  constexpr bool SHARE = (ABL & 128) != 0;
+  constexpr int X1 = 0, X2 = SHARE ? 0 : NPL * X1PL;   // LDS regions
+  constexpr int X2P = SHARE ? X1PL : X2PL;             // X2 plane stride
+  constexpr int RING = SHARE ? 0 : X2;                 // c1 input ring
   constexpr int STG = 128 * ROWB;                // 128 rows x 64 channels per stage
-  static_assert(3 * STG <= NPL * X2PL, "ring fits in X2");
-  constexpr int LDS = X2 + NPL * X2PL;
+  static_assert(3 * STG <= NPL * (SHARE ? X1PL : X2PL), "ring fits");
+  // SHARE keeps the three folded biases in LDS (read at each epilogue) instead of 16 VGPRs
+  constexpr int SB = NPL * X1PL, NBIAS = 2 * CMID + CIN;
+  constexpr int LDS = SHARE ? SB + NBIAS * 4 : X2 + NPL * X2PL;
   constexpr int KT1 = CIN / 64, KT2 = 9 * CMID / 64, NCK = CIN / 256, KT3C = CMID / 64;
   constexpr int NT = KT1 + KT2 + NCK * KT3C;
   constexpr int KS1 = CIN / 32, KS2 = 9 * CMID / 32, KS3 = CMID / 32;
@@ -135,8 +143,11 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
   const int ws = half ? IH - R1 : 0;             // first c1 image row
   const long pix_img = (long)img * IH * IW;
 
-  // ---- zero row of every X1 plane (taps in the padding read it) ----
-  if (tid < NPL * 8) *(uint4*)(smem + X1 + (tid >> 3) * X1PL + P1 * ROWB + (tid & 7) * 16) = make_uint4(0, 0, 0, 0);
+  // ---- zero row of every X1 plane (taps in the padding read it; SHARE: written after the ring's use) ----
+  auto zero_row = [&]() {
+    if (tid < NPL * 8) *(uint4*)(smem + X1 + (tid >> 3) * X1PL + P1 * ROWB + (tid & 7) * 16) = make_uint4(0, 0, 0, 0);
+  };
+  if constexpr (!SHARE) zero_row();
 
   // ---- c1 input ring: k-tile t = channels 64t.., 128 rows (rows >= P1 read zeros) ----
   const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, (int)a.x_bytes, 0x00020000);
@@ -220,7 +231,26 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
+  // SHARE: one 32-deep half's fragments at a time (28 instead of 56 VGPRs)
+  auto mma_half = [&](int ks, const bf16x8 (&af)[MB], const bf16x8 (&b)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
   auto tile_u = [&](const char* base, const bf16x8 (&b)[2][2]) {
+    if constexpr (SHARE) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[MB];
+#pragma unroll
+        for (int i = 0; i < MB; ++i) af[i] = *(const bf16x8*)(base + i * 16 * ROWB + offu[ks]);
+        mma_half(ks, af, b);
+      }
+      return;
+    }
     bf16x8 af[2][MB];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -230,6 +260,16 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
     mma(af, b);
   };
   auto tile_s = [&](const char* base, const bf16x8 (&b)[2][2]) {
+    if constexpr (SHARE) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[MB];
+#pragma unroll
+        for (int i = 0; i < MB; ++i) af[i] = *(const bf16x8*)(base + offs[i][ks]);
+        mma_half(ks, af, b);
+      }
+      return;
+    }
     bf16x8 af[2][MB];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -243,6 +283,10 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
   auto load_bias = [&](const float* bias, int ch0, float4 (&bv)[2]) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + ch0 + wn * 32 + j * 16 + 4 * fh);
+  };
+  auto lds_bias = [&](int ch0, float4 (&bv)[2]) {   // SHARE: bias values from the LDS copy
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(smem + SB + 4 * (ch0 + wn * 32 + j * 16 + 4 * fh));
   };
   auto store_planes = [&](int region, int plane_bytes, const float4 (&bias)[2]) {
     const int plane = wn >> 1;
@@ -266,7 +310,12 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
 
   // ---- prologue ----
   float4 bias_a[2], bias_b[2];
-  load_bias(a.b1, 0, bias_a);
+  if constexpr (SHARE) {   // visible after c1's first barrier
+    float* sb = (float*)(smem + SB);
+    for (int k = tid; k < NBIAS; k += 512) sb[k] = k < CMID ? a.b1[k] : (k < 2 * CMID ? a.b2[k - CMID] : a.b3[k - 2 * CMID]);
+  } else {
+    load_bias(a.b1, 0, bias_a);
+  }
   dma_a(0);
   load_b(0, bq[0]);
   dma_a(1);
@@ -287,24 +336,29 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
     if constexpr (T < KT1) {
       tile_u(smem + RING + (T % 3) * STG, bq[BQ]);
       if constexpr (T == KT1 - 1) {   // c1 epilogue -> X1 (the ring is read for the last time above)
+        if constexpr (SHARE) k_lds_barrier();   // every wave's last ring reads retired before X1 overwrites it
+        if constexpr (SHARE) lds_bias(0, bias_a);
         store_planes(X1, X1PL, bias_a);
+        if constexpr (SHARE) zero_row();
         zero_acc();
         k_lds_barrier();
       }
     } else if constexpr (T < KT1 + KT2) {
       constexpr int t = T - KT1, tap = t / (CMID / 64), pl = t % (CMID / 64);
-      if constexpr (t == 0) load_bias(a.b2, 0, bias_b);
+      if constexpr (t == 0 && !SHARE) load_bias(a.b2, 0, bias_b);
       if constexpr (pl == 0) tap_offsets(tap);
       tile_s(smem + X1 + pl * X1PL, bq[BQ]);
       if constexpr (t == KT2 - 1) {   // c2 epilogue -> X2
-        store_planes(X2, X2PL, bias_b);
+        if constexpr (SHARE) k_lds_barrier();   // every wave's c2 reads of X1 retired before X2 overwrites it
+        if constexpr (SHARE) lds_bias(CMID, bias_b);
+        store_planes(X2, X2P, bias_b);
         zero_acc();
         k_lds_barrier();
       }
     } else {
       constexpr int t = T - KT1 - KT2, ck = t / KT3C, kt = t % KT3C;
-      if constexpr (kt == 0) {   // residual rows + bias of this 256-channel chunk, needed by its epilogue
-        load_bias(a.b3, ck * 256, bias_a);
+      if constexpr (kt == (SHARE ? KT3C - 1 : 0)) {   // residual rows + bias of this chunk, for its epilogue
+        if constexpr (!SHARE) load_bias(a.b3, ck * 256, bias_a);
 #pragma unroll
         for (int i = 0; i < MB; ++i)
 #pragma unroll
@@ -315,11 +369,14 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
             else resv[i][j] = *rp;
           }
       }
-      tile_u(smem + X2 + kt * X2PL, bq[BQ]);
+      tile_u(smem + X2 + kt * X2P, bq[BQ]);
       if constexpr (kt == KT3C - 1) {   // c3 epilogue: bias, fp32 residual add, ReLU, one rounding, 8-B stores
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int ch = ck * 256 + wn * 32 + j * 16 + 4 * fh;
+          if constexpr (SHARE) {
+            if (j == 0) lds_bias(2 * CMID + ck * 256, bias_a);
+          }
           const float4 bv = bias_a[j];
 #pragma unroll
           for (int i = 0; i < MB; ++i) {
@@ -342,6 +399,17 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
       }
     }
   });
+}
+
+template <int PF, int ABL>
+__global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
+  bottleneck_body<14, 7, 1024, 256, PF, ABL>(a);
+}
+// co-residency variant: 57 KB of LDS and at most 168 VGPRs (three waves per SIMD fit), so a decoder
+// workgroup of up to ~100 KB LDS / 2 x 88 VGPRs per SIMD can run on the same CU
+template <int PF, int ABL>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(3))) void bottleneck_kernel_share(KArgs a) {
+  bottleneck_body<14, 7, 1024, 256, PF, ABL | 128>(a);
 }
 
 // [N][K] bf16 -> [N/16][K/32][64 lanes][8]: lane l = (fh << 4) | fr holds row 16 nb + fr, k 32 ks + 8 fh ..
@@ -380,7 +448,8 @@ int g_block_abl = 0;   // diagnostics: ABL bits
 
 template <int PF, int ABL>
 void launch_block(dim3 grid, hipStream_t s, const KArgs& a) {
-  hipLaunchKernelGGL((bottleneck_kernel<14, 7, 1024, 256, PF, ABL>), grid, dim3(512), 0, s, a);
+  if constexpr ((ABL & 128) != 0) hipLaunchKernelGGL((bottleneck_kernel_share<PF, ABL & 127>), grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((bottleneck_kernel<PF, ABL>), grid, dim3(512), 0, s, a);
 }
 template <int PF>
 void launch_block_abl(int abl, dim3 grid, hipStream_t s, const KArgs& a) {
@@ -394,6 +463,7 @@ void launch_block_abl(int abl, dim3 grid, hipStream_t s, const KArgs& a) {
     case 96: launch_block<PF, 96>(grid, s, a); break;
     case 33: launch_block<PF, 33>(grid, s, a); break;
     case 97: launch_block<PF, 97>(grid, s, a); break;
+    case 128: launch_block<PF, 128>(grid, s, a); break;
     default: launch_block<PF, 0>(grid, s, a); break;
   }
 }
@@ -404,7 +474,7 @@ void launch_block_abl(int abl, dim3 grid, hipStream_t s, const KArgs& a) {
 // profiles/r2_s24_block_ablation.txt) and ablation bits (0 = off)
 extern "C" int sat_bottleneck_set_experiment(int pf, int abl) {
   if (pf != 2 || (abl != 0 && abl != 1 && abl != 2 && abl != 4 && abl != 6 && abl != 32 && abl != 64 && abl != 96 &&
-                  abl != 33 && abl != 97)) return SAT_ERR_INVALID;
+                  abl != 33 && abl != 97 && abl != 128)) return SAT_ERR_INVALID;
   g_block_pf = pf;
   g_block_abl = abl;
   g_frag_kmajor = (abl & 64) ? 1 : 0;

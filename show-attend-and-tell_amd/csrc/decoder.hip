@@ -33,7 +33,7 @@ struct WS {
   // backward
   void *dpre_t, *dfh_t, *dfz_t, *dhg_t, *dWs_t, *dpre0_t;
   float *dcomb, *dhd, *dctx_head, *dhg, *dgated, *dh_rec, *dc, *dWs_acc, *dv_acc, *dbv_acc, *part, *demb, *dpre0,
-      *colsum, *de_all;
+      *colsum, *colsum2, *de_all;
 };
 
 // split counts of the per-step skinny GEMMs (M = B rows).  bf16: the LDS-DMA kernel (128 x 64
@@ -138,6 +138,7 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   size_t maxN = V > HG ? V : HG;
   if (D > maxN) maxN = D;
   c.take(w->colsum, sat_colsum_scratch_floats((int)R, (int)maxN) * f);
+  c.take(w->colsum2, sat_colsum_scratch_floats((int)R, (int)maxN) * f);   // the side stream's column sums
   return c.off + 256;
 }
 
@@ -507,6 +508,28 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
   return 0;
 }
 
+namespace {
+
+// Side stream for the output head's weight gradients (phase bit 8): one per host thread, created on
+// first use; the fork / join events are per call site and thread as well, so concurrent decoders on
+// different host threads never share them.  Inside stream capture the event record / wait pairs
+// become graph edges (fork after the head's d logits, join before the call returns).
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork0 = nullptr, fork1 = nullptr, join = nullptr;
+  int init() {
+    if (s) return 0;
+    SAT_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    SAT_CHECK(hipEventCreateWithFlags(&fork0, hipEventDisableTiming));
+    SAT_CHECK(hipEventCreateWithFlags(&fork1, hipEventDisableTiming));
+    SAT_CHECK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+    return 0;
+  }
+};
+thread_local SideStream t_side;
+
+}  // namespace
+
 extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLayout* lay, const float* params,
                                     const void* params_lp, const void* img_features, void* workspace,
                                     size_t workspace_bytes, const void* preds, const float* alphas,
@@ -514,7 +537,10 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
                                     int phase, void* stream) {
   SAT_CHECK((hipError_t)check_dims(dp));
   SAT_REQUIRE(lay && params && img_features && workspace && preds && alphas && d_preds && d_alphas && grads);
-  SAT_REQUIRE((phase & 3) != 0 && phase >= 1 && phase <= 7);   // bit 4: d_preds already ReLU-masked
+  // bit 4: d_preds already ReLU-masked; bit 8 (with bits 1 and 2): the head's weight gradients on a
+  // side stream beside the BPTT loop, joined before returning
+  SAT_REQUIRE((phase & 3) != 0 && phase >= 1 && phase <= 15);
+  SAT_REQUIRE(!(phase & 8) || (phase & 3) == 3);
   SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
   const SatDecoderDims& d = *dp;
   WS w;
@@ -548,6 +574,29 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   auto colsum = [&](const void* X, int dt, long ld, int rows, int N, float* out, float* out2 = nullptr) {
     return sat_colsum(X, dt, ld, rows, N, out, accumulate, out2, w.colsum, s);
   };
+  // head weight gradients: on the side stream (phase bit 8) or in order on s
+  const bool side = (phase & 8) != 0;
+  if (side) SAT_CHECK((hipError_t)t_side.init());
+  hipStream_t hs = side ? t_side.s : s;
+  auto wgrad_h = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo,
+                     int a_tail = 0) {
+    SatGemm g;
+    g.a_tail = a_tail;
+    g.M = M; g.N = N; g.K = K; g.dtype = d.dtype;
+    g.A = X; g.lda = ldx; g.transA = 1;
+    g.B = Y; g.ldb = ldy; g.transB = 1;
+    g.C = out; g.ldc = ldo; g.c_dtype = SAT_F32; g.beta = beta;
+    return sat_gemm_launch(g, hs);
+  };
+  auto colsum_h = [&](const void* X, int dt, long ld, int rows, int N, float* out) {
+    return sat_colsum(X, dt, ld, rows, N, out, accumulate, nullptr, side ? w.colsum2 : w.colsum, hs);
+  };
+  auto fork = [&](hipEvent_t e) -> int {   // the side stream continues after everything issued on s so far
+    if (!side) return 0;
+    SAT_CHECK(hipEventRecord(e, s));
+    SAT_CHECK(hipStreamWaitEvent(hs, e, 0));
+    return 0;
+  };
 
   if (phase & 1) {  // ---------------- output head (decoder.py:117-125,149-158) ----------------
     if (d.ado) {
@@ -562,15 +611,17 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
         SAT_CHECK((hipError_t)sat_relu_mask_mul(d_preds, preds, (long)R * V, d.dtype, w.dpre_t, s));
         dpre = w.dpre_t;
       }
-      SAT_CHECK((hipError_t)wgrad(V, E, R, dpre, ldp, w.comb_t, E, G(lay->fout_w), E, VP != V));
-      SAT_CHECK((hipError_t)colsum(dpre, d.dtype, ldp, R, V, G(lay->fout_b)));
+      SAT_CHECK((hipError_t)fork(t_side.fork0));
+      SAT_CHECK((hipError_t)wgrad_h(V, E, R, dpre, ldp, w.comb_t, E, G(lay->fout_w), E, VP != V));
+      SAT_CHECK((hipError_t)colsum_h(dpre, d.dtype, ldp, R, V, G(lay->fout_b)));
       SAT_CHECK((hipError_t)dgrad_launch(c, R, E, V, dpre, ldp, c.W(lay->fout_w), E, w.dcomb, E, s, nullptr, 0, 0, 0,
                                          VP != V));
       SAT_CHECK((hipError_t)sat_ado_bwd_split(w.dcomb, w.fh, w.fz, (long)R * E, d.dtype, w.dfh_t, w.dfz_t, s));
-      SAT_CHECK((hipError_t)wgrad(E, E, R, w.dfh_t, E, w.hd_t, E, G(lay->fh_w), E));
-      SAT_CHECK((hipError_t)colsum(w.dfh_t, d.dtype, E, R, E, G(lay->fh_b)));
-      SAT_CHECK((hipError_t)wgrad(E, D, R, w.dfz_t, E, w.ctx_t, D, G(lay->fz_w), D));
-      SAT_CHECK((hipError_t)colsum(w.dfz_t, d.dtype, E, R, E, G(lay->fz_b)));
+      SAT_CHECK((hipError_t)fork(t_side.fork1));
+      SAT_CHECK((hipError_t)wgrad_h(E, E, R, w.dfh_t, E, w.hd_t, E, G(lay->fh_w), E));
+      SAT_CHECK((hipError_t)colsum_h(w.dfh_t, d.dtype, E, R, E, G(lay->fh_b)));
+      SAT_CHECK((hipError_t)wgrad_h(E, D, R, w.dfz_t, E, w.ctx_t, D, G(lay->fz_w), D));
+      SAT_CHECK((hipError_t)colsum_h(w.dfz_t, d.dtype, E, R, E, G(lay->fz_b)));
       SAT_CHECK((hipError_t)dgrad(R, E, E, w.dfh_t, E, c.W(lay->fh_w), E, w.dhd, E));
       if (att) SAT_CHECK((hipError_t)dgrad(R, D, E, w.dfz_t, E, c.W(lay->fz_w), D, w.dctx_head, D));
     } else {
@@ -580,8 +631,9 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
         SAT_CHECK((hipError_t)sat_pad_rows(d_preds, nullptr, R, V, VP, d.dtype, w.dpre_t, s));
         dpre = w.dpre_t; ldp = VP;
       }
-      SAT_CHECK((hipError_t)wgrad(V, E, R, dpre, ldp, w.hd_t, E, G(lay->do_w), E, VP != V));
-      SAT_CHECK((hipError_t)colsum(d_preds, d.dtype, V, R, V, G(lay->do_b)));
+      SAT_CHECK((hipError_t)fork(t_side.fork0));
+      SAT_CHECK((hipError_t)wgrad_h(V, E, R, dpre, ldp, w.hd_t, E, G(lay->do_w), E, VP != V));
+      SAT_CHECK((hipError_t)colsum_h(d_preds, d.dtype, V, R, V, G(lay->do_b)));
       SAT_CHECK((hipError_t)dgrad_launch(c, R, E, V, dpre, ldp, c.W(lay->do_w), E, w.dhd, E, s, nullptr, 0, 0, 0,
                                          VP != V));
     }
@@ -634,6 +686,10 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
                                           d.dtype, s));
   SAT_CHECK((hipError_t)wgrad(2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D));
   SAT_CHECK((hipError_t)colsum(w.dpre0, SAT_F32, 2 * E, B, 2 * E, G(lay->init_b)));
+  if (side) {   // join: s continues only after the head's weight gradients
+    SAT_CHECK(hipEventRecord(t_side.join, hs));
+    SAT_CHECK(hipStreamWaitEvent(s, t_side.join, 0));
+  }
   return 0;
 }
 

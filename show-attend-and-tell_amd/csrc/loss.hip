@@ -59,15 +59,28 @@ __global__ __launch_bounds__(256) void loss_rows_kernel(const TT* __restrict__ p
   float m = -INFINITY, se = 0.f, cnt = 0.f;
   constexpr int VEC = 16 / sizeof(TT);
   if (V % VEC == 0) {
-    for (int c = threadIdx.x; c < V / VEC; c += blockDim.x) {
-      uint4 u = *(const uint4*)(x + (long)c * VEC);
-      const TT* h = (const TT*)&u;
+    // LU vectors per thread in flight (the per-thread order c = tid, tid + 256, .. is unchanged)
+    constexpr int LU = 4;
+    const int NV = V / VEC;
+    for (int c0 = threadIdx.x; c0 < NV; c0 += LU * 256) {
+      uint4 u[LU];
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        const float xv = (float)h[j];
-        const int v = c * VEC + j;
-        online_add(m, se, xv);
-        cnt += (xv > xt || (xv == xt && v < tgt)) ? 1.f : 0.f;
+      for (int k = 0; k < LU; ++k) {
+        const int c = c0 + k * 256;
+        u[k] = c < NV ? *(const uint4*)(x + (long)c * VEC) : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int k = 0; k < LU; ++k) {
+        const int c = c0 + k * 256;
+        if (c >= NV) break;
+        const TT* h = (const TT*)&u[k];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const float xv = (float)h[j];
+          const int v = c * VEC + j;
+          online_add(m, se, xv);
+          cnt += (xv > xt || (xv == xt && v < tgt)) ? 1.f : 0.f;
+        }
       }
     }
   } else {
@@ -192,14 +205,26 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const TT* __restrict__ pr
   };
   constexpr int VEC = 16 / sizeof(TT);
   if (V % VEC == 0) {
-    for (int c = threadIdx.x; c < V / VEC; c += blockDim.x) {
-      const uint4 u = *(const uint4*)(x + (long)c * VEC);
-      const TT* h = (const TT*)&u;
-      uint4 o;
-      TT* q = (TT*)&o;
+    constexpr int LU = 4;   // vectors per thread in flight
+    const int NV = V / VEC;
+    for (int c0 = threadIdx.x; c0 < NV; c0 += LU * 256) {
+      uint4 u[LU];
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) q[j] = (TT)grad((float)h[j], c * VEC + j);
-      *(uint4*)(dx + (long)c * VEC) = o;
+      for (int k = 0; k < LU; ++k) {
+        const int c = c0 + k * 256;
+        u[k] = c < NV ? *(const uint4*)(x + (long)c * VEC) : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int k = 0; k < LU; ++k) {
+        const int c = c0 + k * 256;
+        if (c >= NV) break;
+        const TT* h = (const TT*)&u[k];
+        uint4 o;
+        TT* q = (TT*)&o;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) q[j] = (TT)grad((float)h[j], c * VEC + j);
+        *(uint4*)(dx + (long)c * VEC) = o;
+      }
     }
   } else {
     for (int v = threadIdx.x; v < V; v += blockDim.x) dx[v] = (TT)grad((float)x[v], v);

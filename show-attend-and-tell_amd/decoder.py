@@ -401,7 +401,12 @@ class _DecoderFn(torch.autograd.Function):
         accumulate = dec._attach_grads()
         lib = L.lib()
         masked = 4 if getattr(d_preds, "_sat_relu_masked", False) else 0   # phase bit: d_preds already ReLU-masked
-        phases = (1,) if dec._defer_phase2 else (1, 2)
+        if dec._defer_phase2:
+            phases = (1,)
+        elif dec._grad_hooks:   # a hook (DDP bucket all-reduce) runs between the phases
+            phases = (1, 2)
+        else:   # one call: the head's weight gradients on a side stream beside the BPTT loop (bit 8)
+            phases = (3 | 8,)
         for phase in phases:
             L.check(lib.sat_decoder_backward(ctypes.byref(ctx.dims), ctypes.byref(ctx.lay), L.ptr(dec._flat),
                                              L.ptr(ctx.lp), L.ptr(feats), L.ptr(ctx.ws), ctx.ws_bytes, L.ptr(preds),

@@ -1180,3 +1180,46 @@ def test_attention_backward_one_launch_matches_two(sat, dtype, D, bert):
         g0 = grads[1][n]
         err = ((g1 - g0).abs().max() / g0.abs().max().clamp_min(1e-12)).item()
         assert err < tol, (n, err)
+
+
+@pytest.mark.parametrize("ado", [True, False])
+def test_head_wgrads_on_side_stream_bit_identical(sat, ado):
+    """sat_decoder_backward phase bit 8: the output head's weight gradients run on the decoder's side
+    stream beside the BPTT loop (one call) -- every gradient bit-identical to the two-call form a DDP
+    hook forces, also when captured and replayed as a hipGraph."""
+    torch.manual_seed(0)
+    B, Lf, D, V, T = 32, 49, 512, 300, 9
+    dec = sat.Decoder(V, D, tf=True, ado=ado, attention=True).to(DEV).eval()
+    feats = torch.randn(B, Lf, D, generator=torch.Generator().manual_seed(2)).bfloat16().to(DEV)
+    caps = O.make_captions(B, T, V, 1).to(DEV)
+
+    def grads():
+        dec.zero_grad(set_to_none=True)
+        preds, alphas = dec(feats, caps)
+        loss, _ = sat.caption_loss(preds, alphas, caps)
+        loss.backward()
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().clone() for n, p in dec.named_parameters() if p.grad is not None}
+    one = grads()
+    hook = lambda phase, d: None   # noqa: E731  (forces the two-call form)
+    dec._grad_hooks.append(hook)
+    two = grads()
+    dec._grad_hooks.remove(hook)
+    assert set(one) == set(two) and one
+    for n in one:
+        assert torch.equal(one[n], two[n]), n
+    # captured: the fork / join become graph edges
+    dec.zero_grad(set_to_none=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        preds, alphas = dec(feats, caps)
+        loss, _ = sat.caption_loss(preds, alphas, caps)
+        loss.backward()
+    for p in dec.parameters():
+        if p.grad is not None:
+            p.grad.fill_(float("nan"))
+    g.replay()
+    torch.cuda.synchronize()
+    for n, p in dec.named_parameters():
+        if n in one:
+            assert torch.equal(p.grad, one[n]), n
