@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode: run the next batch's encoder after, not beside, this batch's decoder")
-    ap.add_argument("--enc-split", choices=["none", "layer2", "layer3", "layer4"], default="layer3",
+    ap.add_argument("--enc-split", choices=["none", "layer2", "layer3", "layer4"], default="none",
                     help="graph + overlap (ResNet152): the encoder runs as two graphs split at this stage; the "
                          "decoder of batch i runs beside batch i+1's first part only, the second part (the fused, "
                          "chip-filling layer3 blocks) starts when that decoder is done")
@@ -56,6 +56,14 @@ def parse():
                     help="run the layer3 identity bottlenecks as three conv launches (A/B of csrc/convblock.hip)")
     ap.add_argument("--block-variant", choices=["default", "share"], default="default",
                     help="fused bottleneck kernel: 'share' = the co-residency variant (57 KB LDS, <= 168 VGPRs)")
+    ap.add_argument("--bwd", choices=["side", "serial", "split"], default="split",
+                    help="N = 1 decoder backward structure: one call with the head's weight gradients on a side "
+                         "stream (side), one call in order (serial), or two graphs as at N > 1 (split)")
+    ap.add_argument("--cu-split", type=int, default=0,
+                    help="graph + overlap: run the decoder / all-reduce / Adam stream on this many CUs and the "
+                         "next batch's encoder on the rest (CU-masked streams; 0 = shared chip)")
+    ap.add_argument("--cu-layout", choices=["strided", "contig"], default="strided",
+                    help="which CU indices the decoder gets with --cu-split")
     ap.add_argument("--fuse-every", type=int, default=1,
                     help="fuse every n-th layer3 identity bottleneck only (the rest: three conv launches)")
     ap.add_argument("--stream-priority", choices=["decoder-high", "equal"], default="decoder-high",
@@ -387,10 +395,11 @@ def main():
                 with torch.cuda.graph(g_enc[k]):
                     with torch.no_grad():
                         feats_static.append(enc(imgs))
-        # N > 1: backward phase 1 (output head) and phase 2 (BPTT) as two graphs, the head bucket's
-        # all-reduce issued between them; N = 1: one graph, the head's weight gradients on the
-        # decoder's side stream beside the BPTT loop (sat_decoder_backward phase bit 8)
-        split_bwd = world > 1
+        # backward phase 1 (output head) and phase 2 (BPTT) as two graphs, the head bucket's all-reduce
+        # (N > 1) issued between them; --bwd serial / side: one graph (side: the head's weight gradients
+        # on the decoder's side stream beside the BPTT loop, sat_decoder_backward phase bit 8)
+        split_bwd = world > 1 or args.bwd == "split"
+        dec.head_side_stream = args.bwd == "side"
         dec.defer_recurrent_backward(split_bwd)
         for k in range(nbuf):
             opt.zero_grad(set_to_none=True)   # each capture overwrites the gradients (beta = 0)
@@ -408,7 +417,13 @@ def main():
         torch.cuda.synchronize()
 
     enc_events = []
-    if overlap and args.stream_priority == "decoder-high":
+    if overlap and args.cu_split:
+        dec_cus, enc_cus = sat_amd.ops.cu_mask_bits(sat_amd.ops.device_cu_count(), args.cu_split, args.cu_layout)
+        s_main = sat_amd.ops.cu_masked_stream(dec_cus, dev)
+        s_enc = sat_amd.ops.cu_masked_stream(enc_cus, dev)
+        s_main.wait_stream(torch.cuda.current_stream())
+        torch.cuda.set_stream(s_main)
+    elif overlap and args.stream_priority == "decoder-high":
         lo, hi = torch.cuda.Stream.priority_range()
         s_main = torch.cuda.Stream(priority=hi)
         s_enc = torch.cuda.Stream(priority=lo)
@@ -530,7 +545,8 @@ def main():
                                    f"step, V={args.vocab}, T={args.seq}",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": args.seq,
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
-                       "encoder_decoder_overlap": overlap},
+                       "encoder_decoder_overlap": overlap,
+                       "decoder_cus": (args.cu_split or None) if overlap else None},
             "roofline": roof,
             "encoder_trunk": dict(trunk or {}, graph_ms_per_step=(round(enc_ms / args.steps, 3) if enc_ms else None),
                                   split_at=args.enc_split if g_encA is not None else None),

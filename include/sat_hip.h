@@ -89,6 +89,17 @@ typedef struct {
 int sat_abi_version(void);
 const char* sat_error_string(int code);
 
+/* --- streams ---------------------------------------------------------------- */
+/* Compute units of the current device (256 on MI355X). */
+int sat_device_cu_count(int* ncu);
+/* A stream whose kernels run only on the CUs whose bits are set in mask[0..words) (bit i of word w =
+ * CU 32 w + i in the runtime's CU numbering); the decoder and the next batch's encoder run on disjoint
+ * CU sets (train.py:128-164's step, re-scheduled).  Release with sat_stream_destroy. */
+int sat_stream_create_cu_mask(const uint32_t* mask, int words, void** stream_out);
+int sat_stream_destroy(void* stream);
+/* diagnostics: out[2 i] = HW_ID, out[2 i + 1] = XCC_ID register of workgroup i (each spins spin_cycles). */
+int sat_probe_cu_ids(int nblocks, int spin_cycles, uint32_t* out, void* stream);
+
 /* --- generic building blocks -------------------------------------------- */
 /* tuning hook for the bf16 LDS-DMA GEMM (process-global): LDS ring depth (0 = auto | 2 | 3), tile
  * configuration (0 = auto, 1 = 128x128 / 8 waves, 2 = 128x64 / 8, 3 = 128x128 / 4, 4 = 128x256 / 8,

@@ -56,6 +56,10 @@ class SatDecoderLayout(ctypes.Structure):
 _SIGNATURES = [
     ("sat_abi_version", c_int, []),
     ("sat_error_string", ctypes.c_char_p, [c_int]),
+    ("sat_device_cu_count", c_int, [ctypes.POINTER(c_int)]),
+    ("sat_stream_create_cu_mask", c_int, [ctypes.POINTER(ctypes.c_uint32), c_int, ctypes.POINTER(c_void_p)]),
+    ("sat_stream_destroy", c_int, [c_void_p]),
+    ("sat_probe_cu_ids", c_int, [c_int, c_int, c_void_p, c_void_p]),
     ("sat_fast_gemm_set_config", c_int, [c_int, c_int, c_int]),
     ("sat_fast_gemm_set_res_lds", c_int, [c_int]),
     ("sat_fast_gemm_set_trace", c_int, [c_void_p]),

@@ -105,6 +105,9 @@ class Decoder(nn.Module):
         self._seed_host = None
         self._seed_dev = None
         self._defer_phase2 = False     # see defer_recurrent_backward()
+        # one backward call with the head's weight gradients on a side stream beside BPTT (phase bit 8):
+        # off by default -- measured slower (8.35 vs 8.19 ms/step alone, 12.9 vs 8.3 beside the encoder)
+        self.head_side_stream = False
         self._pending_bwd = None
         self.last_tokens = None        # int32 [B, T-1]: token fed at each step of the last forward
 
@@ -406,7 +409,7 @@ class _DecoderFn(torch.autograd.Function):
         elif dec._grad_hooks:   # a hook (DDP bucket all-reduce) runs between the phases
             phases = (1, 2)
         else:   # one call: the head's weight gradients on a side stream beside the BPTT loop (bit 8)
-            phases = (3 | 8,)
+            phases = (3 | 8,) if dec.head_side_stream else (3,)
         for phase in phases:
             L.check(lib.sat_decoder_backward(ctypes.byref(ctx.dims), ctypes.byref(ctx.lay), L.ptr(dec._flat),
                                              L.ptr(ctx.lp), L.ptr(feats), L.ptr(ctx.ws), ctx.ws_bytes, L.ptr(preds),

@@ -206,3 +206,41 @@ def adam_step_(param, grad, exp_avg, exp_avg_sq, param_lp, beta1, beta2, eps, st
     L.check(L.lib().sat_adam_step(L.ptr(param), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), L.ptr(param_lp),
                                   param.numel(), beta1, beta2, eps, step_size, bc2_sqrt, L.stream_of(param)),
             "sat_adam_step")
+
+
+def cu_mask_bits(ncu, n_dec, layout="strided"):
+    """CU index sets for a decoder / encoder partition of the chip: ``strided`` spreads the decoder's
+    ``n_dec`` CUs evenly over the CU numbering (every ncu/n_dec-th), ``contig`` takes the first n_dec."""
+    if not 0 < n_dec < ncu:
+        raise ValueError(f"sat_amd: decoder CU count {n_dec} outside (0, {ncu})")
+    if layout == "strided":
+        step = ncu / n_dec
+        dec = sorted({int(i * step) for i in range(n_dec)})
+    elif layout == "contig":
+        dec = list(range(n_dec))
+    else:
+        raise ValueError(f"sat_amd: unknown CU layout {layout!r}")
+    enc = [i for i in range(ncu) if i not in set(dec)]
+    return dec, enc
+
+
+def cu_masked_stream(cus, device=None):
+    """A torch stream (``torch.cuda.ExternalStream``) whose kernels run only on the CU indices ``cus``
+    (sat_stream_create_cu_mask).  The stream lives for the rest of the process."""
+    ncu = ctypes.c_int(0)
+    L.check(L.lib().sat_device_cu_count(ctypes.byref(ncu)), "sat_device_cu_count")
+    words = (ncu.value + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for c in cus:
+        if not 0 <= c < ncu.value:
+            raise ValueError(f"sat_amd: CU index {c} outside [0, {ncu.value})")
+        mask[c // 32] |= 1 << (c % 32)
+    out = ctypes.c_void_p()
+    L.check(L.lib().sat_stream_create_cu_mask(mask, words, ctypes.byref(out)), "sat_stream_create_cu_mask")
+    return torch.cuda.ExternalStream(out.value, device=device)
+
+
+def device_cu_count():
+    ncu = ctypes.c_int(0)
+    L.check(L.lib().sat_device_cu_count(ctypes.byref(ncu)), "sat_device_cu_count")
+    return ncu.value
