@@ -319,9 +319,6 @@ def main():
     from sat_amd.data import synthetic_captions, synthetic_images
     from sat_amd.distributed import GradAllReduce, allreduce_bucket_async, allreduce_grads
 
-    if not args.no_graph and not args.no_overlap:
-        # the decoder shares the chip with the next batch's encoder: fewer split-K workgroups
-        sat_amd.ops.set_decoder_split_target(args.split_target)
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
@@ -331,6 +328,9 @@ def main():
     torch.manual_seed(42)          # identical decoder init on every rank
     dec = sat_amd.Decoder(args.vocab, D, tf=not args.no_tf, ado=not args.bert, bert=args.bert,
                           attention=True).to(dev).train()
+    if not args.no_graph and not args.no_overlap:
+        # the decoder shares the chip with the next batch's encoder: fewer split-K workgroups
+        dec.split_target = args.split_target
     pad_id, skip_ids = sat_amd.special_ids(args.bert)
     opt = sat_amd.Adam(dec.parameters(), lr=1e-4)
     g = torch.Generator().manual_seed(1000 + rank)

@@ -72,6 +72,10 @@ typedef struct {
   /* optional device counter: when set, masks are drawn from (seed ^ *seed_ptr) and the forward
    * increments *seed_ptr on the stream, so a hipGraph replay draws fresh masks every step. */
   uint64_t* seed_ptr;
+  /* workgroups the per-step split-K GEMMs aim for (0 = the library default, sat_decoder_set_split_target):
+   * per call, so two decoders in one process can differ and a captured graph keeps the value its
+   * workspace was sized with */
+  int split_target;
 } SatDecoderDims;
 
 /* Element offsets of every decoder parameter inside one flat fp32 buffer.  Keys

@@ -41,7 +41,7 @@ class SatDecoderDims(ctypes.Structure):
     _fields_ = [("B", c_int), ("L", c_int), ("D", c_int), ("E", c_int), ("V", c_int), ("T", c_int),
                 ("tf", c_int), ("ado", c_int), ("attention", c_int), ("bert", c_int), ("training", c_int),
                 ("dtype", c_int), ("start_token", c_int), ("has_dropout_mask", c_int), ("seed", c_uint64),
-                ("seed_ptr", c_void_p)]
+                ("seed_ptr", c_void_p), ("split_target", c_int)]
 
 
 LAYOUT_FIELDS = ("embedding", "init_w", "init_b", "hcat_w", "hcat_b", "attW_w", "attW_b", "v_w", "v_b", "wih",

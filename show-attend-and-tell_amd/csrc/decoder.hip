@@ -48,10 +48,10 @@ struct Splits { int h, c, g, dh, i; };
 // decoder prefers 192: 10.24 vs 10.48 ms sequential).  sat_decoder_set_split_target.
 int g_split_target = 192;
 
-inline int pick_splits(int M, int N, int K, int dtype, bool kmajor_w) {
+inline int pick_splits(int M, int N, int K, int dtype, bool kmajor_w, int target) {
   if (dtype != SAT_BF16 || K % 64) return 1;
   const long tiles = (long)sat_cdiv(M, 128) * sat_cdiv(N, kmajor_w ? 128 : 64);
-  long want = (g_split_target + tiles - 1) / tiles;
+  long want = (target + tiles - 1) / tiles;
   if (want > 32) want = 32;
   const int kt = K / 64;
   int best = 1;
@@ -64,12 +64,13 @@ inline int forced(int f, int K, int auto_s) { return (f > 0 && K % 64 == 0 && (K
 inline Splits splits_for(const SatDecoderDims& d) {
   const int E = d.E, D = d.D, HG = 5 * E + D;
   const bool bf = d.dtype == SAT_BF16;
+  const int tg = d.split_target > 0 ? d.split_target : g_split_target;
   Splits s;
-  s.h = pick_splits(d.B, d.attention ? HG : 4 * E, E, d.dtype, false);
-  s.c = pick_splits(d.B, 4 * E, D, d.dtype, false);
-  s.g = pick_splits(d.B, D, 4 * E, d.dtype, true);
-  s.dh = pick_splits(d.B, E, d.attention ? HG : 4 * E, d.dtype, true);
-  s.i = pick_splits(d.B, 2 * E, D, d.dtype, false);
+  s.h = pick_splits(d.B, d.attention ? HG : 4 * E, E, d.dtype, false, tg);
+  s.c = pick_splits(d.B, 4 * E, D, d.dtype, false, tg);
+  s.g = pick_splits(d.B, D, 4 * E, d.dtype, true, tg);
+  s.dh = pick_splits(d.B, E, d.attention ? HG : 4 * E, d.dtype, true, tg);
+  s.i = pick_splits(d.B, 2 * E, D, d.dtype, false, tg);
   if (bf) {
     s.h = forced(g_force_splits.h, E, s.h);
     s.c = forced(g_force_splits.c, D, s.c);
@@ -397,6 +398,7 @@ int check_dims(const SatDecoderDims* d) {
   if (d->B <= 0 || d->L <= 0 || d->D <= 0 || d->E <= 0 || d->V <= 0 || d->T < 3) return SAT_ERR_INVALID;
   if (d->dtype != SAT_F32 && d->dtype != SAT_BF16) return SAT_ERR_INVALID;
   if (d->E % 8 != 0 || d->D % 8 != 0 || d->E > 1024 || d->L > 1024) return SAT_ERR_INVALID;
+  if (d->split_target < 0 || d->split_target > 4096) return SAT_ERR_INVALID;
   return 0;
 }
 

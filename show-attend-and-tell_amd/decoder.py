@@ -108,6 +108,9 @@ class Decoder(nn.Module):
         # one backward call with the head's weight gradients on a side stream beside BPTT (phase bit 8):
         # off by default -- measured slower (8.35 vs 8.19 ms/step alone, 12.9 vs 8.3 beside the encoder)
         self.head_side_stream = False
+        # workgroups the per-step split-K GEMMs aim for (SatDecoderDims.split_target; 0 = library
+        # default): 64 when the decoder shares the chip with the next batch's encoder (bench / train.py)
+        self.split_target = 0
         self._pending_bwd = None
         self.last_tokens = None        # int32 [B, T-1]: token fed at each step of the last forward
 
@@ -265,6 +268,7 @@ class Decoder(nn.Module):
         d.dtype = L.dtype_code(feats.dtype)
         d.start_token = self.tokenizer.cls_token_id if self.use_bert else 0
         d.has_dropout_mask = int(self.training and self.dropout_mask is not None)
+        d.split_target = int(self.split_target)
         # dropout masks: host seed drawn once per module from torch's RNG (train.py:37-43 seeding)
         # XOR a device step counter the forward itself advances -> graph replays draw fresh masks
         if self.training:

@@ -362,7 +362,7 @@ def main(argv=None):
 
     encoder, decoder, word_dict, dt = build(args, device)
     if not args.no_overlap:   # the decoder shares the chip with the next batch's encoder
-        sat_amd.ops.set_decoder_split_target(64)
+        decoder.split_target = 64
     opt = sat_amd.Adam(decoder.parameters(), lr=args.lr)
     grad_ar = sat_dist.GradAllReduce(decoder) if world > 1 else None
     sched = torch.optim.lr_scheduler.StepLR(opt, args.step_size)

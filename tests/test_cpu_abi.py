@@ -48,7 +48,7 @@ int main(void) {
          sizeof(SatGemmArgs), sizeof(SatDecoderDims), sizeof(SatDecoderLayout), sizeof(SatConvGeom));
   P(SatGemmArgs, B) P(SatGemmArgs, C) P(SatGemmArgs, alpha) P(SatGemmArgs, bias) P(SatGemmArgs, add1)
   P(SatGemmArgs, act) P(SatGemmArgs, aux) P(SatGemmArgs, aux_dtype)
-  P(SatDecoderDims, dtype) P(SatDecoderDims, seed) P(SatDecoderDims, seed_ptr)
+  P(SatDecoderDims, dtype) P(SatDecoderDims, seed) P(SatDecoderDims, seed_ptr) P(SatDecoderDims, split_target)
   P(SatDecoderLayout, do_b) P(SatDecoderLayout, total)
   return 0;
 }

@@ -469,9 +469,10 @@ def test_decoder_split_target(sat):
     feats = torch.randn(B, Lf, D, device=DEV).bfloat16()
     caps = O.make_captions(B, T, V, 1).to(DEV)
     out = []
-    try:
-        for target in (192, 64):
-            ops.set_decoder_split_target(target)
+    try:   # the per-decoder field (SatDecoderDims.split_target) and the process default
+        for target, default in ((192, 0), (64, 0), (0, 64)):
+            ops.set_decoder_split_target(default)
+            dec.split_target = target
             for p in dec.parameters():
                 p.grad = None
             preds, alphas = dec(feats, caps)
@@ -480,6 +481,9 @@ def test_decoder_split_target(sat):
             out.append((loss.item(), dec._grad_flat.clone()))
     finally:
         ops.set_decoder_split_target(0)
+    # field 64 == default 64: the same splits (only the atomic embedding gradient's order may differ)
+    assert out[2][0] == out[1][0]
+    assert ((out[2][1] - out[1][1]).norm() / out[1][1].norm()).item() < 1e-5
     assert abs(out[0][0] - out[1][0]) < 1e-3 * abs(out[0][0])
     assert ((out[0][1] - out[1][1]).norm() / out[0][1].norm()).item() < 2e-2
 
@@ -1066,7 +1070,7 @@ def test_cli_karpathy_fixture_streaming(sat, tmp_path, capsys):
         try:
             T.main(argv)
         finally:
-            ops.set_decoder_split_target(0)   # main() sets the overlap split target process-wide
+            ops.set_decoder_split_target(0)
         out = capsys.readouterr().out
         logs[mode] = [_json.loads(l) for l in out.splitlines() if l.startswith("{")]
     a = [r for r in logs["stream"] if "epoch_seconds" not in r]
