@@ -62,9 +62,14 @@ def parse():
     ap.add_argument("--cu-split", type=int, default=0,
                     help="graph + overlap: run the decoder / all-reduce / Adam stream on this many CUs and the "
                          "next batch's encoder on the rest (CU-masked streams; 0 = shared chip)")
-    ap.add_argument("--cu-layout", choices=["strided", "contig"], default="strided",
-                    help="which CU indices the decoder gets with --cu-split")
-    ap.add_argument("--fuse-every", type=int, default=1,
+    ap.add_argument("--cu-layout", choices=["strided", "contig"], default="contig",
+                    help="which CU-mask bits the decoder gets with --cu-split (the runtime interleaves mask bits "
+                         "over the 8 XCDs: bits 0..31 = 4 CUs on every XCD; a mask that leaves an XCD empty is "
+                         "ignored, tools/cu_probe.py)")
+    ap.add_argument("--cu-dec-all", action="store_true",
+                    help="with --cu-split: the decoder stream may use every CU (the encoder still keeps off its "
+                         "--cu-split reserved CUs)")
+    ap.add_argument("--fuse-every", type=int, default=3,
                     help="fuse every n-th layer3 identity bottleneck only (the rest: three conv launches)")
     ap.add_argument("--stream-priority", choices=["decoder-high", "equal"], default="decoder-high",
                     help="graph + overlap: the decoder / all-reduce / Adam stream gets the higher HIP stream "
@@ -419,7 +424,8 @@ def main():
     enc_events = []
     if overlap and args.cu_split:
         dec_cus, enc_cus = sat_amd.ops.cu_mask_bits(sat_amd.ops.device_cu_count(), args.cu_split, args.cu_layout)
-        s_main = sat_amd.ops.cu_masked_stream(dec_cus, dev)
+        lo, hi = torch.cuda.Stream.priority_range()
+        s_main = torch.cuda.Stream(priority=hi) if args.cu_dec_all else sat_amd.ops.cu_masked_stream(dec_cus, dev)
         s_enc = sat_amd.ops.cu_masked_stream(enc_cus, dev)
         s_main.wait_stream(torch.cuda.current_stream())
         torch.cuda.set_stream(s_main)

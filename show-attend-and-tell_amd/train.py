@@ -363,6 +363,7 @@ def main(argv=None):
     encoder, decoder, word_dict, dt = build(args, device)
     if not args.no_overlap:   # the decoder shares the chip with the next batch's encoder
         decoder.split_target = 64
+        encoder.fuse_blocks = 3   # every 3rd layer3 block fused: the rest leave CUs to the decoder (bench.py)
     opt = sat_amd.Adam(decoder.parameters(), lr=args.lr)
     grad_ar = sat_dist.GradAllReduce(decoder) if world > 1 else None
     sched = torch.optim.lr_scheduler.StepLR(opt, args.step_size)
