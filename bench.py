@@ -69,6 +69,10 @@ def parse():
     ap.add_argument("--cu-dec-all", action="store_true",
                     help="with --cu-split: the decoder stream may use every CU (the encoder still keeps off its "
                          "--cu-split reserved CUs)")
+    ap.add_argument("--no-skinny", action="store_true",
+                    help="per-step decoder GEMMs on the LDS-DMA tile kernel instead of csrc/skinny.hip (A/B)")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N > 1: RCCL (one rank per GPU) or gloo (rehearsal: several ranks may share a GPU)")
     ap.add_argument("--fuse-every", type=int, default=3,
                     help="fuse every n-th layer3 identity bottleneck only (the rest: three conv launches)")
     ap.add_argument("--stream-priority", choices=["decoder-high", "equal"], default="decoder-high",
@@ -315,15 +319,23 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; --dist-backend gloo rehearses the N > 1 path with several ranks on one GPU
+    # (device = LOCAL_RANK modulo the visible GPUs; device_count() does not initialise the GPU)
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     import sat_amd
     from sat_amd.data import synthetic_captions, synthetic_images
     from sat_amd.distributed import GradAllReduce, allreduce_bucket_async, allreduce_grads
 
+    if args.no_skinny:
+        assert sat_amd._lib.lib().sat_skinny_set_mode(0) == 0
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
@@ -510,7 +522,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev)
+        t = torch.tensor([elapsed], device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     launches = conv_launches(args.network, B, fused=enc.fuse_blocks)

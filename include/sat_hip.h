@@ -181,6 +181,10 @@ int sat_attention_forward(int B, int L, int D, int E, int dtype, const void* img
                           const float* v_w, const float* v_b, float* ws_scratch,
                           float* context, float* alpha, void* stream);
 
+/* tuning hook (process-global): the register-direct skinny kernel for bf16 NT GEMMs with M <= 128 and fp32
+ * (partial-slab) output: 1 (default) = the decoder's per-step context GEMM and init GEMM (decoder.py:107-115,
+ * 137-147; split into 256-deep K slabs for it), 2 = every eligible problem (tests), 0 = off (A/B). */
+int sat_skinny_set_mode(int on);
 /* tuning hook (process-global): the attention backward of a decoder step as ONE launch per step
  * (1, default: a workgroup per batch row) or the two-launch form (0, A/B). */
 int sat_attention_set_bwd_mode(int fused);

@@ -71,6 +71,12 @@ inline Splits splits_for(const SatDecoderDims& d) {
   s.g = pick_splits(d.B, D, 4 * E, d.dtype, true, tg);
   s.dh = pick_splits(d.B, E, d.attention ? HG : 4 * E, d.dtype, true, tg);
   s.i = pick_splits(d.B, 2 * E, D, d.dtype, false, tg);
+  if (bf) {   // per-step products the skinny kernel runs (csrc/skinny.hip): its own K split
+    int k;
+    if ((k = sat_skinny_splits(d.B, d.attention ? HG : 4 * E, E))) s.h = k;
+    if ((k = sat_skinny_splits(d.B, 4 * E, D))) s.c = k;
+    if ((k = sat_skinny_splits(d.B, 2 * E, D))) s.i = k;
+  }
   if (bf) {
     s.h = forced(g_force_splits.h, E, s.h);
     s.c = forced(g_force_splits.c, D, s.c);

@@ -355,6 +355,7 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s) {
   SAT_REQUIRE(g.dtype == SAT_F32 || g.dtype == SAT_BF16);
   {
     int err = 0;
+    if (sat_skinny_try(g, s, &err)) return err;
     if (sat_conv_stream_try(g, s, &err)) return err;
     if (sat_conv_halo_try(g, s, &err)) return err;
     if (sat_conv_pipe_try(g, s, &err)) return err;

@@ -92,3 +92,7 @@ int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err);
 int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err);
 // 3x3 / stride 1 convs with a per-channel-chunk input halo (convhalo.hip); returns 1 when it launched.
 int sat_conv_halo_try(const SatGemm& g, hipStream_t s, int* err);
+// register-direct skinny GEMM (M <= 128, NT, fp32 / partial-slab output: the decoder's per-step
+// products, skinny.hip); returns 1 when it launched.
+int sat_skinny_try(const SatGemm& g, hipStream_t s, int* err);
+int sat_skinny_splits(int M, int N, int K);   // partial splits the skinny kernel prefers (0 = not eligible)

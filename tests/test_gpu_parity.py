@@ -1236,3 +1236,69 @@ def test_head_wgrads_on_side_stream_match(sat, ado):
     for n, p in dec.named_parameters():
         if n in one:
             assert same(p.grad, one[n], n), n
+
+
+@pytest.mark.parametrize("M,N,K,bias", [(128, 4608, 512, True), (128, 2048, 2048, False), (100, 1024, 1024, True),
+                                        (32, 64, 96, False), (7, 96, 32, True)])
+def test_skinny_gemm_direct(sat, M, N, K, bias):
+    """skinny_gemm_kernel (csrc/skinny.hip): bf16 NT, fp32 output, M <= 128 (the decoder's per-step
+    products) against an fp64 product of the same bf16 operands, and against the LDS-DMA tile kernel
+    it replaces (sat_skinny_set_mode(0))."""
+    from sat_amd import ops
+    lib = sat._lib.lib()
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    Bm = torch.randn(N, K, generator=g).bfloat16()
+    b = torch.randn(N, generator=g) if bias else None
+    ref = A.double() @ Bm.double().T + (b.double() if bias else 0)
+    outs = []
+    try:
+        for mode in (2, 0):   # 2: every eligible problem on the skinny kernel
+            assert lib.sat_skinny_set_mode(mode) == 0
+            C = torch.full((M, N), float("nan"), device=DEV)
+            ops.gemm(A.to(DEV), Bm.to(DEV), C, bias=b.to(DEV) if bias else None)
+            torch.cuda.synchronize()
+            outs.append(C.cpu().double())
+    finally:
+        lib.sat_skinny_set_mode(1)
+    for C in outs:
+        assert torch.isfinite(C).all()
+        assert ((C - ref).abs().max() / ref.abs().max()).item() < 1e-5
+    assert ((outs[0] - outs[1]).abs().max() / ref.abs().max()).item() < 1e-5
+
+
+@pytest.mark.parametrize("tf", [True, False])
+def test_decoder_skinny_matches_tile_kernel(sat, tf):
+    """The decoder's per-step GEMMs (partial-slab split-K) on the skinny kernel vs the LDS-DMA tile
+    kernel: predictions, alphas, loss and every gradient within bf16-path summation-order noise; greedy
+    ids (no teacher forcing) identical."""
+    lib = sat._lib.lib()
+    B, Lf, D, V, T = 128, 49, 2048, 1000, 12
+    res = []
+    try:
+        for mode in (1, 0):
+            assert lib.sat_skinny_set_mode(mode) == 0
+            torch.manual_seed(0)
+            dec = sat.Decoder(V, D, tf=tf, ado=True, attention=True).to(DEV).eval()
+            dec.split_target = 64
+            g = torch.Generator().manual_seed(5)
+            feats = torch.randn(B, Lf, D, generator=g).bfloat16().to(DEV)
+            caps = O.make_captions(B, T, V, 1).to(DEV)
+            preds, alphas = dec(feats, caps)
+            loss, _ = sat.caption_loss(preds, alphas, caps)
+            loss.backward()
+            torch.cuda.synchronize()
+            res.append((preds.float().cpu(), alphas.cpu(), loss.item(), dec.last_tokens.cpu().clone(),
+                        {n: p.grad.float().cpu().clone() for n, p in dec.named_parameters() if p.grad is not None}))
+    finally:
+        lib.sat_skinny_set_mode(1)
+    (p1, a1, l1, t1, g1), (p0, a0, l0, t0, g0) = res
+    if not torch.equal(t1, t0):   # greedy: a near-tie argmax may flip under a different summation order
+        assert not tf and (t1 == t0).float().mean().item() > 0.98
+        return
+    assert ((p1 - p0).abs().max() / p0.abs().max()).item() < 2e-2
+    assert (a1 - a0).abs().max().item() < 2e-2
+    assert abs(l1 - l0) < 1e-3 * abs(l0)
+    for n, g in g0.items():
+        scale = g0["attention.v.weight"] if n == "attention.v.bias" else g
+        assert ((g1[n] - g).norm() / scale.norm().clamp_min(1e-12)).item() < 3e-2, n
