@@ -75,7 +75,7 @@ def parse():
                     help="N > 1: RCCL (one rank per GPU) or gloo (rehearsal: several ranks may share a GPU)")
     ap.add_argument("--fuse-every", type=int, default=3,
                     help="fuse every n-th layer3 identity bottleneck only (the rest: three conv launches)")
-    ap.add_argument("--stream-priority", choices=["decoder-high", "equal"], default="decoder-high",
+    ap.add_argument("--stream-priority", choices=["decoder-high", "equal", "encoder-high"], default="decoder-high",
                     help="graph + overlap: the decoder / all-reduce / Adam stream gets the higher HIP stream "
                          "priority, so its short per-step kernels are dispatched first when CUs free up")
     ap.add_argument("--fp32-steps", type=int, default=3,
@@ -441,10 +441,11 @@ def main():
         s_enc = sat_amd.ops.cu_masked_stream(enc_cus, dev)
         s_main.wait_stream(torch.cuda.current_stream())
         torch.cuda.set_stream(s_main)
-    elif overlap and args.stream_priority == "decoder-high":
+    elif overlap and args.stream_priority != "equal":
         lo, hi = torch.cuda.Stream.priority_range()
-        s_main = torch.cuda.Stream(priority=hi)
-        s_enc = torch.cuda.Stream(priority=lo)
+        dec_hi = args.stream_priority == "decoder-high"
+        s_main = torch.cuda.Stream(priority=hi if dec_hi else lo)
+        s_enc = torch.cuda.Stream(priority=lo if dec_hi else hi)
         s_main.wait_stream(torch.cuda.current_stream())
         torch.cuda.set_stream(s_main)
     else:
