@@ -73,6 +73,9 @@ def parse():
                     help="per-step decoder GEMMs on the LDS-DMA tile kernel instead of csrc/skinny.hip (A/B)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="N > 1: RCCL (one rank per GPU) or gloo (rehearsal: several ranks may share a GPU)")
+    ap.add_argument("--gemm-stages", type=int, default=0, choices=[0, 2, 3],
+                    help="LDS ring depth of the bf16 tile GEMM kernel (0 = auto: 3 for the decoder's per-step "
+                         "split-K GEMMs, 2 otherwise)")
     ap.add_argument("--fuse-every", type=int, default=3,
                     help="fuse every n-th layer3 identity bottleneck only (the rest: three conv launches)")
     ap.add_argument("--stream-priority", choices=["decoder-high", "equal", "encoder-high"], default="decoder-high",
@@ -336,6 +339,8 @@ def main():
 
     if args.no_skinny:
         assert sat_amd._lib.lib().sat_skinny_set_mode(0) == 0
+    if args.gemm_stages:
+        assert sat_amd._lib.lib().sat_fast_gemm_set_config(args.gemm_stages, 0, 1) == 0
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()

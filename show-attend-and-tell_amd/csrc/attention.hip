@@ -91,7 +91,9 @@ __global__ __launch_bounds__(FNW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
   constexpr int VN = V16<T>::N;            // elements per 16-byte vector
   constexpr int COLS = 64 * VN * FDV;      // context columns of one workgroup
   __shared__ float s_alpha[kMaxL];
-  __shared__ float s_red[FNW][COLS];
+  // the 16 waves' context partials fold through 8 LDS rows in two rounds (36 KB of LDS instead of 68:
+  // the kernel then fits beside a 98-122 KB encoder workgroup on the same CU)
+  __shared__ float s_red[FNW / 2][COLS];
   const int b = blockIdx.x, s = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = a.L, D = a.D, E = a.E;
@@ -227,16 +229,25 @@ __global__ __launch_bounds__(FNW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
       }
     }
   }
+  // fixed summation order over the wave partials: c = sum over q = 0, 2, .., 14 of (p_q + p_(q+1)),
+  // waves 0-7 first, then waves 8-15 through the same 8 rows
+  float c = 0.f;
 #pragma unroll
-  for (int v = 0; v < FDV; ++v)
+  for (int half = 0; half < 2; ++half) {
+    if ((w >> 3) == half) {
 #pragma unroll
-    for (int j = 0; j < VN; ++j) s_red[w][v * 64 * VN + lane * VN + j] = part[v][j];
-  __syncthreads();
+      for (int v = 0; v < FDV; ++v)
+#pragma unroll
+        for (int j = 0; j < VN; ++j) s_red[w & 7][v * 64 * VN + lane * VN + j] = part[v][j];
+    }
+    __syncthreads();
+    if (out_ok) {
+#pragma unroll
+      for (int q = 0; q < FNW / 2; q += 2) c += s_red[q][tid] + s_red[q + 1][tid];
+    }
+    if (half == 0) __syncthreads();
+  }
   if (out_ok) {
-    // fixed summation order over the wave partials
-    float c = 0.f;
-#pragma unroll
-    for (int q = 0; q < FNW; q += 2) c += s_red[q][tid] + s_red[q + 1][tid];
     a.ctx[(long)b * a.ctx_ld + dout] = c;
     if (a.ctx_t) ((T*)a.ctx_t)[(long)b * a.ctx_t_ld + dout] = (T)c;
     if (a.gate_pre) {
