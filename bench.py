@@ -50,8 +50,9 @@ def parse():
                     help="graph + overlap (ResNet152): the encoder runs as two graphs split at this stage; the "
                          "decoder of batch i runs beside batch i+1's first part only, the second part (the fused, "
                          "chip-filling layer3 blocks) starts when that decoder is done")
-    ap.add_argument("--split-target", type=int, default=64,
-                    help="graph + overlap: workgroups the decoder's per-step split-K GEMMs aim for")
+    ap.add_argument("--split-target", type=int, default=None,
+                    help="graph + overlap: workgroups the decoder's per-step split-K GEMMs aim for (default: "
+                         "64 with ResNet152 features, 128 with VGG19's: profiles/r2_s54_sched.txt)")
     ap.add_argument("--no-fuse-blocks", action="store_true",
                     help="run the layer3 identity bottlenecks as three conv launches (A/B of csrc/convblock.hip)")
     ap.add_argument("--block-variant", choices=["default", "share"], default="default",
@@ -76,8 +77,10 @@ def parse():
     ap.add_argument("--gemm-stages", type=int, default=0, choices=[0, 2, 3],
                     help="LDS ring depth of the bf16 tile GEMM kernel (0 = auto: 3 for the decoder's per-step "
                          "split-K GEMMs, 2 otherwise)")
-    ap.add_argument("--fuse-every", type=int, default=3,
-                    help="fuse every n-th layer3 identity bottleneck only (the rest: three conv launches)")
+    ap.add_argument("--fuse-every", type=int, default=None,
+                    help="fuse every n-th layer3 identity bottleneck only, the rest run as three conv launches "
+                         "(default: 3 with teacher forcing, 0 = none without: the greedy decoder chain is longer; "
+                         "profiles/r2_s54_sched.txt)")
     ap.add_argument("--stream-priority", choices=["decoder-high", "equal", "encoder-high"], default="decoder-high",
                     help="graph + overlap: the decoder / all-reduce / Adam stream gets the higher HIP stream "
                          "priority, so its short per-step kernels are dispatched first when CUs free up")
@@ -344,7 +347,12 @@ def main():
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
-    enc.fuse_blocks = False if args.no_fuse_blocks else (True if args.fuse_every == 1 else args.fuse_every)
+    if args.fuse_every is None:
+        args.fuse_every = 0 if args.no_tf else 3
+    if args.split_target is None:
+        args.split_target = 128 if args.network == "vgg19" else 64
+    enc.fuse_blocks = (False if args.no_fuse_blocks or args.fuse_every == 0 else
+                       (True if args.fuse_every == 1 else args.fuse_every))
     if args.block_variant == "share":
         assert sat_amd._lib.lib().sat_bottleneck_set_experiment(2, 128) == 0
     torch.manual_seed(42)          # identical decoder init on every rank
