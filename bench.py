@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--gemm-stages", type=int, default=0, choices=[0, 2, 3],
                     help="LDS ring depth of the bf16 tile GEMM kernel (0 = auto: 3 for the decoder's per-step "
                          "split-K GEMMs, 2 otherwise)")
+    ap.add_argument("--no-ws3x3", action="store_true",
+                    help="64 -> 64 3x3 convs on the implicit-GEMM tile kernel instead of csrc/conv3x3ws.hip (A/B)")
     ap.add_argument("--fuse-every", type=int, default=None,
                     help="fuse every n-th layer3 identity bottleneck only, the rest run as three conv launches "
                          "(default: 3 with teacher forcing, 0 = none without: the greedy decoder chain is longer; "
@@ -342,6 +344,8 @@ def main():
 
     if args.no_skinny:
         assert sat_amd._lib.lib().sat_skinny_set_mode(0) == 0
+    if args.no_ws3x3:
+        assert sat_amd._lib.lib().sat_conv3x3_ws_set_mode(0) == 0
     if args.gemm_stages:
         assert sat_amd._lib.lib().sat_fast_gemm_set_config(args.gemm_stages, 0, 1) == 0
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream

@@ -181,6 +181,10 @@ int sat_attention_forward(int B, int L, int D, int E, int dtype, const void* img
                           const float* v_w, const float* v_b, float* ws_scratch,
                           float* context, float* alpha, void* stream);
 
+/* tuning hook (process-global): 3x3 / stride-1 / pad-1 convs with 64 input and output channels at width
+ * 56 or 224 (ResNet152 layer1 c2, VGG19 conv1_2; encoder.py:13-17,23-27) on the weight-stationary halo
+ * kernel (1, default) or the implicit-GEMM tile kernel (0, A/B). */
+int sat_conv3x3_ws_set_mode(int on);
 /* tuning hook (process-global): the register-direct skinny kernel for bf16 NT GEMMs with M <= 128 and fp32
  * (partial-slab) output: 1 (default) = the decoder's per-step context GEMM and init GEMM (decoder.py:107-115,
  * 137-147; split into 256-deep K slabs for it), 2 = every eligible problem (tests), 0 = off (A/B). */

@@ -68,6 +68,7 @@ _SIGNATURES = [
     ("sat_conv_stream_set_mode", c_int, [c_int]),
     ("sat_conv_halo_set_mode", c_int, [c_int]),
     ("sat_skinny_set_mode", c_int, [c_int]),
+    ("sat_conv3x3_ws_set_mode", c_int, [c_int]),
     ("sat_attention_set_bwd_mode", c_int, [c_int]),
     ("sat_decoder_set_splits", c_int, [c_int, c_int, c_int, c_int]),
     ("sat_decoder_set_split_target", c_int, [c_int]),

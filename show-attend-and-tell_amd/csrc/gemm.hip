@@ -356,6 +356,7 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s) {
   {
     int err = 0;
     if (sat_skinny_try(g, s, &err)) return err;
+    if (sat_conv3x3_ws_try(g, s, &err)) return err;
     if (sat_conv_stream_try(g, s, &err)) return err;
     if (sat_conv_halo_try(g, s, &err)) return err;
     if (sat_conv_pipe_try(g, s, &err)) return err;

@@ -95,4 +95,6 @@ int sat_conv_halo_try(const SatGemm& g, hipStream_t s, int* err);
 // register-direct skinny GEMM (M <= 128, NT, fp32 / partial-slab output: the decoder's per-step
 // products, skinny.hip); returns 1 when it launched.
 int sat_skinny_try(const SatGemm& g, hipStream_t s, int* err);
-int sat_skinny_splits(int M, int N, int K);   // partial splits the skinny kernel prefers (0 = not eligible)
+int sat_skinny_splits(int M, int N, int K);
+// weight-stationary 3x3 / stride-1 conv, 64 -> 64 channels, W 56 or 224 (conv3x3ws.hip); returns 1 when it launched.
+int sat_conv3x3_ws_try(const SatGemm& g, hipStream_t s, int* err);   // partial splits the skinny kernel prefers (0 = not eligible)
