@@ -34,8 +34,7 @@ typedef __attribute__((address_space(3))) void w_lds_void;
 typedef unsigned __attribute__((ext_vector_type(2))) w_u32x2;
 
 constexpr int WS_NW = 8;                 // waves per workgroup: 4 channel groups x 2 pixel halves
-constexpr int WS_C = 64;                 // input = output channels
-constexpr int WS_KS = 9 * WS_C / 32;     // 18 k-steps of 32
+constexpr int WS_NOUT = 64;              // output channels (4 groups of 16)
 constexpr int WS_MB = 7;                 // 16-pixel m-blocks per wave (112 of the item's 224 pixels)
 constexpr unsigned WS_OOB = 0x80000000u;
 
@@ -53,13 +52,18 @@ __device__ __forceinline__ void w_wait_barrier_n() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+// KK x KK window with PADT rows / columns of top-left padding over C input channels (3 / 64 / 1: the
+// 3x3 convs; 4 / 16 / 2: ResNet152's stem as a 4x4 conv over the 2x2 space-to-depth input);
 // TR x TW output pixels per item (TR * TW = 224); HP halo pixels, DMA rounds of 8 KB (16 B per lane)
-template <int TR, int TW, int NSTG, int ACT>
-__global__ __launch_bounds__(WS_NW * 64) void conv3x3_ws_kernel(WArgs a) {
+template <int KK, int C, int PADT, int TR, int TW, int NSTG, int ACT>
+__global__ __launch_bounds__(WS_NW * 64) void conv_ws_kernel(WArgs a) {
   static_assert(TR * TW == 2 * WS_MB * 16, "224 pixels per item");
   static_assert(NSTG == 2 || NSTG == 3, "ring depth");
-  constexpr int HW_ = TW + 2, HP = (TR + 2) * HW_;
-  constexpr int ROWB = WS_C * 2;                           // 128 B per halo pixel
+  static_assert(C == 64 || C == 16, "8 or 2 16-B chunks per pixel");
+  constexpr int K = KK * KK * C, KSN = K / 32;             // k-steps of 32
+  constexpr int CPX = C / 8;                               // 16-B chunks per halo pixel
+  constexpr int HW_ = TW + KK - 1, HP = (TR + KK - 1) * HW_;
+  constexpr int ROWB = C * 2;                              // bytes per halo pixel
   constexpr int NDMA = (HP * ROWB + WS_NW * 1024 - 1) / (WS_NW * 1024);   // DMA instructions per lane per item
   constexpr int STG = NDMA * WS_NW * 1024;                 // LDS bytes per stage
   static_assert(NSTG * STG <= 160 * 1024, "ring fits in LDS");
@@ -71,17 +75,17 @@ __global__ __launch_bounds__(WS_NW * 64) void conv3x3_ws_kernel(WArgs a) {
   const int cg = w & 3, ph = w >> 2;                      // channel group, pixel half
   const int fr = lane & 15, fh = lane >> 4;
 
-  // weight fragments of this wave's 16 channels for all of K (k = tap * 64 + ci), loaded once
-  bf16x8 bq[WS_KS];
+  // weight fragments of this wave's 16 channels for all of K (k = tap * C + ci), loaded once
+  bf16x8 bq[KSN];
 #pragma unroll
-  for (int ks = 0; ks < WS_KS; ++ks) bq[ks] = *(const bf16x8*)(a.w + (long)(16 * cg + fr) * (9 * WS_C) + ks * 32 + 8 * fh);
+  for (int ks = 0; ks < KSN; ++ks) bq[ks] = *(const bf16x8*)(a.w + (long)(16 * cg + fr) * K + ks * 32 + 8 * fh);
   float bias4[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) bias4[j] = a.bias ? a.bias[16 * cg + 4 * fh + j] : 0.f;
   // consume the weights and biases here: otherwise the compiler's vmcnt tracking still sees them
   // pending inside the item loop and inserts waits that also drain the next items' halo DMAs
 #pragma unroll
-  for (int ks = 0; ks < WS_KS; ++ks) asm volatile("" ::"v"(bq[ks]));
+  for (int ks = 0; ks < KSN; ++ks) asm volatile("" ::"v"(bq[ks]));
 #pragma unroll
   for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(bias4[j]));
 
@@ -96,7 +100,8 @@ __global__ __launch_bounds__(WS_NW * 64) void conv3x3_ws_kernel(WArgs a) {
     x0 = (r - ty * a.tiles_x) * TW;
   };
   // halo of item `it` into stage `buf`: LDS byte b = (d * NW + w) * 1024 + lane * 16 holds chunk
-  // pc = (b % 128) / 16 of halo pixel hp = b / 128, i.e. logical chunk c = pc ^ (hp & 7)
+  // pc = (b % ROWB) / 16 of halo pixel hp = b / ROWB, i.e. logical chunk c = pc ^ (hp & 7) (C = 64;
+  // two chunks per pixel at C = 16 need no swizzle)
   auto stage = [&](int it, int buf) {
     int n, y0, x0;
     item_origin(it, n, y0, x0);
@@ -104,20 +109,20 @@ __global__ __launch_bounds__(WS_NW * 64) void conv3x3_ws_kernel(WArgs a) {
 #pragma unroll
     for (int d = 0; d < NDMA; ++d) {
       const int byte = (d * WS_NW + w) * 1024 + lane * 16;
-      const int hp = byte >> 7, pc = (byte >> 4) & 7, c = pc ^ (hp & 7);
+      const int hp = byte / ROWB, pc = (byte % ROWB) >> 4, c = CPX == 8 ? pc ^ (hp & 7) : pc;
       const int hy = hp / HW_, hx = hp - hy * HW_;
-      const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+      const int yy = y0 + hy - PADT, xx = x0 + hx - PADT;
       const bool ok = hp < HP && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
-      const unsigned off = ok && !(a.abl & 4) ? (unsigned)(((((long)n * a.H + yy) * a.W + xx) * WS_C + 8 * c) * 2) : WS_OOB;
+      const unsigned off = ok && !(a.abl & 4) ? (unsigned)(((((long)n * a.H + yy) * a.W + xx) * C + 8 * c) * 2) : WS_OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (w_lds_void*)(st + (d * WS_NW + w) * 1024), 16, (int)off, 0, 0, 0);
     }
   };
-  // the halo pixel of output pixel i*16 + fr under tap (0, 0) shifted by (dh, dw) = hp0[i] + dh * HW_ + dw
+  // the halo pixel of output pixel i*16 + fr under tap (kh, kw) = hp0[i] + kh * HW_ + kw
   int hp0[WS_MB];
 #pragma unroll
   for (int i = 0; i < WS_MB; ++i) {
     const int p = (ph * WS_MB + i) * 16 + fr, py = p / TW, px = p - py * TW;
-    hp0[i] = (py + 1) * HW_ + px + 1;
+    hp0[i] = py * HW_ + px;
   }
 
   int it = blockIdx.x;
@@ -155,17 +160,17 @@ __global__ __launch_bounds__(WS_NW * 64) void conv3x3_ws_kernel(WArgs a) {
     f32x4 acc[WS_MB];
 #pragma unroll
     for (int i = 0; i < WS_MB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto afrag = [&](int i, int ks) {
-      const int tap = ks >> 1, dh = tap / 3 - 1, dw = tap % 3 - 1;
-      const int hp = hp0[i] + dh * HW_ + dw, c = (ks & 1) * 4 + fh;
-      return *(const bf16x8*)(base + hp * ROWB + 16 * (c ^ (hp & 7)));
+    auto afrag = [&](int i, int ks) {   // k = ks * 32 + 8 fh: tap k / C, chunk (k % C) / 8
+      const int k = ks * 32 + 8 * fh, tap = k / C, c = (k % C) >> 3;
+      const int hp = hp0[i] + (tap / KK) * HW_ + tap % KK;
+      return *(const bf16x8*)(base + hp * ROWB + 16 * (CPX == 8 ? c ^ (hp & 7) : c));
     };
     bf16x8 af[2][WS_MB];
 #pragma unroll
     for (int i = 0; i < WS_MB; ++i) af[0][i] = afrag(i, 0);
 #pragma unroll
-    for (int ks = 0; ks < WS_KS; ++ks) {
-      if (ks + 1 < WS_KS) {
+    for (int ks = 0; ks < KSN; ++ks) {
+      if (ks + 1 < KSN) {
 #pragma unroll
         for (int i = 0; i < WS_MB; ++i) af[(ks + 1) & 1][i] = afrag(i, ks + 1);
       }
@@ -182,7 +187,7 @@ __global__ __launch_bounds__(WS_NW * 64) void conv3x3_ws_kernel(WArgs a) {
       bf16* ob = (bf16*)&o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) ob[j] = (bf16)apply_act(acc[i][j] + bias4[j], ACT);
-      const unsigned off = (a.abl & 2) ? WS_OOB : (unsigned)(((((long)n * a.H + y0 + py) * a.W + x0 + px) * WS_C + 16 * cg + 4 * fh) * 2);
+      const unsigned off = (a.abl & 2) ? WS_OOB : (unsigned)(((((long)n * a.H + y0 + py) * a.W + x0 + px) * WS_NOUT + 16 * cg + 4 * fh) * 2);
       __builtin_amdgcn_raw_buffer_store_b64(o, rY, (int)off, 0, 0);
     }
     it += step;
@@ -197,32 +202,35 @@ int g_ws_cus = 0;
 
 inline bool wal16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <int TR, int TW, int NSTG>
+template <int KK, int C, int PADT, int TR, int TW, int NSTG>
 void launch_ws(int act, dim3 grid, hipStream_t s, const WArgs& a) {
-  if (act == SAT_ACT_RELU) hipLaunchKernelGGL((conv3x3_ws_kernel<TR, TW, NSTG, SAT_ACT_RELU>), grid, dim3(WS_NW * 64), 0, s, a);
-  else hipLaunchKernelGGL((conv3x3_ws_kernel<TR, TW, NSTG, SAT_ACT_NONE>), grid, dim3(WS_NW * 64), 0, s, a);
+  if (act == SAT_ACT_RELU)
+    hipLaunchKernelGGL((conv_ws_kernel<KK, C, PADT, TR, TW, NSTG, SAT_ACT_RELU>), grid, dim3(WS_NW * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_ws_kernel<KK, C, PADT, TR, TW, NSTG, SAT_ACT_NONE>), grid, dim3(WS_NW * 64), 0, s, a);
 }
 
 }  // namespace
 
-// Returns 1 if the 3x3 64 -> 64 conv was launched by the weight-stationary kernel, 0 otherwise.
+// Returns 1 if the conv was launched by the weight-stationary kernel (3x3 / pad 1 over 64 channels at
+// width 56 or 224; the 4x4 / top-left-pad-2 stem over the 16-channel space-to-depth input at width
+// 112), 0 otherwise.
 int sat_conv3x3_ws_try(const SatGemm& g, hipStream_t s, int* err) {
   *err = 0;
   if (g_ws_mode == 0) return 0;
   const SatConvGeom& cv = g.conv;
-  if (cv.C != WS_C || g.N != WS_C || cv.KH != 3 || cv.KW != 3 || cv.stride != 1 || cv.pad != 1) return 0;
-  if (cv.OH != cv.H || cv.OW != cv.W) return 0;
+  const bool c3 = cv.C == 64 && cv.KH == 3 && cv.KW == 3 && cv.pad == 1 && (cv.W == 56 || cv.W == 224);
+  const bool stem = cv.C == 16 && cv.KH == 4 && cv.KW == 4 && cv.pad == 2 && cv.W == 112;
+  if (!(c3 || stem) || g.N != WS_NOUT || cv.stride != 1 || cv.OH != cv.H || cv.OW != cv.W) return 0;
   if (g.dtype != SAT_BF16 || g.c_dtype != SAT_BF16 || g.batch != 1 || g.aux || g.transB || g.add1) return 0;
   if (g.beta != 0.f || g.alpha != 1.f || g.partial_splits > 1) return 0;
   if (g.act != SAT_ACT_NONE && g.act != SAT_ACT_RELU) return 0;
-  if (g.ldb != 9 * WS_C || g.ldc != WS_C) return 0;
+  if (g.ldb != cv.KH * cv.KW * cv.C || g.ldc != WS_NOUT) return 0;
   if (!wal16(g.A) || !wal16(g.B) || !wal16(g.C) || (g.bias && !wal16(g.bias))) return 0;
-  int TR, TW;
-  if (cv.W == 56 && cv.H % 4 == 0) { TR = 4; TW = 56; }
-  else if (cv.W == 224 && cv.H % 2 == 0) { TR = 2; TW = 112; }
-  else return 0;
-  const long bytes = 2L * cv.N * cv.H * cv.W * WS_C;
-  if (bytes >= (1L << 31)) return 0;
+  const int TR = cv.W == 56 ? 4 : 2, TW = cv.W == 56 ? 56 : 112;
+  if (cv.H % TR) return 0;
+  const long xb = 2L * cv.N * cv.H * cv.W * cv.C, yb = 2L * cv.N * cv.H * cv.W * WS_NOUT;
+  if (xb >= (1L << 31) || yb >= (1L << 31)) return 0;
   if (g_ws_cus == 0) {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
@@ -235,11 +243,14 @@ int sat_conv3x3_ws_try(const SatGemm& g, hipStream_t s, int* err) {
   a.tiles_x = cv.W / TW;
   a.items_per_img = (cv.H / TR) * a.tiles_x;
   a.items = cv.N * a.items_per_img;
-  a.x_bytes = (unsigned)bytes; a.y_bytes = (unsigned)bytes;
+  a.x_bytes = (unsigned)xb; a.y_bytes = (unsigned)yb;
   a.abl = g_ws_abl;
-  const int grid = a.items < g_ws_cus ? a.items : g_ws_cus;
-  if (TR == 4) launch_ws<4, 56, 3>(g.act, dim3(grid), s, a);
-  else launch_ws<2, 112, 2>(g.act, dim3(grid), s, a);
+  // the stem variant (72 KB of LDS, 108 VGPRs) fits two workgroups per CU
+  const int slots = g_ws_cus * (stem ? 2 : 1);
+  const int grid = a.items < slots ? a.items : slots;
+  if (stem) launch_ws<4, 16, 2, 2, 112, 3>(g.act, dim3(grid), s, a);
+  else if (cv.W == 56) launch_ws<3, 64, 1, 4, 56, 3>(g.act, dim3(grid), s, a);
+  else launch_ws<3, 64, 1, 2, 112, 2>(g.act, dim3(grid), s, a);
   *err = (int)hipGetLastError();
   return 1;
 }

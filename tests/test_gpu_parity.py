@@ -1304,28 +1304,32 @@ def test_decoder_skinny_matches_tile_kernel(sat, tf):
         assert ((g1[n] - g).norm() / scale.norm().clamp_min(1e-12)).item() < 3e-2, n
 
 
-@pytest.mark.parametrize("N,H,relu,bias", [(4, 56, True, True), (3, 56, False, True), (2, 224, True, True),
-                                           (1, 224, False, False), (130, 56, True, True)])
-def test_conv3x3_ws_kernel(sat, N, H, relu, bias):
-    """conv3x3_ws_kernel (csrc/conv3x3ws.hip: weight-stationary, input halo once per item) on the
-    64 -> 64 3x3 convs of ResNet152 layer1 / VGG19 conv1_2: against an fp64 conv of the same bf16
+@pytest.mark.parametrize("N,H,relu,bias,stem", [(4, 56, True, True, False), (3, 56, False, True, False),
+                                                (2, 224, True, True, False), (1, 224, False, False, False),
+                                                (130, 56, True, True, False), (3, 112, True, True, True),
+                                                (2, 112, False, False, True)])
+def test_conv3x3_ws_kernel(sat, N, H, relu, bias, stem):
+    """conv_ws_kernel (csrc/conv3x3ws.hip: weight-stationary, input halo once per item) on the
+    64 -> 64 3x3 convs of ResNet152 layer1 / VGG19 conv1_2 and ResNet152's stem (4x4 over the 2x2
+    space-to-depth input, top-left pad 2): against an fp64 conv of the same bf16
     operands (bf16 output rounding) and bit for bit against the implicit-GEMM tile kernel it replaces
     (same MFMA, same k order).  N = 130: more items than CUs, every ring stage reused."""
     from sat_amd import ops
     lib = sat._lib.lib()
     g = torch.Generator().manual_seed(N * 31 + H)
-    x = torch.randn(N, H, H, 64, generator=g).bfloat16()
-    w = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).bfloat16()
+    C, KK, pad = (16, 4, 2) if stem else (64, 3, 1)   # stem: 4x4 / top-left pad 2 over the s2d input
+    x = torch.randn(N, H, H, C, generator=g).bfloat16()
+    w = (torch.randn(64, KK, KK, C, generator=g) * 0.05).bfloat16()
     b = torch.randn(64, generator=g) if bias else None
-    ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2),
-                                     b.double() if bias else None, padding=1).permute(0, 2, 3, 1)
+    xp = torch.nn.functional.pad(x.double().permute(0, 3, 1, 2), (pad, KK - 1 - pad, pad, KK - 1 - pad))
+    ref = torch.nn.functional.conv2d(xp, w.double().permute(0, 3, 1, 2), b.double() if bias else None).permute(0, 2, 3, 1)
     if relu:
         ref = ref.clamp_min(0)
     outs = []
     try:
         for mode in (1, 0):
             assert lib.sat_conv3x3_ws_set_mode(mode) == 0
-            y = ops.conv2d_nhwc(x.to(DEV), w.to(DEV), b.to(DEV) if bias else None, 1, 1, relu)
+            y = ops.conv2d_nhwc(x.to(DEV), w.to(DEV), b.to(DEV) if bias else None, 1, pad, relu, out_hw=(H, H))
             torch.cuda.synchronize()
             outs.append(y.cpu())
     finally:

@@ -13,25 +13,25 @@ from sat_amd import ops  # noqa: E402
 def main():
     lib = sat_amd._lib.lib()
     dev = torch.device("cuda")
-    for name, H in (("L1c2", 56), ("vgg_conv1_2", 224)):
-        x = torch.randn(128, H, H, 64, device=dev).bfloat16()
-        w = (torch.randn(64, 3, 3, 64, device=dev) * 0.05).bfloat16()
+    for name, H, C, KK, pad in (("L1c2", 56, 64, 3, 1), ("vgg_conv1_2", 224, 64, 3, 1), ("stem_s2d", 112, 16, 4, 2)):
+        x = torch.randn(128, H, H, C, device=dev).bfloat16()
+        w = (torch.randn(64, KK, KK, C, device=dev) * 0.05).bfloat16()
         b = torch.randn(64, device=dev)
-        y = torch.empty_like(x)
+        y = torch.empty(128, H, H, 64, device=dev).bfloat16()
         for mode in ((1, 0, 1, 0) + tuple(1 | (b << 1) for b in (2, 4, 6)) if len(sys.argv) > 1 else (1, 0, 1, 0)):
             assert lib.sat_conv3x3_ws_set_mode(mode) == 0
             for _ in range(3):
-                ops.conv2d_nhwc(x, w, b, 1, 1, True, out=y)
+                ops.conv2d_nhwc(x, w, b, 1, pad, True, out=y, out_hw=(H, H))
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             reps = 20
             st.record()
             for _ in range(reps):
-                ops.conv2d_nhwc(x, w, b, 1, 1, True, out=y)
+                ops.conv2d_nhwc(x, w, b, 1, pad, True, out=y, out_hw=(H, H))
             en.record()
             torch.cuda.synchronize()
             us = st.elapsed_time(en) * 1e3 / reps
-            flops = 2 * 128 * H * H * 64 * 576
-            byts = 2 * 2 * 128 * H * H * 64
+            flops = 2 * 128 * H * H * 64 * KK * KK * C
+            byts = 2 * 128 * H * H * (64 + C)
             print(f"{name:12s} mode {mode:2d}: {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s  {byts / us / 1e3:7.1f} GB/s")
     lib.sat_conv3x3_ws_set_mode(1)
 
