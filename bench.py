@@ -190,6 +190,8 @@ def trunk_roofline(enc, imgs, launches, reps=3):
     def launch(a):
         if a[0] == "fused":
             ops.bottleneck_fused(a[1], *a[2])
+        elif a[0] == "c2frag":
+            ops.conv3x3_frag(a[1], a[2])
         else:
             x, w, b, s, p, relu, res, hw = a
             ops.conv2d_nhwc(x, w, b, s, p, relu, residual=res, out_hw=hw)
@@ -212,7 +214,9 @@ def trunk_roofline(enc, imgs, launches, reps=3):
     floor_us = sum(max(l["flops"] / (BF16_DENSE_PEAK_TFLOPS * 1e12), l["bytes"] / (PEAK_HBM_ACHIEVABLE_GBS * 1e9))
                    for l in launches) * 1e6
     trunk_us = sum(dur) * 1e3
-    kname = "bottleneck_kernel (csrc/convblock.hip), fused block" if dom.get("fused") else "conv kernels, conv class"
+    kname = "bottleneck_kernel (csrc/convblock.hip), fused block" if dom.get("fused") else (
+        "conv3x3_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c2frag" for i in idx)
+        else "conv kernels, conv class")
     return dict(kernel=f"{kname} {name} ({dom['n']} launches/forward)", cls=name,
                 bound=dom["bound"], achieved=round(achieved, 2), peak=peak, unit=unit,
                 frac=round(achieved / peak, 4), avg_launch_us=round(avg_s * 1e6, 2),

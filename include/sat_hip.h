@@ -168,6 +168,17 @@ int sat_bottleneck_fused_supported(int H, int W, int Cin, int Cmid, int dtype);
 int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int dtype, const void* x, const void* w1f,
                          const float* b1, const void* w2f, const float* b2, const void* w3f, const float* b3,
                          void* y, void* stream);
+/* 1 if sat_conv3x3_frag runs this geometry (today: bf16, 14x14, C 256 -- the c2 of ResNet152's layer3
+ * identity blocks), else 0. */
+int sat_conv3x3_frag_supported(int H, int W, int C, int dtype);
+/* 3x3 / stride 1 / pad 1 conv C -> C + folded bias + ReLU (a bottleneck's c2, encoder.py:13-17 through
+ * torchvision), one workgroup per half image with its input rows staged once in LDS and the weights
+ * streamed register-direct.  x, y NHWC [N,H,W,C] (x != y); wf: sat_mfma_frag_layout of the folded
+ * [C][3*3*C] (tap-major) weight; b: fp32 bias.  Bit-identical to sat_conv2d_nhwc on the same operands. */
+int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const void* x, const void* wf, const float* b, void* y,
+                     void* stream);
+/* experiment hook (process-global, tools/c2_ab.py): sat_conv3x3_frag's weight prefetch distance (2 | 3 | 4). */
+int sat_conv3x3_frag_set_experiment(int pf);
 /* MaxPool2d (floor mode, -inf padding) on NHWC. */
 int sat_maxpool2d_nhwc(int N, int H, int W, int C, int k, int stride, int pad, int dtype,
                        const void* x, void* y, int OH, int OW, void* stream);

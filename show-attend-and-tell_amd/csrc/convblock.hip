@@ -412,6 +412,123 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(3))) void b
   bottleneck_body<14, 7, 1024, 256, PF, ABL | 128>(a);
 }
 
+// The bottleneck's c2 phase as a conv of its own (the layer3 blocks the trunk leaves unfused, so the
+// decoder running beside the encoder finds CUs between launches): y = relu(conv3x3(x) + b) for
+// x, y [N][IW][IW][C].  The 256 x 128 tile kernel (convpipe.hip) runs this shape as 196 tiles on 256
+// CUs and streams a 256-row im2col A tile plus a 128-column weight tile per k-tile (48 KB); here one
+// workgroup per half image (256 workgroups for B = 128) loads its 8 input rows ONCE into the
+// conflict-free X1 plane image (57 KB: two workgroups fit one CU's LDS) and streams only weights,
+// register-direct from the fragment layout (32 KB per k-tile for 112 x 256 outputs).  Same k order
+// (tap-major, 64-deep k-tiles ascending), bias, ReLU and one rounding as the tile kernel: bit-identical.
+template <int IW, int RO, int C, int PF>
+__device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                  const float* __restrict__ bias, bf16* __restrict__ y) {
+  static_assert(IW / RO == 2 && IW % RO == 0 && C == 256, "two workgroups per image, 256 channels");
+  constexpr int IH = IW, PO = RO * IW, R1 = RO + 1, P1 = R1 * IW;
+  constexpr int MB = (P1 + 15) / 16;
+  static_assert(MB * 16 == P1, "whole m-blocks of input rows");
+  constexpr int ROWB = 128, X1PL = (P1 + 1) * ROWB, NPL = C / 64;
+  constexpr int NT = 9 * C / 64, KS = 9 * C / 32;
+  constexpr int NCHUNK = P1 * C / 8, PER_T = NCHUNK / 512;
+  static_assert(NCHUNK % 512 == 0, "whole input chunks per thread");
+  __shared__ __attribute__((aligned(16))) char smem[NPL * X1PL];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fh = lane >> 4;
+  const int img = blockIdx.x >> 1, half = blockIdx.x & 1;
+  const int y0 = half * RO, ws = half ? IH - R1 : 0;
+  const long pix_img = (long)img * IH * IW;
+
+  // input rows ws .. ws + R1 - 1 are one contiguous block: chunk q = 16 B of pixel q / 32
+  uint4 xin[PER_T];
+  const uint4* xs = (const uint4*)(x + (pix_img + (long)ws * IW) * C);
+#pragma unroll
+  for (int u = 0; u < PER_T; ++u) xin[u] = xs[u * 512 + tid];
+  float4 bv[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + w * 32 + j * 16 + 4 * fh);
+
+  bf16x8 bq[PF + 1][2][2];
+  auto load_b = [&](int T, bf16x8 (&dst)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        dst[ks][j] = *(const bf16x8*)(wf + ((long)((w * 2 + j) * KS + 2 * T + ks) * 64 + lane) * 8);
+  };
+  static_for<PF>([&](auto e) { load_b(decltype(e)::value, bq[decltype(e)::value]); });
+
+#pragma unroll
+  for (int u = 0; u < PER_T; ++u) {
+    const int q = u * 512 + tid, r = q / (C / 8), c = q % (C / 8);
+    *(uint4*)(smem + (c >> 3) * X1PL + r * ROWB + 16 * ((c & 7) ^ (r & 7))) = xin[u];
+  }
+  if (tid < NPL * 8) *(uint4*)(smem + (tid >> 3) * X1PL + P1 * ROWB + (tid & 7) * 16) = make_uint4(0, 0, 0, 0);
+  k_lds_barrier();
+
+  int offs[MB][2];
+  auto tap_offsets = [&](int tap) {
+    const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int p = i * 16 + fr, py = p / IW, pxx = p - py * IW;
+      const bool ok = p < PO && (unsigned)(y0 + py + dh) < (unsigned)IH && (unsigned)(pxx + dw) < (unsigned)IW;
+      const int q = ok ? p + (y0 - ws + dh) * IW + dw : P1;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) offs[i][ks] = q * ROWB + 16 * ((ks * 4 + fh) ^ (q & 7));
+    }
+  };
+  f32x4 acc[MB][2];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  static_for<NT>([&](auto Tc) {
+    constexpr int T = decltype(Tc)::value, pl = T % NPL;
+    if constexpr (T + PF < NT) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
+    if constexpr (pl == 0) tap_offsets(T / NPL);
+    const bf16x8 (&b)[2][2] = bq[T % (PF + 1)];
+    bf16x8 af[2][MB];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < MB; ++i) af[ks][i] = *(const bf16x8*)(smem + pl * X1PL + offs[i][ks]);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  });
+
+  // epilogue: the lane holds channels w*32 + j*16 + 4fh .. +3 of output pixel i*16 + fr
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int ch = w * 32 + j * 16 + 4 * fh;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int p = i * 16 + fr;
+      u32x2 o;
+      bf16* ob = (bf16*)&o;
+      ob[0] = (bf16)fmaxf(acc[i][j][0] + bv[j].x, 0.f);
+      ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
+      ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
+      ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
+      if (p < PO) *(u32x2*)(y + (pix_img + (long)y0 * IW + p) * C + ch) = o;
+    }
+  }
+}
+
+template <int PF>
+__global__ __launch_bounds__(512) void conv3x3_frag_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                           const float* __restrict__ bias, bf16* __restrict__ y) {
+  conv3x3_frag_body<14, 7, 256, PF>(x, wf, bias, y);
+}
+
 // [N][K] bf16 -> [N/16][K/32][64 lanes][8]: lane l = (fh << 4) | fr holds row 16 nb + fr, k 32 ks + 8 fh ..
 __global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst, int N, int K, int kmajor) {
   const long n8 = (long)N * K / 8;
@@ -501,5 +618,32 @@ extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int 
   a.b1 = b1; a.b2 = b2; a.b3 = b3;
   a.x_bytes = (unsigned)x_bytes;
   launch_block_abl<2>(g_block_abl, dim3(2 * N), (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+static int g_c3f_pf = 2;   // weight prefetch distance of conv3x3_frag_kernel (experiment hook)
+
+extern "C" int sat_conv3x3_frag_set_experiment(int pf) {
+  if (pf != 2 && pf != 3 && pf != 4) return SAT_ERR_INVALID;
+  g_c3f_pf = pf;
+  return 0;
+}
+
+extern "C" int sat_conv3x3_frag_supported(int H, int W, int C, int dtype) {
+  return dtype == SAT_BF16 && H == 14 && W == 14 && C == 256;
+}
+
+extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const void* x, const void* wf, const float* b,
+                                void* y, void* stream) {
+  SAT_REQUIRE(N > 0 && x && wf && b && y && x != y);
+  SAT_REQUIRE(sat_conv3x3_frag_supported(H, W, C, dtype));
+  auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
+  SAT_REQUIRE(al(x, 16) && al(y, 16) && al(wf, 16) && al(b, 16));
+  const hipStream_t s = (hipStream_t)stream;
+  const bf16 *xp = (const bf16*)x, *wp = (const bf16*)wf;
+  bf16* yp = (bf16*)y;
+  if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_frag_kernel<3>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
+  else if (g_c3f_pf == 4) hipLaunchKernelGGL(conv3x3_frag_kernel<4>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
+  else hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
   return (int)hipGetLastError();
 }

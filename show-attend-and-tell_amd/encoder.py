@@ -150,6 +150,10 @@ class Encoder(nn.Module):
         # an int n fuses every n-th eligible block only (the unfused ones leave CUs to a decoder
         # running beside the encoder: bench.py --fuse-every)
         self.fuse_blocks = True
+        # the c2 of an identity block left unfused runs on the half-image conv kernel
+        # (sat_conv3x3_frag: input rows staged once in LDS, fragment-layout weights); False = the
+        # tile kernel (A/B, tests)
+        self.c2_frag = True
 
     def _conv(self, x, f, relu, residual=None, out_hw=None):
         w, b, s, p = f
@@ -160,6 +164,18 @@ class Encoder(nn.Module):
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st.record()
         y = ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual, out_hw=out_hw)
+        en.record()
+        self.timing.append((st, en))
+        return y
+
+    def _conv3x3_frag(self, x, f):
+        if self.timing_args is not None:
+            self.timing_args.append(("c2frag", x, f))
+        if self.timing is None:
+            return ops.conv3x3_frag(x, f)
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        y = ops.conv3x3_frag(x, f)
         en.record()
         self.timing.append((st, en))
         return y
@@ -315,6 +331,10 @@ class Encoder(nn.Module):
             self.timing.append((st, en))
             return out
         out = self._conv(y, c1, True)
-        out = self._conv(out, c2, True)
+        if fused is not None and self.c2_frag and ops.conv3x3_frag_supported(out.shape[1], out.shape[2], out.shape[3],
+                                                                           out.dtype):
+            out = self._conv3x3_frag(out, fused[1])
+        else:
+            out = self._conv(out, c2, True)
         idn = self._conv(y, ds, False) if ds is not None else y
         return self._conv(out, c3, True, residual=idn)

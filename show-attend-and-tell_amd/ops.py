@@ -184,6 +184,23 @@ def bottleneck_fused(x, f1, f2, f3, out=None):
     return y
 
 
+def conv3x3_frag_supported(H, W, C, dtype):
+    return bool(L.lib().sat_conv3x3_frag_supported(H, W, C, L.dtype_code(dtype)))
+
+
+def conv3x3_frag(x, f, out=None):
+    """relu(conv3x3(x, pad 1) + b) with f = (fragment-layout weight, fp32 bias) of a folded [C][3][3][C]
+    conv (a layer3 bottleneck's c2).  x NHWC [N,H,W,C]; bit-identical to conv2d_nhwc."""
+    L.require_device(x)
+    if not x.is_contiguous():
+        raise ValueError("conv3x3_frag: x must be a contiguous NHWC tensor")
+    N, H, W, C = x.shape
+    y = out if out is not None else torch.empty_like(x)
+    L.check(L.lib().sat_conv3x3_frag(N, H, W, C, L.dtype_code(x.dtype), L.ptr(x), L.ptr(f[0]), L.ptr(f[1]),
+                                     L.ptr(y), L.stream_of(y)), "sat_conv3x3_frag")
+    return y
+
+
 def maxpool2d_nhwc(x, k, stride, pad=0):
     L.require_device(x)
     N, H, W, C = x.shape

@@ -1132,6 +1132,41 @@ def test_bottleneck_fused_bit_identical(sat, N):
     assert rel(nchw(y), t3) < 2e-2
 
 
+@pytest.mark.parametrize("N", [1, 2, 5])
+def test_conv3x3_frag_bit_identical(sat, N):
+    """csrc/convblock.hip's half-image 3x3 kernel (a layer3 c2 left unfused: 14x14, 256 -> 256) is
+    bit-identical to the tile kernel on the same operands, and close to torch fp32."""
+    from sat_amd import ops
+    g = torch.Generator().manual_seed(40 + N)
+    x = torch.randn(N, 14, 14, 256, generator=g).relu().bfloat16().to(DEV)
+    w = (torch.randn(256, 3, 3, 256, generator=g) * math.sqrt(2.0 / 2304)).bfloat16().to(DEV)
+    b = (0.1 * torch.randn(256, generator=g)).to(DEV)
+    ref = ops.conv2d_nhwc(x, w, b, 1, 1, True)
+    y = ops.conv3x3_frag(x, (ops.mfma_frag_layout(w.reshape(256, -1)), b))
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref), f"max |frag - tile| = {(y.float() - ref.float()).abs().max().item()}"
+    t = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2).cpu(), w.float().permute(0, 3, 1, 2).cpu(), b.cpu(),
+                            padding=1))
+    assert rel(y.float().permute(0, 3, 1, 2).cpu(), t) < 1e-2
+
+
+def test_encoder_c2_frag_equal_tile(sat):
+    """ResNet152 trunk at 224 x 224 with every layer3 block unfused: the c2s on sat_conv3x3_frag change
+    no output bit against the tile kernel."""
+    torch.manual_seed(0)
+    p = O.make_resnet152_params(4)
+    enc = sat.Encoder("resnet152", dtype=torch.bfloat16)
+    enc.load_state_dict(p, strict=True)
+    enc = enc.to(DEV).eval()
+    enc.fuse_blocks = False
+    x = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(7)).to(DEV)
+    with torch.no_grad():
+        y_f = enc(x)
+        enc.c2_frag = False
+        y_t = enc(x)
+    assert torch.equal(y_f, y_t)
+
+
 def test_encoder_fused_blocks_equal_unfused(sat):
     """ResNet152 trunk at 224 x 224: the fused layer3 blocks change no output bit."""
     torch.manual_seed(0)

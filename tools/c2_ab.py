@@ -1,0 +1,48 @@
+"""A/B of ResNet152 layer3's c2 (14 x 14, 256 -> 256, B = 128): sat_conv3x3_frag (csrc/convblock.hip,
+half-image workgroups, weight prefetch 2 / 3 / 4) vs the tile kernel, HIP-event timed back to back."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import sat_amd  # noqa: E402
+from sat_amd import ops  # noqa: E402
+
+
+def timeit(fn, reps=50):
+    for _ in range(3):
+        fn()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(reps):
+        fn()
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) * 1e3 / reps
+
+
+def main():
+    lib = sat_amd._lib.lib()
+    dev = torch.device("cuda")
+    B = 128
+    x = torch.randn(B, 14, 14, 256, device=dev).relu().bfloat16()
+    w = (torch.randn(256, 3, 3, 256, device=dev) * 0.03).bfloat16()
+    b = torch.randn(256, device=dev) * 0.1
+    f = (ops.mfma_frag_layout(w.reshape(256, -1)), b)
+    y = torch.empty_like(x)
+    flops = 2.0 * B * 196 * 256 * 2304
+    us = timeit(lambda: ops.conv2d_nhwc(x, w, b, 1, 1, True, out=y))
+    print(f"tile kernel      : {us:7.2f} us  {flops / us / 1e6:7.1f} TFLOP/s  frac {flops / us / 1e6 / 2500:.3f}")
+    ref = y.clone()
+    for pf in (2, 3, 4):
+        assert lib.sat_conv3x3_frag_set_experiment(pf) == 0
+        us = timeit(lambda: ops.conv3x3_frag(x, f, out=y))
+        same = torch.equal(y, ref)
+        print(f"frag kernel pf {pf}: {us:7.2f} us  {flops / us / 1e6:7.1f} TFLOP/s  frac {flops / us / 1e6 / 2500:.3f}"
+              f"  bit-identical {same}")
+    lib.sat_conv3x3_frag_set_experiment(2)
+
+
+if __name__ == "__main__":
+    main()
