@@ -81,8 +81,8 @@ def parse():
                     help="64 -> 64 3x3 convs on the implicit-GEMM tile kernel instead of csrc/conv3x3ws.hip (A/B)")
     ap.add_argument("--fuse-every", type=int, default=None,
                     help="fuse every n-th layer3 identity bottleneck only, the rest run as three conv launches "
-                         "(default: 3 with teacher forcing, 0 = none without: the greedy decoder chain is longer; "
-                         "profiles/r2_s54_sched.txt)")
+                         "(default 0 = none: with the layer3 c2 / c3 on the half-image frag kernels the unfused "
+                         "trunk shares CUs with the decoder best; profiles/r2_s62_sched.txt)")
     ap.add_argument("--stream-priority", choices=["decoder-high", "equal", "encoder-high"], default="decoder-high",
                     help="graph + overlap: the decoder / all-reduce / Adam stream gets the higher HIP stream "
                          "priority, so its short per-step kernels are dispatched first when CUs free up")
@@ -192,6 +192,8 @@ def trunk_roofline(enc, imgs, launches, reps=3):
             ops.bottleneck_fused(a[1], *a[2])
         elif a[0] == "c2frag":
             ops.conv3x3_frag(a[1], a[2])
+        elif a[0] == "c3frag":
+            ops.conv1x1_res_frag(a[1], a[2], a[3])
         else:
             x, w, b, s, p, relu, res, hw = a
             ops.conv2d_nhwc(x, w, b, s, p, relu, residual=res, out_hw=hw)
@@ -216,6 +218,7 @@ def trunk_roofline(enc, imgs, launches, reps=3):
     trunk_us = sum(dur) * 1e3
     kname = "bottleneck_kernel (csrc/convblock.hip), fused block" if dom.get("fused") else (
         "conv3x3_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c2frag" for i in idx)
+        else "conv1x1_res_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c3frag" for i in idx)
         else "conv kernels, conv class")
     return dict(kernel=f"{kname} {name} ({dom['n']} launches/forward)", cls=name,
                 bound=dom["bound"], achieved=round(achieved, 2), peak=peak, unit=unit,
@@ -356,7 +359,7 @@ def main():
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
     if args.fuse_every is None:
-        args.fuse_every = 0 if args.no_tf else 3
+        args.fuse_every = 0   # profiles/r2_s62: none fused 6.79 ms, every 3rd 7.15, every block 7.48
     if args.split_target is None:
         args.split_target = 128 if args.network == "vgg19" else 64
     enc.fuse_blocks = (False if args.no_fuse_blocks or args.fuse_every == 0 else

@@ -88,6 +88,10 @@ _SIGNATURES = [
     ("sat_conv3x3_frag_supported", c_int, [c_int, c_int, c_int, c_int]),
     ("sat_conv3x3_frag", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p]),
+    ("sat_conv1x1_res_frag_set_experiment", c_int, [c_int]),
+    ("sat_conv1x1_res_frag_supported", c_int, [c_int, c_int, c_int, c_int, c_int]),
+    ("sat_conv1x1_res_frag", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_void_p, c_void_p]),
     ("sat_maxpool2d_nhwc", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                    c_int, c_int, c_void_p]),
     ("sat_attention_forward", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -523,6 +523,123 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
   }
 }
 
+// The bottleneck's c3 phase as a conv of its own: y = relu(x . W^T + b + res) for x [N][IW][IW][CM],
+// res, y [N][IW][IW][CO] (1x1, stride 1).  One workgroup per half image: its 98 input pixels are staged
+// once in LDS (CM = 256: 50 KB), the CO x CM weight streams register-direct (fragment layout), the
+// residual rows go straight to registers a chunk ahead of their epilogue.  The weight-stationary
+// streaming kernel (convstream.hip) runs this shape at ~30 us for B = 128; the same sums (64-deep
+// k-tiles ascending), bias, residual add and one rounding: bit-identical.
+template <int IW, int RO, int CM, int CO, int PF>
+__device__ __forceinline__ void conv1x1_res_frag_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                      const float* __restrict__ bias, const bf16* __restrict__ res,
+                                                      bf16* __restrict__ y) {
+  static_assert(IW / RO == 2 && IW % RO == 0 && CM == 256 && CO % 256 == 0, "two workgroups per image");
+  constexpr int IH = IW, PO = RO * IW, MB = (PO + 15) / 16;
+  constexpr int ROWB = 128, XPL = MB * 16 * ROWB, NPL = CM / 64;
+  constexpr int KT = CM / 64, NCK = CO / 256, NT = NCK * KT, KS = CM / 32;
+  constexpr int NCHUNK = PO * CM / 8, PER_T = (NCHUNK + 511) / 512;
+  __shared__ __attribute__((aligned(16))) char smem[NPL * XPL];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fh = lane >> 4;
+  const int img = blockIdx.x >> 1, half = blockIdx.x & 1;
+  const long pix0 = (long)img * IH * IW + (long)half * PO;   // first pixel of this half image
+
+  // the half image's input rows are one contiguous block of PO pixels (rows >= PO of the LDS image
+  // stay unwritten: their outputs are never stored)
+  uint4 xin[PER_T];
+  const uint4* xs = (const uint4*)(x + pix0 * CM);
+#pragma unroll
+  for (int u = 0; u < PER_T; ++u) xin[u] = xs[min(u * 512 + tid, NCHUNK - 1)];   // clamped: no branch, no scratch
+  // every global access = a wave-uniform base (SGPRs) + a 32-bit per-lane byte offset, so the unrolled
+  // schedule keeps one offset register per access pattern instead of a 64-bit address per access
+  const unsigned lane_b = (unsigned)lane * 16;
+  const char* res_s = (const char*)(res + pix0 * CO + w * 32);
+  char* y_s = (char*)(y + pix0 * CO + w * 32);
+  const unsigned row_b = (unsigned)(fr * CO + 4 * fh) * 2;                        // m-blocks 0 .. MB-2
+  const unsigned row_last = (unsigned)(min((MB - 1) * 16 + fr, PO - 1) - (MB - 1) * 16) * CO * 2 + 8 * fh;
+  bf16x8 bq[PF + 1][2][2];
+  auto load_b = [&](int T, bf16x8 (&dst)[2][2]) {
+    const int ck = T / KT, kt = T % KT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        dst[ks][j] = *(const bf16x8*)((const char*)wf + (size_t)((ck * 16 + w * 2 + j) * KS + 2 * kt + ks) * 1024 +
+                                      lane_b);
+  };
+  static_for<PF>([&](auto e) { load_b(decltype(e)::value, bq[decltype(e)::value]); });
+#pragma unroll
+  for (int u = 0; u < PER_T; ++u) {
+    const int q = u * 512 + tid, r = q / (CM / 8), c = q % (CM / 8);
+    if (q < NCHUNK) *(uint4*)(smem + (c >> 3) * XPL + r * ROWB + 16 * ((c & 7) ^ (r & 7))) = xin[u];
+  }
+  k_lds_barrier();
+
+  int offu[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) offu[ks] = fr * ROWB + 16 * ((ks * 4 + fh) ^ (fr & 7));
+  f32x4 acc[MB][2];
+  u32x2 resv[MB][2];
+  float4 bv[2];
+
+  static_for<NT>([&](auto Tc) {
+    constexpr int T = decltype(Tc)::value, ck = T / KT, kt = T % KT;
+    __builtin_amdgcn_sched_barrier(0);   // keep the scheduler from hoisting later tiles' loads (register spills)
+    if constexpr (kt == 0) {   // this chunk's residual rows + bias (rows past PO load a valid row, never stored)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + ck * 256 + w * 32 + j * 16 + 4 * fh);
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          resv[i][j] = *(const u32x2*)(res_s + (size_t)(i * 16 * CO + ck * 256 + j * 16) * 2 +
+                                        (i == MB - 1 ? row_last : row_b));
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    if constexpr (T + PF < NT) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
+    const bf16x8 (&b)[2][2] = bq[T % (PF + 1)];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {   // one 32-deep half's A fragments at a time (the residual rows
+      bf16x8 af[MB];                   // held across the chunk leave no room for both halves)
+#pragma unroll
+      for (int i = 0; i < MB; ++i) af[i] = *(const bf16x8*)(smem + kt * XPL + i * 16 * ROWB + offu[ks]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    if constexpr (kt == KT - 1) {   // epilogue: bias, fp32 residual add, ReLU, one rounding, 8-B stores
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+#pragma unroll
+        for (int i = 0; i < MB; ++i) {
+          const int p = i * 16 + fr;
+          const bf16* rh = (const bf16*)&resv[i][j];
+          const float v[4] = {acc[i][j][0] + bv[j].x, acc[i][j][1] + bv[j].y, acc[i][j][2] + bv[j].z,
+                              acc[i][j][3] + bv[j].w};
+          u32x2 o;
+          bf16* ob = (bf16*)&o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ob[e] = (bf16)fmaxf(v[e] + (float)rh[e], 0.f);
+          if (p < PO) *(u32x2*)(y_s + (size_t)(i * 16 * CO + ck * 256 + j * 16) * 2 + row_b) = o;
+        }
+      }
+    }
+  });
+}
+
+template <int PF>
+__global__ __launch_bounds__(512) void conv1x1_res_frag_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                               const float* __restrict__ bias,
+                                                               const bf16* __restrict__ res, bf16* __restrict__ y) {
+  conv1x1_res_frag_body<14, 7, 256, 1024, PF>(x, wf, bias, res, y);
+}
+
 template <int PF>
 __global__ __launch_bounds__(512) void conv3x3_frag_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                            const float* __restrict__ bias, bf16* __restrict__ y) {
@@ -645,5 +762,31 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_frag_kernel<3>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
   else if (g_c3f_pf == 4) hipLaunchKernelGGL(conv3x3_frag_kernel<4>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
   else hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
+  return (int)hipGetLastError();
+}
+
+static int g_c1r_pf = 2;   // weight prefetch distance of conv1x1_res_frag_kernel (experiment hook)
+
+extern "C" int sat_conv1x1_res_frag_set_experiment(int pf) {
+  if (pf != 2 && pf != 3) return SAT_ERR_INVALID;
+  g_c1r_pf = pf;
+  return 0;
+}
+
+extern "C" int sat_conv1x1_res_frag_supported(int H, int W, int Cin, int Cout, int dtype) {
+  return dtype == SAT_BF16 && H == 14 && W == 14 && Cin == 256 && Cout == 1024;
+}
+
+extern "C" int sat_conv1x1_res_frag(int N, int H, int W, int Cin, int Cout, int dtype, const void* x, const void* wf,
+                                    const float* b, const void* res, void* y, void* stream) {
+  SAT_REQUIRE(N > 0 && x && wf && b && res && y && x != y && res != y);
+  SAT_REQUIRE(sat_conv1x1_res_frag_supported(H, W, Cin, Cout, dtype));
+  auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
+  SAT_REQUIRE(al(x, 16) && al(y, 16) && al(wf, 16) && al(b, 16) && al(res, 16));
+  const hipStream_t s = (hipStream_t)stream;
+  const bf16 *xp = (const bf16*)x, *wp = (const bf16*)wf, *rp = (const bf16*)res;
+  bf16* yp = (bf16*)y;
+  if (g_c1r_pf == 3) hipLaunchKernelGGL(conv1x1_res_frag_kernel<3>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, rp, yp);
+  else hipLaunchKernelGGL(conv1x1_res_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, rp, yp);
   return (int)hipGetLastError();
 }

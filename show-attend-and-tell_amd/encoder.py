@@ -154,6 +154,9 @@ class Encoder(nn.Module):
         # (sat_conv3x3_frag: input rows staged once in LDS, fragment-layout weights); False = the
         # tile kernel (A/B, tests)
         self.c2_frag = True
+        # ... and its c3 (+ identity residual) on the half-image 1x1 kernel (sat_conv1x1_res_frag): off,
+        # the weight-stationary streaming kernel is faster there (28.3 vs 33.9 us, profiles/r2_s64_c3_ab.txt)
+        self.c3_frag = False
 
     def _conv(self, x, f, relu, residual=None, out_hw=None):
         w, b, s, p = f
@@ -168,14 +171,15 @@ class Encoder(nn.Module):
         self.timing.append((st, en))
         return y
 
-    def _conv3x3_frag(self, x, f):
+    def _frag_conv(self, kind, fn, x, f, *extra):
+        """A half-image fragment-weight conv launch (csrc/convblock.hip), with the bench's timing hooks."""
         if self.timing_args is not None:
-            self.timing_args.append(("c2frag", x, f))
+            self.timing_args.append((kind, x, f) + extra)
         if self.timing is None:
-            return ops.conv3x3_frag(x, f)
+            return fn(x, f, *extra)
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st.record()
-        y = ops.conv3x3_frag(x, f)
+        y = fn(x, f, *extra)
         en.record()
         self.timing.append((st, en))
         return y
@@ -333,8 +337,11 @@ class Encoder(nn.Module):
         out = self._conv(y, c1, True)
         if fused is not None and self.c2_frag and ops.conv3x3_frag_supported(out.shape[1], out.shape[2], out.shape[3],
                                                                            out.dtype):
-            out = self._conv3x3_frag(out, fused[1])
+            out = self._frag_conv("c2frag", ops.conv3x3_frag, out, fused[1])
         else:
             out = self._conv(out, c2, True)
         idn = self._conv(y, ds, False) if ds is not None else y
+        if fused is not None and ds is None and self.c3_frag and ops.conv1x1_res_frag_supported(
+                out.shape[1], out.shape[2], out.shape[3], c3[0].shape[0], out.dtype):
+            return self._frag_conv("c3frag", ops.conv1x1_res_frag, out, fused[2], idn)
         return self._conv(out, c3, True, residual=idn)

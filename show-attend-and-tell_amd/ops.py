@@ -201,6 +201,28 @@ def conv3x3_frag(x, f, out=None):
     return y
 
 
+def conv1x1_res_frag_supported(H, W, Cin, Cout, dtype):
+    return bool(L.lib().sat_conv1x1_res_frag_supported(H, W, Cin, Cout, L.dtype_code(dtype)))
+
+
+def conv1x1_res_frag(x, f, residual, out=None):
+    """relu(x . W^T + b + residual) with f = (fragment-layout weight, fp32 bias) of a folded [Cout][Cin]
+    1x1 conv (a layer3 bottleneck's c3).  x NHWC [N,H,W,Cin], residual [N,H,W,Cout]; bit-identical to
+    conv2d_nhwc(..., residual=residual)."""
+    L.require_device(x, residual)
+    if not (x.is_contiguous() and residual.is_contiguous()):
+        raise ValueError("conv1x1_res_frag: x and residual must be contiguous NHWC tensors")
+    N, H, W, C = x.shape
+    Cout = f[1].shape[0]
+    if tuple(residual.shape) != (N, H, W, Cout) or residual.dtype != x.dtype:
+        raise ValueError(f"conv1x1_res_frag: residual {tuple(residual.shape)} does not match {(N, H, W, Cout)}")
+    y = out if out is not None else torch.empty_like(residual)
+    L.check(L.lib().sat_conv1x1_res_frag(N, H, W, C, Cout, L.dtype_code(x.dtype), L.ptr(x), L.ptr(f[0]),
+                                         L.ptr(f[1]), L.ptr(residual), L.ptr(y), L.stream_of(y)),
+            "sat_conv1x1_res_frag")
+    return y
+
+
 def maxpool2d_nhwc(x, k, stride, pad=0):
     L.require_device(x)
     N, H, W, C = x.shape

@@ -363,8 +363,9 @@ def main(argv=None):
     encoder, decoder, word_dict, dt = build(args, device)
     if not args.no_overlap:   # the decoder shares the chip with the next batch's encoder (bench.py defaults)
         decoder.split_target = 128 if args.network == "vgg19" else 64
-        # every 3rd layer3 block fused (the rest leave CUs to the decoder); none for the longer greedy chain
-        encoder.fuse_blocks = 3 if args.tf else False
+        # no layer3 block fused: the unfused c2 / c3 half-image kernels leave CUs to the decoder
+        # (profiles/r2_s62_sched.txt)
+        encoder.fuse_blocks = False
     opt = sat_amd.Adam(decoder.parameters(), lr=args.lr)
     grad_ar = sat_dist.GradAllReduce(decoder) if world > 1 else None
     sched = torch.optim.lr_scheduler.StepLR(opt, args.step_size)

@@ -1,4 +1,4 @@
-"""A/B of ResNet152 layer3's c2 (14 x 14, 256 -> 256, B = 128): sat_conv3x3_frag (csrc/convblock.hip,
+"""A/B of ResNet152 layer3's c2 and c3 (14 x 14, 256 -> 256, B = 128): sat_conv3x3_frag (csrc/convblock.hip,
 half-image workgroups, weight prefetch 2 / 3 / 4) vs the tile kernel, HIP-event timed back to back."""
 import os
 import sys
@@ -42,6 +42,23 @@ def main():
         print(f"frag kernel pf {pf}: {us:7.2f} us  {flops / us / 1e6:7.1f} TFLOP/s  frac {flops / us / 1e6 / 2500:.3f}"
               f"  bit-identical {same}")
     lib.sat_conv3x3_frag_set_experiment(2)
+    # c3: 1x1 256 -> 1024 + identity residual
+    x3 = torch.randn(B, 14, 14, 256, device=dev).relu().bfloat16()
+    r3 = torch.randn(B, 14, 14, 1024, device=dev).relu().bfloat16()
+    w3 = (torch.randn(1024, 1, 1, 256, device=dev) * 0.05).bfloat16()
+    b3 = torch.randn(1024, device=dev) * 0.1
+    f3 = (ops.mfma_frag_layout(w3.reshape(1024, -1)), b3)
+    y3 = torch.empty_like(r3)
+    byts = 2.0 * (B * 196 * (256 + 2 * 1024) + 1024 * 256)
+    us = timeit(lambda: ops.conv2d_nhwc(x3, w3, b3, 1, 0, True, residual=r3, out=y3))
+    print(f"c3 stream kernel : {us:7.2f} us  {byts / us / 1e3:7.1f} GB/s  frac {byts / us / 1e3 / 8000:.3f}")
+    ref3 = y3.clone()
+    for pf in (2, 3):
+        assert lib.sat_conv1x1_res_frag_set_experiment(pf) == 0
+        us = timeit(lambda: ops.conv1x1_res_frag(x3, f3, r3, out=y3))
+        print(f"c3 frag pf {pf}     : {us:7.2f} us  {byts / us / 1e3:7.1f} GB/s  frac {byts / us / 1e3 / 8000:.3f}"
+              f"  bit-identical {torch.equal(y3, ref3)}")
+    lib.sat_conv1x1_res_frag_set_experiment(2)
 
 
 if __name__ == "__main__":
