@@ -523,6 +523,120 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
   }
 }
 
+// The same idea for a band of RO output rows of a larger image (ResNet152 layer2's c2: 28 x 28, 128 ->
+// 128, RO = 7: four workgroups per image, 512 for B = 128): the band's input rows plus a one-row halo on
+// each side that lies inside the image are staged once in LDS (slot s holds image row y0 - 1 + s; taps
+// outside the image read the zero row), the C x 9C weight streams register-direct, each of the 8 waves
+// owns NJ = C / 128 n-blocks of 16 channels and every m-block of the band.  Same k order, bias, ReLU and
+// rounding as the tile kernel: bit-identical.
+template <int IW, int RO, int C, int PF>
+__device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                  const float* __restrict__ bias, bf16* __restrict__ y) {
+  constexpr int IH = IW, NPART = IH / RO, PO = RO * IW, MB = (PO + 15) / 16;
+  constexpr int SLOTS = RO + 2, ZR = SLOTS * IW;        // LDS pixel rows + the zero row
+  constexpr int ROWB = 128, XPL = (ZR + 1) * ROWB, NPL = C / 64, NJ = C / 128;
+  constexpr int NT = 9 * C / 64, KS = 9 * C / 32, CPP = C / 8;   // CPP: 16-B chunks per pixel
+  constexpr int PER_T = (ZR * CPP + 511) / 512;
+  static_assert(IH % RO == 0 && C % 128 == 0 && NJ >= 1, "whole bands, 16-channel n-blocks per wave");
+  __shared__ __attribute__((aligned(16))) char smem[NPL * XPL];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fh = lane >> 4;
+  const int img = blockIdx.x / NPART, part = blockIdx.x % NPART;
+  const int y0 = part * RO;
+  const int s_lo = y0 == 0 ? 1 : 0, s_hi = y0 + RO == IH ? RO : RO + 1;   // slots inside the image
+  const int nchunk = (s_hi - s_lo + 1) * IW * CPP;
+  const long pix_img = (long)img * IH * IW;
+  const unsigned lane_b = (unsigned)lane * 16;
+
+  // the valid slots are one contiguous block of image rows
+  uint4 xin[PER_T];
+  const uint4* xs = (const uint4*)(x + (pix_img + (long)(y0 - 1 + s_lo) * IW) * C);
+#pragma unroll
+  for (int u = 0; u < PER_T; ++u) xin[u] = xs[min(u * 512 + tid, nchunk - 1)];
+  float4 bv[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) bv[j] = *(const float4*)(bias + (w * NJ + j) * 16 + 4 * fh);
+  bf16x8 bq[PF + 1][2][NJ];
+  auto load_b = [&](int T, bf16x8 (&dst)[2][NJ]) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        dst[ks][j] = *(const bf16x8*)((const char*)wf + (size_t)((w * NJ + j) * KS + 2 * T + ks) * 1024 + lane_b);
+  };
+  static_for<PF>([&](auto e) { load_b(decltype(e)::value, bq[decltype(e)::value]); });
+#pragma unroll
+  for (int u = 0; u < PER_T; ++u) {
+    const int q = u * 512 + tid, r = s_lo * IW + q / CPP, c = q % CPP;
+    if (q < nchunk) *(uint4*)(smem + (c >> 3) * XPL + r * ROWB + 16 * ((c & 7) ^ (r & 7))) = xin[u];
+  }
+  if (tid < NPL * 8) *(uint4*)(smem + (tid >> 3) * XPL + ZR * ROWB + (tid & 7) * 16) = make_uint4(0, 0, 0, 0);
+  k_lds_barrier();
+
+  int offs[MB][2];
+  auto tap_offsets = [&](int tap) {
+    const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int p = i * 16 + fr, py = p / IW, pxx = p - py * IW;
+      const bool ok = p < PO && (unsigned)(y0 + py + dh) < (unsigned)IH && (unsigned)(pxx + dw) < (unsigned)IW;
+      const int q = ok ? (py + 1 + dh) * IW + pxx + dw : ZR;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) offs[i][ks] = q * ROWB + 16 * ((ks * 4 + fh) ^ (q & 7));
+    }
+  };
+  f32x4 acc[MB][NJ];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  static_for<NT>([&](auto Tc) {
+    constexpr int T = decltype(Tc)::value, pl = T % NPL;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (T + PF < NT) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
+    if constexpr (pl == 0) tap_offsets(T / NPL);
+    const bf16x8 (&b)[2][NJ] = bq[T % (PF + 1)];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[MB];
+#pragma unroll
+      for (int i = 0; i < MB; ++i) af[i] = *(const bf16x8*)(smem + pl * XPL + offs[i][ks]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  });
+
+  char* y_s = (char*)(y + (pix_img + (long)y0 * IW) * C + w * NJ * 16);
+  const unsigned row_b = (unsigned)(fr * C + 4 * fh) * 2;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int p = i * 16 + fr;
+      u32x2 o;
+      bf16* ob = (bf16*)&o;
+      ob[0] = (bf16)fmaxf(acc[i][j][0] + bv[j].x, 0.f);
+      ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
+      ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
+      ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
+      if (p < PO) *(u32x2*)(y_s + (size_t)(i * 16 * C + j * 16) * 2 + row_b) = o;
+    }
+  }
+}
+
+template <int PF>
+__global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                           const float* __restrict__ bias, bf16* __restrict__ y) {
+  conv3x3_band_body<28, 7, 128, PF>(x, wf, bias, y);
+}
+
 // The bottleneck's c3 phase as a conv of its own: y = relu(x . W^T + b + res) for x [N][IW][IW][CM],
 // res, y [N][IW][IW][CO] (1x1, stride 1).  One workgroup per half image: its 98 input pixels are staged
 // once in LDS (CM = 256: 50 KB), the CO x CM weight streams register-direct (fragment layout), the
@@ -747,7 +861,7 @@ extern "C" int sat_conv3x3_frag_set_experiment(int pf) {
 }
 
 extern "C" int sat_conv3x3_frag_supported(int H, int W, int C, int dtype) {
-  return dtype == SAT_BF16 && H == 14 && W == 14 && C == 256;
+  return dtype == SAT_BF16 && ((H == 14 && W == 14 && C == 256) || (H == 28 && W == 28 && C == 128));
 }
 
 extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const void* x, const void* wf, const float* b,
@@ -759,6 +873,11 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   const hipStream_t s = (hipStream_t)stream;
   const bf16 *xp = (const bf16*)x, *wp = (const bf16*)wf;
   bf16* yp = (bf16*)y;
+  if (H == 28) {   // layer2 c2: 7-row bands, four workgroups per image
+    if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_band_kernel<3>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp);
+    else hipLaunchKernelGGL(conv3x3_band_kernel<2>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp);
+    return (int)hipGetLastError();
+  }
   if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_frag_kernel<3>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
   else if (g_c3f_pf == 4) hipLaunchKernelGGL(conv3x3_frag_kernel<4>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
   else hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);

@@ -214,8 +214,10 @@ class Encoder(nn.Module):
             for layer in mods[4:]:
                 for blk in layer:
                     ds = self._fold(blk.downsample[0], blk.downsample[1]) if blk.downsample is not None else None
+                    fused = self._fused_weights(plan, blk, ds)
                     plan.append(("block", self._fold(blk.conv1, blk.bn1), self._fold(blk.conv2, blk.bn2),
-                                 self._fold(blk.conv3, blk.bn3), ds, self._fused_weights(plan, blk, ds)))
+                                 self._fold(blk.conv3, blk.bn3), ds, fused,
+                                 fused[1] if fused is not None else self._c2_frag_weights(blk)))
         else:
             first = True
             for i, m in enumerate(mods):
@@ -243,6 +245,17 @@ class Encoder(nn.Module):
             w, b, _, _ = self._fold(conv, bn)
             frags.append((ops.mfma_frag_layout(w.reshape(w.shape[0], -1)), b))
         return tuple(frags)
+
+    def _c2_frag_weights(self, blk):
+        """Fragment-layout c2 weights of a stride-1 block whose 3x3 the band kernel runs (layer2), else None."""
+        if blk.conv2.stride[0] != 1 or self.compute_dtype != torch.bfloat16 or not blk.conv2.weight.is_cuda:
+            return None
+        cmid = blk.conv2.out_channels
+        hw = {64: 56, 128: 28, 256: 14, 512: 7}.get(cmid)
+        if hw is None or not ops.conv3x3_frag_supported(hw, hw, cmid, self.compute_dtype):
+            return None
+        w, b, _, _ = self._fold(blk.conv2, blk.bn2)
+        return ops.mfma_frag_layout(w.reshape(w.shape[0], -1)), b
 
     def compiled_plan(self, device, dtype):
         key = self._state_key(device, dtype)
@@ -321,7 +334,7 @@ class Encoder(nn.Module):
             return self._conv(y, step[1], step[2])
         if step[0] == "pool":
             return ops.maxpool2d_nhwc(y, step[1], step[2], step[3])
-        _, c1, c2, c3, ds, fused = step
+        _, c1, c2, c3, ds, fused, c2f = step
         if (fused is not None and self.fuse_blocks is not False and self._fuse_this(self._plan, step)
                 and ops.bottleneck_fused_supported(y.shape[1], y.shape[2], y.shape[3], c1[0].shape[0], y.dtype)):
             if self.timing_args is not None:
@@ -335,9 +348,9 @@ class Encoder(nn.Module):
             self.timing.append((st, en))
             return out
         out = self._conv(y, c1, True)
-        if fused is not None and self.c2_frag and ops.conv3x3_frag_supported(out.shape[1], out.shape[2], out.shape[3],
-                                                                           out.dtype):
-            out = self._frag_conv("c2frag", ops.conv3x3_frag, out, fused[1])
+        if c2f is not None and self.c2_frag and ops.conv3x3_frag_supported(out.shape[1], out.shape[2], out.shape[3],
+                                                                         out.dtype):
+            out = self._frag_conv("c2frag", ops.conv3x3_frag, out, c2f)
         else:
             out = self._conv(out, c2, True)
         idn = self._conv(y, ds, False) if ds is not None else y

@@ -1132,17 +1132,18 @@ def test_bottleneck_fused_bit_identical(sat, N):
     assert rel(nchw(y), t3) < 2e-2
 
 
-@pytest.mark.parametrize("N", [1, 2, 5])
-def test_conv3x3_frag_bit_identical(sat, N):
-    """csrc/convblock.hip's half-image 3x3 kernel (a layer3 c2 left unfused: 14x14, 256 -> 256) is
-    bit-identical to the tile kernel on the same operands, and close to torch fp32."""
+@pytest.mark.parametrize("N,H,C", [(1, 14, 256), (2, 14, 256), (5, 14, 256), (1, 28, 128), (3, 28, 128)])
+def test_conv3x3_frag_bit_identical(sat, N, H, C):
+    """csrc/convblock.hip's half-image 3x3 kernel (a layer3 c2 left unfused: 14x14, 256 -> 256) and its
+    7-row band form (layer2 c2: 28x28, 128 -> 128) are bit-identical to the tile kernel on the same
+    operands, and close to torch fp32."""
     from sat_amd import ops
-    g = torch.Generator().manual_seed(40 + N)
-    x = torch.randn(N, 14, 14, 256, generator=g).relu().bfloat16().to(DEV)
-    w = (torch.randn(256, 3, 3, 256, generator=g) * math.sqrt(2.0 / 2304)).bfloat16().to(DEV)
-    b = (0.1 * torch.randn(256, generator=g)).to(DEV)
+    g = torch.Generator().manual_seed(40 + N + H)
+    x = torch.randn(N, H, H, C, generator=g).relu().bfloat16().to(DEV)
+    w = (torch.randn(C, 3, 3, C, generator=g) * math.sqrt(2.0 / (9 * C))).bfloat16().to(DEV)
+    b = (0.1 * torch.randn(C, generator=g)).to(DEV)
     ref = ops.conv2d_nhwc(x, w, b, 1, 1, True)
-    y = ops.conv3x3_frag(x, (ops.mfma_frag_layout(w.reshape(256, -1)), b))
+    y = ops.conv3x3_frag(x, (ops.mfma_frag_layout(w.reshape(C, -1)), b))
     torch.cuda.synchronize()
     assert torch.equal(y, ref), f"max |frag - tile| = {(y.float() - ref.float()).abs().max().item()}"
     t = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2).cpu(), w.float().permute(0, 3, 1, 2).cpu(), b.cpu(),

@@ -42,6 +42,22 @@ def main():
         print(f"frag kernel pf {pf}: {us:7.2f} us  {flops / us / 1e6:7.1f} TFLOP/s  frac {flops / us / 1e6 / 2500:.3f}"
               f"  bit-identical {same}")
     lib.sat_conv3x3_frag_set_experiment(2)
+    # layer2 c2: 28 x 28, 128 -> 128 (7-row bands)
+    x2 = torch.randn(B, 28, 28, 128, device=dev).relu().bfloat16()
+    w2 = (torch.randn(128, 3, 3, 128, device=dev) * 0.04).bfloat16()
+    b2 = torch.randn(128, device=dev) * 0.1
+    f2 = (ops.mfma_frag_layout(w2.reshape(128, -1)), b2)
+    y2 = torch.empty_like(x2)
+    fl2 = 2.0 * B * 784 * 128 * 1152
+    us = timeit(lambda: ops.conv2d_nhwc(x2, w2, b2, 1, 1, True, out=y2))
+    print(f"L2c2 tile kernel : {us:7.2f} us  {fl2 / us / 1e6:7.1f} TFLOP/s  frac {fl2 / us / 1e6 / 2500:.3f}")
+    ref2 = y2.clone()
+    for pf in (2, 3):
+        assert lib.sat_conv3x3_frag_set_experiment(pf) == 0
+        us = timeit(lambda: ops.conv3x3_frag(x2, f2, out=y2))
+        print(f"L2c2 band pf {pf}   : {us:7.2f} us  {fl2 / us / 1e6:7.1f} TFLOP/s  frac {fl2 / us / 1e6 / 2500:.3f}"
+              f"  bit-identical {torch.equal(y2, ref2)}")
+    lib.sat_conv3x3_frag_set_experiment(2)
     # c3: 1x1 256 -> 1024 + identity residual
     x3 = torch.randn(B, 14, 14, 256, device=dev).relu().bfloat16()
     r3 = torch.randn(B, 14, 14, 1024, device=dev).relu().bfloat16()
