@@ -22,7 +22,8 @@ from bench import conv_launches  # noqa: E402
 
 
 CONV_KERNELS = ("fast_gemm_kernel", "conv_pipe_kernel", "conv1x1_stream_kernel", "conv3x3_halo_kernel",
-                "bottleneck_kernel")
+                "bottleneck_kernel", "conv_ws_kernel", "conv3x3_frag_kernel", "conv3x3_band_kernel",
+                "conv1x1_res_frag_kernel")
 
 
 def is_conv_kernel(name):
@@ -66,7 +67,7 @@ def main():
     fdir, wdir = sys.argv[1], sys.argv[2]
     network = sys.argv[3] if len(sys.argv) > 3 else "resnet152"
     B = int(sys.argv[4]) if len(sys.argv) > 4 else 128
-    launches = conv_launches(network, B)
+    launches = conv_launches(network, B, fused=False)   # bench.py's default schedule: no block fused
     n = len(launches)
     out = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes, --kernel-trace), "
                      "bench.py --no-graph; FETCH_SIZE x2 (gfx950), KiB -> bytes",
