@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--stream-priority", choices=["decoder-high", "equal", "encoder-high"], default="decoder-high",
                     help="graph + overlap: the decoder / all-reduce / Adam stream gets the higher HIP stream "
                          "priority, so its short per-step kernels are dispatched first when CUs free up")
+    ap.add_argument("--tail-side", action="store_true",
+                    help="the weight gradients after BPTT in two graph branches (attention + init-state "
+                         "gradients on a side stream, Decoder.tail_side_stream)")
     ap.add_argument("--fp32-steps", type=int, default=3,
                     help="timed steps of the fp32 leg (the reference's precision, the exact-parity path; 0 = skip)")
     ap.add_argument("--no-diagnostics", action="store_true",
@@ -441,6 +444,7 @@ def main():
         # on the decoder's side stream beside the BPTT loop, sat_decoder_backward phase bit 8)
         split_bwd = world > 1 or args.bwd == "split"
         dec.head_side_stream = args.bwd == "side"
+        dec.tail_side_stream = args.tail_side
         dec.defer_recurrent_backward(split_bwd)
         for k in range(nbuf):
             opt.zero_grad(set_to_none=True)   # each capture overwrites the gradients (beta = 0)

@@ -547,8 +547,11 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   SAT_REQUIRE(lay && params && img_features && workspace && preds && alphas && d_preds && d_alphas && grads);
   // bit 4: d_preds already ReLU-masked; bit 8 (with bits 1 and 2): the head's weight gradients on a
   // side stream beside the BPTT loop, joined before returning
-  SAT_REQUIRE((phase & 3) != 0 && phase >= 1 && phase <= 15);
+  // bit 16 (with bit 2): the weight gradients after BPTT in two branches -- attention and init-state
+  // gradients on the side stream beside the LSTM-weight and embedding gradients -- joined before returning
+  SAT_REQUIRE((phase & 3) != 0 && phase >= 1 && phase <= 31);
   SAT_REQUIRE(!(phase & 8) || (phase & 3) == 3);
+  SAT_REQUIRE(!(phase & 16) || (phase & 2));
   SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
   const SatDecoderDims& d = *dp;
   WS w;
@@ -583,8 +586,8 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
     return sat_colsum(X, dt, ld, rows, N, out, accumulate, out2, w.colsum, s);
   };
   // head weight gradients: on the side stream (phase bit 8) or in order on s
-  const bool side = (phase & 8) != 0;
-  if (side) SAT_CHECK((hipError_t)t_side.init());
+  const bool side = (phase & 8) != 0, tail = (phase & 16) != 0;
+  if (side || tail) SAT_CHECK((hipError_t)t_side.init());
   hipStream_t hs = side ? t_side.s : s;
   auto wgrad_h = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo,
                      int a_tail = 0) {
@@ -664,6 +667,38 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   }
 
   // ---------------- weight gradients, batched over all B*(T-1) rows ----------------
+  // tail branch (bit 16): attention + init-state gradients on the side stream (its own column-sum
+  // scratch), issued after everything BPTT wrote
+  hipStream_t ts = tail ? t_side.s : s;
+  if (tail) {
+    SAT_CHECK(hipEventRecord(t_side.fork1, s));
+    SAT_CHECK(hipStreamWaitEvent(ts, t_side.fork1, 0));
+  }
+  auto wgrad_t = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo) {
+    SatGemm g;
+    g.M = M; g.N = N; g.K = K; g.dtype = d.dtype;
+    g.A = X; g.lda = ldx; g.transA = 1;
+    g.B = Y; g.ldb = ldy; g.transB = 1;
+    g.C = out; g.ldc = ldo; g.c_dtype = SAT_F32; g.beta = beta;
+    return sat_gemm_launch(g, ts);
+  };
+  auto colsum_t = [&](const void* X, int dt, long ld, int rows, int N, float* out) {
+    return sat_colsum(X, dt, ld, rows, N, out, accumulate, nullptr, tail ? w.colsum2 : w.colsum, ts);
+  };
+  if (att) {
+    SAT_CHECK((hipError_t)sat_attention_dws_launch(w.Ws, w.uh_all, w.de_all, c.F(lay->v_w), B, L, E, T1, d.dtype,
+                                                   w.dWs_acc, w.dWs_t, ts));
+    SAT_CHECK((hipError_t)wgrad_t(E, D, B * L, w.dWs_t, E, img_features, D, G(lay->attW_w), D));
+    SAT_CHECK((hipError_t)colsum_t(w.dWs_acc, SAT_F32, E, B * L, E, G(lay->attW_b)));
+    SAT_CHECK((hipError_t)colsum_t(w.dv_acc, SAT_F32, E, B, E, G(lay->v_w)));
+    SAT_CHECK((hipError_t)colsum_t(w.dbv_acc, SAT_F32, 1, B, 1, G(lay->v_b)));
+  }
+  // init_h / init_c (decoder.py:137-147): dh0 = dh_rec, dc0 = dc after the t = 0 step
+  SAT_CHECK((hipError_t)sat_tanh_pair_bwd(w.dh_rec, sp.dh, (long)B * E, w.dc, w.hc0, B, E, w.dpre0, w.dpre0_t,
+                                          d.dtype, ts));
+  SAT_CHECK((hipError_t)wgrad_t(2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D));
+  SAT_CHECK((hipError_t)colsum_t(w.dpre0, SAT_F32, 2 * E, B, 2 * E, G(lay->init_b)));
+
   const void* dg_t = c.at(w.dhg_t, E + D);   // d gates rows (ld HG)
   const float* dg_f = w.dhg + E + D;
   if (att) {
@@ -681,21 +716,8 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
     if (!accumulate) SAT_CHECK((hipError_t)sat_zero_rows(G(lay->embedding), (long)V * E, 1, (long)V * E, s));
     SAT_CHECK((hipError_t)sat_embed_scatter_add(w.demb, w.tok, R, E, G(lay->embedding), s));
   }
-  if (att) {
-    SAT_CHECK((hipError_t)sat_attention_dws_launch(w.Ws, w.uh_all, w.de_all, c.F(lay->v_w), B, L, E, T1, d.dtype,
-                                                   w.dWs_acc, w.dWs_t, s));
-    SAT_CHECK((hipError_t)wgrad(E, D, B * L, w.dWs_t, E, img_features, D, G(lay->attW_w), D));
-    SAT_CHECK((hipError_t)colsum(w.dWs_acc, SAT_F32, E, B * L, E, G(lay->attW_b)));
-    SAT_CHECK((hipError_t)colsum(w.dv_acc, SAT_F32, E, B, E, G(lay->v_w)));
-    SAT_CHECK((hipError_t)colsum(w.dbv_acc, SAT_F32, 1, B, 1, G(lay->v_b)));
-  }
-  // init_h / init_c (decoder.py:137-147): dh0 = dh_rec, dc0 = dc after the t = 0 step
-  SAT_CHECK((hipError_t)sat_tanh_pair_bwd(w.dh_rec, sp.dh, (long)B * E, w.dc, w.hc0, B, E, w.dpre0, w.dpre0_t,
-                                          d.dtype, s));
-  SAT_CHECK((hipError_t)wgrad(2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D));
-  SAT_CHECK((hipError_t)colsum(w.dpre0, SAT_F32, 2 * E, B, 2 * E, G(lay->init_b)));
-  if (side) {   // join: s continues only after the head's weight gradients
-    SAT_CHECK(hipEventRecord(t_side.join, hs));
+  if (side || tail) {   // join: s continues only after the side stream's weight gradients
+    SAT_CHECK(hipEventRecord(t_side.join, t_side.s));
     SAT_CHECK(hipStreamWaitEvent(s, t_side.join, 0));
   }
   return 0;

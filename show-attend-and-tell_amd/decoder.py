@@ -108,6 +108,9 @@ class Decoder(nn.Module):
         # one backward call with the head's weight gradients on a side stream beside BPTT (phase bit 8):
         # off by default -- measured slower (8.35 vs 8.19 ms/step alone, 12.9 vs 8.3 beside the encoder)
         self.head_side_stream = False
+        # the weight gradients after BPTT in two branches: attention + init-state gradients on a side
+        # stream beside the LSTM-weight / embedding gradients (phase bit 16)
+        self.tail_side_stream = False
         # workgroups the per-step split-K GEMMs aim for (SatDecoderDims.split_target; 0 = library
         # default): 64 when the decoder shares the chip with the next batch's encoder (bench / train.py)
         self.split_target = 0
@@ -249,7 +252,8 @@ class Decoder(nn.Module):
         L.check(lib.sat_decoder_backward(ctypes.byref(dims), ctypes.byref(lay), L.ptr(self._flat), L.ptr(lp),
                                          L.ptr(feats), L.ptr(ws), ws_bytes, L.ptr(preds), L.ptr(alphas),
                                          L.ptr(d_preds), L.ptr(d_alphas), L.ptr(self._grad_flat), int(accumulate),
-                                         2 | masked, L.stream_of(preds)), "sat_decoder_backward")
+                                         2 | masked | (16 if self.tail_side_stream else 0), L.stream_of(preds)),
+                "sat_decoder_backward")
         self._pending_bwd = None
         for hook in self._grad_hooks:
             hook(2, self)
@@ -414,6 +418,8 @@ class _DecoderFn(torch.autograd.Function):
             phases = (1, 2)
         else:   # one call: the head's weight gradients on a side stream beside the BPTT loop (bit 8)
             phases = (3 | 8,) if dec.head_side_stream else (3,)
+        tail = 16 if dec.tail_side_stream else 0
+        phases = tuple(p | tail if p & 2 else p for p in phases)
         for phase in phases:
             L.check(lib.sat_decoder_backward(ctypes.byref(ctx.dims), ctypes.byref(ctx.lay), L.ptr(dec._flat),
                                              L.ptr(ctx.lp), L.ptr(feats), L.ptr(ctx.ws), ctx.ws_bytes, L.ptr(preds),

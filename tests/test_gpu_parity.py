@@ -1248,6 +1248,50 @@ def test_attention_backward_one_launch_matches_two(sat, dtype, D, bert):
         assert err < tol, (n, err)
 
 
+@pytest.mark.parametrize("ado,attention", [(True, True), (False, True), (True, False)])
+def test_tail_wgrads_on_side_stream_match(sat, ado, attention):
+    """sat_decoder_backward phase bit 16: the attention / init-state weight gradients after BPTT run on
+    the side stream beside the LSTM-weight and embedding gradients -- every gradient equal (to fp32
+    atomic-order noise) to the one-stream order, eager and captured + replayed as a hipGraph."""
+    torch.manual_seed(0)
+    B, Lf, D, V, T = 32, 49, 512, 300, 9
+    dec = sat.Decoder(V, D, tf=True, ado=ado, attention=attention).to(DEV).eval()
+    feats = torch.randn(B, Lf, D, generator=torch.Generator().manual_seed(4)).bfloat16().to(DEV)
+    caps = O.make_captions(B, T, V, 1).to(DEV)
+
+    def step():
+        preds, alphas = dec(feats, caps)
+        loss, _ = sat.caption_loss(preds, alphas, caps)
+        loss.backward()
+
+    def grads():
+        dec.zero_grad(set_to_none=True)
+        step()
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().clone() for n, p in dec.named_parameters() if p.grad is not None}
+    serial = grads()
+    dec.tail_side_stream = True
+    branched = grads()
+    assert set(serial) == set(branched) and serial
+
+    def same(a, b):   # fp32 atomics (embedding scatter, atomic split-K) sum in run-dependent order
+        return ((a - b).abs().max() <= 1e-5 * b.abs().max()).item()
+    for n in serial:
+        assert same(branched[n], serial[n]), n
+    dec.zero_grad(set_to_none=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    for p in dec.parameters():
+        if p.grad is not None:
+            p.grad.fill_(float("nan"))
+    g.replay()
+    torch.cuda.synchronize()
+    for n, p in dec.named_parameters():
+        if n in serial:
+            assert same(p.grad, serial[n]), n
+
+
 @pytest.mark.parametrize("ado", [True, False])
 def test_head_wgrads_on_side_stream_match(sat, ado):
     """sat_decoder_backward phase bit 8: the output head's weight gradients run on the decoder's side
