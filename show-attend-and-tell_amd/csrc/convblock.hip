@@ -527,24 +527,32 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
 // 128, RO = 7: four workgroups per image, 512 for B = 128): the band's input rows plus a one-row halo on
 // each side that lies inside the image are staged once in LDS (slot s holds image row y0 - 1 + s; taps
 // outside the image read the zero row), the C x 9C weight streams register-direct, each of the 8 waves
-// owns NJ = C / 128 n-blocks of 16 channels and every m-block of the band.  Same k order, bias, ReLU and
-// rounding as the tile kernel: bit-identical.
-template <int IW, int RO, int C, int PF>
+// owns NJ = C / (128 NSL) n-blocks of 16 channels and every m-block of the band.  NSL > 1 splits the
+// output channels over NSL workgroups per band (ResNet152 layer3's c2 as one 14-row band = one image per
+// workgroup, two 128-channel slices: each workgroup streams half the weights -- 0.59 MB -- for 196 output
+// pixels, where the half-image kernel streams all 1.18 MB for 98).  Same k order, bias, ReLU and rounding
+// as the tile kernel: bit-identical.
+template <int IW, int RO, int C, int NSL, int PF>
 __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                   const float* __restrict__ bias, bf16* __restrict__ y) {
   constexpr int IH = IW, NPART = IH / RO, PO = RO * IW, MB = (PO + 15) / 16;
   constexpr int SLOTS = RO + 2, ZR = SLOTS * IW;        // LDS pixel rows + the zero row
-  constexpr int ROWB = 128, XPL = (ZR + 1) * ROWB, NPL = C / 64, NJ = C / 128;
+  constexpr int ROWB = 128, XPL = (ZR + 1) * ROWB, NPL = C / 64, NJ = C / (128 * NSL), CS = C / NSL;
   constexpr int NT = 9 * C / 64, KS = 9 * C / 32, CPP = C / 8;   // CPP: 16-B chunks per pixel
   constexpr int PER_T = (ZR * CPP + 511) / 512;
-  static_assert(IH % RO == 0 && C % 128 == 0 && NJ >= 1, "whole bands, 16-channel n-blocks per wave");
+  static_assert(IH % RO == 0 && C % (128 * NSL) == 0 && NJ >= 1, "whole bands, 16-channel n-blocks per wave");
   __shared__ __attribute__((aligned(16))) char smem[NPL * XPL];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fh = lane >> 4;
-  const int img = blockIdx.x / NPART, part = blockIdx.x % NPART;
+  // slice-major over groups of 8 consecutive workgroups (one per XCD under round-robin placement), so the
+  // NSL slices of one band land on one XCD and share its input rows in L2
+  const int slice = NSL == 1 ? 0 : (int)((blockIdx.x >> 3) % NSL);
+  const int band = NSL == 1 ? (int)blockIdx.x : (int)((blockIdx.x / (8 * NSL)) * 8 + (blockIdx.x & 7));
+  const int img = band / NPART, part = band % NPART;
   const int y0 = part * RO;
+  const int cb = slice * CS;                       // first output channel of this workgroup
   const int s_lo = y0 == 0 ? 1 : 0, s_hi = y0 + RO == IH ? RO : RO + 1;   // slots inside the image
   const int nchunk = (s_hi - s_lo + 1) * IW * CPP;
   const long pix_img = (long)img * IH * IW;
@@ -557,14 +565,15 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
   for (int u = 0; u < PER_T; ++u) xin[u] = xs[min(u * 512 + tid, nchunk - 1)];
   float4 bv[NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) bv[j] = *(const float4*)(bias + (w * NJ + j) * 16 + 4 * fh);
+  for (int j = 0; j < NJ; ++j) bv[j] = *(const float4*)(bias + cb + (w * NJ + j) * 16 + 4 * fh);
   bf16x8 bq[PF + 1][2][NJ];
   auto load_b = [&](int T, bf16x8 (&dst)[2][NJ]) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-        dst[ks][j] = *(const bf16x8*)((const char*)wf + (size_t)((w * NJ + j) * KS + 2 * T + ks) * 1024 + lane_b);
+        dst[ks][j] = *(const bf16x8*)((const char*)wf + (size_t)((cb / 16 + w * NJ + j) * KS + 2 * T + ks) * 1024 +
+                                      lane_b);
   };
   static_for<PF>([&](auto e) { load_b(decltype(e)::value, bq[decltype(e)::value]); });
 #pragma unroll
@@ -613,7 +622,7 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
     }
   });
 
-  char* y_s = (char*)(y + (pix_img + (long)y0 * IW) * C + w * NJ * 16);
+  char* y_s = (char*)(y + (pix_img + (long)y0 * IW) * C + cb + w * NJ * 16);
   const unsigned row_b = (unsigned)(fr * C + 4 * fh) * 2;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -634,7 +643,14 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
 template <int PF>
 __global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                            const float* __restrict__ bias, bf16* __restrict__ y) {
-  conv3x3_band_body<28, 7, 128, PF>(x, wf, bias, y);
+  conv3x3_band_body<28, 7, 128, 1, PF>(x, wf, bias, y);
+}
+
+// ResNet152 layer3's c2 as whole-image workgroups with two 128-channel output slices (256 for B = 128)
+template <int PF>
+__global__ __launch_bounds__(512) void conv3x3_slice_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                            const float* __restrict__ bias, bf16* __restrict__ y) {
+  conv3x3_band_body<14, 14, 256, 2, PF>(x, wf, bias, y);
 }
 
 // The bottleneck's c3 phase as a conv of its own: y = relu(x . W^T + b + res) for x [N][IW][IW][CM],
@@ -852,11 +868,17 @@ extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int 
   return (int)hipGetLastError();
 }
 
-static int g_c3f_pf = 2;   // weight prefetch distance of conv3x3_frag_kernel (experiment hook)
+static int g_c3f_pf = 2;      // weight prefetch distance of the 3x3 frag kernels (experiment hook)
+// 14 x 14: the whole-image two-slice kernel (1) or the half-image kernel (0, default): the slice kernel
+// streams half the weight bytes per output but each A fragment feeds one MFMA instead of two, and its
+// LDS reads (7.5 MB per workgroup) bound it: 34.4 vs 31.5 us (profiles/r2_s70_conv_ab.txt)
+static int g_c3f_slice = 0;
 
 extern "C" int sat_conv3x3_frag_set_experiment(int pf) {
-  if (pf != 2 && pf != 3 && pf != 4) return SAT_ERR_INVALID;
-  g_c3f_pf = pf;
+  const int p = pf & 15;
+  if (p != 2 && p != 3 && p != 4) return SAT_ERR_INVALID;
+  g_c3f_pf = p;
+  g_c3f_slice = (pf & 16) ? 1 : 0;   // bit 4: the whole-image two-slice kernel for 14 x 14 (A/B)
   return 0;
 }
 
@@ -876,6 +898,11 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   if (H == 28) {   // layer2 c2: 7-row bands, four workgroups per image
     if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_band_kernel<3>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp);
     else hipLaunchKernelGGL(conv3x3_band_kernel<2>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp);
+    return (int)hipGetLastError();
+  }
+  if (g_c3f_slice && N % 8 == 0) {   // slice-major grid over groups of 8 images
+    if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_slice_kernel<3>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
+    else hipLaunchKernelGGL(conv3x3_slice_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
     return (int)hipGetLastError();
   }
   if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_frag_kernel<3>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);

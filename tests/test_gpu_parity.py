@@ -1132,7 +1132,8 @@ def test_bottleneck_fused_bit_identical(sat, N):
     assert rel(nchw(y), t3) < 2e-2
 
 
-@pytest.mark.parametrize("N,H,C", [(1, 14, 256), (2, 14, 256), (5, 14, 256), (1, 28, 128), (3, 28, 128)])
+@pytest.mark.parametrize("N,H,C", [(1, 14, 256), (2, 14, 256), (5, 14, 256), (8, 14, 256), (16, 14, 256),
+                                   (1, 28, 128), (3, 28, 128)])
 def test_conv3x3_frag_bit_identical(sat, N, H, C):
     """csrc/convblock.hip's half-image 3x3 kernel (a layer3 c2 left unfused: 14x14, 256 -> 256) and its
     7-row band form (layer2 c2: 28x28, 128 -> 128) are bit-identical to the tile kernel on the same
@@ -1143,9 +1144,16 @@ def test_conv3x3_frag_bit_identical(sat, N, H, C):
     w = (torch.randn(C, 3, 3, C, generator=g) * math.sqrt(2.0 / (9 * C))).bfloat16().to(DEV)
     b = (0.1 * torch.randn(C, generator=g)).to(DEV)
     ref = ops.conv2d_nhwc(x, w, b, 1, 1, True)
-    y = ops.conv3x3_frag(x, (ops.mfma_frag_layout(w.reshape(C, -1)), b))
+    f = (ops.mfma_frag_layout(w.reshape(C, -1)), b)
+    y = ops.conv3x3_frag(x, f)
     torch.cuda.synchronize()
     assert torch.equal(y, ref), f"max |frag - tile| = {(y.float() - ref.float()).abs().max().item()}"
+    lib = sat._lib.lib()
+    try:   # experiment bit 16: the whole-image two-slice kernel at 14 x 14 (N % 8 == 0; else unchanged)
+        assert lib.sat_conv3x3_frag_set_experiment(2 | 16) == 0
+        assert torch.equal(ops.conv3x3_frag(x, f), ref)
+    finally:
+        lib.sat_conv3x3_frag_set_experiment(2)
     t = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2).cpu(), w.float().permute(0, 3, 1, 2).cpu(), b.cpu(),
                             padding=1))
     assert rel(y.float().permute(0, 3, 1, 2).cpu(), t) < 1e-2

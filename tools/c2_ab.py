@@ -35,11 +35,12 @@ def main():
     us = timeit(lambda: ops.conv2d_nhwc(x, w, b, 1, 1, True, out=y))
     print(f"tile kernel      : {us:7.2f} us  {flops / us / 1e6:7.1f} TFLOP/s  frac {flops / us / 1e6 / 2500:.3f}")
     ref = y.clone()
-    for pf in (2, 3, 4):
+    for pf in (2, 3, 2 | 16, 3 | 16):
         assert lib.sat_conv3x3_frag_set_experiment(pf) == 0
         us = timeit(lambda: ops.conv3x3_frag(x, f, out=y))
         same = torch.equal(y, ref)
-        print(f"frag kernel pf {pf}: {us:7.2f} us  {flops / us / 1e6:7.1f} TFLOP/s  frac {flops / us / 1e6 / 2500:.3f}"
+        kind = "slice     " if pf & 16 else "half-image"
+        print(f"{kind} pf {pf & 15}: {us:7.2f} us  {flops / us / 1e6:7.1f} TFLOP/s  frac {flops / us / 1e6 / 2500:.3f}"
               f"  bit-identical {same}")
     lib.sat_conv3x3_frag_set_experiment(2)
     # layer2 c2: 28 x 28, 128 -> 128 (7-row bands)
