@@ -532,20 +532,22 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
 // workgroup, two 128-channel slices: each workgroup streams half the weights -- 0.59 MB -- for 196 output
 // pixels, where the half-image kernel streams all 1.18 MB for 98).  Same k order, bias, ReLU and rounding
 // as the tile kernel: bit-identical.
-template <int IW, int RO, int C, int NSL, int PF>
+template <int IW, int RO, int C, int NSL, int WM, int PF>
 __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                   const float* __restrict__ bias, bf16* __restrict__ y) {
-  constexpr int IH = IW, NPART = IH / RO, PO = RO * IW, MB = (PO + 15) / 16;
+  constexpr int IH = IW, NPART = IH / RO, PO = RO * IW, MBT = (PO + 15) / 16;
+  constexpr int MB = (MBT + WM - 1) / WM, WN = 8 / WM;   // m-blocks per wave; waves = WM m-groups x WN
   constexpr int SLOTS = RO + 2, ZR = SLOTS * IW;        // LDS pixel rows + the zero row
-  constexpr int ROWB = 128, XPL = (ZR + 1) * ROWB, NPL = C / 64, NJ = C / (128 * NSL), CS = C / NSL;
+  constexpr int ROWB = 128, XPL = (ZR + 1) * ROWB, NPL = C / 64, NJ = C / (16 * WN * NSL), CS = C / NSL;
   constexpr int NT = 9 * C / 64, KS = 9 * C / 32, CPP = C / 8;   // CPP: 16-B chunks per pixel
   constexpr int PER_T = (ZR * CPP + 511) / 512;
-  static_assert(IH % RO == 0 && C % (128 * NSL) == 0 && NJ >= 1, "whole bands, 16-channel n-blocks per wave");
+  static_assert(IH % RO == 0 && C % (16 * WN * NSL) == 0 && NJ >= 1 && 8 % WM == 0, "whole bands, 16-channel n-blocks per wave");
   __shared__ __attribute__((aligned(16))) char smem[NPL * XPL];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fh = lane >> 4;
+  const int wm = w % WM, wn = w / WM;              // this wave's m-group and n-group
   // slice-major over groups of 8 consecutive workgroups (one per XCD under round-robin placement), so the
   // NSL slices of one band land on one XCD and share its input rows in L2
   const int slice = NSL == 1 ? 0 : (int)((blockIdx.x >> 3) % NSL);
@@ -565,14 +567,14 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
   for (int u = 0; u < PER_T; ++u) xin[u] = xs[min(u * 512 + tid, nchunk - 1)];
   float4 bv[NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) bv[j] = *(const float4*)(bias + cb + (w * NJ + j) * 16 + 4 * fh);
+  for (int j = 0; j < NJ; ++j) bv[j] = *(const float4*)(bias + cb + (wn * NJ + j) * 16 + 4 * fh);
   bf16x8 bq[PF + 1][2][NJ];
   auto load_b = [&](int T, bf16x8 (&dst)[2][NJ]) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-        dst[ks][j] = *(const bf16x8*)((const char*)wf + (size_t)((cb / 16 + w * NJ + j) * KS + 2 * T + ks) * 1024 +
+        dst[ks][j] = *(const bf16x8*)((const char*)wf + (size_t)((cb / 16 + wn * NJ + j) * KS + 2 * T + ks) * 1024 +
                                       lane_b);
   };
   static_for<PF>([&](auto e) { load_b(decltype(e)::value, bq[decltype(e)::value]); });
@@ -589,7 +591,7 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
     const int dh = tap / 3 - 1, dw = tap % 3 - 1;
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
-      const int p = i * 16 + fr, py = p / IW, pxx = p - py * IW;
+      const int p = (wm * MB + i) * 16 + fr, py = p / IW, pxx = p - py * IW;
       const bool ok = p < PO && (unsigned)(y0 + py + dh) < (unsigned)IH && (unsigned)(pxx + dw) < (unsigned)IW;
       const int q = ok ? (py + 1 + dh) * IW + pxx + dw : ZR;
 #pragma unroll
@@ -622,13 +624,13 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
     }
   });
 
-  char* y_s = (char*)(y + (pix_img + (long)y0 * IW) * C + cb + w * NJ * 16);
+  char* y_s = (char*)(y + (pix_img + (long)y0 * IW + wm * MB * 16) * C + cb + wn * NJ * 16);
   const unsigned row_b = (unsigned)(fr * C + 4 * fh) * 2;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
-      const int p = i * 16 + fr;
+      const int p = (wm * MB + i) * 16 + fr;
       u32x2 o;
       bf16* ob = (bf16*)&o;
       ob[0] = (bf16)fmaxf(acc[i][j][0] + bv[j].x, 0.f);
@@ -643,14 +645,14 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
 template <int PF>
 __global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                            const float* __restrict__ bias, bf16* __restrict__ y) {
-  conv3x3_band_body<28, 7, 128, 1, PF>(x, wf, bias, y);
+  conv3x3_band_body<28, 7, 128, 1, 1, PF>(x, wf, bias, y);
 }
 
 // ResNet152 layer3's c2 as whole-image workgroups with two 128-channel output slices (256 for B = 128)
-template <int PF>
+template <int SWM, int PF>
 __global__ __launch_bounds__(512) void conv3x3_slice_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                             const float* __restrict__ bias, bf16* __restrict__ y) {
-  conv3x3_band_body<14, 14, 256, 2, PF>(x, wf, bias, y);
+  conv3x3_band_body<14, 14, 256, 2, SWM, PF>(x, wf, bias, y);
 }
 
 // The bottleneck's c3 phase as a conv of its own: y = relu(x . W^T + b + res) for x [N][IW][IW][CM],
@@ -878,7 +880,9 @@ extern "C" int sat_conv3x3_frag_set_experiment(int pf) {
   const int p = pf & 15;
   if (p != 2 && p != 3 && p != 4) return SAT_ERR_INVALID;
   g_c3f_pf = p;
-  g_c3f_slice = (pf & 16) ? 1 : 0;   // bit 4: the whole-image two-slice kernel for 14 x 14 (A/B)
+  // bit 4: the whole-image two-slice kernel for 14 x 14 (A/B); bit 5 with it: waves as 2 m-groups x 4
+  // n-groups (two waves load each weight fragment; the second read can hit the CU's vector L1)
+  g_c3f_slice = (pf & 16) ? ((pf & 32) ? 2 : 1) : 0;
   return 0;
 }
 
@@ -901,8 +905,9 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
     return (int)hipGetLastError();
   }
   if (g_c3f_slice && N % 8 == 0) {   // slice-major grid over groups of 8 images
-    if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_slice_kernel<3>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
-    else hipLaunchKernelGGL(conv3x3_slice_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
+    if (g_c3f_slice == 2) hipLaunchKernelGGL((conv3x3_slice_kernel<2, 2>), dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
+    else if (g_c3f_pf == 3) hipLaunchKernelGGL((conv3x3_slice_kernel<1, 3>), dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
+    else hipLaunchKernelGGL((conv3x3_slice_kernel<1, 2>), dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
     return (int)hipGetLastError();
   }
   if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_frag_kernel<3>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
