@@ -772,6 +772,128 @@ __global__ __launch_bounds__(512) void conv1x1_res_frag_kernel(const bf16* __res
   conv1x1_res_frag_body<14, 7, 256, 1024, PF>(x, wf, bias, res, y);
 }
 
+// Variant of the half-image kernel whose weights travel by LDS-DMA instead of straight into VGPRs:
+// each wave DMAs exactly its own fragments (2 n-blocks x 2 k-halves = 4 x 1 KB per k-tile) into a private
+// 3-stage ring (12 KB per wave, 96 KB + the 58 KB input image) and reads them back with ds_read_b128, so
+// the ring needs no barrier -- a wave waits only on its own vmcnt.  Experiment (bit 64): does the DMA
+// path deliver more bytes per CU than register-direct loads?
+template <int IW, int RO, int C>
+__device__ __forceinline__ void conv3x3_frag_dma_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                      const float* __restrict__ bias, bf16* __restrict__ y) {
+  static_assert(IW / RO == 2 && IW % RO == 0 && C == 256, "two workgroups per image, 256 channels");
+  constexpr int IH = IW, PO = RO * IW, R1 = RO + 1, P1 = R1 * IW;
+  constexpr int MB = (P1 + 15) / 16;
+  constexpr int ROWB = 128, X1PL = (P1 + 1) * ROWB, NPL = C / 64;
+  constexpr int NT = 9 * C / 64, KS = 9 * C / 32;
+  constexpr int NCHUNK = P1 * C / 8, PER_T = NCHUNK / 512;
+  constexpr int RING = NPL * X1PL, WSTG = 4096;   // per-wave stage: 4 fragments of 1 KB
+  __shared__ __attribute__((aligned(16))) char smem[RING + 8 * 3 * WSTG];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fh = lane >> 4;
+  const int img = blockIdx.x >> 1, half = blockIdx.x & 1;
+  const int y0 = half * RO, ws = half ? IH - R1 : 0;
+  const long pix_img = (long)img * IH * IW;
+
+  uint4 xin[PER_T];
+  const uint4* xs = (const uint4*)(x + (pix_img + (long)ws * IW) * C);
+#pragma unroll
+  for (int u = 0; u < PER_T; ++u) xin[u] = xs[u * 512 + tid];
+  float4 bv[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + w * 32 + j * 16 + 4 * fh);
+#pragma unroll
+  for (int u = 0; u < PER_T; ++u) {
+    const int q = u * 512 + tid, r = q / (C / 8), c = q % (C / 8);
+    *(uint4*)(smem + (c >> 3) * X1PL + r * ROWB + 16 * ((c & 7) ^ (r & 7))) = xin[u];
+  }
+  if (tid < NPL * 8) *(uint4*)(smem + (tid >> 3) * X1PL + P1 * ROWB + (tid & 7) * 16) = make_uint4(0, 0, 0, 0);
+
+  const __amdgpu_buffer_rsrc_t rW =
+      __builtin_amdgcn_make_buffer_rsrc((void*)wf, (short)0, (int)(C * 9 * C * 2), 0x00020000);
+  char* const wring = smem + RING + w * 3 * WSTG;
+  auto dma_b = [&](int T) {   // this wave's 4 fragments of k-tile T
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (k_lds_void*)(wring + (T % 3) * WSTG + (j * 2 + ks) * 1024), 16,
+                                                 ((w * 2 + j) * KS + 2 * T + ks) * 1024 + lane * 16, 0, 0, 0);
+  };
+  dma_b(0);
+  dma_b(1);
+  k_lds_barrier();   // the input image is complete
+
+  int offs[MB][2];
+  auto tap_offsets = [&](int tap) {
+    const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int p = i * 16 + fr, py = p / IW, pxx = p - py * IW;
+      const bool ok = p < PO && (unsigned)(y0 + py + dh) < (unsigned)IH && (unsigned)(pxx + dw) < (unsigned)IW;
+      const int q = ok ? p + (y0 - ws + dh) * IW + dw : P1;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) offs[i][ks] = q * ROWB + 16 * ((ks * 4 + fh) ^ (q & 7));
+    }
+  };
+  f32x4 acc[MB][2];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  static_for<NT>([&](auto Tc) {
+    constexpr int T = decltype(Tc)::value, pl = T % NPL;
+    __builtin_amdgcn_sched_barrier(0);
+    // stage (T + 2) % 3 held k-tile T - 1, whose fragments this wave has already read (its MFMAs ran)
+    if constexpr (T + 2 < NT) dma_b(T + 2);
+    // this wave's DMAs of k-tile T have landed: younger are T + 1's and T + 2's (4 each, if issued)
+    constexpr int younger = (T + 1 < NT ? 4 : 0) + (T + 2 < NT ? 4 : 0);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(younger) : "memory");
+    if constexpr (pl == 0) tap_offsets(T / NPL);
+    bf16x8 b[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) b[ks][j] = *(const bf16x8*)(wring + (T % 3) * WSTG + (j * 2 + ks) * 1024 + lane * 16);
+    bf16x8 af[2][MB];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < MB; ++i) af[ks][i] = *(const bf16x8*)(smem + pl * X1PL + offs[i][ks]);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  });
+
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int ch = w * 32 + j * 16 + 4 * fh;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int p = i * 16 + fr;
+      u32x2 o;
+      bf16* ob = (bf16*)&o;
+      ob[0] = (bf16)fmaxf(acc[i][j][0] + bv[j].x, 0.f);
+      ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
+      ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
+      ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
+      if (p < PO) *(u32x2*)(y + (pix_img + (long)y0 * IW + p) * C + ch) = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(512) void conv3x3_frag_dma_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                               const float* __restrict__ bias, bf16* __restrict__ y) {
+  conv3x3_frag_dma_body<14, 7, 256>(x, wf, bias, y);
+}
+
 template <int PF>
 __global__ __launch_bounds__(512) void conv3x3_frag_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                            const float* __restrict__ bias, bf16* __restrict__ y) {
@@ -875,6 +997,7 @@ static int g_c3f_pf = 2;      // weight prefetch distance of the 3x3 frag kernel
 // streams half the weight bytes per output but each A fragment feeds one MFMA instead of two, and its
 // LDS reads (7.5 MB per workgroup) bound it: 34.4 vs 31.5 us (profiles/r2_s70_conv_ab.txt)
 static int g_c3f_slice = 0;
+static int g_c3f_dma = 0;
 
 extern "C" int sat_conv3x3_frag_set_experiment(int pf) {
   const int p = pf & 15;
@@ -883,6 +1006,7 @@ extern "C" int sat_conv3x3_frag_set_experiment(int pf) {
   // bit 4: the whole-image two-slice kernel for 14 x 14 (A/B); bit 5 with it: waves as 2 m-groups x 4
   // n-groups (two waves load each weight fragment; the second read can hit the CU's vector L1)
   g_c3f_slice = (pf & 16) ? ((pf & 32) ? 2 : 1) : 0;
+  g_c3f_dma = (pf & 64) ? 1 : 0;   // bit 6: the half-image kernel with its weights by LDS-DMA
   return 0;
 }
 
@@ -902,6 +1026,10 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   if (H == 28) {   // layer2 c2: 7-row bands, four workgroups per image
     if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_band_kernel<3>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp);
     else hipLaunchKernelGGL(conv3x3_band_kernel<2>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp);
+    return (int)hipGetLastError();
+  }
+  if (g_c3f_dma && !g_c3f_slice) {
+    hipLaunchKernelGGL(conv3x3_frag_dma_kernel, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
     return (int)hipGetLastError();
   }
   if (g_c3f_slice && N % 8 == 0) {   // slice-major grid over groups of 8 images

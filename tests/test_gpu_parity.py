@@ -1150,7 +1150,7 @@ def test_conv3x3_frag_bit_identical(sat, N, H, C):
     assert torch.equal(y, ref), f"max |frag - tile| = {(y.float() - ref.float()).abs().max().item()}"
     lib = sat._lib.lib()
     try:   # experiment bit 16: the whole-image two-slice kernel at 14 x 14 (N % 8 == 0; else unchanged)
-        for mode in (2 | 16, 2 | 16 | 32):   # bit 32: 2 m-groups x 4 n-groups of waves
+        for mode in (2 | 16, 2 | 16 | 32, 2 | 64):   # bit 32: 2 m-groups x 4 n-groups of waves; 64: LDS-DMA weights
             assert lib.sat_conv3x3_frag_set_experiment(mode) == 0
             assert torch.equal(ops.conv3x3_frag(x, f), ref), mode
     finally:

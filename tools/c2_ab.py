@@ -35,11 +35,11 @@ def main():
     us = timeit(lambda: ops.conv2d_nhwc(x, w, b, 1, 1, True, out=y))
     print(f"tile kernel      : {us:7.2f} us  {flops / us / 1e6:7.1f} TFLOP/s  frac {flops / us / 1e6 / 2500:.3f}")
     ref = y.clone()
-    for pf in (2, 3, 2 | 16, 2 | 16 | 32):
+    for pf in (2, 3, 2 | 16, 2 | 16 | 32, 2 | 64):
         assert lib.sat_conv3x3_frag_set_experiment(pf) == 0
         us = timeit(lambda: ops.conv3x3_frag(x, f, out=y))
         same = torch.equal(y, ref)
-        kind = ("slice 2x4 " if pf & 32 else "slice     ") if pf & 16 else "half-image"
+        kind = ("slice 2x4 " if pf & 32 else "slice     ") if pf & 16 else ("half-dma  " if pf & 64 else "half-image")
         print(f"{kind} pf {pf & 15}: {us:7.2f} us  {flops / us / 1e6:7.1f} TFLOP/s  frac {flops / us / 1e6 / 2500:.3f}"
               f"  bit-identical {same}")
     lib.sat_conv3x3_frag_set_experiment(2)
