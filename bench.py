@@ -195,6 +195,8 @@ def trunk_roofline(enc, imgs, launches, reps=3):
             ops.bottleneck_fused(a[1], *a[2])
         elif a[0] == "c2frag":
             ops.conv3x3_frag(a[1], a[2])
+        elif a[0] == "c1frag":
+            ops.conv1x1_frag(a[1], a[2])
         elif a[0] == "c3frag":
             ops.conv1x1_res_frag(a[1], a[2], a[3])
         else:
@@ -222,6 +224,7 @@ def trunk_roofline(enc, imgs, launches, reps=3):
     kname = "bottleneck_kernel (csrc/convblock.hip), fused block" if dom.get("fused") else (
         "conv3x3_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c2frag" for i in idx)
         else "conv1x1_res_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c3frag" for i in idx)
+        else "conv1x1_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c1frag" for i in idx)
         else "conv kernels, conv class")
     return dict(kernel=f"{kname} {name} ({dom['n']} launches/forward)", cls=name,
                 bound=dom["bound"], achieved=round(achieved, 2), peak=peak, unit=unit,

@@ -179,6 +179,15 @@ int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const void* x, const
                      void* stream);
 /* experiment hook (process-global, tools/c2_ab.py): sat_conv3x3_frag's weight prefetch distance (2 | 3 | 4). */
 int sat_conv3x3_frag_set_experiment(int pf);
+/* 1 if sat_conv1x1_frag runs this geometry (today: bf16, 14x14, Cin 1024, Cout 256 -- the c1 of ResNet152's
+ * layer3 identity blocks), else 0. */
+int sat_conv1x1_frag_supported(int H, int W, int Cin, int Cout, int dtype);
+/* 1x1 conv Cin -> Cout + folded bias + ReLU (a bottleneck's c1, encoder.py:13-17 through torchvision), one
+ * workgroup per half image: input slabs by LDS-DMA, weights register-direct.  x NHWC [N,H,W,Cin], y
+ * [N,H,W,Cout] (x != y); wf: sat_mfma_frag_layout of the folded [Cout][Cin] weight.  Bit-identical to
+ * sat_conv2d_nhwc. */
+int sat_conv1x1_frag(int N, int H, int W, int Cin, int Cout, int dtype, const void* x, const void* wf,
+                     const float* b, void* y, void* stream);
 /* 1 if sat_conv1x1_res_frag runs this geometry (today: bf16, 14x14, Cin 256, Cout 1024 -- the c3 of
  * ResNet152's layer3 identity blocks), else 0. */
 int sat_conv1x1_res_frag_supported(int H, int W, int Cin, int Cout, int dtype);

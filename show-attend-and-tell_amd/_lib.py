@@ -88,6 +88,9 @@ _SIGNATURES = [
     ("sat_conv3x3_frag_supported", c_int, [c_int, c_int, c_int, c_int]),
     ("sat_conv3x3_frag", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p]),
+    ("sat_conv1x1_frag_supported", c_int, [c_int, c_int, c_int, c_int, c_int]),
+    ("sat_conv1x1_frag", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p]),
     ("sat_conv1x1_res_frag_set_experiment", c_int, [c_int]),
     ("sat_conv1x1_res_frag_supported", c_int, [c_int, c_int, c_int, c_int, c_int]),
     ("sat_conv1x1_res_frag", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,

@@ -772,6 +772,117 @@ __global__ __launch_bounds__(512) void conv1x1_res_frag_kernel(const bf16* __res
   conv1x1_res_frag_body<14, 7, 256, 1024, PF>(x, wf, bias, res, y);
 }
 
+// The bottleneck's c1 phase as a conv of its own (the unfused layer3 blocks): y = relu(x . W^T + b) for
+// x [N][IW][IW][CI], y [N][IW][IW][CM] (1x1, CI = 1024 -> CM = 256).  One workgroup per half image: its
+// 98 input pixels stream through a 3-stage LDS-DMA ring of 64-channel slabs (the fused kernel's c1 ring,
+// counted vmcnt + one barrier per k-tile), the weights register-direct two k-tiles ahead.  The tile
+// kernel (convpipe.hip) runs this shape as 196 tiles of 256 x 128 that each fetch 768 KB; here 256
+// workgroups each fetch 712 KB.  Same k order, bias, ReLU and rounding: bit-identical.
+template <int IW, int RO, int CI, int CM, int PF>
+__device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                  const float* __restrict__ bias, bf16* __restrict__ y,
+                                                  unsigned x_bytes) {
+  static_assert(IW / RO == 2 && IW % RO == 0 && CM == 256 && CI % 64 == 0, "two workgroups per image");
+  constexpr int IH = IW, PO = RO * IW, MB = (PO + 15) / 16;
+  constexpr int ROWB = 128, STG = 128 * ROWB;   // ring stage: 128 rows x 64 channels
+  static_assert(MB * 16 <= 128, "one stage holds the half image's rows");
+  constexpr int NT = CI / 64, KS = CI / 32;
+  __shared__ __attribute__((aligned(16))) char smem[3 * STG];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fh = lane >> 4;
+  const long pix0 = (long)(blockIdx.x >> 1) * IH * IW + (long)(blockIdx.x & 1) * PO;
+
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)x_bytes, 0x00020000);
+  unsigned dsrc[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int d = w * 2 + u, r = d * 8 + (lane >> 3), c = (lane & 7) ^ (lane >> 3);
+    dsrc[u] = r < PO ? (unsigned)(((pix0 + r) * CI + 8 * c) * 2) : K_OOB;
+  }
+  auto dma_a = [&](int t) {
+    char* st = smem + (t % 3) * STG;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (k_lds_void*)(st + (w * 2 + u) * 1024), 16,
+                                               dsrc[u] == K_OOB ? (int)K_OOB : (int)(dsrc[u] + t * 128), 0, 0, 0);
+  };
+  bf16x8 bq[PF + 1][2][2];
+  auto load_b = [&](int T, bf16x8 (&dst)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        dst[ks][j] = *(const bf16x8*)(wf + ((long)((w * 2 + j) * KS + 2 * T + ks) * 64 + lane) * 8);
+  };
+  float4 bv[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + w * 32 + j * 16 + 4 * fh);
+  int offu[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) offu[ks] = fr * ROWB + 16 * ((ks * 4 + fh) ^ (fr & 7));
+  f32x4 acc[MB][2];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // issue order A0 B0 A1 B1 B2 .. B(PF-1), then per k-tile after its wait A(T+2), B(T+PF): the order
+  // younger_than_a() counts (bias loads are older than A0 and retire first)
+  dma_a(0);
+  load_b(0, bq[0]);
+  dma_a(1);
+  load_b(1, bq[1]);
+  static_for<PF - 2>([&](auto e) { load_b(2 + decltype(e)::value, bq[2 + decltype(e)::value]); });
+
+  static_for<NT>([&](auto Tc) {
+    constexpr int T = decltype(Tc)::value;
+    // this wave's DMAs of tile T have landed, every wave's too after the barrier; the barrier also
+    // retires every wave's reads of stage (T + 2) % 3 (tile T - 1) before it is refilled
+    k_wait_barrier<younger_than_a(T, NT, NT, PF, true)>();
+    if constexpr (T + 2 < NT) dma_a(T + 2);
+    if constexpr (T + PF < NT) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
+    const bf16x8 (&b)[2][2] = bq[T % (PF + 1)];
+    const char* st = smem + (T % 3) * STG;
+    bf16x8 af[2][MB];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < MB; ++i) af[ks][i] = *(const bf16x8*)(st + i * 16 * ROWB + offu[ks]);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  });
+
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int ch = w * 32 + j * 16 + 4 * fh;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int p = i * 16 + fr;
+      u32x2 o;
+      bf16* ob = (bf16*)&o;
+      ob[0] = (bf16)fmaxf(acc[i][j][0] + bv[j].x, 0.f);
+      ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
+      ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
+      ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
+      if (p < PO) *(u32x2*)(y + (pix0 + p) * CM + ch) = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(512) void conv1x1_frag_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                           const float* __restrict__ bias, bf16* __restrict__ y,
+                                                           unsigned x_bytes) {
+  conv1x1_frag_body<14, 7, 1024, 256, 2>(x, wf, bias, y, x_bytes);
+}
+
 // Variant of the half-image kernel whose weights travel by LDS-DMA instead of straight into VGPRs:
 // each wave DMAs exactly its own fragments (2 n-blocks x 2 k-halves = 4 x 1 KB per k-tile) into a private
 // 3-stage ring (12 KB per wave, 96 KB + the 58 KB input image) and reads them back with ds_read_b128, so
@@ -1041,6 +1152,23 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_frag_kernel<3>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
   else if (g_c3f_pf == 4) hipLaunchKernelGGL(conv3x3_frag_kernel<4>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
   else hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
+  return (int)hipGetLastError();
+}
+
+extern "C" int sat_conv1x1_frag_supported(int H, int W, int Cin, int Cout, int dtype) {
+  return dtype == SAT_BF16 && H == 14 && W == 14 && Cin == 1024 && Cout == 256;
+}
+
+extern "C" int sat_conv1x1_frag(int N, int H, int W, int Cin, int Cout, int dtype, const void* x, const void* wf,
+                                const float* b, void* y, void* stream) {
+  SAT_REQUIRE(N > 0 && x && wf && b && y && x != y);
+  SAT_REQUIRE(sat_conv1x1_frag_supported(H, W, Cin, Cout, dtype));
+  auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
+  SAT_REQUIRE(al(x, 16) && al(y, 16) && al(wf, 16) && al(b, 16));
+  const long x_bytes = 2L * N * H * W * Cin;
+  SAT_REQUIRE(x_bytes < (1L << 31));
+  hipLaunchKernelGGL(conv1x1_frag_kernel, dim3(2 * N), dim3(512), 0, (hipStream_t)stream, (const bf16*)x,
+                     (const bf16*)wf, b, (bf16*)y, (unsigned)x_bytes);
   return (int)hipGetLastError();
 }
 

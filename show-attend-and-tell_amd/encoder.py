@@ -154,6 +154,9 @@ class Encoder(nn.Module):
         # (sat_conv3x3_frag: input rows staged once in LDS, fragment-layout weights); False = the
         # tile kernel (A/B, tests)
         self.c2_frag = True
+        # ... its c1 on the half-image 1x1 kernel (sat_conv1x1_frag: input slabs by LDS-DMA, weights
+        # register-direct)
+        self.c1_frag = False
         # ... and its c3 (+ identity residual) on the half-image 1x1 kernel (sat_conv1x1_res_frag): off,
         # the weight-stationary streaming kernel is faster there (28.3 vs 33.9 us, profiles/r2_s64_c3_ab.txt)
         self.c3_frag = False
@@ -347,7 +350,11 @@ class Encoder(nn.Module):
             en.record()
             self.timing.append((st, en))
             return out
-        out = self._conv(y, c1, True)
+        if fused is not None and self.c1_frag and ops.conv1x1_frag_supported(y.shape[1], y.shape[2], y.shape[3],
+                                                                           c1[0].shape[0], y.dtype):
+            out = self._frag_conv("c1frag", ops.conv1x1_frag, y, fused[0])
+        else:
+            out = self._conv(y, c1, True)
         if c2f is not None and self.c2_frag and ops.conv3x3_frag_supported(out.shape[1], out.shape[2], out.shape[3],
                                                                          out.dtype):
             out = self._frag_conv("c2frag", ops.conv3x3_frag, out, c2f)

@@ -201,6 +201,24 @@ def conv3x3_frag(x, f, out=None):
     return y
 
 
+def conv1x1_frag_supported(H, W, Cin, Cout, dtype):
+    return bool(L.lib().sat_conv1x1_frag_supported(H, W, Cin, Cout, L.dtype_code(dtype)))
+
+
+def conv1x1_frag(x, f, out=None):
+    """relu(x . W^T + b) with f = (fragment-layout weight, fp32 bias) of a folded [Cout][Cin] 1x1 conv (a
+    layer3 bottleneck's c1).  x NHWC [N,H,W,Cin]; bit-identical to conv2d_nhwc."""
+    L.require_device(x)
+    if not x.is_contiguous():
+        raise ValueError("conv1x1_frag: x must be a contiguous NHWC tensor")
+    N, H, W, C = x.shape
+    Cout = f[1].shape[0]
+    y = out if out is not None else torch.empty(N, H, W, Cout, dtype=x.dtype, device=x.device)
+    L.check(L.lib().sat_conv1x1_frag(N, H, W, C, Cout, L.dtype_code(x.dtype), L.ptr(x), L.ptr(f[0]), L.ptr(f[1]),
+                                     L.ptr(y), L.stream_of(y)), "sat_conv1x1_frag")
+    return y
+
+
 def conv1x1_res_frag_supported(H, W, Cin, Cout, dtype):
     return bool(L.lib().sat_conv1x1_res_frag_supported(H, W, Cin, Cout, L.dtype_code(dtype)))
 

@@ -1179,6 +1179,23 @@ def test_conv1x1_res_frag_bit_identical(sat, N):
     assert rel(y.float().permute(0, 3, 1, 2).cpu(), t) < 1e-2
 
 
+@pytest.mark.parametrize("N", [1, 2, 5])
+def test_conv1x1_frag_bit_identical(sat, N):
+    """csrc/convblock.hip's half-image 1x1 kernel (a layer3 c1 left unfused: 14x14, 1024 -> 256, input
+    slabs by LDS-DMA) is bit-identical to sat_conv2d_nhwc on the same operands, and close to torch fp32."""
+    from sat_amd import ops
+    g = torch.Generator().manual_seed(60 + N)
+    x = torch.randn(N, 14, 14, 1024, generator=g).relu().bfloat16().to(DEV)
+    w = (torch.randn(256, 1, 1, 1024, generator=g) * math.sqrt(2.0 / 1024)).bfloat16().to(DEV)
+    b = (0.1 * torch.randn(256, generator=g)).to(DEV)
+    ref = ops.conv2d_nhwc(x, w, b, 1, 0, True)
+    y = ops.conv1x1_frag(x, (ops.mfma_frag_layout(w.reshape(256, -1)), b))
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref), f"max |frag - conv| = {(y.float() - ref.float()).abs().max().item()}"
+    t = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2).cpu(), w.float().permute(0, 3, 1, 2).cpu(), b.cpu()))
+    assert rel(y.float().permute(0, 3, 1, 2).cpu(), t) < 1e-2
+
+
 def test_encoder_c2_frag_equal_tile(sat):
     """ResNet152 trunk at 224 x 224 with every layer3 block unfused: the c2s on sat_conv3x3_frag and the
     c3s on sat_conv1x1_res_frag change no output bit against the tile / streaming kernels."""
@@ -1190,10 +1207,11 @@ def test_encoder_c2_frag_equal_tile(sat):
     enc.fuse_blocks = False
     x = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(7)).to(DEV)
     with torch.no_grad():
-        enc.c2_frag, enc.c3_frag = True, True
+        enc.c1_frag, enc.c2_frag, enc.c3_frag = True, True, True
         y_f = enc(x)
-        enc.c2_frag = False
+        enc.c1_frag, enc.c2_frag = False, False
         y_t = enc(x)
+        enc.c1_frag = True
         enc.c2_frag, enc.c3_frag = True, False
         y_3 = enc(x)
     assert torch.equal(y_f, y_t)

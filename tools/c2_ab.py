@@ -59,6 +59,19 @@ def main():
         print(f"L2c2 band pf {pf}   : {us:7.2f} us  {fl2 / us / 1e6:7.1f} TFLOP/s  frac {fl2 / us / 1e6 / 2500:.3f}"
               f"  bit-identical {torch.equal(y2, ref2)}")
     lib.sat_conv3x3_frag_set_experiment(2)
+    # c1: 1x1 1024 -> 256
+    x1 = torch.randn(B, 14, 14, 1024, device=dev).relu().bfloat16()
+    w1 = (torch.randn(256, 1, 1, 1024, device=dev) * 0.03).bfloat16()
+    b1 = torch.randn(256, device=dev) * 0.1
+    f1 = (ops.mfma_frag_layout(w1.reshape(256, -1)), b1)
+    y1 = torch.empty(B, 14, 14, 256, device=dev).bfloat16()
+    fl1 = 2.0 * B * 196 * 256 * 1024
+    us = timeit(lambda: ops.conv2d_nhwc(x1, w1, b1, 1, 0, True, out=y1))
+    print(f"c1 tile kernel   : {us:7.2f} us  {fl1 / us / 1e6:7.1f} TFLOP/s  frac {fl1 / us / 1e6 / 2500:.3f}")
+    ref1 = y1.clone()
+    us = timeit(lambda: ops.conv1x1_frag(x1, f1, out=y1))
+    print(f"c1 frag kernel   : {us:7.2f} us  {fl1 / us / 1e6:7.1f} TFLOP/s  frac {fl1 / us / 1e6 / 2500:.3f}"
+          f"  bit-identical {torch.equal(y1, ref1)}")
     # c3: 1x1 256 -> 1024 + identity residual
     x3 = torch.randn(B, 14, 14, 256, device=dev).relu().bfloat16()
     r3 = torch.randn(B, 14, 14, 1024, device=dev).relu().bfloat16()
