@@ -156,7 +156,7 @@ class Encoder(nn.Module):
         self.c2_frag = True
         # ... its c1 on the half-image 1x1 kernel (sat_conv1x1_frag: input slabs by LDS-DMA, weights
         # register-direct)
-        self.c1_frag = False
+        self.c1_frag = True
         # ... and its c3 (+ identity residual) on the half-image 1x1 kernel (sat_conv1x1_res_frag): off,
         # the weight-stationary streaming kernel is faster there (28.3 vs 33.9 us, profiles/r2_s64_c3_ab.txt)
         self.c3_frag = False
