@@ -55,21 +55,9 @@ def parse():
                          "64 with ResNet152 features, 128 with VGG19's: profiles/r2_s54_sched.txt)")
     ap.add_argument("--no-fuse-blocks", action="store_true",
                     help="run the layer3 identity bottlenecks as three conv launches (A/B of csrc/convblock.hip)")
-    ap.add_argument("--block-variant", choices=["default", "share"], default="default",
-                    help="fused bottleneck kernel: 'share' = the co-residency variant (57 KB LDS, <= 168 VGPRs)")
-    ap.add_argument("--bwd", choices=["side", "serial", "split"], default="split",
-                    help="N = 1 decoder backward structure: one call with the head's weight gradients on a side "
-                         "stream (side), one call in order (serial), or two graphs as at N > 1 (split)")
-    ap.add_argument("--cu-split", type=int, default=0,
-                    help="graph + overlap: run the decoder / all-reduce / Adam stream on this many CUs and the "
-                         "next batch's encoder on the rest (CU-masked streams; 0 = shared chip)")
-    ap.add_argument("--cu-layout", choices=["strided", "contig"], default="contig",
-                    help="which CU-mask bits the decoder gets with --cu-split (the runtime interleaves mask bits "
-                         "over the 8 XCDs: bits 0..31 = 4 CUs on every XCD; a mask that leaves an XCD empty is "
-                         "ignored, tools/cu_probe.py)")
-    ap.add_argument("--cu-dec-all", action="store_true",
-                    help="with --cu-split: the decoder stream may use every CU (the encoder still keeps off its "
-                         "--cu-split reserved CUs)")
+    ap.add_argument("--bwd", choices=["serial", "split"], default="split",
+                    help="N = 1 decoder backward structure: one graph in order (serial), or two graphs as at N > 1 "
+                         "(split)")
     ap.add_argument("--no-skinny", action="store_true",
                     help="per-step decoder GEMMs on the LDS-DMA tile kernel instead of csrc/skinny.hip (A/B)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -86,9 +74,6 @@ def parse():
     ap.add_argument("--stream-priority", choices=["decoder-high", "equal", "encoder-high"], default="decoder-high",
                     help="graph + overlap: the decoder / all-reduce / Adam stream gets the higher HIP stream "
                          "priority, so its short per-step kernels are dispatched first when CUs free up")
-    ap.add_argument("--tail-side", action="store_true",
-                    help="the weight gradients after BPTT in two graph branches (attention + init-state "
-                         "gradients on a side stream, Decoder.tail_side_stream)")
     ap.add_argument("--fp32-steps", type=int, default=3,
                     help="timed steps of the fp32 leg (the reference's precision, the exact-parity path; 0 = skip)")
     ap.add_argument("--no-diagnostics", action="store_true",
@@ -197,11 +182,9 @@ def trunk_roofline(enc, imgs, launches, reps=3):
             ops.conv3x3_frag(a[1], a[2])
         elif a[0] == "c1frag":
             ops.conv1x1_frag(a[1], a[2])
-        elif a[0] == "c3frag":
-            ops.conv1x1_res_frag(a[1], a[2], a[3])
         else:
             x, w, b, s, p, relu, res, hw = a
-            ops.conv2d_nhwc(x, w, b, s, p, relu, residual=res, out_hw=hw)
+            ops.conv2d_nhwc(x, w, b, s, p, relu, residual=res, out_hw=hw, policy=enc.policy)
 
     with torch.no_grad():
         for i in idx[:2]:   # warm
@@ -223,7 +206,6 @@ def trunk_roofline(enc, imgs, launches, reps=3):
     trunk_us = sum(dur) * 1e3
     kname = "bottleneck_kernel (csrc/convblock.hip), fused block" if dom.get("fused") else (
         "conv3x3_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c2frag" for i in idx)
-        else "conv1x1_res_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c3frag" for i in idx)
         else "conv1x1_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c1frag" for i in idx)
         else "conv kernels, conv class")
     return dict(kernel=f"{kname} {name} ({dom['n']} launches/forward)", cls=name,
@@ -355,12 +337,11 @@ def main():
     from sat_amd.data import synthetic_captions, synthetic_images
     from sat_amd.distributed import GradAllReduce, allreduce_bucket_async, allreduce_grads
 
-    if args.no_skinny:
-        assert sat_amd._lib.lib().sat_skinny_set_mode(0) == 0
-    if args.no_ws3x3:
-        assert sat_amd._lib.lib().sat_conv3x3_ws_set_mode(0) == 0
-    if args.gemm_stages:
-        assert sat_amd._lib.lib().sat_fast_gemm_set_config(args.gemm_stages, 0, 1) == 0
+    # per-call kernel selection for the A/B flags (None = the library's defaults)
+    policy = None
+    if args.no_skinny or args.no_ws3x3 or args.gemm_stages:
+        policy = sat_amd.Policy(skinny=1 if args.no_skinny else 0, conv3x3_ws=1 if args.no_ws3x3 else 0,
+                                gemm_stages=args.gemm_stages)
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
@@ -370,11 +351,11 @@ def main():
         args.split_target = 128 if args.network == "vgg19" else 64
     enc.fuse_blocks = (False if args.no_fuse_blocks or args.fuse_every == 0 else
                        (True if args.fuse_every == 1 else args.fuse_every))
-    if args.block_variant == "share":
-        assert sat_amd._lib.lib().sat_bottleneck_set_experiment(2, 128) == 0
+    enc.policy = policy
     torch.manual_seed(42)          # identical decoder init on every rank
     dec = sat_amd.Decoder(args.vocab, D, tf=not args.no_tf, ado=not args.bert, bert=args.bert,
                           attention=True).to(dev).train()
+    dec.policy = policy
     if not args.no_graph and not args.no_overlap:
         # the decoder shares the chip with the next batch's encoder: fewer split-K workgroups
         dec.split_target = args.split_target
@@ -443,11 +424,8 @@ def main():
                     with torch.no_grad():
                         feats_static.append(enc(imgs))
         # backward phase 1 (output head) and phase 2 (BPTT) as two graphs, the head bucket's all-reduce
-        # (N > 1) issued between them; --bwd serial / side: one graph (side: the head's weight gradients
-        # on the decoder's side stream beside the BPTT loop, sat_decoder_backward phase bit 8)
+        # (N > 1) issued between them; --bwd serial: one graph
         split_bwd = world > 1 or args.bwd == "split"
-        dec.head_side_stream = args.bwd == "side"
-        dec.tail_side_stream = args.tail_side
         dec.defer_recurrent_backward(split_bwd)
         for k in range(nbuf):
             opt.zero_grad(set_to_none=True)   # each capture overwrites the gradients (beta = 0)
@@ -465,14 +443,7 @@ def main():
         torch.cuda.synchronize()
 
     enc_events = []
-    if overlap and args.cu_split:
-        dec_cus, enc_cus = sat_amd.ops.cu_mask_bits(sat_amd.ops.device_cu_count(), args.cu_split, args.cu_layout)
-        lo, hi = torch.cuda.Stream.priority_range()
-        s_main = torch.cuda.Stream(priority=hi) if args.cu_dec_all else sat_amd.ops.cu_masked_stream(dec_cus, dev)
-        s_enc = sat_amd.ops.cu_masked_stream(enc_cus, dev)
-        s_main.wait_stream(torch.cuda.current_stream())
-        torch.cuda.set_stream(s_main)
-    elif overlap and args.stream_priority != "equal":
+    if overlap and args.stream_priority != "equal":
         lo, hi = torch.cuda.Stream.priority_range()
         dec_hi = args.stream_priority == "decoder-high"
         s_main = torch.cuda.Stream(priority=hi if dec_hi else lo)
@@ -595,8 +566,7 @@ def main():
                                    f"step, V={args.vocab}, T={args.seq}",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": args.seq,
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
-                       "encoder_decoder_overlap": overlap,
-                       "decoder_cus": (args.cu_split or None) if overlap else None},
+                       "encoder_decoder_overlap": overlap},
             "roofline": roof,
             "encoder_trunk": dict(trunk or {}, graph_ms_per_step=(round(enc_ms / args.steps, 3) if enc_ms else None),
                                   split_at=args.enc_split if g_encA is not None else None),

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SAT_ABI_VERSION 1
+#define SAT_ABI_VERSION 2
 
 enum { SAT_F32 = 0, SAT_BF16 = 1 };
 enum { SAT_ACT_NONE = 0, SAT_ACT_RELU = 1, SAT_ACT_TANH = 2, SAT_ACT_SIGMOID = 3 };
@@ -43,6 +43,28 @@ enum { SAT_OK = 0, SAT_ERR_INVALID = 9001 };
 typedef struct {
   int N, H, W, C, KH, KW, stride, pad, OH, OW;
 } SatConvGeom;
+
+/* Per-call kernel selection.  Every field 0 = the library's choice (what the product runs); the
+ * other values force or exclude one kernel for a single call -- A/B measurements and the tests that
+ * compare two kernels bit for bit.  Passed by pointer (nullable = all defaults) to every entry point
+ * that dispatches among kernels: SatGemmArgs.policy, sat_conv2d_nhwc, SatDecoderDims.policy.  There
+ * is no process-global tuning state: two callers in one process never see each other's policy. */
+typedef struct {
+  int conv_pipe;        /* 256x128 pipelined conv / GEMM kernel: 0 auto (long-K, chip-filling), 1 off, 2 every eligible */
+  int conv_stream;      /* weight-stationary 1x1 kernel (K <= 512): 0 auto, 1 off, 2 every eligible */
+  int conv3x3_ws;       /* 64 -> 64 3x3 weight-stationary halo kernel: 0 on, 1 off */
+  int skinny;           /* register-direct skinny GEMM (M <= 128): 0 the decoder's K/256-split products, 1 off,
+                         * 2 every eligible problem */
+  int gemm_stages;      /* LDS ring depth of the bf16 tile kernel: 0 auto, 2, 3 */
+  int gemm_tile;        /* tile configuration: 0 auto, 1 = 128x128 / 8 waves, 2 = 128x64 / 8, 3 = 128x128 / 4,
+                         * 4 = 128x256 / 8, 5 = 256x128 / 8 (k-major operands use 1 or 3) */
+  int gemm_linear_order;/* 1 = plain tile order instead of the XCD-aware one */
+  int gemm_epilogue;    /* bf16-output epilogue of 128-row tiles: 0 bf16 LDS epilogue for every eligible launch,
+                         * 1 for residual launches only, 2 fp32 tile staged in LDS */
+  int attn_bwd;         /* attention backward per decoder step: 0 auto, 1 the two-launch form */
+  int decoder_splits[4];/* split-K counts of the per-step bf16 decoder GEMMs -- h: [U; f_beta; W_hh] h, c: context
+                         * part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic */
+} SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),
  * A(m,k) = transA ? A[k*lda+m] : A[m*lda+k];  B(n,k) = transB ? B[k*ldb+n] : B[n*ldb+k].
@@ -59,6 +81,7 @@ typedef struct {
   const void* add1; int64_t ld_add1; int add1_dtype;
   int act;
   void* aux; int64_t ld_aux; int aux_dtype;
+  const SatPolicy* policy;    /* nullable: library defaults */
 } SatGemmArgs;
 
 /* Decoder problem description (decoder.py:9-67 constructor flags + shapes). */
@@ -72,10 +95,10 @@ typedef struct {
   /* optional device counter: when set, masks are drawn from (seed ^ *seed_ptr) and the forward
    * increments *seed_ptr on the stream, so a hipGraph replay draws fresh masks every step. */
   uint64_t* seed_ptr;
-  /* workgroups the per-step split-K GEMMs aim for (0 = the library default, sat_decoder_set_split_target):
-   * per call, so two decoders in one process can differ and a captured graph keeps the value its
-   * workspace was sized with */
+  /* workgroups the per-step split-K GEMMs aim for (0 = the library default, 192): per call, so two
+   * decoders in one process can differ and a captured graph keeps the value its workspace was sized with */
   int split_target;
+  const SatPolicy* policy;    /* nullable: library defaults (must be the same for a forward and its backward) */
 } SatDecoderDims;
 
 /* Element offsets of every decoder parameter inside one flat fp32 buffer.  Keys
@@ -93,42 +116,7 @@ typedef struct {
 int sat_abi_version(void);
 const char* sat_error_string(int code);
 
-/* --- streams ---------------------------------------------------------------- */
-/* Compute units of the current device (256 on MI355X). */
-int sat_device_cu_count(int* ncu);
-/* A stream whose kernels run only on the CUs whose bits are set in mask[0..words) (bit i of word w =
- * CU 32 w + i in the runtime's CU numbering); the decoder and the next batch's encoder run on disjoint
- * CU sets (train.py:128-164's step, re-scheduled).  Release with sat_stream_destroy. */
-int sat_stream_create_cu_mask(const uint32_t* mask, int words, void** stream_out);
-int sat_stream_destroy(void* stream);
-/* diagnostics: out[2 i] = HW_ID, out[2 i + 1] = XCC_ID register of workgroup i (each spins spin_cycles). */
-int sat_probe_cu_ids(int nblocks, int spin_cycles, uint32_t* out, void* stream);
-
 /* --- generic building blocks -------------------------------------------- */
-/* tuning hook for the bf16 LDS-DMA GEMM (process-global): LDS ring depth (0 = auto | 2 | 3), tile
- * configuration (0 = auto, 1 = 128x128 / 8 waves, 2 = 128x64 / 8, 3 = 128x128 / 4, 4 = 128x256 / 8,
- * 5 = 256x128 / 8; k-major operands use 1 or 3), XCD-aware tile order (0 | 1, default 1). */
-int sat_fast_gemm_set_config(int stages, int tile, int xcd_remap);
-/* tuning hook (process-global): epilogue of 128-row tiles with bf16 output -- 0 = fp32 tile staged in
- * LDS; 1 = bf16 LDS epilogue for residual launches (residual tile LDS-DMA'd during the last k-tile,
- * added in the accumulator layout); 2 (default) = bf16 LDS epilogue for every eligible launch. */
-int sat_fast_gemm_set_res_lds(int mode);
-/* diagnostics (process-global): when buf is non-null every data-parallel launch of the bf16 GEMM
- * writes, per workgroup (linear block id), 4 x u64 = [start, main loop done, end, XCC_ID << 32 |
- * HW_ID] on the 100 MHz realtime clock into buf (tools/conv_trace.py); null disables. */
-int sat_fast_gemm_set_trace(void* buf);
-/* tuning hook (process-global) for the 256x128 pipelined conv / GEMM kernel (convpipe.hip): 0 = off,
- * 1 = automatic (default: long-K problems that fill the chip), 2 = every eligible problem. */
-int sat_conv_pipe_set_mode(int mode);
-/* experiment hook (process-global, tools/pipe_ab.py): waves per workgroup of the pipelined kernel
- * (8 | 4) and diagnostic ablation bits (conv + ReLU launches only; 0 = off). */
-int sat_conv_pipe_set_experiment(int waves, int ablate);
-/* tuning hook (process-global) for the weight-stationary streaming kernel of K <= 512 1x1 convs
- * (convstream.hip): 0 = off, 1 = automatic (default), 2 = every eligible problem. */
-int sat_conv_stream_set_mode(int mode);
-/* tuning hook (process-global) for the 3x3 / stride-1 halo kernel (convhalo.hip): 0 = off (default),
- * 1 = automatic, 2 = every eligible problem. */
-int sat_conv_halo_set_mode(int mode);
 int sat_gemm(const SatGemmArgs* args, void* stream);
 /* elementwise cast between SAT_F32 and SAT_BF16 storage (n elements). */
 int sat_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, void* stream);
@@ -148,15 +136,12 @@ int sat_nchw_to_s2d(int N, int C, int H, int W, int dtype, const float* x, void*
  * top/left padding, OH/OW are taken as given (bottom/right padding = whatever they imply);
  * covers Conv2d+ReLU (VGG19) and Conv2d+BatchNorm(eval, folded)+[residual]+ReLU (ResNet152). */
 int sat_conv2d_nhwc(const SatConvGeom* g, int Cout, int dtype, const void* x, const void* w,
-                    const float* bias, const void* residual, int relu, void* y, void* stream);
+                    const float* bias, const void* residual, int relu, void* y, const SatPolicy* policy,
+                    void* stream);
 /* Weight re-layout for register-direct MFMA fragment loads (once per weight version):
  * src [N][K] bf16 row-major -> dst [N/16][K/32][64][8], lane l = 16*(k8 % 4) + (n % 16) of block
  * (n / 16, k / 32) holding src[n][32*(k/32) + 8*(l >> 4) .. +8].  N % 16 == 0, K % 32 == 0. */
 int sat_mfma_frag_layout(int N, int K, const void* src, void* dst, void* stream);
-/* experiment hook (process-global, tools/block_ab.py) of the fused bottleneck kernel: weight prefetch
- * distance in k-tiles (2 | 3) and diagnostic ablation bits (1 no MFMA, 2 no weight streaming, 4 no
- * LDS fragment reads; 0 = off). */
-int sat_bottleneck_set_experiment(int pf, int abl);
 /* 1 if sat_bottleneck_fused runs this geometry (today: bf16, 14x14, Cin 1024, Cmid 256 -- the 35
  * identity blocks of ResNet152 layer3), else 0. */
 int sat_bottleneck_fused_supported(int H, int W, int Cin, int Cmid, int dtype);
@@ -177,8 +162,6 @@ int sat_conv3x3_frag_supported(int H, int W, int C, int dtype);
  * [C][3*3*C] (tap-major) weight; b: fp32 bias.  Bit-identical to sat_conv2d_nhwc on the same operands. */
 int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const void* x, const void* wf, const float* b, void* y,
                      void* stream);
-/* experiment hook (process-global, tools/c2_ab.py): sat_conv3x3_frag's weight prefetch distance (2 | 3 | 4). */
-int sat_conv3x3_frag_set_experiment(int pf);
 /* 1 if sat_conv1x1_frag runs this geometry (today: bf16, 14x14, Cin 1024, Cout 256 -- the c1 of ResNet152's
  * layer3 identity blocks), else 0. */
 int sat_conv1x1_frag_supported(int H, int W, int Cin, int Cout, int dtype);
@@ -188,17 +171,6 @@ int sat_conv1x1_frag_supported(int H, int W, int Cin, int Cout, int dtype);
  * sat_conv2d_nhwc. */
 int sat_conv1x1_frag(int N, int H, int W, int Cin, int Cout, int dtype, const void* x, const void* wf,
                      const float* b, void* y, void* stream);
-/* 1 if sat_conv1x1_res_frag runs this geometry (today: bf16, 14x14, Cin 256, Cout 1024 -- the c3 of
- * ResNet152's layer3 identity blocks), else 0. */
-int sat_conv1x1_res_frag_supported(int H, int W, int Cin, int Cout, int dtype);
-/* 1x1 conv Cin -> Cout + folded bias + residual + ReLU (a bottleneck's c3 with its identity shortcut,
- * encoder.py:13-17 through torchvision), one workgroup per half image, input staged once in LDS,
- * weights streamed register-direct.  x NHWC [N,H,W,Cin]; res, y [N,H,W,Cout] (y distinct from both);
- * wf: sat_mfma_frag_layout of the folded [Cout][Cin] weight.  Bit-identical to sat_conv2d_nhwc. */
-int sat_conv1x1_res_frag(int N, int H, int W, int Cin, int Cout, int dtype, const void* x, const void* wf,
-                         const float* b, const void* res, void* y, void* stream);
-/* experiment hook (process-global, tools/c2_ab.py): sat_conv1x1_res_frag's weight prefetch distance (2 | 3). */
-int sat_conv1x1_res_frag_set_experiment(int pf);
 /* MaxPool2d (floor mode, -inf padding) on NHWC. */
 int sat_maxpool2d_nhwc(int N, int H, int W, int C, int k, int stride, int pad, int dtype,
                        const void* x, void* y, int OH, int OW, void* stream);
@@ -212,23 +184,8 @@ int sat_attention_forward(int B, int L, int D, int E, int dtype, const void* img
                           const float* v_w, const float* v_b, float* ws_scratch,
                           float* context, float* alpha, void* stream);
 
-/* tuning hook (process-global): 3x3 / stride-1 / pad-1 convs with 64 input and output channels at width
- * 56 or 224 (ResNet152 layer1 c2, VGG19 conv1_2; encoder.py:13-17,23-27) on the weight-stationary halo
- * kernel (1, default) or the implicit-GEMM tile kernel (0, A/B). */
-int sat_conv3x3_ws_set_mode(int on);
-/* tuning hook (process-global): the register-direct skinny kernel for bf16 NT GEMMs with M <= 128 and fp32
- * (partial-slab) output: 1 (default) = the decoder's per-step context GEMM and init GEMM (decoder.py:107-115,
- * 137-147; split into 256-deep K slabs for it), 2 = every eligible problem (tests), 0 = off (A/B). */
-int sat_skinny_set_mode(int on);
-/* tuning hook (process-global): the attention backward of a decoder step as ONE launch per step
- * (1, default: a workgroup per batch row) or the two-launch form (0, A/B). */
-int sat_attention_set_bwd_mode(int fused);
 
 /* --- decoder (decoder.py:69-158) ----------------------------------------- */
-/* tuning hook (process-global): split-K counts of the per-step bf16 decoder GEMMs -- h: [U; f_beta; W_hh] h,
- * c: context part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic.  Must be set
- * before sat_decoder_workspace_bytes. */
-int sat_decoder_set_splits(int h, int c, int g, int dh);
 /* diagnostics (bench.py): after sat_decoder_forward + sat_decoder_backward filled `workspace`, re-issue
  * each per-step kernel group of step (T-1)/2 `reps` times back to back between HIP events on `stream`;
  * us_out[8] = average us per launch: h GEMM, attention fwd, context GEMM, LSTM fwd, LSTM bwd, d(gated
@@ -237,9 +194,6 @@ int sat_decoder_set_splits(int h, int c, int g, int dh);
 int sat_decoder_step_bench(const SatDecoderDims* dims, const SatDecoderLayout* layout, const float* params,
                            const void* params_lp, const void* img_features, void* workspace, size_t workspace_bytes,
                            float* alphas, const float* d_alphas, int reps, float* us_out, void* stream);
-/* process-global: workgroups the automatic per-step split-K aims for (0 = default 192; 64 when the decoder
- * shares the GPU with a concurrent encoder stream).  Set before the first workspace query. */
-int sat_decoder_set_split_target(int workgroups);
 size_t sat_decoder_workspace_bytes(const SatDecoderDims* d);
 /* preds [B,T-1,V] (dtype), alphas [B,T-1,L] fp32, tokens [B,T-1] int32 = token fed at each step. */
 int sat_decoder_forward(const SatDecoderDims* d, const SatDecoderLayout* lay, const float* params,

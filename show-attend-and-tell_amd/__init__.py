@@ -6,6 +6,7 @@ keys and CLI flags; compute runs in hand-written gfx950 HIP kernels behind the
 C ABI in include/sat_hip.h (libsat_hip.so, loaded with ctypes).
 """
 from . import _lib
+from ._lib import SatPolicy as Policy
 from .attention import Attention
 from .data import PackedImages, collate_packed
 from .decoder import Decoder

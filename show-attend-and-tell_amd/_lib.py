@@ -25,6 +25,22 @@ class SatConvGeom(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("N", "H", "W", "C", "KH", "KW", "stride", "pad", "OH", "OW")]
 
 
+ABI_VERSION = 2   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
+
+
+class SatPolicy(ctypes.Structure):
+    """Per-call kernel selection (include/sat_hip.h SatPolicy); all zeros = the library's defaults."""
+    _fields_ = [(n, c_int) for n in ("conv_pipe", "conv_stream", "conv3x3_ws", "skinny", "gemm_stages", "gemm_tile",
+                                     "gemm_linear_order", "gemm_epilogue", "attn_bwd")] + \
+               [("decoder_splits", c_int * 4)]
+
+    def __init__(self, **kw):
+        splits = kw.pop("decoder_splits", None)
+        super().__init__(**kw)
+        if splits is not None:
+            self.decoder_splits[:] = list(splits)
+
+
 class SatGemmArgs(ctypes.Structure):
     _fields_ = [("M", c_int), ("N", c_int), ("K", c_int), ("dtype", c_int),
                 ("A", c_void_p), ("lda", c_int64), ("transA", c_int),
@@ -34,14 +50,15 @@ class SatGemmArgs(ctypes.Structure):
                 ("bias", c_void_p),
                 ("add1", c_void_p), ("ld_add1", c_int64), ("add1_dtype", c_int),
                 ("act", c_int),
-                ("aux", c_void_p), ("ld_aux", c_int64), ("aux_dtype", c_int)]
+                ("aux", c_void_p), ("ld_aux", c_int64), ("aux_dtype", c_int),
+                ("policy", ctypes.POINTER(SatPolicy))]
 
 
 class SatDecoderDims(ctypes.Structure):
     _fields_ = [("B", c_int), ("L", c_int), ("D", c_int), ("E", c_int), ("V", c_int), ("T", c_int),
                 ("tf", c_int), ("ado", c_int), ("attention", c_int), ("bert", c_int), ("training", c_int),
                 ("dtype", c_int), ("start_token", c_int), ("has_dropout_mask", c_int), ("seed", c_uint64),
-                ("seed_ptr", c_void_p), ("split_target", c_int)]
+                ("seed_ptr", c_void_p), ("split_target", c_int), ("policy", ctypes.POINTER(SatPolicy))]
 
 
 LAYOUT_FIELDS = ("embedding", "init_w", "init_b", "hcat_w", "hcat_b", "attW_w", "attW_b", "v_w", "v_b", "wih",
@@ -56,45 +73,23 @@ class SatDecoderLayout(ctypes.Structure):
 _SIGNATURES = [
     ("sat_abi_version", c_int, []),
     ("sat_error_string", ctypes.c_char_p, [c_int]),
-    ("sat_device_cu_count", c_int, [ctypes.POINTER(c_int)]),
-    ("sat_stream_create_cu_mask", c_int, [ctypes.POINTER(ctypes.c_uint32), c_int, ctypes.POINTER(c_void_p)]),
-    ("sat_stream_destroy", c_int, [c_void_p]),
-    ("sat_probe_cu_ids", c_int, [c_int, c_int, c_void_p, c_void_p]),
-    ("sat_fast_gemm_set_config", c_int, [c_int, c_int, c_int]),
-    ("sat_fast_gemm_set_res_lds", c_int, [c_int]),
-    ("sat_fast_gemm_set_trace", c_int, [c_void_p]),
-    ("sat_conv_pipe_set_mode", c_int, [c_int]),
-    ("sat_conv_pipe_set_experiment", c_int, [c_int, c_int]),
-    ("sat_conv_stream_set_mode", c_int, [c_int]),
-    ("sat_conv_halo_set_mode", c_int, [c_int]),
-    ("sat_skinny_set_mode", c_int, [c_int]),
-    ("sat_conv3x3_ws_set_mode", c_int, [c_int]),
-    ("sat_attention_set_bwd_mode", c_int, [c_int]),
-    ("sat_decoder_set_splits", c_int, [c_int, c_int, c_int, c_int]),
-    ("sat_decoder_set_split_target", c_int, [c_int]),
     ("sat_gemm", c_int, [ctypes.POINTER(SatGemmArgs), c_void_p]),
     ("sat_cast", c_int, [c_void_p, c_int, c_void_p, c_int, c_int64, c_void_p]),
     ("sat_mean_rows_abi", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     ("sat_nchw_to_nhwc", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     ("sat_nchw_to_s2d", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     ("sat_conv2d_nhwc", c_int, [ctypes.POINTER(SatConvGeom), c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                                c_int, c_void_p, c_void_p]),
+                                c_int, c_void_p, ctypes.POINTER(SatPolicy), c_void_p]),
     ("sat_mfma_frag_layout", c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p]),
-    ("sat_bottleneck_set_experiment", c_int, [c_int, c_int]),
     ("sat_bottleneck_fused_supported", c_int, [c_int, c_int, c_int, c_int, c_int]),
     ("sat_bottleneck_fused", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    ("sat_conv3x3_frag_set_experiment", c_int, [c_int]),
     ("sat_conv3x3_frag_supported", c_int, [c_int, c_int, c_int, c_int]),
     ("sat_conv3x3_frag", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p]),
     ("sat_conv1x1_frag_supported", c_int, [c_int, c_int, c_int, c_int, c_int]),
     ("sat_conv1x1_frag", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p]),
-    ("sat_conv1x1_res_frag_set_experiment", c_int, [c_int]),
-    ("sat_conv1x1_res_frag_supported", c_int, [c_int, c_int, c_int, c_int, c_int]),
-    ("sat_conv1x1_res_frag", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                                     c_void_p, c_void_p, c_void_p]),
     ("sat_maxpool2d_nhwc", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                    c_int, c_int, c_void_p]),
     ("sat_attention_forward", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -147,6 +142,10 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        version = handle.sat_abi_version()
+        if version != ABI_VERSION:
+            raise RuntimeError(f"sat_amd: {LIB_PATH} has C-ABI version {version}, this package binds version "
+                               f"{ABI_VERSION}; rebuild it (make -C show-attend-and-tell_amd/csrc)")
         _lib = handle
     return _lib
 
@@ -173,6 +172,11 @@ def require_device(*tensors):
 
 def ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def policy_ptr(policy):
+    """ctypes pointer to a SatPolicy (None -> NULL = the library's defaults)."""
+    return None if policy is None else ctypes.pointer(policy)
 
 
 def stream_of(t):

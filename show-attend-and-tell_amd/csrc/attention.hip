@@ -654,8 +654,9 @@ __global__ __launch_bounds__(FBW * 64) void attn_bwd_fused_kernel(AttnBwdArgs a)
 // and a 256-wide e-chunk (lane: 4 consecutive e): each uh[b,t,e..e+3] load feeds DWS_LG x 4 tanh and
 // the next step's uh is requested before the current step's arithmetic; the wave's de[b,:,l0..]
 // block is staged in LDS once (a scalar load per step would wait on the scalar cache every step).
-// Ws is read once.  VALU-bound: B*L*E*(T-1) tanh.
-constexpr int DWS_LG = 4, DWS_WAVES = 4, DWS_TMAX = 128;   // T - 1 <= 128 caption steps
+// Ws is read once.  VALU-bound: B*L*E*(T-1) tanh.  Any caption length: the de block is staged in
+// chunks of DWS_TMAX steps (newest chunk first, so the summation order stays T1-1 .. 0).
+constexpr int DWS_LG = 4, DWS_WAVES = 4, DWS_TMAX = 128;   // caption steps per LDS chunk
 template <typename T>
 __global__ __launch_bounds__(DWS_WAVES * 64) void attn_dws_kernel(const T* Ws, const float* uh_all,
                                                                  const float* de_all, const float* v_w, int B, int L,
@@ -667,39 +668,44 @@ __global__ __launch_bounds__(DWS_WAVES * 64) void attn_dws_kernel(const T* Ws, c
   const bool wok = wid < B * n_ech * n_lg;
   const int lg = wid % n_lg, ec = (wid / n_lg) % n_ech, b = wok ? wid / (n_lg * n_ech) : 0;
   const int l0 = lg * DWS_LG, e = ec * 256 + lane * 4;
-  // stage de[b, t, l0 + r] -> s_de[wv][t * DWS_LG + r]
-  for (int i = lane; i < T1 * DWS_LG; i += 64) {
-    const int t = i / DWS_LG, r = i - t * DWS_LG;
-    s_de[wv][i] = (wok && l0 + r < L) ? de_all[((long)b * T1 + t) * L + l0 + r] : 0.f;
-  }
-  __syncthreads();
-  if (!wok) return;   // wave-uniform; no barriers below
   const bool eok = e < E;
   float xw[DWS_LG][4], acc[DWS_LG][4], vw[4];
-  load_e4<float>(v_w + e, eok, vw);
+  load_e4<float>(v_w + e, wok && eok, vw);
 #pragma unroll
   for (int r = 0; r < DWS_LG; ++r) {
-    load_e4<T>(Ws + ((long)b * L + l0 + r) * E + e, eok && l0 + r < L, xw[r]);
+    load_e4<T>(Ws + ((long)b * L + l0 + r) * E + e, wok && eok && l0 + r < L, xw[r]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[r][j] = 0.f;
   }
   const float* uh = uh_all + (long)b * T1 * E + e;
   float un[4];
-  load_e4<float>(uh + (long)(T1 - 1) * E, eok, un);
-  for (int t = T1 - 1; t >= 0; --t) {
-    float uu[4] = {un[0], un[1], un[2], un[3]};
-    if (t > 0) load_e4<float>(uh + (long)(t - 1) * E, eok, un);
-    const float4 d4 = *(const float4*)&s_de[wv][t * DWS_LG];
-    const float d[DWS_LG] = {d4.x, d4.y, d4.z, d4.w};
+  load_e4<float>(uh + (long)(T1 - 1) * E, wok && eok, un);
+  // every wave takes part in every chunk's staging barriers (the chunk count depends on T1 only)
+  for (int c0 = (T1 - 1) / DWS_TMAX * DWS_TMAX; c0 >= 0; c0 -= DWS_TMAX) {
+    const int c1 = min(T1, c0 + DWS_TMAX);
+    __syncthreads();   // the previous chunk's reads are done
+    // stage de[b, t, l0 + r] (t in [c0, c1)) -> s_de[wv][(t - c0) * DWS_LG + r]
+    for (int i = lane; i < (c1 - c0) * DWS_LG; i += 64) {
+      const int t = c0 + i / DWS_LG, r = i % DWS_LG;
+      s_de[wv][i] = (wok && l0 + r < L) ? de_all[((long)b * T1 + t) * L + l0 + r] : 0.f;
+    }
+    __syncthreads();
+    if (!wok) continue;   // wave-uniform
+    for (int t = c1 - 1; t >= c0; --t) {
+      float uu[4] = {un[0], un[1], un[2], un[3]};
+      if (t > 0) load_e4<float>(uh + (long)(t - 1) * E, eok, un);
+      const float4 d4 = *(const float4*)&s_de[wv][(t - c0) * DWS_LG];
+      const float d[DWS_LG] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
-    for (int r = 0; r < DWS_LG; ++r)
+      for (int r = 0; r < DWS_LG; ++r)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float th = tanh_t<T>(xw[r][j] + uu[j]);
-        acc[r][j] += d[r] * vw[j] * (1.f - th * th);
-      }
+        for (int j = 0; j < 4; ++j) {
+          const float th = tanh_t<T>(xw[r][j] + uu[j]);
+          acc[r][j] += d[r] * vw[j] * (1.f - th * th);
+        }
+    }
   }
-  if (!eok) return;
+  if (!wok || !eok) return;
 #pragma unroll
   for (int r = 0; r < DWS_LG; ++r) {
     if (l0 + r >= L) break;
@@ -748,8 +754,6 @@ int sat_attention_fwd_launch(const AttnFwdArgs& a, hipStream_t s) {
 
 namespace {
 
-int g_attn_bwd_fused = 1;   // 1: attn_bwd_fused_kernel where it applies, 0: the two-launch form (A/B)
-
 template <typename T, int DCH>
 bool launch_bwd_fused_e(int ech, hipStream_t s, const AttnBwdArgs& a) {
   constexpr int NW = DCH >= 4 ? 8 : 16, NU = DCH >= 4 ? 7 : 4;
@@ -779,17 +783,11 @@ bool launch_bwd_fused(const AttnBwdArgs& a, hipStream_t s) {
 
 }  // namespace
 
-extern "C" int sat_attention_set_bwd_mode(int fused) {
-  if (fused != 0 && fused != 1) return SAT_ERR_INVALID;
-  g_attn_bwd_fused = fused;
-  return 0;
-}
-
 int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s) {
   const int VD = a.dtype == SAT_BF16 ? 8 : 4;
   SAT_REQUIRE(a.L <= kMaxL && a.E % VD == 0 && a.E <= 1024);
   SAT_REQUIRE(a.D % VD == 0);
-  if (g_attn_bwd_fused && (a.uh_ld % 4) == 0 && (a.E % 4) == 0) {
+  if (sat_policy().attn_bwd != 1 && (a.uh_ld % 4) == 0 && (a.E % 4) == 0) {
     const bool ok = a.dtype == SAT_BF16 ? launch_bwd_fused<bf16>(a, s) : launch_bwd_fused<float>(a, s);
     if (ok) return (int)hipGetLastError();
   }
@@ -806,7 +804,7 @@ int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s) {
 
 int sat_attention_dws_launch(const void* Ws, const float* uh_all, const float* de_all, const float* v_w, int B,
                              int L, int E, int T1, int dtype, float* out_f32, void* out_t, hipStream_t s) {
-  SAT_REQUIRE(E % 4 == 0 && E <= 1024 && L > 0 && B > 0 && T1 > 0 && T1 <= DWS_TMAX);
+  SAT_REQUIRE(E % 4 == 0 && E <= 1024 && L > 0 && B > 0 && T1 > 0);
   static_assert(DWS_LG == 4, "s_de rows are read as one float4 per step");
   const int n_ech = sat_cdiv(E, 256), n_lg = sat_cdiv(L, DWS_LG);
   const dim3 grid(sat_cdiv((long)B * n_ech * n_lg, DWS_WAVES));

@@ -43,7 +43,6 @@ struct WArgs {
   int N, H, W;                           // images, height, width (= output height, width)
   int items, items_per_img, tiles_x;     // items = N * (H / TR) * tiles_x
   unsigned x_bytes, y_bytes;
-  int abl;                               // diagnostics (tools/ws_ab.py): 2 no stores, 4 no halo DMA
 };
 
 template <int N>
@@ -113,7 +112,7 @@ __global__ __launch_bounds__(WS_NW * 64) void conv_ws_kernel(WArgs a) {
       const int hy = hp / HW_, hx = hp - hy * HW_;
       const int yy = y0 + hy - PADT, xx = x0 + hx - PADT;
       const bool ok = hp < HP && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
-      const unsigned off = ok && !(a.abl & 4) ? (unsigned)(((((long)n * a.H + yy) * a.W + xx) * C + 8 * c) * 2) : WS_OOB;
+      const unsigned off = ok ? (unsigned)(((((long)n * a.H + yy) * a.W + xx) * C + 8 * c) * 2) : WS_OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (w_lds_void*)(st + (d * WS_NW + w) * 1024), 16, (int)off, 0, 0, 0);
     }
   };
@@ -187,7 +186,7 @@ __global__ __launch_bounds__(WS_NW * 64) void conv_ws_kernel(WArgs a) {
       bf16* ob = (bf16*)&o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) ob[j] = (bf16)apply_act(acc[i][j] + bias4[j], ACT);
-      const unsigned off = (a.abl & 2) ? WS_OOB : (unsigned)(((((long)n * a.H + y0 + py) * a.W + x0 + px) * WS_NOUT + 16 * cg + 4 * fh) * 2);
+      const unsigned off = (unsigned)(((((long)n * a.H + y0 + py) * a.W + x0 + px) * WS_NOUT + 16 * cg + 4 * fh) * 2);
       __builtin_amdgcn_raw_buffer_store_b64(o, rY, (int)off, 0, 0);
     }
     it += step;
@@ -196,9 +195,7 @@ __global__ __launch_bounds__(WS_NW * 64) void conv_ws_kernel(WArgs a) {
   }
 }
 
-int g_ws_mode = 1;   // 0 off (A/B), 1 on
-int g_ws_abl = 0;    // diagnostics: WArgs::abl
-int g_ws_cus = 0;
+int g_ws_cus = 0;    // CU count (queried once)
 
 inline bool wal16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -217,7 +214,7 @@ void launch_ws(int act, dim3 grid, hipStream_t s, const WArgs& a) {
 // 112), 0 otherwise.
 int sat_conv3x3_ws_try(const SatGemm& g, hipStream_t s, int* err) {
   *err = 0;
-  if (g_ws_mode == 0) return 0;
+  if (sat_policy().conv3x3_ws == 1) return 0;
   const SatConvGeom& cv = g.conv;
   const bool c3 = cv.C == 64 && cv.KH == 3 && cv.KW == 3 && cv.pad == 1 && (cv.W == 56 || cv.W == 224);
   const bool stem = cv.C == 16 && cv.KH == 4 && cv.KW == 4 && cv.pad == 2 && cv.W == 112;
@@ -244,7 +241,6 @@ int sat_conv3x3_ws_try(const SatGemm& g, hipStream_t s, int* err) {
   a.items_per_img = (cv.H / TR) * a.tiles_x;
   a.items = cv.N * a.items_per_img;
   a.x_bytes = (unsigned)xb; a.y_bytes = (unsigned)yb;
-  a.abl = g_ws_abl;
   // the stem variant (72 KB of LDS, 108 VGPRs) fits two workgroups per CU
   const int slots = g_ws_cus * (stem ? 2 : 1);
   const int grid = a.items < slots ? a.items : slots;
@@ -253,11 +249,4 @@ int sat_conv3x3_ws_try(const SatGemm& g, hipStream_t s, int* err) {
   else launch_ws<3, 64, 1, 2, 112, 2>(g.act, dim3(grid), s, a);
   *err = (int)hipGetLastError();
   return 1;
-}
-
-extern "C" int sat_conv3x3_ws_set_mode(int on) {   // bit 0: on; bits 1-3: diagnostic ablations (WArgs::abl)
-  if (on < 0 || on > 15) return SAT_ERR_INVALID;
-  g_ws_mode = on & 1;
-  g_ws_abl = on >> 1;
-  return 0;
 }

@@ -405,12 +405,6 @@ template <int PF, int ABL>
 __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
   bottleneck_body<14, 7, 1024, 256, PF, ABL>(a);
 }
-// co-residency variant: 57 KB of LDS and at most 168 VGPRs (three waves per SIMD fit), so a decoder
-// workgroup of up to ~100 KB LDS / 2 x 88 VGPRs per SIMD can run on the same CU
-template <int PF, int ABL>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(3))) void bottleneck_kernel_share(KArgs a) {
-  bottleneck_body<14, 7, 1024, 256, PF, ABL | 128>(a);
-}
 
 // The bottleneck's c2 phase as a conv of its own (the layer3 blocks the trunk leaves unfused, so the
 // decoder running beside the encoder finds CUs between launches): y = relu(conv3x3(x) + b) for
@@ -648,129 +642,7 @@ __global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restric
   conv3x3_band_body<28, 7, 128, 1, 1, PF>(x, wf, bias, y);
 }
 
-// ResNet152 layer3's c2 as whole-image workgroups with two 128-channel output slices (256 for B = 128)
-template <int SWM, int PF>
-__global__ __launch_bounds__(512) void conv3x3_slice_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
-                                                            const float* __restrict__ bias, bf16* __restrict__ y) {
-  conv3x3_band_body<14, 14, 256, 2, SWM, PF>(x, wf, bias, y);
-}
 
-// The bottleneck's c3 phase as a conv of its own: y = relu(x . W^T + b + res) for x [N][IW][IW][CM],
-// res, y [N][IW][IW][CO] (1x1, stride 1).  One workgroup per half image: its 98 input pixels are staged
-// once in LDS (CM = 256: 50 KB), the CO x CM weight streams register-direct (fragment layout), the
-// residual rows go straight to registers a chunk ahead of their epilogue.  The weight-stationary
-// streaming kernel (convstream.hip) runs this shape at ~30 us for B = 128; the same sums (64-deep
-// k-tiles ascending), bias, residual add and one rounding: bit-identical.
-template <int IW, int RO, int CM, int CO, int PF>
-__device__ __forceinline__ void conv1x1_res_frag_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
-                                                      const float* __restrict__ bias, const bf16* __restrict__ res,
-                                                      bf16* __restrict__ y) {
-  static_assert(IW / RO == 2 && IW % RO == 0 && CM == 256 && CO % 256 == 0, "two workgroups per image");
-  constexpr int IH = IW, PO = RO * IW, MB = (PO + 15) / 16;
-  constexpr int ROWB = 128, XPL = MB * 16 * ROWB, NPL = CM / 64;
-  constexpr int KT = CM / 64, NCK = CO / 256, NT = NCK * KT, KS = CM / 32;
-  constexpr int NCHUNK = PO * CM / 8, PER_T = (NCHUNK + 511) / 512;
-  __shared__ __attribute__((aligned(16))) char smem[NPL * XPL];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int fr = lane & 15, fh = lane >> 4;
-  const int img = blockIdx.x >> 1, half = blockIdx.x & 1;
-  const long pix0 = (long)img * IH * IW + (long)half * PO;   // first pixel of this half image
-
-  // the half image's input rows are one contiguous block of PO pixels (rows >= PO of the LDS image
-  // stay unwritten: their outputs are never stored)
-  uint4 xin[PER_T];
-  const uint4* xs = (const uint4*)(x + pix0 * CM);
-#pragma unroll
-  for (int u = 0; u < PER_T; ++u) xin[u] = xs[min(u * 512 + tid, NCHUNK - 1)];   // clamped: no branch, no scratch
-  // every global access = a wave-uniform base (SGPRs) + a 32-bit per-lane byte offset, so the unrolled
-  // schedule keeps one offset register per access pattern instead of a 64-bit address per access
-  const unsigned lane_b = (unsigned)lane * 16;
-  const char* res_s = (const char*)(res + pix0 * CO + w * 32);
-  char* y_s = (char*)(y + pix0 * CO + w * 32);
-  const unsigned row_b = (unsigned)(fr * CO + 4 * fh) * 2;                        // m-blocks 0 .. MB-2
-  const unsigned row_last = (unsigned)(min((MB - 1) * 16 + fr, PO - 1) - (MB - 1) * 16) * CO * 2 + 8 * fh;
-  bf16x8 bq[PF + 1][2][2];
-  auto load_b = [&](int T, bf16x8 (&dst)[2][2]) {
-    const int ck = T / KT, kt = T % KT;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        dst[ks][j] = *(const bf16x8*)((const char*)wf + (size_t)((ck * 16 + w * 2 + j) * KS + 2 * kt + ks) * 1024 +
-                                      lane_b);
-  };
-  static_for<PF>([&](auto e) { load_b(decltype(e)::value, bq[decltype(e)::value]); });
-#pragma unroll
-  for (int u = 0; u < PER_T; ++u) {
-    const int q = u * 512 + tid, r = q / (CM / 8), c = q % (CM / 8);
-    if (q < NCHUNK) *(uint4*)(smem + (c >> 3) * XPL + r * ROWB + 16 * ((c & 7) ^ (r & 7))) = xin[u];
-  }
-  k_lds_barrier();
-
-  int offu[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) offu[ks] = fr * ROWB + 16 * ((ks * 4 + fh) ^ (fr & 7));
-  f32x4 acc[MB][2];
-  u32x2 resv[MB][2];
-  float4 bv[2];
-
-  static_for<NT>([&](auto Tc) {
-    constexpr int T = decltype(Tc)::value, ck = T / KT, kt = T % KT;
-    __builtin_amdgcn_sched_barrier(0);   // keep the scheduler from hoisting later tiles' loads (register spills)
-    if constexpr (kt == 0) {   // this chunk's residual rows + bias (rows past PO load a valid row, never stored)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + ck * 256 + w * 32 + j * 16 + 4 * fh);
-#pragma unroll
-      for (int i = 0; i < MB; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          resv[i][j] = *(const u32x2*)(res_s + (size_t)(i * 16 * CO + ck * 256 + j * 16) * 2 +
-                                        (i == MB - 1 ? row_last : row_b));
-          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-    }
-    if constexpr (T + PF < NT) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
-    const bf16x8 (&b)[2][2] = bq[T % (PF + 1)];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {   // one 32-deep half's A fragments at a time (the residual rows
-      bf16x8 af[MB];                   // held across the chunk leave no room for both halves)
-#pragma unroll
-      for (int i = 0; i < MB; ++i) af[i] = *(const bf16x8*)(smem + kt * XPL + i * 16 * ROWB + offu[ks]);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < MB; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[i], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    if constexpr (kt == KT - 1) {   // epilogue: bias, fp32 residual add, ReLU, one rounding, 8-B stores
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-#pragma unroll
-        for (int i = 0; i < MB; ++i) {
-          const int p = i * 16 + fr;
-          const bf16* rh = (const bf16*)&resv[i][j];
-          const float v[4] = {acc[i][j][0] + bv[j].x, acc[i][j][1] + bv[j].y, acc[i][j][2] + bv[j].z,
-                              acc[i][j][3] + bv[j].w};
-          u32x2 o;
-          bf16* ob = (bf16*)&o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) ob[e] = (bf16)fmaxf(v[e] + (float)rh[e], 0.f);
-          if (p < PO) *(u32x2*)(y_s + (size_t)(i * 16 * CO + ck * 256 + j * 16) * 2 + row_b) = o;
-        }
-      }
-    }
-  });
-}
-
-template <int PF>
-__global__ __launch_bounds__(512) void conv1x1_res_frag_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
-                                                               const float* __restrict__ bias,
-                                                               const bf16* __restrict__ res, bf16* __restrict__ y) {
-  conv1x1_res_frag_body<14, 7, 256, 1024, PF>(x, wf, bias, res, y);
-}
 
 // The bottleneck's c1 phase as a conv of its own (the unfused layer3 blocks): y = relu(x . W^T + b) for
 // x [N][IW][IW][CI], y [N][IW][IW][CM] (1x1, CI = 1024 -> CM = 256).  One workgroup per half image: its
@@ -883,127 +755,6 @@ __global__ __launch_bounds__(512) void conv1x1_frag_kernel(const bf16* __restric
   conv1x1_frag_body<14, 7, 1024, 256, 2>(x, wf, bias, y, x_bytes);
 }
 
-// Variant of the half-image kernel whose weights travel by LDS-DMA instead of straight into VGPRs:
-// each wave DMAs exactly its own fragments (2 n-blocks x 2 k-halves = 4 x 1 KB per k-tile) into a private
-// 3-stage ring (12 KB per wave, 96 KB + the 58 KB input image) and reads them back with ds_read_b128, so
-// the ring needs no barrier -- a wave waits only on its own vmcnt.  Experiment (bit 64): does the DMA
-// path deliver more bytes per CU than register-direct loads?
-template <int IW, int RO, int C>
-__device__ __forceinline__ void conv3x3_frag_dma_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
-                                                      const float* __restrict__ bias, bf16* __restrict__ y) {
-  static_assert(IW / RO == 2 && IW % RO == 0 && C == 256, "two workgroups per image, 256 channels");
-  constexpr int IH = IW, PO = RO * IW, R1 = RO + 1, P1 = R1 * IW;
-  constexpr int MB = (P1 + 15) / 16;
-  constexpr int ROWB = 128, X1PL = (P1 + 1) * ROWB, NPL = C / 64;
-  constexpr int NT = 9 * C / 64, KS = 9 * C / 32;
-  constexpr int NCHUNK = P1 * C / 8, PER_T = NCHUNK / 512;
-  constexpr int RING = NPL * X1PL, WSTG = 4096;   // per-wave stage: 4 fragments of 1 KB
-  __shared__ __attribute__((aligned(16))) char smem[RING + 8 * 3 * WSTG];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int fr = lane & 15, fh = lane >> 4;
-  const int img = blockIdx.x >> 1, half = blockIdx.x & 1;
-  const int y0 = half * RO, ws = half ? IH - R1 : 0;
-  const long pix_img = (long)img * IH * IW;
-
-  uint4 xin[PER_T];
-  const uint4* xs = (const uint4*)(x + (pix_img + (long)ws * IW) * C);
-#pragma unroll
-  for (int u = 0; u < PER_T; ++u) xin[u] = xs[u * 512 + tid];
-  float4 bv[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + w * 32 + j * 16 + 4 * fh);
-#pragma unroll
-  for (int u = 0; u < PER_T; ++u) {
-    const int q = u * 512 + tid, r = q / (C / 8), c = q % (C / 8);
-    *(uint4*)(smem + (c >> 3) * X1PL + r * ROWB + 16 * ((c & 7) ^ (r & 7))) = xin[u];
-  }
-  if (tid < NPL * 8) *(uint4*)(smem + (tid >> 3) * X1PL + P1 * ROWB + (tid & 7) * 16) = make_uint4(0, 0, 0, 0);
-
-  const __amdgpu_buffer_rsrc_t rW =
-      __builtin_amdgcn_make_buffer_rsrc((void*)wf, (short)0, (int)(C * 9 * C * 2), 0x00020000);
-  char* const wring = smem + RING + w * 3 * WSTG;
-  auto dma_b = [&](int T) {   // this wave's 4 fragments of k-tile T
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (k_lds_void*)(wring + (T % 3) * WSTG + (j * 2 + ks) * 1024), 16,
-                                                 ((w * 2 + j) * KS + 2 * T + ks) * 1024 + lane * 16, 0, 0, 0);
-  };
-  dma_b(0);
-  dma_b(1);
-  k_lds_barrier();   // the input image is complete
-
-  int offs[MB][2];
-  auto tap_offsets = [&](int tap) {
-    const int dh = tap / 3 - 1, dw = tap % 3 - 1;
-#pragma unroll
-    for (int i = 0; i < MB; ++i) {
-      const int p = i * 16 + fr, py = p / IW, pxx = p - py * IW;
-      const bool ok = p < PO && (unsigned)(y0 + py + dh) < (unsigned)IH && (unsigned)(pxx + dw) < (unsigned)IW;
-      const int q = ok ? p + (y0 - ws + dh) * IW + dw : P1;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) offs[i][ks] = q * ROWB + 16 * ((ks * 4 + fh) ^ (q & 7));
-    }
-  };
-  f32x4 acc[MB][2];
-#pragma unroll
-  for (int i = 0; i < MB; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  static_for<NT>([&](auto Tc) {
-    constexpr int T = decltype(Tc)::value, pl = T % NPL;
-    __builtin_amdgcn_sched_barrier(0);
-    // stage (T + 2) % 3 held k-tile T - 1, whose fragments this wave has already read (its MFMAs ran)
-    if constexpr (T + 2 < NT) dma_b(T + 2);
-    // this wave's DMAs of k-tile T have landed: younger are T + 1's and T + 2's (4 each, if issued)
-    constexpr int younger = (T + 1 < NT ? 4 : 0) + (T + 2 < NT ? 4 : 0);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(younger) : "memory");
-    if constexpr (pl == 0) tap_offsets(T / NPL);
-    bf16x8 b[2][2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) b[ks][j] = *(const bf16x8*)(wring + (T % 3) * WSTG + (j * 2 + ks) * 1024 + lane * 16);
-    bf16x8 af[2][MB];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < MB; ++i) af[ks][i] = *(const bf16x8*)(smem + pl * X1PL + offs[i][ks]);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < MB; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  });
-
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int ch = w * 32 + j * 16 + 4 * fh;
-#pragma unroll
-    for (int i = 0; i < MB; ++i) {
-      const int p = i * 16 + fr;
-      u32x2 o;
-      bf16* ob = (bf16*)&o;
-      ob[0] = (bf16)fmaxf(acc[i][j][0] + bv[j].x, 0.f);
-      ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
-      ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
-      ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
-      if (p < PO) *(u32x2*)(y + (pix_img + (long)y0 * IW + p) * C + ch) = o;
-    }
-  }
-}
-
-__global__ __launch_bounds__(512) void conv3x3_frag_dma_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
-                                                               const float* __restrict__ bias, bf16* __restrict__ y) {
-  conv3x3_frag_dma_body<14, 7, 256>(x, wf, bias, y);
-}
 
 template <int PF>
 __global__ __launch_bounds__(512) void conv3x3_frag_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
@@ -1012,7 +763,7 @@ __global__ __launch_bounds__(512) void conv3x3_frag_kernel(const bf16* __restric
 }
 
 // [N][K] bf16 -> [N/16][K/32][64 lanes][8]: lane l = (fh << 4) | fr holds row 16 nb + fr, k 32 ks + 8 fh ..
-__global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst, int N, int K, int kmajor) {
+__global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst, int N, int K) {
   const long n8 = (long)N * K / 8;
   for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < n8; v += (long)gridDim.x * blockDim.x) {
     const long e = v * 8;                      // destination element
@@ -1020,7 +771,7 @@ __global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restric
     const long blk = e / 512;                  // (nb, ks)
     const int KS = K / 32;
     const int NB = N / 16;
-    const int nb = kmajor ? (int)(blk % NB) : (int)(blk / KS), ks = kmajor ? (int)(blk / NB) : (int)(blk % KS);
+    const int nb = (int)(blk / KS), ks = (int)(blk % KS);
     const int row = nb * 16 + (lane & 15), k = ks * 32 + (lane >> 4) * 8;
     *(uint4*)(dst + e) = *(const uint4*)(src + (long)row * K + k);
   }
@@ -1028,56 +779,13 @@ __global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restric
 
 }  // namespace
 
-static int g_frag_kmajor = 0;   // experiment: k-major fragment layout (ABL bit 6)
-
 extern "C" int sat_mfma_frag_layout(int N, int K, const void* src, void* dst, void* stream) {
   SAT_REQUIRE(src && dst && N > 0 && K > 0 && N % 16 == 0 && K % 32 == 0);
   SAT_REQUIRE(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0);
   const long n8 = (long)N * K / 8;
   const int g = (int)((n8 + 255) / 256 < 4096 ? (n8 + 255) / 256 : 4096);
-  hipLaunchKernelGGL(frag_layout_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16*)src, (bf16*)dst, N, K,
-                     g_frag_kmajor);
+  hipLaunchKernelGGL(frag_layout_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, (const bf16*)src, (bf16*)dst, N, K);
   return (int)hipGetLastError();
-}
-
-namespace {
-
-int g_block_pf = 2;    // weight prefetch distance (k-tiles)
-int g_block_abl = 0;   // diagnostics: ABL bits
-
-template <int PF, int ABL>
-void launch_block(dim3 grid, hipStream_t s, const KArgs& a) {
-  if constexpr ((ABL & 128) != 0) hipLaunchKernelGGL((bottleneck_kernel_share<PF, ABL & 127>), grid, dim3(512), 0, s, a);
-  else hipLaunchKernelGGL((bottleneck_kernel<PF, ABL>), grid, dim3(512), 0, s, a);
-}
-template <int PF>
-void launch_block_abl(int abl, dim3 grid, hipStream_t s, const KArgs& a) {
-  switch (abl) {
-    case 1: launch_block<PF, 1>(grid, s, a); break;
-    case 2: launch_block<PF, 2>(grid, s, a); break;
-    case 4: launch_block<PF, 4>(grid, s, a); break;
-    case 6: launch_block<PF, 6>(grid, s, a); break;
-    case 32: launch_block<PF, 32>(grid, s, a); break;
-    case 64: launch_block<PF, 64>(grid, s, a); break;
-    case 96: launch_block<PF, 96>(grid, s, a); break;
-    case 33: launch_block<PF, 33>(grid, s, a); break;
-    case 97: launch_block<PF, 97>(grid, s, a); break;
-    case 128: launch_block<PF, 128>(grid, s, a); break;
-    default: launch_block<PF, 0>(grid, s, a); break;
-  }
-}
-
-}  // namespace
-
-// experiment hook (tools/block_ab.py): weight prefetch distance (2; 3 measured no faster:
-// profiles/r2_s24_block_ablation.txt) and ablation bits (0 = off)
-extern "C" int sat_bottleneck_set_experiment(int pf, int abl) {
-  if (pf != 2 || (abl != 0 && abl != 1 && abl != 2 && abl != 4 && abl != 6 && abl != 32 && abl != 64 && abl != 96 &&
-                  abl != 33 && abl != 97 && abl != 128)) return SAT_ERR_INVALID;
-  g_block_pf = pf;
-  g_block_abl = abl;
-  g_frag_kmajor = (abl & 64) ? 1 : 0;
-  return 0;
 }
 
 extern "C" int sat_bottleneck_fused_supported(int H, int W, int Cin, int Cmid, int dtype) {
@@ -1099,26 +807,8 @@ extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int 
   a.w1 = (const bf16*)w1f; a.w2 = (const bf16*)w2f; a.w3 = (const bf16*)w3f;
   a.b1 = b1; a.b2 = b2; a.b3 = b3;
   a.x_bytes = (unsigned)x_bytes;
-  launch_block_abl<2>(g_block_abl, dim3(2 * N), (hipStream_t)stream, a);
+  hipLaunchKernelGGL((bottleneck_kernel<2, 0>), dim3(2 * N), dim3(512), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
-}
-
-static int g_c3f_pf = 2;      // weight prefetch distance of the 3x3 frag kernels (experiment hook)
-// 14 x 14: the whole-image two-slice kernel (1) or the half-image kernel (0, default): the slice kernel
-// streams half the weight bytes per output but each A fragment feeds one MFMA instead of two, and its
-// LDS reads (7.5 MB per workgroup) bound it: 34.4 vs 31.5 us (profiles/r2_s70_conv_ab.txt)
-static int g_c3f_slice = 0;
-static int g_c3f_dma = 0;
-
-extern "C" int sat_conv3x3_frag_set_experiment(int pf) {
-  const int p = pf & 15;
-  if (p != 2 && p != 3 && p != 4) return SAT_ERR_INVALID;
-  g_c3f_pf = p;
-  // bit 4: the whole-image two-slice kernel for 14 x 14 (A/B); bit 5 with it: waves as 2 m-groups x 4
-  // n-groups (two waves load each weight fragment; the second read can hit the CU's vector L1)
-  g_c3f_slice = (pf & 16) ? ((pf & 32) ? 2 : 1) : 0;
-  g_c3f_dma = (pf & 64) ? 1 : 0;   // bit 6: the half-image kernel with its weights by LDS-DMA
-  return 0;
 }
 
 extern "C" int sat_conv3x3_frag_supported(int H, int W, int C, int dtype) {
@@ -1134,24 +824,10 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   const hipStream_t s = (hipStream_t)stream;
   const bf16 *xp = (const bf16*)x, *wp = (const bf16*)wf;
   bf16* yp = (bf16*)y;
-  if (H == 28) {   // layer2 c2: 7-row bands, four workgroups per image
-    if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_band_kernel<3>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp);
-    else hipLaunchKernelGGL(conv3x3_band_kernel<2>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp);
-    return (int)hipGetLastError();
-  }
-  if (g_c3f_dma && !g_c3f_slice) {
-    hipLaunchKernelGGL(conv3x3_frag_dma_kernel, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
-    return (int)hipGetLastError();
-  }
-  if (g_c3f_slice && N % 8 == 0) {   // slice-major grid over groups of 8 images
-    if (g_c3f_slice == 2) hipLaunchKernelGGL((conv3x3_slice_kernel<2, 2>), dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
-    else if (g_c3f_pf == 3) hipLaunchKernelGGL((conv3x3_slice_kernel<1, 3>), dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
-    else hipLaunchKernelGGL((conv3x3_slice_kernel<1, 2>), dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
-    return (int)hipGetLastError();
-  }
-  if (g_c3f_pf == 3) hipLaunchKernelGGL(conv3x3_frag_kernel<3>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
-  else if (g_c3f_pf == 4) hipLaunchKernelGGL(conv3x3_frag_kernel<4>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
-  else hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
+  if (H == 28)   // layer2 c2: 7-row bands, four workgroups per image
+    hipLaunchKernelGGL(conv3x3_band_kernel<2>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp);
+  else           // layer3 c2: half images, two workgroups per image
+    hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
   return (int)hipGetLastError();
 }
 
@@ -1169,31 +845,5 @@ extern "C" int sat_conv1x1_frag(int N, int H, int W, int Cin, int Cout, int dtyp
   SAT_REQUIRE(x_bytes < (1L << 31));
   hipLaunchKernelGGL(conv1x1_frag_kernel, dim3(2 * N), dim3(512), 0, (hipStream_t)stream, (const bf16*)x,
                      (const bf16*)wf, b, (bf16*)y, (unsigned)x_bytes);
-  return (int)hipGetLastError();
-}
-
-static int g_c1r_pf = 2;   // weight prefetch distance of conv1x1_res_frag_kernel (experiment hook)
-
-extern "C" int sat_conv1x1_res_frag_set_experiment(int pf) {
-  if (pf != 2 && pf != 3) return SAT_ERR_INVALID;
-  g_c1r_pf = pf;
-  return 0;
-}
-
-extern "C" int sat_conv1x1_res_frag_supported(int H, int W, int Cin, int Cout, int dtype) {
-  return dtype == SAT_BF16 && H == 14 && W == 14 && Cin == 256 && Cout == 1024;
-}
-
-extern "C" int sat_conv1x1_res_frag(int N, int H, int W, int Cin, int Cout, int dtype, const void* x, const void* wf,
-                                    const float* b, const void* res, void* y, void* stream) {
-  SAT_REQUIRE(N > 0 && x && wf && b && res && y && x != y && res != y);
-  SAT_REQUIRE(sat_conv1x1_res_frag_supported(H, W, Cin, Cout, dtype));
-  auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
-  SAT_REQUIRE(al(x, 16) && al(y, 16) && al(wf, 16) && al(b, 16) && al(res, 16));
-  const hipStream_t s = (hipStream_t)stream;
-  const bf16 *xp = (const bf16*)x, *wp = (const bf16*)wf, *rp = (const bf16*)res;
-  bf16* yp = (bf16*)y;
-  if (g_c1r_pf == 3) hipLaunchKernelGGL(conv1x1_res_frag_kernel<3>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, rp, yp);
-  else hipLaunchKernelGGL(conv1x1_res_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, rp, yp);
   return (int)hipGetLastError();
 }

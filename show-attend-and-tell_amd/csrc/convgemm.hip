@@ -53,7 +53,6 @@ struct FArgs {
   int splitk, kchunk;      // atomic split-K (fp32 C, act NONE): blockIdx.z = split
   int xcd_remap;
   int partial; long split_stride;   // partial-output split-K: split s stores plain into C + s*split_stride
-  unsigned long* trace;    // diagnostics (tools/conv_trace.py): per-workgroup timestamps, or null
   int res_lds;             // fast_gemm_kernel<..., RL = true> epilogue (host-checked shape)
 };
 
@@ -151,8 +150,6 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
   const int m0 = (tile / gridDim.x) * BM, n0 = (tile % gridDim.x) * BN;
   const int M = a.M, N = a.N;
   const int split = blockIdx.z;
-  unsigned long tr_t0 = 0, tr_t1 = 0;
-  if (a.trace) tr_t0 = __builtin_amdgcn_s_memrealtime();
   const int kbeg = split * a.kchunk;
   const int K = min(a.K, kbeg + a.kchunk);
 
@@ -335,7 +332,6 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
   }
   if constexpr (RL) {
     wait_vm_barrier<0>();   // residual landed, every wave done with the ring
-    if (a.trace) tr_t1 = __builtin_amdgcn_s_memrealtime();
     constexpr int ROWB2 = BN * 2, CPR = BN / 8;
     const char* rs = smem + (nk % NS) * STAGE;          // residual tile
     char* os = smem + ((nk + NS - 1) % NS) * STAGE;     // finished bf16 tile
@@ -372,7 +368,6 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
     }
   } else {
   __syncthreads();   // every wave done reading the ring before the epilogue reuses the LDS
-  if (a.trace) tr_t1 = __builtin_amdgcn_s_memrealtime();
 
   if (a.splitk > 1 && !a.partial) {   // atomic split-K: fp32 C, bias in split 0, act NONE (host-checked)
 #pragma unroll
@@ -473,26 +468,11 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
     }
   }
   }   // !RL
-  if (a.trace) {
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned long t2 = __builtin_amdgcn_s_memrealtime();
-      const int lin = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-      unsigned long* rec = a.trace + (long)lin * 4;
-      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
-      const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
-      rec[0] = tr_t0; rec[1] = tr_t1; rec[2] = t2; rec[3] = ((unsigned long)xcc << 32) | hw;
-    }
-  }
 }
 
 __device__ __attribute__((aligned(16))) bf16 g_zero16[64];
 
-// experiment overrides (tools/bench_conv.py): 0 = automatic
-int g_force_stages = 0, g_force_tile = 0, g_xcd_remap = 1, g_res_lds = 2;
-unsigned long* g_trace = nullptr;
-
-// tile configurations (ids of sat_fast_gemm_set_config)
+// tile configurations (ids of SatPolicy::gemm_tile)
 enum { T_AUTO = 0, T128x128W8 = 1, T128x64W8 = 2, T128x128W4 = 3, T128x256W8 = 4, T256x128W8 = 5 };
 inline int tile_bm(int t) { return t == T256x128W8 ? 256 : 128; }
 inline int tile_bn(int t) { return t == T128x64W8 ? 64 : t == T128x256W8 ? 256 : 128; }
@@ -533,6 +513,10 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   *err = 0;
   if (g.dtype != SAT_BF16 || g.batch != 1 || g.aux) return 0;
+  const SatPolicy& pol = sat_policy();
+  const int force_tile = pol.gemm_tile >= T128x128W8 && pol.gemm_tile <= T256x128W8 ? pol.gemm_tile : 0;
+  const int force_stages = pol.gemm_stages == 2 || pol.gemm_stages == 3 ? pol.gemm_stages : 0;
+  const int res_lds = pol.gemm_epilogue == 1 ? 1 : (pol.gemm_epilogue == 2 ? 0 : 2);
   if (!al16(g.B) || !al16(g.A)) return 0;
   const bool conv = g.conv.C > 0;
   const bool at = g.transA != 0, bt = g.transB != 0;
@@ -550,7 +534,7 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   // narrow N tiles: skinny N, partial-split problems, and single-k-tile convs (ResNet152 L1 1x1
   // convs with K = 64: three 128x64 workgroups per CU move their epilogue bytes faster, 111 -> 103 us)
   int tcfg = ((g.N <= 64 || partial || (conv && g.K <= BK)) && !at && !bt) ? T128x64W8 : T128x128W8;
-  if (g_force_tile && !partial) tcfg = g_force_tile;
+  if (force_tile && !partial) tcfg = force_tile;
   if ((at || bt) && tcfg != T128x128W4) tcfg = T128x128W8;
   const int bm = tile_bm(tcfg);
   int bn = tile_bn(tcfg);
@@ -571,7 +555,7 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
     }
     // no split: still the LDS-DMA kernel (the register-staged one is slower per tile); narrow
     // N tiles double the block count of non-transposed problems
-    if (splitk == 1 && !at && !bt && !g_force_tile && tcfg == T128x128W8) {
+    if (splitk == 1 && !at && !bt && !force_tile && tcfg == T128x128W8) {
       tcfg = T128x64W8;
       bn = tile_bn(tcfg);
     }
@@ -619,40 +603,20 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
     a.H = g.conv.H; a.W = g.conv.W; a.Cin = g.conv.C; a.KW = g.conv.KW;
     a.stride = g.conv.stride; a.pad = g.conv.pad; a.OH = g.conv.OH; a.OW = g.conv.OW;
   }
-  a.xcd_remap = g_xcd_remap;
-  a.trace = g_trace;
-  a.res_lds = g_res_lds && (tcfg == T128x128W8 || tcfg == T128x64W8) && !at && !bt && a.splitk == 1 && !partial &&
+  a.xcd_remap = pol.gemm_linear_order ? 0 : 1;
+  a.res_lds = res_lds && (tcfg == T128x128W8 || tcfg == T128x64W8) && !at && !bt && a.splitk == 1 && !partial &&
               a.c_bf16 && (!g.add1 || (a.add1_bf16 && g.ld_add1 % 8 == 0)) && g.N % bn == 0 && g.ldc % 8 == 0 &&
               al16(g.C) &&
-              (g.add1 || g_res_lds > 1) &&
-              (g_force_stages == 0 || g_force_stages == 2);
+              (g.add1 || res_lds > 1) &&
+              (force_stages == 0 || force_stages == 2);
   dim3 grid(sat_cdiv(g.N, bn), sat_cdiv(g.M, bm), a.splitk);
   // skinny partial-split GEMMs run 2-4 k-tiles per block: a 3-deep ring puts the first two in
   // flight at once (their block counts leave LDS occupancy irrelevant)
-  const int ns = g_force_stages ? g_force_stages : (partial ? 3 : 2);
+  const int ns = force_stages ? force_stages : (partial ? 3 : 2);
   if (at && bt) launch_tile<true, true>(tcfg, ns, grid, s, a);
   else if (at) launch_tile<true, false>(tcfg, ns, grid, s, a);
   else if (bt) launch_tile<false, true>(tcfg, ns, grid, s, a);
   else launch_tile<false, false>(tcfg, ns, grid, s, a);
   *err = (int)hipGetLastError();
   return 1;
-}
-
-extern "C" int sat_fast_gemm_set_res_lds(int on) {
-  g_res_lds = on < 0 ? 0 : on;   // 1: residual epilogues, 2: also plain bf16 epilogues
-  return 0;
-}
-
-// diagnostics: per-workgroup [start, main loop done, end, hw id] records (4 x u64, 100 MHz clock)
-extern "C" int sat_fast_gemm_set_trace(void* buf) {
-  g_trace = (unsigned long*)buf;
-  return 0;
-}
-
-extern "C" int sat_fast_gemm_set_config(int stages, int tile, int xcd_remap) {
-  if (stages < 0 || stages > 3 || stages == 1 || tile < 0 || tile > T256x128W8) return SAT_ERR_INVALID;
-  g_force_stages = stages;
-  g_force_tile = tile;
-  g_xcd_remap = xcd_remap != 0;
-  return 0;
 }

@@ -324,35 +324,16 @@ __global__ __launch_bounds__(NW * 64) void conv_pipe_kernel(PArgs a) {
 
 __device__ __attribute__((aligned(16))) bf16 g_pipe_zero16[64];
 
-// 0: off, 1: automatic (shape heuristic), 2: every eligible problem (A/B experiments)
-int g_pipe_mode = 1;
-int g_pipe_waves = 8;     // experiment: 8 | 4 waves per workgroup
-int g_pipe_ablate = 0;    // diagnostics: ABL bits (conv, ReLU, no residual only)
-int g_pipe_buf = 1;       // experiment: 1 = buffer-resource LDS-DMA, 0 = global_load_lds
-int g_pipe_var = 2;       // DMA placement bits (PArgs::var); 2 = A before / B after the first MFMA half
+// DMA placement (PArgs::var): A before / B after the first MFMA half (measured best of the variants)
+constexpr int kPipeVar = 2;
 
 template <int NW, int AM, bool RES>
 void launch_act(int act, dim3 grid, hipStream_t s, const PArgs& a) {
-  if (!g_pipe_buf) {
-    if (act == SAT_ACT_RELU) hipLaunchKernelGGL((conv_pipe_kernel<NW, AM, SAT_ACT_RELU, RES, 0, false>), grid, dim3(NW * 64), 0, s, a);
-    else hipLaunchKernelGGL((conv_pipe_kernel<NW, AM, SAT_ACT_NONE, RES, 0, false>), grid, dim3(NW * 64), 0, s, a);
-    return;
-  }
   if (act == SAT_ACT_RELU) hipLaunchKernelGGL((conv_pipe_kernel<NW, AM, SAT_ACT_RELU, RES, 0, true>), grid, dim3(NW * 64), 0, s, a);
   else hipLaunchKernelGGL((conv_pipe_kernel<NW, AM, SAT_ACT_NONE, RES, 0, true>), grid, dim3(NW * 64), 0, s, a);
 }
 template <int NW>
 void launch_nw(bool conv, bool res, int act, dim3 grid, hipStream_t s, const PArgs& a) {
-  if (conv && !res && act == SAT_ACT_RELU && g_pipe_ablate) {
-    switch (g_pipe_ablate) {
-      case 1: hipLaunchKernelGGL((conv_pipe_kernel<NW, 1, SAT_ACT_RELU, false, 1, true>), grid, dim3(NW * 64), 0, s, a); return;
-      case 2: hipLaunchKernelGGL((conv_pipe_kernel<NW, 1, SAT_ACT_RELU, false, 2, true>), grid, dim3(NW * 64), 0, s, a); return;
-      case 3: hipLaunchKernelGGL((conv_pipe_kernel<NW, 1, SAT_ACT_RELU, false, 3, true>), grid, dim3(NW * 64), 0, s, a); return;
-      case 4: hipLaunchKernelGGL((conv_pipe_kernel<NW, 1, SAT_ACT_RELU, false, 4, true>), grid, dim3(NW * 64), 0, s, a); return;
-      case 6: hipLaunchKernelGGL((conv_pipe_kernel<NW, 1, SAT_ACT_RELU, false, 6, true>), grid, dim3(NW * 64), 0, s, a); return;
-      default: break;
-    }
-  }
   if (conv) {
     if (res) launch_act<NW, 1, true>(act, grid, s, a);
     else launch_act<NW, 1, false>(act, grid, s, a);
@@ -369,7 +350,8 @@ inline bool pal16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // Returns 1 if the problem was launched by the pipelined kernel (error code in *err), 0 otherwise.
 int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err) {
   *err = 0;
-  if (g_pipe_mode == 0) return 0;
+  const int mode = sat_policy().conv_pipe;   // 0 auto, 1 off, 2 every eligible problem
+  if (mode == 1) return 0;
   if (g.dtype != SAT_BF16 || g.c_dtype != SAT_BF16 || g.batch != 1 || g.aux || g.transA || g.transB) return 0;
   if (g.beta != 0.f || g.alpha != 1.f || g.partial_splits > 1) return 0;
   if (g.act != SAT_ACT_NONE && g.act != SAT_ACT_RELU) return 0;
@@ -385,7 +367,7 @@ int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err) {
   }
   if ((long)g.N * g.ldb >= (1L << 31)) return 0;
   const long tiles = (long)sat_cdiv(g.M, PBM) * sat_cdiv(g.N, PBN);
-  if (g_pipe_mode == 1) {
+  if (mode == 0) {
     // long-K problems that fill most of the chip with 256 x 128 tiles (tools/pipe_ab.py: ResNet152
     // L3 c1/c2, L2 c2, L4, every VGG19 conv from 128 channels on: 1.05-1.26x); short-K problems,
     // N < 128 and the residual 1x1 convs stay on fast_gemm_kernel (two workgroups per CU)
@@ -412,7 +394,7 @@ int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err) {
   a.zero16 = zero;
   a.tiles_n = sat_cdiv(g.N, PBN);
   a.xcd_remap = 1;
-  a.var = g_pipe_var;
+  a.var = kPipeVar;
   {
     const long a_bytes = conv ? 2L * g.conv.N * g.conv.H * g.conv.W * g.conv.C : 2L * ((long)(g.M - 1) * g.lda + g.K);
     const long b_bytes = 2L * ((long)(g.N - 1) * g.ldb + g.K);
@@ -421,24 +403,7 @@ int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err) {
     a.b_bytes = (unsigned)b_bytes;
   }
   const dim3 grid((unsigned)tiles);
-  if (g_pipe_waves == 4) launch_nw<4>(conv, g.add1 != nullptr, g.act, grid, s, a);
-  else launch_nw<8>(conv, g.add1 != nullptr, g.act, grid, s, a);
+  launch_nw<8>(conv, g.add1 != nullptr, g.act, grid, s, a);
   *err = (int)hipGetLastError();
   return 1;
-}
-
-extern "C" int sat_conv_pipe_set_mode(int mode) {
-  if (mode < 0 || mode > 2) return SAT_ERR_INVALID;
-  g_pipe_mode = mode;
-  return 0;
-}
-
-// experiment hook (tools/pipe_ab.py): waves per workgroup (8 | 4) and ablation bits
-extern "C" int sat_conv_pipe_set_experiment(int waves, int ablate) {
-  if ((waves != 4 && waves != 8) || ablate < 0 || ablate > 255) return SAT_ERR_INVALID;
-  g_pipe_waves = waves;
-  g_pipe_ablate = ablate & 7;     // bits 0-2: ablation
-  g_pipe_buf = !(ablate & 8);     // bit 3: global_load_lds instead of buffer LDS-DMA
-  g_pipe_var = (ablate >> 4) & 7; // bits 4-6: DMA placement variant
-  return 0;
 }

@@ -48,7 +48,6 @@ struct SArgs {
   int slices, per_slice, items;      // N / 128, workgroups per slice, M-tiles
   int xcd_group;                     // 1: slice = (b / 8) % slices (one M-tile sequence per XCD)
   unsigned a_bytes;
-  int abl;                           // diagnostics (tools/pipe_ab.py): 1 no MFMA, 2 no stores, 4 no A DMA
 };
 
 template <int N>
@@ -148,7 +147,6 @@ __global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
         }
         off = (unsigned)((pix * K + 8 * c) * 2);
       }
-      if (a.abl & 4) off = S_OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (s_lds_void*)(st + (d * S_NW + w) * 1024), 16, (int)off, 0, 0, 0);
     }
     if constexpr (RES) {   // residual rows of this slice's columns, 16-B chunk c at slot c ^ (r & 15) in 256-B groups
@@ -204,16 +202,11 @@ __global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) af[(ks + 1) & 1][mb] = afrag(base, mb, ks + 1);
       }
-      if (a.abl & 1) {
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) asm volatile("" ::"v"(af[ks & 1][mb]));
-      } else {
+      for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-          for (int nb = 0; nb < NB; ++nb)
-            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks][nb], af[ks & 1][mb], acc[mb][nb], 0, 0, 0);
-      }
+        for (int nb = 0; nb < NB; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks][nb], af[ks & 1][mb], acc[mb][nb], 0, 0, 0);
     }
     // epilogue: lane holds C[m0 + mb*16 + fr][ns + wc + nb*16 + 4 fh + j], j = 0..3.  bias, the residual
     // (from the stage's R/O tile), activation, one bf16 rounding; the 8 result bytes go back to the
@@ -251,7 +244,7 @@ __global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
       const int pc = (lc & ~15) | ((lc & 15) ^ (r & 15));
       const uint4 u = *(const uint4*)(ro + r * RROWB + 16 * pc);
       const int m = it * MT + r;
-      const unsigned off = (m < a.M && !(a.abl & 2)) ? (unsigned)(((long)m * a.N + ns + 8 * lc) * 2) : S_OOB;
+      const unsigned off = m < a.M ? (unsigned)(((long)m * a.N + ns + 8 * lc) * 2) : S_OOB;
       typedef unsigned __attribute__((ext_vector_type(4))) u32x4;
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rC, (int)off, 0, 0);
     }
@@ -261,8 +254,6 @@ __global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
   }
 }
 
-int g_stream_mode = 1;   // 0 off, 1 auto, 2 every eligible problem (A/B)
-int g_stream_abl = 0;    // diagnostics: SArgs::abl
 int g_stream_cus = 0;    // CU count (queried once)
 
 template <int KT, int MB, int NB, bool RES, bool STRIDED>
@@ -290,7 +281,8 @@ inline bool sal16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // Returns 1 if the 1x1 conv was launched by the streaming kernel (error code in *err), 0 otherwise.
 int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err) {
   *err = 0;
-  if (g_stream_mode == 0) return 0;
+  const int mode = sat_policy().conv_stream;   // 0 auto, 1 off, 2 every eligible problem
+  if (mode == 1) return 0;
   const SatConvGeom& cv = g.conv;
   if (cv.C <= 0 || cv.KH != 1 || cv.KW != 1 || cv.pad != 0) return 0;
   if (g.dtype != SAT_BF16 || g.c_dtype != SAT_BF16 || g.batch != 1 || g.aux || g.transB) return 0;
@@ -317,7 +309,7 @@ int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err) {
   const int MT = MB * 16;
   const int slices = g.N / (S_BN * NB);
   const int items = sat_cdiv(g.M, MT);
-  if (g_stream_mode == 1) {
+  if (mode == 0) {
     // HBM-bound shapes only: enough items per workgroup to pipeline (>= ~3)
     if ((long)items * slices < 2L * g_stream_cus) return 0;
   }
@@ -335,7 +327,6 @@ int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err) {
   a.slices = slices; a.per_slice = per_slice; a.items = items;
   a.xcd_group = (per_slice * slices) % (8 * slices) == 0 && per_slice % 8 == 0;
   a.a_bytes = (unsigned)a_bytes;
-  a.abl = g_stream_abl;
   const dim3 grid(per_slice * slices);
   const bool res = g.add1 != nullptr;
   if (NB == 2) {
@@ -355,11 +346,4 @@ int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err) {
   }
   *err = (int)hipGetLastError();
   return 1;
-}
-
-extern "C" int sat_conv_stream_set_mode(int mode) {
-  if (mode < 0 || mode > 2 + 4 * 7) return SAT_ERR_INVALID;
-  g_stream_mode = mode & 3;
-  g_stream_abl = mode >> 2;   // diagnostics: ablation bits in mode bits 2-4 (tools/pipe_ab.py)
-  return 0;
 }

@@ -33,7 +33,7 @@ struct WS {
   // backward
   void *dpre_t, *dfh_t, *dfz_t, *dhg_t, *dWs_t, *dpre0_t;
   float *dcomb, *dhd, *dctx_head, *dhg, *dgated, *dh_rec, *dc, *dWs_acc, *dv_acc, *dbv_acc, *part, *demb, *dpre0,
-      *colsum, *colsum2, *de_all;
+      *colsum, *de_all;
 };
 
 // split counts of the per-step skinny GEMMs (M = B rows).  bf16: the LDS-DMA kernel (128 x 64
@@ -45,8 +45,8 @@ struct Splits { int h, c, g, dh, i; };
 // Workgroups the split-K of one per-step GEMM aims for: 192 when the decoder has the chip to
 // itself; 64 when it shares it with the next batch's encoder (bench.py / train.py overlap): fewer,
 // longer workgroups cost the concurrent conv trunk less (overlapped step 8.23 -> 8.07 ms; alone the
-// decoder prefers 192: 10.24 vs 10.48 ms sequential).  sat_decoder_set_split_target.
-int g_split_target = 192;
+// decoder prefers 192: 10.24 vs 10.48 ms sequential).  SatDecoderDims::split_target, 0 = 192.
+constexpr int kSplitTargetDefault = 192;
 
 inline int pick_splits(int M, int N, int K, int dtype, bool kmajor_w, int target) {
   if (dtype != SAT_BF16 || K % 64) return 1;
@@ -59,12 +59,11 @@ inline int pick_splits(int M, int N, int K, int dtype, bool kmajor_w, int target
     if (kt % s == 0) best = s;
   return best;
 }
-Splits g_force_splits{0, 0, 0, 0, 0};   // tuning override (sat_decoder_set_splits), 0 = automatic
 inline int forced(int f, int K, int auto_s) { return (f > 0 && K % 64 == 0 && (K / 64) % f == 0) ? f : auto_s; }
 inline Splits splits_for(const SatDecoderDims& d) {
   const int E = d.E, D = d.D, HG = 5 * E + D;
   const bool bf = d.dtype == SAT_BF16;
-  const int tg = d.split_target > 0 ? d.split_target : g_split_target;
+  const int tg = d.split_target > 0 ? d.split_target : kSplitTargetDefault;
   Splits s;
   s.h = pick_splits(d.B, d.attention ? HG : 4 * E, E, d.dtype, false, tg);
   s.c = pick_splits(d.B, 4 * E, D, d.dtype, false, tg);
@@ -77,11 +76,12 @@ inline Splits splits_for(const SatDecoderDims& d) {
     if ((k = sat_skinny_splits(d.B, 4 * E, D))) s.c = k;
     if ((k = sat_skinny_splits(d.B, 2 * E, D))) s.i = k;
   }
-  if (bf) {
-    s.h = forced(g_force_splits.h, E, s.h);
-    s.c = forced(g_force_splits.c, D, s.c);
-    s.g = forced(g_force_splits.g, 4 * E, s.g);
-    s.dh = forced(g_force_splits.dh, d.attention ? HG : 4 * E, s.dh);
+  if (bf) {   // per-call overrides (SatPolicy::decoder_splits, 0 = automatic)
+    const int* f = sat_policy().decoder_splits;
+    s.h = forced(f[0], E, s.h);
+    s.c = forced(f[1], D, s.c);
+    s.g = forced(f[2], 4 * E, s.g);
+    s.dh = forced(f[3], d.attention ? HG : 4 * E, s.dh);
   }
   return s;
 }
@@ -145,7 +145,6 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   size_t maxN = V > HG ? V : HG;
   if (D > maxN) maxN = D;
   c.take(w->colsum, sat_colsum_scratch_floats((int)R, (int)maxN) * f);
-  c.take(w->colsum2, sat_colsum_scratch_floats((int)R, (int)maxN) * f);   // the side stream's column sums
   return c.off + 256;
 }
 
@@ -405,28 +404,18 @@ int check_dims(const SatDecoderDims* d) {
   if (d->dtype != SAT_F32 && d->dtype != SAT_BF16) return SAT_ERR_INVALID;
   if (d->E % 8 != 0 || d->D % 8 != 0 || d->E > 1024 || d->L > 1024) return SAT_ERR_INVALID;
   if (d->split_target < 0 || d->split_target > 4096) return SAT_ERR_INVALID;
+  if (d->policy) {
+    for (int i = 0; i < 4; ++i)
+      if (d->policy->decoder_splits[i] < 0 || d->policy->decoder_splits[i] > 64) return SAT_ERR_INVALID;
+  }
   return 0;
 }
 
 }  // namespace
 
-// tuning hook: split-K counts of the per-step bf16 GEMMs (h: [U;f_beta;W_hh] h, c: context gate
-// GEMM, g: dL/d gated context, dh: recurrent dL/dh); 0 = automatic.  Set before the workspace query.
-extern "C" int sat_decoder_set_splits(int h, int c, int g, int dh) {
-  if (h < 0 || c < 0 || g < 0 || dh < 0 || h > 64 || c > 64 || g > 64 || dh > 64) return SAT_ERR_INVALID;
-  g_force_splits = Splits{h, c, g, dh, 0};
-  return 0;
-}
-
-// workgroup target of the automatic per-step split-K (0 = default 192); set before any workspace query
-extern "C" int sat_decoder_set_split_target(int workgroups) {
-  if (workgroups < 0 || workgroups > 4096) return SAT_ERR_INVALID;
-  g_split_target = workgroups ? workgroups : 192;
-  return 0;
-}
-
 extern "C" size_t sat_decoder_workspace_bytes(const SatDecoderDims* d) {
   if (check_dims(d)) return 0;
+  SatPolicyScope scope(d->policy);
   WS w;
   return carve(*d, nullptr, &w);
 }
@@ -439,6 +428,7 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
   SAT_REQUIRE(lay && params && img_features && captions && workspace && preds && alphas);
   SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
   SAT_REQUIRE(!(dp->training && dp->has_dropout_mask) || dropout_mask);
+  SatPolicyScope scope(dp->policy);
   const SatDecoderDims& d = *dp;
   WS w;
   SAT_REQUIRE(carve(d, nullptr, &w) <= workspace_bytes);
@@ -516,28 +506,6 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
   return 0;
 }
 
-namespace {
-
-// Side stream for the output head's weight gradients (phase bit 8): one per host thread, created on
-// first use; the fork / join events are per call site and thread as well, so concurrent decoders on
-// different host threads never share them.  Inside stream capture the event record / wait pairs
-// become graph edges (fork after the head's d logits, join before the call returns).
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork0 = nullptr, fork1 = nullptr, join = nullptr;
-  int init() {
-    if (s) return 0;
-    SAT_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    SAT_CHECK(hipEventCreateWithFlags(&fork0, hipEventDisableTiming));
-    SAT_CHECK(hipEventCreateWithFlags(&fork1, hipEventDisableTiming));
-    SAT_CHECK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
-    return 0;
-  }
-};
-thread_local SideStream t_side;
-
-}  // namespace
-
 extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLayout* lay, const float* params,
                                     const void* params_lp, const void* img_features, void* workspace,
                                     size_t workspace_bytes, const void* preds, const float* alphas,
@@ -545,14 +513,10 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
                                     int phase, void* stream) {
   SAT_CHECK((hipError_t)check_dims(dp));
   SAT_REQUIRE(lay && params && img_features && workspace && preds && alphas && d_preds && d_alphas && grads);
-  // bit 4: d_preds already ReLU-masked; bit 8 (with bits 1 and 2): the head's weight gradients on a
-  // side stream beside the BPTT loop, joined before returning
-  // bit 16 (with bit 2): the weight gradients after BPTT in two branches -- attention and init-state
-  // gradients on the side stream beside the LSTM-weight and embedding gradients -- joined before returning
-  SAT_REQUIRE((phase & 3) != 0 && phase >= 1 && phase <= 31);
-  SAT_REQUIRE(!(phase & 8) || (phase & 3) == 3);
-  SAT_REQUIRE(!(phase & 16) || (phase & 2));
+  // bit 4: d_preds already ReLU-masked (sat_caption_loss_backward_relu)
+  SAT_REQUIRE((phase & 3) != 0 && phase >= 1 && phase <= 7);
   SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
+  SatPolicyScope scope(dp->policy);
   const SatDecoderDims& d = *dp;
   WS w;
   SAT_REQUIRE(carve(d, nullptr, &w) <= workspace_bytes);
@@ -585,29 +549,6 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   auto colsum = [&](const void* X, int dt, long ld, int rows, int N, float* out, float* out2 = nullptr) {
     return sat_colsum(X, dt, ld, rows, N, out, accumulate, out2, w.colsum, s);
   };
-  // head weight gradients: on the side stream (phase bit 8) or in order on s
-  const bool side = (phase & 8) != 0, tail = (phase & 16) != 0;
-  if (side || tail) SAT_CHECK((hipError_t)t_side.init());
-  hipStream_t hs = side ? t_side.s : s;
-  auto wgrad_h = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo,
-                     int a_tail = 0) {
-    SatGemm g;
-    g.a_tail = a_tail;
-    g.M = M; g.N = N; g.K = K; g.dtype = d.dtype;
-    g.A = X; g.lda = ldx; g.transA = 1;
-    g.B = Y; g.ldb = ldy; g.transB = 1;
-    g.C = out; g.ldc = ldo; g.c_dtype = SAT_F32; g.beta = beta;
-    return sat_gemm_launch(g, hs);
-  };
-  auto colsum_h = [&](const void* X, int dt, long ld, int rows, int N, float* out) {
-    return sat_colsum(X, dt, ld, rows, N, out, accumulate, nullptr, side ? w.colsum2 : w.colsum, hs);
-  };
-  auto fork = [&](hipEvent_t e) -> int {   // the side stream continues after everything issued on s so far
-    if (!side) return 0;
-    SAT_CHECK(hipEventRecord(e, s));
-    SAT_CHECK(hipStreamWaitEvent(hs, e, 0));
-    return 0;
-  };
 
   if (phase & 1) {  // ---------------- output head (decoder.py:117-125,149-158) ----------------
     if (d.ado) {
@@ -622,17 +563,15 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
         SAT_CHECK((hipError_t)sat_relu_mask_mul(d_preds, preds, (long)R * V, d.dtype, w.dpre_t, s));
         dpre = w.dpre_t;
       }
-      SAT_CHECK((hipError_t)fork(t_side.fork0));
-      SAT_CHECK((hipError_t)wgrad_h(V, E, R, dpre, ldp, w.comb_t, E, G(lay->fout_w), E, VP != V));
-      SAT_CHECK((hipError_t)colsum_h(dpre, d.dtype, ldp, R, V, G(lay->fout_b)));
+      SAT_CHECK((hipError_t)wgrad(V, E, R, dpre, ldp, w.comb_t, E, G(lay->fout_w), E, VP != V));
+      SAT_CHECK((hipError_t)colsum(dpre, d.dtype, ldp, R, V, G(lay->fout_b)));
       SAT_CHECK((hipError_t)dgrad_launch(c, R, E, V, dpre, ldp, c.W(lay->fout_w), E, w.dcomb, E, s, nullptr, 0, 0, 0,
                                          VP != V));
       SAT_CHECK((hipError_t)sat_ado_bwd_split(w.dcomb, w.fh, w.fz, (long)R * E, d.dtype, w.dfh_t, w.dfz_t, s));
-      SAT_CHECK((hipError_t)fork(t_side.fork1));
-      SAT_CHECK((hipError_t)wgrad_h(E, E, R, w.dfh_t, E, w.hd_t, E, G(lay->fh_w), E));
-      SAT_CHECK((hipError_t)colsum_h(w.dfh_t, d.dtype, E, R, E, G(lay->fh_b)));
-      SAT_CHECK((hipError_t)wgrad_h(E, D, R, w.dfz_t, E, w.ctx_t, D, G(lay->fz_w), D));
-      SAT_CHECK((hipError_t)colsum_h(w.dfz_t, d.dtype, E, R, E, G(lay->fz_b)));
+      SAT_CHECK((hipError_t)wgrad(E, E, R, w.dfh_t, E, w.hd_t, E, G(lay->fh_w), E));
+      SAT_CHECK((hipError_t)colsum(w.dfh_t, d.dtype, E, R, E, G(lay->fh_b)));
+      SAT_CHECK((hipError_t)wgrad(E, D, R, w.dfz_t, E, w.ctx_t, D, G(lay->fz_w), D));
+      SAT_CHECK((hipError_t)colsum(w.dfz_t, d.dtype, E, R, E, G(lay->fz_b)));
       SAT_CHECK((hipError_t)dgrad(R, E, E, w.dfh_t, E, c.W(lay->fh_w), E, w.dhd, E));
       if (att) SAT_CHECK((hipError_t)dgrad(R, D, E, w.dfz_t, E, c.W(lay->fz_w), D, w.dctx_head, D));
     } else {
@@ -642,9 +581,8 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
         SAT_CHECK((hipError_t)sat_pad_rows(d_preds, nullptr, R, V, VP, d.dtype, w.dpre_t, s));
         dpre = w.dpre_t; ldp = VP;
       }
-      SAT_CHECK((hipError_t)fork(t_side.fork0));
-      SAT_CHECK((hipError_t)wgrad_h(V, E, R, dpre, ldp, w.hd_t, E, G(lay->do_w), E, VP != V));
-      SAT_CHECK((hipError_t)colsum_h(d_preds, d.dtype, V, R, V, G(lay->do_b)));
+      SAT_CHECK((hipError_t)wgrad(V, E, R, dpre, ldp, w.hd_t, E, G(lay->do_w), E, VP != V));
+      SAT_CHECK((hipError_t)colsum(d_preds, d.dtype, V, R, V, G(lay->do_b)));
       SAT_CHECK((hipError_t)dgrad_launch(c, R, E, V, dpre, ldp, c.W(lay->do_w), E, w.dhd, E, s, nullptr, 0, 0, 0,
                                          VP != V));
     }
@@ -667,37 +605,19 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   }
 
   // ---------------- weight gradients, batched over all B*(T-1) rows ----------------
-  // tail branch (bit 16): attention + init-state gradients on the side stream (its own column-sum
-  // scratch), issued after everything BPTT wrote
-  hipStream_t ts = tail ? t_side.s : s;
-  if (tail) {
-    SAT_CHECK(hipEventRecord(t_side.fork1, s));
-    SAT_CHECK(hipStreamWaitEvent(ts, t_side.fork1, 0));
-  }
-  auto wgrad_t = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo) {
-    SatGemm g;
-    g.M = M; g.N = N; g.K = K; g.dtype = d.dtype;
-    g.A = X; g.lda = ldx; g.transA = 1;
-    g.B = Y; g.ldb = ldy; g.transB = 1;
-    g.C = out; g.ldc = ldo; g.c_dtype = SAT_F32; g.beta = beta;
-    return sat_gemm_launch(g, ts);
-  };
-  auto colsum_t = [&](const void* X, int dt, long ld, int rows, int N, float* out) {
-    return sat_colsum(X, dt, ld, rows, N, out, accumulate, nullptr, tail ? w.colsum2 : w.colsum, ts);
-  };
   if (att) {
     SAT_CHECK((hipError_t)sat_attention_dws_launch(w.Ws, w.uh_all, w.de_all, c.F(lay->v_w), B, L, E, T1, d.dtype,
-                                                   w.dWs_acc, w.dWs_t, ts));
-    SAT_CHECK((hipError_t)wgrad_t(E, D, B * L, w.dWs_t, E, img_features, D, G(lay->attW_w), D));
-    SAT_CHECK((hipError_t)colsum_t(w.dWs_acc, SAT_F32, E, B * L, E, G(lay->attW_b)));
-    SAT_CHECK((hipError_t)colsum_t(w.dv_acc, SAT_F32, E, B, E, G(lay->v_w)));
-    SAT_CHECK((hipError_t)colsum_t(w.dbv_acc, SAT_F32, 1, B, 1, G(lay->v_b)));
+                                                   w.dWs_acc, w.dWs_t, s));
+    SAT_CHECK((hipError_t)wgrad(E, D, B * L, w.dWs_t, E, img_features, D, G(lay->attW_w), D));
+    SAT_CHECK((hipError_t)colsum(w.dWs_acc, SAT_F32, E, B * L, E, G(lay->attW_b)));
+    SAT_CHECK((hipError_t)colsum(w.dv_acc, SAT_F32, E, B, E, G(lay->v_w)));
+    SAT_CHECK((hipError_t)colsum(w.dbv_acc, SAT_F32, 1, B, 1, G(lay->v_b)));
   }
   // init_h / init_c (decoder.py:137-147): dh0 = dh_rec, dc0 = dc after the t = 0 step
   SAT_CHECK((hipError_t)sat_tanh_pair_bwd(w.dh_rec, sp.dh, (long)B * E, w.dc, w.hc0, B, E, w.dpre0, w.dpre0_t,
-                                          d.dtype, ts));
-  SAT_CHECK((hipError_t)wgrad_t(2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D));
-  SAT_CHECK((hipError_t)colsum_t(w.dpre0, SAT_F32, 2 * E, B, 2 * E, G(lay->init_b)));
+                                          d.dtype, s));
+  SAT_CHECK((hipError_t)wgrad(2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D));
+  SAT_CHECK((hipError_t)colsum(w.dpre0, SAT_F32, 2 * E, B, 2 * E, G(lay->init_b)));
 
   const void* dg_t = c.at(w.dhg_t, E + D);   // d gates rows (ld HG)
   const float* dg_f = w.dhg + E + D;
@@ -716,10 +636,6 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
     if (!accumulate) SAT_CHECK((hipError_t)sat_zero_rows(G(lay->embedding), (long)V * E, 1, (long)V * E, s));
     SAT_CHECK((hipError_t)sat_embed_scatter_add(w.demb, w.tok, R, E, G(lay->embedding), s));
   }
-  if (side || tail) {   // join: s continues only after the side stream's weight gradients
-    SAT_CHECK(hipEventRecord(t_side.join, t_side.s));
-    SAT_CHECK(hipStreamWaitEvent(s, t_side.join, 0));
-  }
   return 0;
 }
 
@@ -736,6 +652,7 @@ extern "C" int sat_decoder_step_bench(const SatDecoderDims* dp, const SatDecoder
   SAT_CHECK((hipError_t)check_dims(dp));
   SAT_REQUIRE(lay && params && img_features && workspace && alphas && d_alphas && us_out && reps > 0);
   SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
+  SatPolicyScope scope(dp->policy);
   const SatDecoderDims& d = *dp;
   WS w;
   SAT_REQUIRE(carve(d, nullptr, &w) <= workspace_bytes);

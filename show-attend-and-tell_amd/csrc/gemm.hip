@@ -358,7 +358,6 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s) {
     if (sat_skinny_try(g, s, &err)) return err;
     if (sat_conv3x3_ws_try(g, s, &err)) return err;
     if (sat_conv_stream_try(g, s, &err)) return err;
-    if (sat_conv_halo_try(g, s, &err)) return err;
     if (sat_conv_pipe_try(g, s, &err)) return err;
     if (sat_fast_gemm_try(g, s, &err)) return err;
   }
@@ -419,8 +418,18 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s) {
   return launch_t<float>(k, amode, g.transB, g.batch, s);
 }
 
+namespace {
+thread_local const SatPolicy* t_policy = nullptr;
+const SatPolicy k_default_policy{};
+}  // namespace
+
+const SatPolicy& sat_policy() { return t_policy ? *t_policy : k_default_policy; }
+SatPolicyScope::SatPolicyScope(const SatPolicy* p) : prev(t_policy) { t_policy = p; }
+SatPolicyScope::~SatPolicyScope() { t_policy = prev; }
+
 extern "C" int sat_gemm(const SatGemmArgs* a, void* stream) {
   SAT_REQUIRE(a != nullptr);
+  SatPolicyScope scope(a->policy);
   SatGemm g;
   g.M = a->M; g.N = a->N; g.K = a->K; g.dtype = a->dtype;
   g.A = a->A; g.lda = a->lda; g.transA = a->transA;
@@ -433,8 +442,10 @@ extern "C" int sat_gemm(const SatGemmArgs* a, void* stream) {
 }
 
 extern "C" int sat_conv2d_nhwc(const SatConvGeom* cg, int Cout, int dtype, const void* x, const void* w,
-                               const float* bias, const void* residual, int relu, void* y, void* stream) {
+                               const float* bias, const void* residual, int relu, void* y, const SatPolicy* policy,
+                               void* stream) {
   SAT_REQUIRE(cg != nullptr && x && w && y && Cout > 0);
+  SatPolicyScope scope(policy);
   SatGemm g;
   g.conv = *cg;
   g.M = cg->N * cg->OH * cg->OW;

@@ -303,6 +303,18 @@ extern "C" size_t sat_images_workspace_bytes(int B, int OH, int OW) {
 
 extern "C" int sat_images_max_downscale(void) { return (KMAX - 1) / 2; }
 
+namespace {
+// A resample / coefficient kernel that hit an unreachable-for-validated-sizes limit sets ws[0] and
+// leaves its tile unwritten: turn the whole batch into NaN so the failure shows in the encoder output
+// and the loss instead of passing uninitialised memory on (reads one int when all is well).
+template <typename T>
+__global__ void poison_on_error_kernel(const int* __restrict__ ws, T* __restrict__ out, long n) {
+  if (ws[0] == 0) return;
+  const T nan = (T)__builtin_nanf("");
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) out[i] = nan;
+}
+}  // namespace
+
 extern "C" int sat_images_to_input(const uint8_t* pixels, const int64_t* offsets, const int32_t* sizes, int B,
                                    int max_h, int max_w, int OH, int OW, const float* mean, const float* stdv,
                                    int layout, int c_pad, int dtype, void* out, void* workspace,
@@ -332,5 +344,12 @@ extern "C" int sat_images_to_input(const uint8_t* pixels, const int64_t* offsets
     launch_resample<SAT_IMG_S2D16, bf16>(pixels, offsets, sizes, B, max_h, max_w, OH, OW, 16, mean, stdv, ws, out, s);
   else
     launch_resample<SAT_IMG_S2D16, float>(pixels, offsets, sizes, B, max_h, max_w, OH, OW, 16, mean, stdv, ws, out, s);
+  SAT_CHECK(hipGetLastError());
+  const long n = layout == SAT_IMG_NCHW ? (long)B * 3 * OH * OW
+                 : layout == SAT_IMG_NHWC ? (long)B * OH * OW * c_pad : (long)B * (OH / 2) * (OW / 2) * 16;
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(poison_on_error_kernel<bf16>, dim3(256), dim3(256), 0, s, ws, (bf16*)out, n);
+  else
+    hipLaunchKernelGGL(poison_on_error_kernel<float>, dim3(256), dim3(256), 0, s, ws, (float*)out, n);
   return (int)hipGetLastError();
 }

@@ -24,6 +24,19 @@ typedef __bf16 bf16;
 
 static inline int sat_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// ---- per-call kernel selection (SatPolicy, include/sat_hip.h) ----------------
+// Every C-ABI entry point that dispatches among kernels installs its caller's policy for the duration
+// of the call (SatPolicyScope); the dispatchers below it read sat_policy().  The state is per host
+// thread and restored when the call returns, so it never outlives the call that set it.
+const SatPolicy& sat_policy();
+struct SatPolicyScope {
+  const SatPolicy* prev;
+  explicit SatPolicyScope(const SatPolicy* p);
+  ~SatPolicyScope();
+  SatPolicyScope(const SatPolicyScope&) = delete;
+  SatPolicyScope& operator=(const SatPolicyScope&) = delete;
+};
+
 // ---- scalar load/store helpers for the two storage dtypes -------------------
 __device__ __forceinline__ float ld_as_f32(const void* p, long i, int dt) {
   return dt == SAT_BF16 ? (float)((const bf16*)p)[i] : ((const float*)p)[i];
@@ -90,8 +103,6 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err);
 int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err);
 // weight-stationary streaming kernel for K <= 512 1x1 convs (convstream.hip); returns 1 when it launched.
 int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err);
-// 3x3 / stride 1 convs with a per-channel-chunk input halo (convhalo.hip); returns 1 when it launched.
-int sat_conv_halo_try(const SatGemm& g, hipStream_t s, int* err);
 // register-direct skinny GEMM (M <= 128, NT, fp32 / partial-slab output: the decoder's per-step
 // products, skinny.hip); returns 1 when it launched.
 int sat_skinny_try(const SatGemm& g, hipStream_t s, int* err);

@@ -117,19 +117,18 @@ void launch_mb(int nw, dim3 grid, hipStream_t st, const SkArgs& a) {
   else hipLaunchKernelGGL((skinny_gemm_kernel<MB, 4>), grid, dim3(256), 0, st, a);
 }
 
-int g_skinny_mode = 1;   // 0 off (A/B), 1 the decoder's K/256-split products, 2 every eligible problem
-
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
 
 int sat_skinny_try(const SatGemm& g, hipStream_t st, int* err) {
   *err = 0;
-  if (!g_skinny_mode) return 0;
-  // mode 1: only products the decoder split for this kernel (partial_splits == K / 256, the context
+  const int mode = sat_policy().skinny;   // 0 the decoder's K/256-split products, 1 off, 2 every eligible
+  if (mode == 1) return 0;
+  // mode 0: only products the decoder split for this kernel (partial_splits == K / 256, the context
   // GEMM: 9.2 vs 10.9 us per step); the [U; f_beta; W_hh] h GEMM stays on the tile kernel (8.2 vs 8.6
   // us: with K = 512 every workgroup reads all of A); mode 2: every eligible problem (tests)
-  if (g_skinny_mode == 1 && !(g.partial_splits > 1 && g.K % 256 == 0 && g.partial_splits == g.K / 256)) return 0;
+  if (mode == 0 && !(g.partial_splits > 1 && g.K % 256 == 0 && g.partial_splits == g.K / 256)) return 0;
   if (g.dtype != SAT_BF16 || g.c_dtype != SAT_F32 || g.batch != 1 || g.conv.C > 0) return 0;
   if (g.transA || g.transB || g.aux || g.add1 || g.act != SAT_ACT_NONE || g.beta != 0.f || g.alpha != 1.f) return 0;
   if (g.M < 1 || g.M > 128 || g.N % SK_COLS || g.K % 32 || g.K <= 0) return 0;
@@ -160,12 +159,6 @@ int sat_skinny_try(const SatGemm& g, hipStream_t st, int* err) {
 // splits the decoder asks for when the skinny kernel runs its per-step GEMMs: 256-deep K per split
 // (less A per workgroup: every workgroup reads all M rows of its K range), 0 = not eligible
 int sat_skinny_splits(int M, int N, int K) {
-  if (!g_skinny_mode || M > 128 || N % SK_COLS || K % 256 || K < 1024) return 0;
+  if (sat_policy().skinny == 1 || M > 128 || N % SK_COLS || K % 256 || K < 1024) return 0;
   return K / 256;
-}
-
-extern "C" int sat_skinny_set_mode(int on) {
-  if (on < 0 || on > 2) return SAT_ERR_INVALID;
-  g_skinny_mode = on;
-  return 0;
 }

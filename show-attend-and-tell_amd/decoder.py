@@ -105,12 +105,8 @@ class Decoder(nn.Module):
         self._seed_host = None
         self._seed_dev = None
         self._defer_phase2 = False     # see defer_recurrent_backward()
-        # one backward call with the head's weight gradients on a side stream beside BPTT (phase bit 8):
-        # off by default -- measured slower (8.35 vs 8.19 ms/step alone, 12.9 vs 8.3 beside the encoder)
-        self.head_side_stream = False
-        # the weight gradients after BPTT in two branches: attention + init-state gradients on a side
-        # stream beside the LSTM-weight / embedding gradients (phase bit 16)
-        self.tail_side_stream = False
+        # per-call kernel selection (sat_amd.Policy / SatPolicy; None = the library's defaults): A/B only
+        self.policy = None
         # workgroups the per-step split-K GEMMs aim for (SatDecoderDims.split_target; 0 = library
         # default): 64 when the decoder shares the chip with the next batch's encoder (bench / train.py)
         self.split_target = 0
@@ -247,12 +243,13 @@ class Decoder(nn.Module):
         """Phase 2 of a backward whose recurrent part was deferred (no-op if none is pending)."""
         if self._pending_bwd is None:
             return
-        dims, lay, lp, feats, ws, ws_bytes, preds, alphas, d_preds, d_alphas, accumulate, masked = self._pending_bwd
+        dims, lay, lp, feats, ws, ws_bytes, preds, alphas, d_preds, d_alphas, accumulate, masked, _pol = \
+            self._pending_bwd
         lib = L.lib()
         L.check(lib.sat_decoder_backward(ctypes.byref(dims), ctypes.byref(lay), L.ptr(self._flat), L.ptr(lp),
                                          L.ptr(feats), L.ptr(ws), ws_bytes, L.ptr(preds), L.ptr(alphas),
                                          L.ptr(d_preds), L.ptr(d_alphas), L.ptr(self._grad_flat), int(accumulate),
-                                         2 | masked | (16 if self.tail_side_stream else 0), L.stream_of(preds)),
+                                         2 | masked, L.stream_of(preds)),
                 "sat_decoder_backward")
         self._pending_bwd = None
         for hook in self._grad_hooks:
@@ -273,11 +270,12 @@ class Decoder(nn.Module):
         d.start_token = self.tokenizer.cls_token_id if self.use_bert else 0
         d.has_dropout_mask = int(self.training and self.dropout_mask is not None)
         d.split_target = int(self.split_target)
+        d.policy = L.policy_ptr(self.policy)
         # dropout masks: host seed drawn once per module from torch's RNG (train.py:37-43 seeding)
         # XOR a device step counter the forward itself advances -> graph replays draw fresh masks
         if self.training:
             if self._seed_host is None:
-                self._seed_host = int(torch.randint(0, 2 ** 62, (1,)).item())
+                self._seed_host = _rank_seed(int(torch.randint(0, 2 ** 62, (1,)).item()))
             if self._seed_dev is None or self._seed_dev.device != feats.device:
                 self._seed_dev = torch.zeros(1, dtype=torch.int64, device=feats.device)
             d.seed = self._seed_host
@@ -356,6 +354,16 @@ class Decoder(nn.Module):
         return h, c
 
 
+def _rank_seed(seed):
+    """Mix the data-parallel rank into the dropout seed.  Every rank seeds torch identically (identical
+    decoder init, train.py:46), so without this rank r's sample i would draw rank 0's sample-i mask;
+    the reference draws an independent Bernoulli mask per sample (decoder.py:67,121-125)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        seed = (seed + dist.get_rank() * 0x9E3779B97F4A7C15) % (1 << 64)
+    return seed
+
+
 def _mean_rows(feats):
     """img_features.mean(dim=1) (decoder.py:139) on the HIP path; returns (f32, feats.dtype) copies."""
     B, Lf, D = feats.shape
@@ -416,10 +424,8 @@ class _DecoderFn(torch.autograd.Function):
             phases = (1,)
         elif dec._grad_hooks:   # a hook (DDP bucket all-reduce) runs between the phases
             phases = (1, 2)
-        else:   # one call: the head's weight gradients on a side stream beside the BPTT loop (bit 8)
-            phases = (3 | 8,) if dec.head_side_stream else (3,)
-        tail = 16 if dec.tail_side_stream else 0
-        phases = tuple(p | tail if p & 2 else p for p in phases)
+        else:
+            phases = (3,)
         for phase in phases:
             L.check(lib.sat_decoder_backward(ctypes.byref(ctx.dims), ctypes.byref(ctx.lay), L.ptr(dec._flat),
                                              L.ptr(ctx.lp), L.ptr(feats), L.ptr(ctx.ws), ctx.ws_bytes, L.ptr(preds),
@@ -431,7 +437,7 @@ class _DecoderFn(torch.autograd.Function):
                 hook(phase, dec)
         if dec._defer_phase2:   # phase 2 runs in dec.finish_backward()
             dec._pending_bwd = (ctx.dims, ctx.lay, ctx.lp, feats, ctx.ws, ctx.ws_bytes, preds, alphas, d_preds,
-                                d_alphas, accumulate, masked)
+                                d_alphas, accumulate, masked, dec.policy)
         ctx.ws = None
         n_params = len(ctx.needs_input_grad) - 3
         return (None, None, None) + (None,) * n_params

@@ -157,19 +157,19 @@ class Encoder(nn.Module):
         # ... its c1 on the half-image 1x1 kernel (sat_conv1x1_frag: input slabs by LDS-DMA, weights
         # register-direct)
         self.c1_frag = True
-        # ... and its c3 (+ identity residual) on the half-image 1x1 kernel (sat_conv1x1_res_frag): off,
-        # the weight-stationary streaming kernel is faster there (28.3 vs 33.9 us, profiles/r2_s64_c3_ab.txt)
-        self.c3_frag = False
+        # per-call kernel selection for the conv launches (sat_amd.Policy / SatPolicy; None = the library's
+        # defaults): A/B measurements and tests only
+        self.policy = None
 
     def _conv(self, x, f, relu, residual=None, out_hw=None):
         w, b, s, p = f
         if self.timing_args is not None:
             self.timing_args.append((x, w, b, s, p, relu, residual, out_hw))
         if self.timing is None:
-            return ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual, out_hw=out_hw)
+            return ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual, out_hw=out_hw, policy=self.policy)
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st.record()
-        y = ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual, out_hw=out_hw)
+        y = ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual, out_hw=out_hw, policy=self.policy)
         en.record()
         self.timing.append((st, en))
         return y
@@ -361,7 +361,4 @@ class Encoder(nn.Module):
         else:
             out = self._conv(out, c2, True)
         idn = self._conv(y, ds, False) if ds is not None else y
-        if fused is not None and ds is None and self.c3_frag and ops.conv1x1_res_frag_supported(
-                out.shape[1], out.shape[2], out.shape[3], c3[0].shape[0], out.dtype):
-            return self._frag_conv("c3frag", ops.conv1x1_res_frag, out, fused[2], idn)
         return self._conv(out, c3, True, residual=idn)

@@ -64,7 +64,9 @@ def load_model(model_path, model_config_path=None, dtype=torch.float32, device="
         vocab = len(word_dict)
     encoder = sat_amd.Encoder(cfg["network"], dtype=dtype)
     enc_w = encoder_weights or cfg.get("encoder_weights")
-    if enc_w and not os.path.isabs(enc_w) and not os.path.exists(enc_w):
+    if enc_w and not os.path.exists(enc_w):
+        # the model directory was copied or moved (train.py records an absolute path): the weights sit
+        # next to model_config.json
         enc_w = os.path.join(os.path.dirname(model_config_path) or ".", os.path.basename(enc_w))
     if enc_w:
         encoder.load_state_dict(torch.load(enc_w, map_location="cpu", weights_only=True))

@@ -30,8 +30,9 @@ def linear(x, weight, bias=None, act=L.ACT_NONE, out_dtype=None, weight_lp=None)
 
 
 def gemm(A, B, C, *, transA=False, transB=False, alpha=1.0, beta=0.0, bias=None, add1=None, act=L.ACT_NONE,
-         aux=None):
-    """C = act(alpha * A' B'^T + bias + add1 + beta*C) with A' = A or A^T, B'(n,k) = B[n,k] or B[k,n]."""
+         aux=None, policy=None):
+    """C = act(alpha * A' B'^T + bias + add1 + beta*C) with A' = A or A^T, B'(n,k) = B[n,k] or B[k,n].
+    ``policy``: an optional ``sat_amd.Policy`` (per-call kernel selection; None = library defaults)."""
     L.require_device(A, B, C)
     dt = L.dtype_code(A.dtype)
     if B.dtype != A.dtype:
@@ -57,6 +58,7 @@ def gemm(A, B, C, *, transA=False, transB=False, alpha=1.0, beta=0.0, bias=None,
     a.act = act
     if aux is not None:
         a.aux, a.ld_aux, a.aux_dtype = aux.data_ptr(), aux.stride(0), L.dtype_code(aux.dtype)
+    a.policy = L.policy_ptr(policy)
     L.check(L.lib().sat_gemm(ctypes.byref(a), L.stream_of(C)), "sat_gemm")
     return C
 
@@ -136,9 +138,10 @@ def images_to_input(packed, layout=L.IMG_NCHW, dtype=torch.float32, c_pad=8, siz
     return out
 
 
-def conv2d_nhwc(x, w, bias, stride, pad, relu, residual=None, out=None, out_hw=None):
+def conv2d_nhwc(x, w, bias, stride, pad, relu, residual=None, out=None, out_hw=None, policy=None):
     """x [N,H,W,C] ; w [Cout,KH,KW,C] (same dtype) ; bias f32 [Cout].  ``pad`` pads top/left;
-    ``out_hw`` (default: symmetric padding) fixes the output size."""
+    ``out_hw`` (default: symmetric padding) fixes the output size; ``policy``: optional per-call kernel
+    selection (``sat_amd.Policy``)."""
     L.require_device(x, w)
     N, H, W, C = x.shape
     Cout, KH, KW, Cw = w.shape
@@ -153,7 +156,8 @@ def conv2d_nhwc(x, w, bias, stride, pad, relu, residual=None, out=None, out_hw=N
     if residual is not None:
         assert residual.shape == y.shape and residual.dtype == y.dtype
     L.check(L.lib().sat_conv2d_nhwc(ctypes.byref(g), Cout, L.dtype_code(x.dtype), L.ptr(x), L.ptr(w), L.ptr(bias),
-                                    L.ptr(residual), int(relu), L.ptr(y), L.stream_of(y)), "sat_conv2d_nhwc")
+                                    L.ptr(residual), int(relu), L.ptr(y), L.policy_ptr(policy), L.stream_of(y)),
+            "sat_conv2d_nhwc")
     return y
 
 
@@ -219,28 +223,6 @@ def conv1x1_frag(x, f, out=None):
     return y
 
 
-def conv1x1_res_frag_supported(H, W, Cin, Cout, dtype):
-    return bool(L.lib().sat_conv1x1_res_frag_supported(H, W, Cin, Cout, L.dtype_code(dtype)))
-
-
-def conv1x1_res_frag(x, f, residual, out=None):
-    """relu(x . W^T + b + residual) with f = (fragment-layout weight, fp32 bias) of a folded [Cout][Cin]
-    1x1 conv (a layer3 bottleneck's c3).  x NHWC [N,H,W,Cin], residual [N,H,W,Cout]; bit-identical to
-    conv2d_nhwc(..., residual=residual)."""
-    L.require_device(x, residual)
-    if not (x.is_contiguous() and residual.is_contiguous()):
-        raise ValueError("conv1x1_res_frag: x and residual must be contiguous NHWC tensors")
-    N, H, W, C = x.shape
-    Cout = f[1].shape[0]
-    if tuple(residual.shape) != (N, H, W, Cout) or residual.dtype != x.dtype:
-        raise ValueError(f"conv1x1_res_frag: residual {tuple(residual.shape)} does not match {(N, H, W, Cout)}")
-    y = out if out is not None else torch.empty_like(residual)
-    L.check(L.lib().sat_conv1x1_res_frag(N, H, W, C, Cout, L.dtype_code(x.dtype), L.ptr(x), L.ptr(f[0]),
-                                         L.ptr(f[1]), L.ptr(residual), L.ptr(y), L.stream_of(y)),
-            "sat_conv1x1_res_frag")
-    return y
-
-
 def maxpool2d_nhwc(x, k, stride, pad=0):
     L.require_device(x)
     N, H, W, C = x.shape
@@ -252,52 +234,7 @@ def maxpool2d_nhwc(x, k, stride, pad=0):
     return y
 
 
-def set_decoder_split_target(workgroups):
-    """Workgroups the decoder's automatic per-step split-K aims for (0 = default 192).  64 suits a
-    decoder that shares the GPU with a concurrent encoder stream (bench.py / train.py overlap).
-    Process-global; call before the first decoder forward."""
-    L.check(L.lib().sat_decoder_set_split_target(int(workgroups)), "sat_decoder_set_split_target")
-
-
 def adam_step_(param, grad, exp_avg, exp_avg_sq, param_lp, beta1, beta2, eps, step_size, bc2_sqrt):
     L.check(L.lib().sat_adam_step(L.ptr(param), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), L.ptr(param_lp),
                                   param.numel(), beta1, beta2, eps, step_size, bc2_sqrt, L.stream_of(param)),
             "sat_adam_step")
-
-
-def cu_mask_bits(ncu, n_dec, layout="strided"):
-    """CU index sets for a decoder / encoder partition of the chip: ``strided`` spreads the decoder's
-    ``n_dec`` CUs evenly over the CU numbering (every ncu/n_dec-th), ``contig`` takes the first n_dec."""
-    if not 0 < n_dec < ncu:
-        raise ValueError(f"sat_amd: decoder CU count {n_dec} outside (0, {ncu})")
-    if layout == "strided":
-        step = ncu / n_dec
-        dec = sorted({int(i * step) for i in range(n_dec)})
-    elif layout == "contig":
-        dec = list(range(n_dec))
-    else:
-        raise ValueError(f"sat_amd: unknown CU layout {layout!r}")
-    enc = [i for i in range(ncu) if i not in set(dec)]
-    return dec, enc
-
-
-def cu_masked_stream(cus, device=None):
-    """A torch stream (``torch.cuda.ExternalStream``) whose kernels run only on the CU indices ``cus``
-    (sat_stream_create_cu_mask).  The stream lives for the rest of the process."""
-    ncu = ctypes.c_int(0)
-    L.check(L.lib().sat_device_cu_count(ctypes.byref(ncu)), "sat_device_cu_count")
-    words = (ncu.value + 31) // 32
-    mask = (ctypes.c_uint32 * words)()
-    for c in cus:
-        if not 0 <= c < ncu.value:
-            raise ValueError(f"sat_amd: CU index {c} outside [0, {ncu.value})")
-        mask[c // 32] |= 1 << (c % 32)
-    out = ctypes.c_void_p()
-    L.check(L.lib().sat_stream_create_cu_mask(mask, words, ctypes.byref(out)), "sat_stream_create_cu_mask")
-    return torch.cuda.ExternalStream(out.value, device=device)
-
-
-def device_cu_count():
-    ncu = ctypes.c_int(0)
-    L.check(L.lib().sat_device_cu_count(ctypes.byref(ncu)), "sat_device_cu_count")
-    return ncu.value

@@ -1,0 +1,127 @@
+"""One rank of the data-parallel GPU test (tests/test_gpu_dp.py launches two of these, gloo, both on
+cuda:0).  Not a test module: run as ``python tests/dp_rank_worker.py RANK WORLD INIT_FILE OUT``.
+
+Each rank takes its contiguous half of a global fp32 batch and runs the train step (train.py:128-164)
+through the HIP decoder twice:
+  eager  -- backward with GradAllReduce's phase hooks (bucket 1 all-reduced from inside backward);
+  graph  -- bench.py's schedule: forward + loss + backward phase 1 captured as one hipGraph, phase 2
+            (BPTT) as a second, allreduce_bucket_async between / after the replays;
+each followed by the fused Adam step.  It also runs one train-mode forward with library-drawn dropout
+masks on the SAME inputs on every rank (the per-rank mask streams must differ, decoder.py:121-125
+draws a fresh Bernoulli mask per sample).  Results go to OUT (torch.save) for the parent to compare
+with a single-process full-batch run.
+"""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+DP_CASE = dict(V=500, D=256, L=16, E=512, T=10, B=8, seed=41, lr=1e-4)
+
+
+def case_inputs():
+    import numpy as np
+    from oracle import sat_oracle as O
+    c = DP_CASE
+    p = O.make_decoder_params(c["V"], c["D"], c["E"], True, c["seed"])
+    rng = np.random.default_rng(c["seed"] + 1)
+    feats = torch.from_numpy(np.maximum(rng.standard_normal((c["B"], c["L"], c["D"])), 0).astype(np.float32))
+    caps = O.make_captions(c["B"], c["T"], c["V"], c["seed"] + 2)
+    masks = O.make_dropout_masks(c["B"], c["T"] - 1, c["E"], c["seed"] + 3)   # [T-1, B, E]
+    return p, feats, caps, masks.permute(1, 0, 2).contiguous().to(torch.uint8)   # [B, T-1, E]
+
+
+def make_decoder(sat_amd, p, dev):
+    c = DP_CASE
+    dec = sat_amd.Decoder(c["V"], c["D"], tf=True, ado=True, attention=True)
+    dec.load_state_dict(p, strict=True)
+    return dec.to(dev).train()
+
+
+def snapshot(dec):
+    params = dict(dec.named_parameters())
+    return {n: params[n].grad.detach().cpu().clone() for n in dec.active_param_names()}
+
+
+def weights(dec):
+    params = dict(dec.named_parameters())
+    return {n: params[n].detach().cpu().clone() for n in dec.active_param_names()}
+
+
+def main():
+    rank, world, init_file, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    import sat_amd
+    from sat_amd.distributed import GradAllReduce, allreduce_bucket_async, shard_batch
+    p, feats, caps, mask = case_inputs()
+    f_loc = shard_batch(feats, rank, world).contiguous().to(dev)
+    c_loc = shard_batch(caps, rank, world).contiguous().to(dev)
+    m_loc = shard_batch(mask, rank, world).contiguous().to(dev)   # on the device: no copy inside a capture
+    res = {}
+
+    # -- eager: hook-driven bucket all-reduce
+    dec = make_decoder(sat_amd, p, dev)
+    dec.dropout_mask = m_loc
+    opt = sat_amd.Adam(dec.parameters(), lr=DP_CASE["lr"])
+    ar = GradAllReduce(dec)
+    opt.zero_grad()
+    preds, alphas = dec(f_loc, c_loc)
+    loss, _ = sat_amd.caption_loss(preds, alphas, c_loc)
+    loss.backward()
+    ar.wait()
+    torch.cuda.synchronize()
+    res["eager_grads"] = snapshot(dec)
+    opt.step()
+    torch.cuda.synchronize()
+    res["eager_weights"] = weights(dec)
+
+    # -- graph: two captured decoder graphs (phase 1, phase 2), async bucket all-reduce between
+    dec = make_decoder(sat_amd, p, dev)
+    dec.dropout_mask = m_loc
+    opt = sat_amd.Adam(dec.parameters(), lr=DP_CASE["lr"])
+    opt.zero_grad()   # warm-up eager step: builds the flat buffers and the allocator pools
+    preds, alphas = dec(f_loc, c_loc)
+    sat_amd.caption_loss(preds, alphas, c_loc)[0].backward()
+    torch.cuda.synchronize()
+    dec.defer_recurrent_backward(True)
+    opt.zero_grad(set_to_none=True)
+    g_dec, g_rec = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_dec):
+        preds, alphas = dec(f_loc, c_loc)
+        sat_amd.caption_loss(preds, alphas, c_loc)[0].backward()
+    with torch.cuda.graph(g_rec):
+        dec.finish_backward()
+    dec.defer_recurrent_backward(False)
+    dec._grad_flat.fill_(float("nan"))   # every replay must overwrite the whole gradient
+    g_dec.replay()
+    w1 = allreduce_bucket_async(dec, 1)
+    g_rec.replay()
+    w2 = allreduce_bucket_async(dec, 2)
+    w1.wait()
+    w2.wait()
+    torch.cuda.synchronize()
+    res["graph_grads"] = snapshot(dec)
+    opt.step()
+    torch.cuda.synchronize()
+    res["graph_weights"] = weights(dec)
+
+    # -- library-drawn dropout masks: identical inputs and weights on every rank
+    dec = make_decoder(sat_amd, p, dev)
+    same_f, same_c = feats[:2].contiguous().to(dev), caps[:2].contiguous().to(dev)
+    with torch.no_grad():
+        res["train_preds"] = dec(same_f, same_c)[0].cpu()
+        dec.eval()
+        res["eval_preds"] = dec(same_f, same_c)[0].cpu()
+    torch.save(res, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -23,8 +23,38 @@ def test_library_exports_every_declared_symbol():
     lib = sat_amd._lib.lib()
     missing = [f for f in declared_functions() if not hasattr(lib, f)]
     assert not missing, missing
-    assert lib.sat_abi_version() == 1
+    assert lib.sat_abi_version() == sat_amd._lib.ABI_VERSION == header_abi_version() == 2
     assert set(declared_functions()) == set(sat_amd._lib.EXPORTED)
+
+
+def header_abi_version():
+    return int(re.search(r"#define SAT_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+
+
+def test_no_process_global_tuning_state():
+    """Kernel selection is a per-call argument (SatPolicy), not process-global state: the header
+    declares no setter / mode / experiment hook, and the library exports none."""
+    import sat_amd
+    names = declared_functions()
+    bad = [f for f in names if re.search(r"_set_|_mode\b|experiment|cu_mask|trace", f)]
+    assert not bad, bad
+    exported = subprocess.run(["nm", "-D", "--defined-only", sat_amd._lib.LIB_PATH], capture_output=True,
+                              text=True, check=True).stdout
+    syms = re.findall(r" T (sat_\w+)", exported)
+    assert sorted(syms) == names, sorted(set(syms) ^ set(names))
+    text = open(HEADER).read()
+    assert "SatPolicy* policy" in text.replace("const SatPolicy", "SatPolicy")
+
+
+def test_library_refuses_other_abi_version(monkeypatch):
+    import sat_amd
+    L = sat_amd._lib
+    monkeypatch.setattr(L, "_lib", None)
+    monkeypatch.setattr(L, "ABI_VERSION", 1)
+    with pytest.raises(RuntimeError, match="C-ABI version"):
+        L.lib()
+    monkeypatch.undo()
+    assert L.lib().sat_abi_version() == 2
 
 
 def test_error_strings():
@@ -44,11 +74,13 @@ def test_struct_layouts_match_c(tmp_path):
 #include "sat_hip.h"
 #define P(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 int main(void) {
-  printf("SatGemmArgs %zu\nSatDecoderDims %zu\nSatDecoderLayout %zu\nSatConvGeom %zu\n",
-         sizeof(SatGemmArgs), sizeof(SatDecoderDims), sizeof(SatDecoderLayout), sizeof(SatConvGeom));
+  printf("SatGemmArgs %zu\nSatDecoderDims %zu\nSatDecoderLayout %zu\nSatConvGeom %zu\nSatPolicy %zu\n",
+         sizeof(SatGemmArgs), sizeof(SatDecoderDims), sizeof(SatDecoderLayout), sizeof(SatConvGeom),
+         sizeof(SatPolicy));
   P(SatGemmArgs, B) P(SatGemmArgs, C) P(SatGemmArgs, alpha) P(SatGemmArgs, bias) P(SatGemmArgs, add1)
-  P(SatGemmArgs, act) P(SatGemmArgs, aux) P(SatGemmArgs, aux_dtype)
+  P(SatGemmArgs, act) P(SatGemmArgs, aux) P(SatGemmArgs, aux_dtype) P(SatGemmArgs, policy)
   P(SatDecoderDims, dtype) P(SatDecoderDims, seed) P(SatDecoderDims, seed_ptr) P(SatDecoderDims, split_target)
+  P(SatDecoderDims, policy) P(SatPolicy, attn_bwd) P(SatPolicy, decoder_splits)
   P(SatDecoderLayout, do_b) P(SatDecoderLayout, total)
   return 0;
 }
@@ -61,6 +93,7 @@ int main(void) {
     assert int(out["SatDecoderDims"]) == ctypes.sizeof(L.SatDecoderDims)
     assert int(out["SatDecoderLayout"]) == ctypes.sizeof(L.SatDecoderLayout)
     assert int(out["SatConvGeom"]) == ctypes.sizeof(L.SatConvGeom)
+    assert int(out["SatPolicy"]) == ctypes.sizeof(L.SatPolicy)
     for key, val in out.items():
         if "." in key:
             struct, field = key.split(".")

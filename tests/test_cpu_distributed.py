@@ -59,7 +59,10 @@ def _worker(rank, world, init_file, results):
         scale = g_full[k].abs().max().item()
         if scale > 1e-7 and (g - g_full[k]).abs().max().item() > 1e-4 * scale:
             ok3 = False
-    results[rank] = (ok1, ok2, ok3)
+    # (3) per-rank dropout streams: the decoder mixes the rank into its mask seed (decoder.py:121-125
+    #     draws an independent mask per sample; every rank seeds torch identically)
+    from sat_amd.decoder import _rank_seed
+    results[rank] = (ok1, ok2, ok3, _rank_seed(12345))
     dist.destroy_process_group()
 
 
@@ -70,7 +73,9 @@ def test_gloo_world_size_2():
         mgr = mp.Manager()
         results = mgr.dict()
         mp.spawn(_worker, args=(world, init_file, results), nprocs=world, join=True)
-        assert dict(results) == {0: (True, True, True), 1: (True, True, True)}
+        res = dict(results)
+        assert res[0][:3] == (True, True, True) and res[1][:3] == (True, True, True)
+        assert res[0][3] == 12345 and res[1][3] != res[0][3] and 0 <= res[1][3] < 2 ** 64
 
 
 # ---------------------------------------------------------------------------- real bucket slicing

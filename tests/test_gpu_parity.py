@@ -111,7 +111,7 @@ def test_maxpool(sat, k, stride, pad):
 def test_bf16_lds_epilogue(sat, N, C, H, Cout, relu, resid):
     """1x1 conv + bias (+ bf16 residual) (+ ReLU) through the bf16 LDS epilogue (residual DMA'd
     during the last k-tile, added in the accumulator layout; the finished bf16 tile staged for
-    16-B row stores) vs torch fp32 and vs the staged-fp32 epilogue (sat_fast_gemm_set_res_lds(0))."""
+    16-B row stores) vs torch fp32 and vs the staged-fp32 epilogue (SatPolicy.gemm_epilogue = 2)."""
     from sat_amd import ops
     lib = sat._lib.lib()
     g = torch.Generator().manual_seed(N * Cout + C)
@@ -125,13 +125,9 @@ def test_bf16_lds_epilogue(sat, N, C, H, Cout, relu, resid):
     wd = w.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
     rd = res.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV) if resid else None
     outs = []
-    try:
-        for mode in (2, 0):
-            lib.sat_fast_gemm_set_res_lds(mode)
-            y = ops.conv2d_nhwc(xd, wd, b.to(DEV), 1, 0, relu, residual=rd)
-            outs.append(y.float().permute(0, 3, 1, 2).cpu())
-    finally:
-        lib.sat_fast_gemm_set_res_lds(2)
+    for epi in (0, 2):
+        y = ops.conv2d_nhwc(xd, wd, b.to(DEV), 1, 0, relu, residual=rd, policy=sat.Policy(gemm_epilogue=epi))
+        outs.append(y.float().permute(0, 3, 1, 2).cpu())
     assert rel(outs[0], ref) < 1e-2
     assert torch.equal(outs[0], outs[1])   # same fp32 sums, same single rounding
 
@@ -469,21 +465,18 @@ def test_decoder_split_target(sat):
     feats = torch.randn(B, Lf, D, device=DEV).bfloat16()
     caps = O.make_captions(B, T, V, 1).to(DEV)
     out = []
-    try:   # the per-decoder field (SatDecoderDims.split_target) and the process default
-        for target, default in ((192, 0), (64, 0), (0, 64)):
-            ops.set_decoder_split_target(default)
-            dec.split_target = target
-            for p in dec.parameters():
-                p.grad = None
-            preds, alphas = dec(feats, caps)
-            loss, _ = sat.caption_loss(preds, alphas, caps)
-            loss.backward()
-            out.append((loss.item(), dec._grad_flat.clone()))
-    finally:
-        ops.set_decoder_split_target(0)
-    # field 64 == default 64: the same splits (only the atomic embedding gradient's order may differ)
-    assert out[2][0] == out[1][0]
-    assert ((out[2][1] - out[1][1]).norm() / out[1][1].norm()).item() < 1e-5
+    # the per-decoder field (SatDecoderDims.split_target; 0 = the library default, 192)
+    for target in (192, 64, 0):
+        dec.split_target = target
+        for p in dec.parameters():
+            p.grad = None
+        preds, alphas = dec(feats, caps)
+        loss, _ = sat.caption_loss(preds, alphas, caps)
+        loss.backward()
+        out.append((loss.item(), dec._grad_flat.clone()))
+    # field 0 == field 192: the same splits (only the atomic embedding gradient's order may differ)
+    assert out[2][0] == out[0][0]
+    assert ((out[2][1] - out[0][1]).norm() / out[0][1].norm()).item() < 1e-5
     assert abs(out[0][0] - out[1][0]) < 1e-3 * abs(out[0][0])
     assert ((out[0][1] - out[1][1]).norm() / out[0][1].norm()).item() < 2e-2
 
@@ -617,13 +610,9 @@ def test_conv_pipe_kernel(sat, N, C, H, Cout, k, stride, pad, relu, resid):
     wd = w.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
     rd = res.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV) if resid else None
     outs = []
-    try:
-        for mode in (2, 0):
-            assert lib.sat_conv_pipe_set_mode(mode) == 0
-            y = ops.conv2d_nhwc(xd, wd, b.to(DEV), stride, pad, relu, residual=rd)
-            outs.append(y.float().permute(0, 3, 1, 2).cpu())
-    finally:
-        lib.sat_conv_pipe_set_mode(1)
+    for mode in (2, 1):   # every eligible problem on the pipelined kernel, then never
+        y = ops.conv2d_nhwc(xd, wd, b.to(DEV), stride, pad, relu, residual=rd, policy=sat.Policy(conv_pipe=mode))
+        outs.append(y.float().permute(0, 3, 1, 2).cpu())
     assert rel(outs[0], ref) < 1e-2
     assert ((outs[0] - ref).abs() <= 1e-2 * ref.abs() + 2e-2).all()
     assert torch.equal(outs[0], outs[1])
@@ -654,54 +643,12 @@ def test_conv_stream_kernel(sat, N, C, H, Cout, stride, relu, resid):
     wd = w.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
     rd = res.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV) if resid else None
     outs = []
-    try:
-        for mode in (2, 0):
-            assert lib.sat_conv_stream_set_mode(mode) == 0
-            y = ops.conv2d_nhwc(xd, wd, b.to(DEV), stride, 0, relu, residual=rd)
-            outs.append(y.float().permute(0, 3, 1, 2).cpu())
-    finally:
-        lib.sat_conv_stream_set_mode(1)
+    for mode in (2, 1):   # every eligible 1x1 on the streaming kernel, then never
+        y = ops.conv2d_nhwc(xd, wd, b.to(DEV), stride, 0, relu, residual=rd, policy=sat.Policy(conv_stream=mode))
+        outs.append(y.float().permute(0, 3, 1, 2).cpu())
     assert rel(outs[0], ref) < 1e-2
     assert ((outs[0] - ref).abs() <= 1e-2 * ref.abs() + 2e-2).all()
     assert torch.equal(outs[0], outs[1])
-
-
-@pytest.mark.parametrize("N,C,H,Cout,relu,resid", [
-    (2, 256, 14, 256, True, False),    # L3 c2: 4 chunks x 9 taps, M tail (392 rows)
-    (1, 128, 28, 128, True, False),    # L2 c2: halo rows span image rows and the image end
-    (2, 64, 56, 64, True, False),      # L1 c2: W = 56 (384 halo rows), N = 64 half tile
-    (3, 512, 7, 512, False, True),     # L4 c2 shape class, residual, no activation, 3 images per tile
-    (1, 64, 5, 200, True, False),      # tiny image, N tail, single chunk
-    (2, 256, 14, 136, True, True)])    # N tail + residual
-def test_conv_halo_kernel(sat, N, C, H, Cout, relu, resid):
-    """convhalo.hip (input halo per 64-channel chunk, taps as row shifts with border masks) forced on
-    every eligible 3x3 shape vs torch fp32 (chunk-major k order: fp32-summation-order close to the
-    other kernels, not bit-identical)."""
-    from sat_amd import ops
-    lib = sat._lib.lib()
-    g = torch.Generator().manual_seed(N * C + Cout + H)
-    x = torch.randn(N, C, H, H, generator=g).bfloat16().float()
-    w = (torch.randn(Cout, C, 3, 3, generator=g) / math.sqrt(C * 9)).bfloat16().float()
-    b = torch.randn(Cout, generator=g)
-    ref = F.conv2d(x, w, b, padding=1)
-    res = torch.randn_like(ref).bfloat16().float() if resid else None
-    ref = ref + res if resid else ref
-    ref = torch.relu(ref) if relu else ref
-    xd = x.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
-    wd = w.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
-    rd = res.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV) if resid else None
-    outs = []
-    try:
-        for mode in (2, 0):
-            assert lib.sat_conv_halo_set_mode(mode) == 0
-            y = ops.conv2d_nhwc(xd, wd, b.to(DEV), 1, 1, relu, residual=rd)
-            outs.append(y.float().permute(0, 3, 1, 2).cpu())
-    finally:
-        lib.sat_conv_halo_set_mode(1)
-    assert rel(outs[0], ref) < 1e-2
-    assert ((outs[0] - ref).abs() <= 1e-2 * ref.abs() + 2e-2).all()
-    # vs the implicit-GEMM kernels: same products, k summed chunk-major -> one bf16 ulp at most
-    assert ((outs[0] - outs[1]).abs() <= 2 ** -7 * outs[1].abs() + 1e-4).all()
 
 
 @pytest.mark.parametrize("M,N,K", [(3328, 10000, 512), (6272, 512, 2048), (300, 136, 192)])
@@ -717,14 +664,11 @@ def test_conv_pipe_gemm(sat, M, N, K):
     add1 = torch.randn(M, N, generator=g).bfloat16()
     ref = torch.relu(A.float() @ Bm.float().T + bias + add1.float())
     outs = []
-    try:
-        for mode in (2, 0):
-            assert lib.sat_conv_pipe_set_mode(mode) == 0
-            C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-            ops.gemm(A.to(DEV), Bm.to(DEV), C, bias=bias.to(DEV), add1=add1.to(DEV), act=sat._lib.ACT_RELU)
-            outs.append(C.float().cpu())
-    finally:
-        lib.sat_conv_pipe_set_mode(1)
+    for mode in (2, 1):
+        C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ops.gemm(A.to(DEV), Bm.to(DEV), C, bias=bias.to(DEV), add1=add1.to(DEV), act=sat._lib.ACT_RELU,
+                 policy=sat.Policy(conv_pipe=mode))
+        outs.append(C.float().cpu())
     assert rel(outs[0], ref) < 8e-3
     assert torch.equal(outs[0], outs[1])
 
@@ -927,8 +871,8 @@ def test_running_meters_match_average_meter(sat):
 @pytest.mark.parametrize("N,C,H,Cout,k,stride,pad", [(8, 64, 28, 256, 3, 1, 1), (6, 256, 14, 200, 1, 1, 0),
                                                      (4, 8, 40, 64, 7, 2, 3)])
 def test_fast_conv_tile_configs(sat, tile, xcd, N, C, H, Cout, k, stride, pad):
-    """Every tile configuration of the LDS-DMA kernel (sat_fast_gemm_set_config) with and without
-    the XCD tile remap, including M/N tails and the per-lane-tap stem mode."""
+    """Every tile configuration of the LDS-DMA kernel (SatPolicy.gemm_tile) with and without the XCD
+    tile order, including M/N tails and the per-lane-tap stem mode."""
     from sat_amd import ops
     lib = sat._lib.lib()
     g = torch.Generator().manual_seed(N * C + Cout + k + tile)
@@ -941,12 +885,10 @@ def test_fast_conv_tile_configs(sat, tile, xcd, N, C, H, Cout, k, stride, pad):
     xd = x.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
     wd = w.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
     rd = res.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
-    assert lib.sat_fast_gemm_set_config(2, tile, xcd) == 0
-    try:
-        y = ops.conv2d_nhwc(xd, wd, b.to(DEV), stride, pad, True, residual=rd)
-        torch.cuda.synchronize()
-    finally:
-        lib.sat_fast_gemm_set_config(0, 0, 1)
+    pol = sat.Policy(gemm_stages=2, gemm_tile=tile, gemm_linear_order=1 - xcd, conv_pipe=1, conv_stream=1,
+                     conv3x3_ws=1)
+    y = ops.conv2d_nhwc(xd, wd, b.to(DEV), stride, pad, True, residual=rd, policy=pol)
+    torch.cuda.synchronize()
     y = y.float().permute(0, 3, 1, 2).cpu()
     assert ((y - ref_r).abs() <= 1e-2 * ref_r.abs() + 2e-2).all()
 
@@ -962,12 +904,9 @@ def test_fast_gemm_tile_configs_fp32_out(sat, tile):
     bias = torch.randn(N, generator=g)
     ref = A.double() @ Bm.double().T + bias.double()
     C = torch.empty(M, N, device=DEV)
-    assert lib.sat_fast_gemm_set_config(3 if tile in (1, 3) else 2, tile, 1) == 0
-    try:
-        ops.gemm(A.to(DEV), Bm.to(DEV), C, bias=bias.to(DEV))
-        torch.cuda.synchronize()
-    finally:
-        lib.sat_fast_gemm_set_config(0, 0, 1)
+    pol = sat.Policy(gemm_stages=3 if tile in (1, 3) else 2, gemm_tile=tile, conv_pipe=1)
+    ops.gemm(A.to(DEV), Bm.to(DEV), C, bias=bias.to(DEV), policy=pol)
+    torch.cuda.synchronize()
     assert rel(C, ref) < 2e-5
 
 
@@ -1067,10 +1006,7 @@ def test_cli_karpathy_fixture_streaming(sat, tmp_path, capsys):
         if mode == "host":
             argv.append("--host-preprocess")
         capsys.readouterr()
-        try:
-            T.main(argv)
-        finally:
-            ops.set_decoder_split_target(0)
+        T.main(argv)
         out = capsys.readouterr().out
         logs[mode] = [_json.loads(l) for l in out.splitlines() if l.startswith("{")]
     a = [r for r in logs["stream"] if "epoch_seconds" not in r]
@@ -1148,34 +1084,8 @@ def test_conv3x3_frag_bit_identical(sat, N, H, C):
     y = ops.conv3x3_frag(x, f)
     torch.cuda.synchronize()
     assert torch.equal(y, ref), f"max |frag - tile| = {(y.float() - ref.float()).abs().max().item()}"
-    lib = sat._lib.lib()
-    try:   # experiment bit 16: the whole-image two-slice kernel at 14 x 14 (N % 8 == 0; else unchanged)
-        for mode in (2 | 16, 2 | 16 | 32, 2 | 64):   # bit 32: 2 m-groups x 4 n-groups of waves; 64: LDS-DMA weights
-            assert lib.sat_conv3x3_frag_set_experiment(mode) == 0
-            assert torch.equal(ops.conv3x3_frag(x, f), ref), mode
-    finally:
-        lib.sat_conv3x3_frag_set_experiment(2)
     t = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2).cpu(), w.float().permute(0, 3, 1, 2).cpu(), b.cpu(),
                             padding=1))
-    assert rel(y.float().permute(0, 3, 1, 2).cpu(), t) < 1e-2
-
-
-@pytest.mark.parametrize("N", [1, 2, 5])
-def test_conv1x1_res_frag_bit_identical(sat, N):
-    """csrc/convblock.hip's half-image 1x1 + residual kernel (a layer3 c3 left unfused: 14x14, 256 -> 1024)
-    is bit-identical to sat_conv2d_nhwc on the same operands, and close to torch fp32."""
-    from sat_amd import ops
-    g = torch.Generator().manual_seed(50 + N)
-    x = torch.randn(N, 14, 14, 256, generator=g).relu().bfloat16().to(DEV)
-    r = torch.randn(N, 14, 14, 1024, generator=g).relu().bfloat16().to(DEV)
-    w = (torch.randn(1024, 1, 1, 256, generator=g) * math.sqrt(2.0 / 256)).bfloat16().to(DEV)
-    b = (0.1 * torch.randn(1024, generator=g)).to(DEV)
-    ref = ops.conv2d_nhwc(x, w, b, 1, 0, True, residual=r)
-    y = ops.conv1x1_res_frag(x, (ops.mfma_frag_layout(w.reshape(1024, -1)), b), r)
-    torch.cuda.synchronize()
-    assert torch.equal(y, ref), f"max |frag - conv| = {(y.float() - ref.float()).abs().max().item()}"
-    t = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2).cpu(), w.float().permute(0, 3, 1, 2).cpu(), b.cpu())
-                   + r.float().permute(0, 3, 1, 2).cpu())
     assert rel(y.float().permute(0, 3, 1, 2).cpu(), t) < 1e-2
 
 
@@ -1197,8 +1107,8 @@ def test_conv1x1_frag_bit_identical(sat, N):
 
 
 def test_encoder_c2_frag_equal_tile(sat):
-    """ResNet152 trunk at 224 x 224 with every layer3 block unfused: the c2s on sat_conv3x3_frag and the
-    c3s on sat_conv1x1_res_frag change no output bit against the tile / streaming kernels."""
+    """ResNet152 trunk at 224 x 224 with every layer3 block unfused: the c1s on sat_conv1x1_frag and the
+    c2s on sat_conv3x3_frag change no output bit against the tile kernels."""
     torch.manual_seed(0)
     p = O.make_resnet152_params(4)
     enc = sat.Encoder("resnet152", dtype=torch.bfloat16)
@@ -1207,15 +1117,14 @@ def test_encoder_c2_frag_equal_tile(sat):
     enc.fuse_blocks = False
     x = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(7)).to(DEV)
     with torch.no_grad():
-        enc.c1_frag, enc.c2_frag, enc.c3_frag = True, True, True
+        enc.c1_frag, enc.c2_frag = True, True
         y_f = enc(x)
         enc.c1_frag, enc.c2_frag = False, False
         y_t = enc(x)
         enc.c1_frag = True
-        enc.c2_frag, enc.c3_frag = True, False
-        y_3 = enc(x)
+        y_2 = enc(x)
     assert torch.equal(y_f, y_t)
-    assert torch.equal(y_f, y_3)
+    assert torch.equal(y_f, y_2)
 
 
 def test_encoder_fused_blocks_equal_unfused(sat):
@@ -1241,29 +1150,25 @@ def test_attention_backward_one_launch_matches_two(sat, dtype, D, bert):
     """attn_bwd_fused_kernel (one workgroup per batch row, the whole step's attention backward in one
     launch) against the two-launch form it replaces: every decoder gradient at the same inputs, fp32
     within summation-order noise, bf16 within its rounding (E = 768 with BERT embeddings)."""
-    lib = sat._lib.lib()
     B, Lf, T = 32, 49, 9
     V = 30522 if bert else 500
     pad_id, skip_ids = sat.special_ids(bert)
     grads = []
-    try:
-        for mode in (1, 0):
-            assert lib.sat_attention_set_bwd_mode(mode) == 0
-            torch.manual_seed(0)
-            dec = sat.Decoder(V, D, tf=True, ado=not bert, bert=bert, attention=True).to(DEV).eval()
-            if dtype == torch.bfloat16:
-                dec.train()
-            g = torch.Generator().manual_seed(3)
-            feats = torch.randn(B, Lf, D, generator=g).to(DEV).to(dtype)
-            caps = O.make_captions(B, T, V, 1, bert=bert).to(DEV)
-            preds, alphas = dec(feats, caps)
-            loss, _ = sat.caption_loss(preds, alphas, caps, pad_id=pad_id, skip_ids=skip_ids)
-            loss.backward()
-            torch.cuda.synchronize()
-            grads.append({n: p.grad.detach().float().cpu().clone() for n, p in dec.named_parameters()
-                          if p.grad is not None})
-    finally:
-        lib.sat_attention_set_bwd_mode(1)
+    for mode in (0, 1):   # the library's choice, then the two-launch form
+        torch.manual_seed(0)
+        dec = sat.Decoder(V, D, tf=True, ado=not bert, bert=bert, attention=True).to(DEV).eval()
+        dec.policy = sat.Policy(attn_bwd=mode)
+        if dtype == torch.bfloat16:
+            dec.train()
+        g = torch.Generator().manual_seed(3)
+        feats = torch.randn(B, Lf, D, generator=g).to(DEV).to(dtype)
+        caps = O.make_captions(B, T, V, 1, bert=bert).to(DEV)
+        preds, alphas = dec(feats, caps)
+        loss, _ = sat.caption_loss(preds, alphas, caps, pad_id=pad_id, skip_ids=skip_ids)
+        loss.backward()
+        torch.cuda.synchronize()
+        grads.append({n: p.grad.detach().float().cpu().clone() for n, p in dec.named_parameters()
+                      if p.grad is not None})
     tol = 1e-4 if dtype == torch.float32 else 2e-2
     assert set(grads[0]) == set(grads[1]) and grads[0]
     for n, g1 in grads[0].items():
@@ -1275,122 +1180,24 @@ def test_attention_backward_one_launch_matches_two(sat, dtype, D, bert):
         assert err < tol, (n, err)
 
 
-@pytest.mark.parametrize("ado,attention", [(True, True), (False, True), (True, False)])
-def test_tail_wgrads_on_side_stream_match(sat, ado, attention):
-    """sat_decoder_backward phase bit 16: the attention / init-state weight gradients after BPTT run on
-    the side stream beside the LSTM-weight and embedding gradients -- every gradient equal (to fp32
-    atomic-order noise) to the one-stream order, eager and captured + replayed as a hipGraph."""
-    torch.manual_seed(0)
-    B, Lf, D, V, T = 32, 49, 512, 300, 9
-    dec = sat.Decoder(V, D, tf=True, ado=ado, attention=attention).to(DEV).eval()
-    feats = torch.randn(B, Lf, D, generator=torch.Generator().manual_seed(4)).bfloat16().to(DEV)
-    caps = O.make_captions(B, T, V, 1).to(DEV)
-
-    def step():
-        preds, alphas = dec(feats, caps)
-        loss, _ = sat.caption_loss(preds, alphas, caps)
-        loss.backward()
-
-    def grads():
-        dec.zero_grad(set_to_none=True)
-        step()
-        torch.cuda.synchronize()
-        return {n: p.grad.detach().clone() for n, p in dec.named_parameters() if p.grad is not None}
-    serial = grads()
-    dec.tail_side_stream = True
-    branched = grads()
-    assert set(serial) == set(branched) and serial
-
-    def same(a, b):   # fp32 atomics (embedding scatter, atomic split-K) sum in run-dependent order
-        return ((a - b).abs().max() <= 1e-5 * b.abs().max()).item()
-    for n in serial:
-        assert same(branched[n], serial[n]), n
-    dec.zero_grad(set_to_none=True)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        step()
-    for p in dec.parameters():
-        if p.grad is not None:
-            p.grad.fill_(float("nan"))
-    g.replay()
-    torch.cuda.synchronize()
-    for n, p in dec.named_parameters():
-        if n in serial:
-            assert same(p.grad, serial[n]), n
-
-
-@pytest.mark.parametrize("ado", [True, False])
-def test_head_wgrads_on_side_stream_match(sat, ado):
-    """sat_decoder_backward phase bit 8: the output head's weight gradients run on the decoder's side
-    stream beside the BPTT loop (one call) -- every gradient equal (to fp32 atomic-order noise) to the
-    two-call form a DDP hook forces, also when captured and replayed as a hipGraph."""
-    torch.manual_seed(0)
-    B, Lf, D, V, T = 32, 49, 512, 300, 9
-    dec = sat.Decoder(V, D, tf=True, ado=ado, attention=True).to(DEV).eval()
-    dec.head_side_stream = True
-    feats = torch.randn(B, Lf, D, generator=torch.Generator().manual_seed(2)).bfloat16().to(DEV)
-    caps = O.make_captions(B, T, V, 1).to(DEV)
-
-    def grads():
-        dec.zero_grad(set_to_none=True)
-        preds, alphas = dec(feats, caps)
-        loss, _ = sat.caption_loss(preds, alphas, caps)
-        loss.backward()
-        torch.cuda.synchronize()
-        return {n: p.grad.detach().clone() for n, p in dec.named_parameters() if p.grad is not None}
-    one = grads()
-    hook = lambda phase, d: None   # noqa: E731  (forces the two-call form)
-    dec._grad_hooks.append(hook)
-    two = grads()
-    dec._grad_hooks.remove(hook)
-    assert set(one) == set(two) and one
-
-    def same(a, b, n):
-        # the embedding scatter-add and the atomic split-K weight gradients (e.g. attention.W) sum in
-        # fp32 atomics, whose order varies run to run: equal to fp32 summation-order noise
-        return ((a - b).abs().max() <= 1e-5 * b.abs().max()).item()
-    for n in one:
-        assert same(one[n], two[n], n), n
-    # captured: the fork / join become graph edges
-    dec.zero_grad(set_to_none=True)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        preds, alphas = dec(feats, caps)
-        loss, _ = sat.caption_loss(preds, alphas, caps)
-        loss.backward()
-    for p in dec.parameters():
-        if p.grad is not None:
-            p.grad.fill_(float("nan"))
-    g.replay()
-    torch.cuda.synchronize()
-    for n, p in dec.named_parameters():
-        if n in one:
-            assert same(p.grad, one[n], n), n
-
-
 @pytest.mark.parametrize("M,N,K,bias", [(128, 4608, 512, True), (128, 2048, 2048, False), (100, 1024, 1024, True),
                                         (32, 64, 96, False), (7, 96, 32, True)])
 def test_skinny_gemm_direct(sat, M, N, K, bias):
     """skinny_gemm_kernel (csrc/skinny.hip): bf16 NT, fp32 output, M <= 128 (the decoder's per-step
     products) against an fp64 product of the same bf16 operands, and against the LDS-DMA tile kernel
-    it replaces (sat_skinny_set_mode(0))."""
+    it replaces (SatPolicy.skinny = 1)."""
     from sat_amd import ops
-    lib = sat._lib.lib()
     g = torch.Generator().manual_seed(M * 7 + N + K)
     A = torch.randn(M, K, generator=g).bfloat16()
     Bm = torch.randn(N, K, generator=g).bfloat16()
     b = torch.randn(N, generator=g) if bias else None
     ref = A.double() @ Bm.double().T + (b.double() if bias else 0)
     outs = []
-    try:
-        for mode in (2, 0):   # 2: every eligible problem on the skinny kernel
-            assert lib.sat_skinny_set_mode(mode) == 0
-            C = torch.full((M, N), float("nan"), device=DEV)
-            ops.gemm(A.to(DEV), Bm.to(DEV), C, bias=b.to(DEV) if bias else None)
-            torch.cuda.synchronize()
-            outs.append(C.cpu().double())
-    finally:
-        lib.sat_skinny_set_mode(1)
+    for mode in (2, 1):   # 2: every eligible problem on the skinny kernel, 1: never
+        C = torch.full((M, N), float("nan"), device=DEV)
+        ops.gemm(A.to(DEV), Bm.to(DEV), C, bias=b.to(DEV) if bias else None, policy=sat.Policy(skinny=mode))
+        torch.cuda.synchronize()
+        outs.append(C.cpu().double())
     for C in outs:
         assert torch.isfinite(C).all()
         assert ((C - ref).abs().max() / ref.abs().max()).item() < 1e-5
@@ -1402,26 +1209,22 @@ def test_decoder_skinny_matches_tile_kernel(sat, tf):
     """The decoder's per-step GEMMs (partial-slab split-K) on the skinny kernel vs the LDS-DMA tile
     kernel: predictions, alphas, loss and every gradient within bf16-path summation-order noise; greedy
     ids (no teacher forcing) identical."""
-    lib = sat._lib.lib()
     B, Lf, D, V, T = 128, 49, 2048, 1000, 12
     res = []
-    try:
-        for mode in (1, 0):
-            assert lib.sat_skinny_set_mode(mode) == 0
-            torch.manual_seed(0)
-            dec = sat.Decoder(V, D, tf=tf, ado=True, attention=True).to(DEV).eval()
-            dec.split_target = 64
-            g = torch.Generator().manual_seed(5)
-            feats = torch.randn(B, Lf, D, generator=g).bfloat16().to(DEV)
-            caps = O.make_captions(B, T, V, 1).to(DEV)
-            preds, alphas = dec(feats, caps)
-            loss, _ = sat.caption_loss(preds, alphas, caps)
-            loss.backward()
-            torch.cuda.synchronize()
-            res.append((preds.float().cpu(), alphas.cpu(), loss.item(), dec.last_tokens.cpu().clone(),
-                        {n: p.grad.float().cpu().clone() for n, p in dec.named_parameters() if p.grad is not None}))
-    finally:
-        lib.sat_skinny_set_mode(1)
+    for mode in (0, 1):   # the library's choice (skinny products), then the tile kernel
+        torch.manual_seed(0)
+        dec = sat.Decoder(V, D, tf=tf, ado=True, attention=True).to(DEV).eval()
+        dec.split_target = 64
+        dec.policy = sat.Policy(skinny=mode)
+        g = torch.Generator().manual_seed(5)
+        feats = torch.randn(B, Lf, D, generator=g).bfloat16().to(DEV)
+        caps = O.make_captions(B, T, V, 1).to(DEV)
+        preds, alphas = dec(feats, caps)
+        loss, _ = sat.caption_loss(preds, alphas, caps)
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append((preds.float().cpu(), alphas.cpu(), loss.item(), dec.last_tokens.cpu().clone(),
+                    {n: p.grad.float().cpu().clone() for n, p in dec.named_parameters() if p.grad is not None}))
     (p1, a1, l1, t1, g1), (p0, a0, l0, t0, g0) = res
     if not torch.equal(t1, t0):   # greedy: a near-tie argmax may flip under a different summation order
         assert not tf and (t1 == t0).float().mean().item() > 0.98
@@ -1445,7 +1248,6 @@ def test_conv3x3_ws_kernel(sat, N, H, relu, bias, stem):
     operands (bf16 output rounding) and bit for bit against the implicit-GEMM tile kernel it replaces
     (same MFMA, same k order).  N = 130: more items than CUs, every ring stage reused."""
     from sat_amd import ops
-    lib = sat._lib.lib()
     g = torch.Generator().manual_seed(N * 31 + H)
     C, KK, pad = (16, 4, 2) if stem else (64, 3, 1)   # stem: 4x4 / top-left pad 2 over the s2d input
     x = torch.randn(N, H, H, C, generator=g).bfloat16()
@@ -1456,13 +1258,10 @@ def test_conv3x3_ws_kernel(sat, N, H, relu, bias, stem):
     if relu:
         ref = ref.clamp_min(0)
     outs = []
-    try:
-        for mode in (1, 0):
-            assert lib.sat_conv3x3_ws_set_mode(mode) == 0
-            y = ops.conv2d_nhwc(x.to(DEV), w.to(DEV), b.to(DEV) if bias else None, 1, pad, relu, out_hw=(H, H))
-            torch.cuda.synchronize()
-            outs.append(y.cpu())
-    finally:
-        lib.sat_conv3x3_ws_set_mode(1)
+    for mode in (0, 1):   # the weight-stationary kernel (default), then off
+        y = ops.conv2d_nhwc(x.to(DEV), w.to(DEV), b.to(DEV) if bias else None, 1, pad, relu, out_hw=(H, H),
+                            policy=sat.Policy(conv3x3_ws=mode))
+        torch.cuda.synchronize()
+        outs.append(y.cpu())
     assert ((outs[0].double() - ref).abs().max() / ref.abs().max()).item() < 8e-3
     assert torch.equal(outs[0], outs[1])

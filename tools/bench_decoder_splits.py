@@ -1,4 +1,4 @@
-"""A/B the split-K counts of the per-step bf16 decoder GEMMs (sat_decoder_set_splits) on the bench
+"""A/B the split-K counts of the per-step bf16 decoder GEMMs (SatPolicy.decoder_splits, per call) on the bench
 workload (B=128, L=49, D=2048, E=512, V=10000, T=27, tf+ado+attention): decoder fwd + loss + bwd
 timed with events, configurations interleaved over rounds in one process.
 
@@ -19,7 +19,6 @@ torch.manual_seed(0)
 dec = sat_amd.Decoder(V, D, tf=True, ado=True, attention=True).to(dev).train()
 feats = torch.randn(B, L, D, device=dev).bfloat16()
 caps = synthetic_captions(B, T, V, generator=torch.Generator().manual_seed(1), device=dev)
-lib = sat_amd._lib.lib()
 CONFIGS = [tuple(int(v) for v in c.split(",")) for c in
            os.environ.get("SPLITS", "0,0,0,0;2,0,0,0;8,0,0,0;0,4,0,0;0,16,0,0;0,0,8,0;0,0,32,0;0,0,0,12;0,0,0,36").split(";")]
 
@@ -33,7 +32,7 @@ def step():
 times = {c: [] for c in CONFIGS}
 for rnd in range(4):
     for cfg in CONFIGS:
-        assert lib.sat_decoder_set_splits(*cfg) == 0
+        dec.policy = sat_amd.Policy(decoder_splits=cfg)
         step()
         torch.cuda.synchronize()
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -43,6 +42,6 @@ for rnd in range(4):
         en.record()
         en.synchronize()
         times[cfg].append(st.elapsed_time(en) / 3)
-lib.sat_decoder_set_splits(0, 0, 0, 0)
+dec.policy = None
 for cfg in CONFIGS:
     print(f"splits h,c,g,dh={cfg}: {statistics.median(times[cfg]):.3f} ms (min {min(times[cfg]):.3f})", flush=True)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests, conv A/B, graph bench, kernel-trace profile, PMC traffic passes.
 # Every GPU step has its own time limit; the script stops at the first failing GPU step.
-# usage: bash tools/gpu_session.sh TAG [steps...]   steps: tests conv bench prof pmc smoke
+# usage: bash tools/gpu_session.sh TAG [steps...]   steps: tests bench prof pmc smoke
 set -u
 TAG=${1:-run}; shift
 STEPS=${*:-"tests bench prof"}
@@ -19,10 +19,9 @@ run() {  # name seconds cmd...
 }
 for s in $STEPS; do
   case $s in
-    tests) run tests 900 python -m pytest tests -m gpu -q --maxfail=30 -p no:cacheprovider
+    tests) run tests 900 python -u -m pytest tests -m gpu -q --maxfail=30 -p no:cacheprovider --timeout 300 --timeout-method thread
            rc=$?; grep -E "^FAILED" "$OUT/tests.log" | head -30; [ $rc -le 1 ] || exit $rc ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
-    conv)  run conv 300 python tools/bench_conv.py || exit $? ;;
     bench) run bench 400 python bench.py || exit $? ;;
     benchno) run benchno 300 python bench.py --steps 50 --no-overlap --no-cpu-baseline --fp32-steps 0 || exit $? ;;
     benchq) run benchq 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline || exit $? ;;

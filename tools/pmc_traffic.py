@@ -21,9 +21,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import conv_launches  # noqa: E402
 
 
-CONV_KERNELS = ("fast_gemm_kernel", "conv_pipe_kernel", "conv1x1_stream_kernel", "conv3x3_halo_kernel",
+CONV_KERNELS = ("fast_gemm_kernel", "conv_pipe_kernel", "conv1x1_stream_kernel",
                 "bottleneck_kernel", "conv_ws_kernel", "conv3x3_frag_kernel", "conv3x3_band_kernel",
-                "conv1x1_res_frag_kernel", "conv1x1_frag_kernel", "conv3x3_slice_kernel", "conv3x3_frag_dma_kernel")
+                "conv1x1_frag_kernel")
 
 
 def is_conv_kernel(name):
