@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--bert", action="store_true",
                     help="cfg5: frozen BERT word embeddings (V=30522, E=768, T=32), simple deep output (--ado off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=2, help="images in the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=8,
+                    help="images per step of the bounded CPU-baseline sample (the reference's cfg1 batch)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode: run the next batch's encoder after, not beside, this batch's decoder")
@@ -88,6 +89,27 @@ def parse():
 
 
 PEAK_HBM_ACHIEVABLE_GBS = 6300.0   # MI355X_MICROARCH.md §HBM (floor estimates only)
+
+_HIP = None
+
+
+def graph_event_record(event, stream=None):
+    """Record a timing event on ``stream`` so that it also works inside a hipGraph capture:
+    hipEventRecordWithFlags(..., hipEventRecordExternal) makes the capture keep it as an event-record
+    node, so every replay re-records it between the kernels around it (a plain record during capture
+    only becomes a dependency edge).  Outside capture it is an ordinary record."""
+    global _HIP
+    import ctypes
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so.7")   # the runtime torch already loaded (same soname)
+        _HIP.hipEventRecordWithFlags.restype = ctypes.c_int
+        _HIP.hipEventRecordWithFlags.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+    stream = stream or torch.cuda.current_stream()
+    if event.cuda_event == 0:   # torch creates the HIP event lazily on its first record: record it once
+        raise RuntimeError("graph_event_record: record the event once outside the capture first")
+    rc = _HIP.hipEventRecordWithFlags(ctypes.c_void_p(event.cuda_event), ctypes.c_void_p(stream.cuda_stream), 1)
+    if rc != 0:
+        raise RuntimeError(f"hipEventRecordWithFlags failed: {rc}")
 
 
 def conv_launches(network, B, H=224, fused=True):
@@ -233,10 +255,30 @@ def pmc_traffic(network, cls):
     return (per["hbm_bytes_per_launch"] if per else None), os.path.relpath(path, REPO)
 
 
+def usable_cores():
+    """(cores this process may run on, cores of the host): the affinity mask capped by a cgroup CPU
+    quota (a GPU box shares its host: os.cpu_count() reports the whole machine)."""
+    host = os.cpu_count() or 1
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else host
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(math.ceil(int(quota) / int(period)))))
+    except (OSError, ValueError):
+        pass
+    return n, host
+
+
 def cpu_baseline(args):
-    """Bounded CPU sample of the same step through the oracle (torch-CPU fp32 port)."""
+    """Bounded CPU sample of the same train step through the oracle (torch-CPU fp32 port of the
+    reference, oracle/sat_oracle.py), on every core this process may use, at --cpu-sample images per
+    step (the reference's own cfg1 batch is 8).  Two variants, each ~8-15 s of host work:
+    the frozen trunk (result-identical; the headline CPU number) and the reference as it runs,
+    whose ResNet152 parameters are not frozen so loss.backward() also back-propagates the whole
+    trunk (encoder.py:13-17 vs 29-31) -- gradients the optimiser never reads."""
     from oracle import sat_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads, host = usable_cores()
     torch.set_num_threads(threads)
     B = args.cpu_sample
     enc_p = O.make_resnet152_params(0) if args.network == "resnet152" else O.make_vgg19_params(0)
@@ -245,18 +287,36 @@ def cpu_baseline(args):
     dec_p = O.make_decoder_params(args.vocab, D, 512, True, 0)
     x = torch.randn(B, 3, 224, 224)
     caps = O.make_captions(B, args.seq, args.vocab, 0)
-    iters, t_total = 0, 0.0
-    while iters < 2 or (t_total < 12.0 and iters < 60):   # ~12 s of host work
-        t0 = time.perf_counter()
-        with torch.no_grad():
-            feats = fwd(enc_p, x)
-        _, _, dec_p, _, _ = O.train_step(dec_p, feats, caps, tf=not args.no_tf, ado=True, attention=True, lr=1e-4,
-                                         training=True, adam_state={})
-        t_total += time.perf_counter() - t0
-        iters += 1
-    return {"value": round(B * iters / t_total, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{iters} steps x {B} images (224x224, {args.network} fp32 trunk + decoder train step, "
-                      f"V={args.vocab}, T={args.seq}) through oracle/sat_oracle.py on host CPU"}
+
+    def run(dead_backward, budget_s, max_iters):
+        nonlocal dec_p
+        iters, t_total = 0, 0.0
+        p_enc = {k: (v.clone().requires_grad_(True) if dead_backward and v.is_floating_point() and "running" not in k
+                     else v) for k, v in enc_p.items()}   # conv / BN affine parameters (nn.Parameters)
+        while iters < 1 or (t_total < budget_s and iters < max_iters):
+            t0 = time.perf_counter()
+            if dead_backward:   # train() without no_grad: the trunk's graph is kept and back-propagated
+                feats = fwd(p_enc, x)
+            else:
+                with torch.no_grad():
+                    feats = fwd(p_enc, x)
+            _, _, dec_p, _, _ = O.train_step(dec_p, feats, caps, tf=not args.no_tf, ado=True, attention=True,
+                                             lr=1e-4, training=True, adam_state={})
+            t_total += time.perf_counter() - t0
+            iters += 1
+        return iters, t_total
+
+    run(False, 0.0, 1)   # warm-up (allocator, thread pool)
+    it_f, t_f = run(False, 10.0, 20)
+    it_d, t_d = run(True, 8.0, 10)
+    wl = f"224x224, {args.network} fp32 trunk + decoder train step, V={args.vocab}, T={args.seq}"
+    return {"value": round(B * it_f / t_f, 3), "unit": "images/s", "cores": threads, "host_cores": host,
+            "batch": B, "kind": "port",
+            "sample": f"{it_f} steps x {B} images ({wl}) through oracle/sat_oracle.py on {threads} of the host's "
+                      f"{host} cores (the process's CPU affinity / cgroup quota); frozen trunk",
+            "reference_as_run": {"value": round(B * it_d / t_d, 3), "unit": "images/s", "steps": it_d,
+                                 "note": "the same step with the reference's dead ResNet152 backward (trunk "
+                                         "parameters not frozen, encoder.py:13-17)"}}
 
 
 def decoder_step_roofline(dec, enc, imgs, caps, reps=20):
