@@ -79,6 +79,9 @@ def parse():
                     help="timed steps of the fp32 leg (the reference's precision, the exact-parity path; 0 = skip)")
     ap.add_argument("--no-diagnostics", action="store_true",
                     help="skip the per-kernel roofline measurements after the timed region")
+    ap.add_argument("--no-step-stamps", action="store_true",
+                    help="graph mode: no in-kernel launch timestamps in the encoder graphs (the in-step conv figures, "
+                         "LaunchStamps)")
     args = ap.parse_args()
     if args.bert:   # generate_json_data_bert.py:47,69: [CLS] + 30 + [SEP]; BertConfig() vocabulary
         args.vocab = 30522
@@ -90,26 +93,74 @@ def parse():
 
 PEAK_HBM_ACHIEVABLE_GBS = 6300.0   # MI355X_MICROARCH.md §HBM (floor estimates only)
 
-_HIP = None
+class LaunchStamps:
+    """In-kernel launch timestamps for a sequence of launches (SatPolicy.stamps): a device buffer of
+    ``cap`` workgroup slots {start, end} per launch, and one SatPolicy per launch pointing at its slice.
+    Every workgroup of a launch records when its first wave started and its last wave finished (the
+    device's 100 MHz real-time counter); the launch's span is max(end) - min(start) -- the kernel's own
+    duration, taken inside the timed, overlapped graph replays with no extra node, event or barrier in
+    the stream (every replay rewrites the slots; read after the timed region).  Event-record nodes
+    spliced into the graph between kernels cost ~3 us each and add that to every bracketed kernel
+    (tools/graph_event_probe.py), so in-step figures come from these stamps."""
+
+    def __init__(self, n_launches, device, base=None, cap=16384):
+        import sat_amd
+        self.n, self.cap = n_launches, cap
+        self.buf = torch.zeros(n_launches, cap, 2, dtype=torch.int64, device=device)
+        self.pols = []
+        for k in range(n_launches):
+            pol = sat_amd.Policy()
+            if base is not None:
+                __import__("ctypes").pointer(pol)[0] = base
+            pol.stamps = self.buf[k].data_ptr()
+            pol.stamp_capacity = cap
+            self.pols.append(pol)
+        self.used = 0
+
+    def next_policy(self):
+        if self.used >= self.n:
+            raise RuntimeError("LaunchStamps: more launches than slots")
+        self.used += 1
+        return self.pols[self.used - 1]
+
+    def spans_us(self):
+        """Per launch (in launch order): max(end) - min(start) over its workgroups, microseconds."""
+        st, en = self.buf[:self.used, :, 0], self.buf[:self.used, :, 1]
+        valid = st > 0
+        big = torch.iinfo(torch.int64).max
+        lo = torch.where(valid, st, torch.full_like(st, big)).min(dim=1).values
+        hi = torch.where(valid, en, torch.zeros_like(en)).max(dim=1).values
+        return [((h - l) / 100.0 if h > 0 else None) for l, h in zip(lo.tolist(), hi.tolist())]   # 100 MHz ticks
 
 
-def graph_event_record(event, stream=None):
-    """Record a timing event on ``stream`` so that it also works inside a hipGraph capture:
-    hipEventRecordWithFlags(..., hipEventRecordExternal) makes the capture keep it as an event-record
-    node, so every replay re-records it between the kernels around it (a plain record during capture
-    only becomes a dependency edge).  Outside capture it is an ordinary record."""
-    global _HIP
-    import ctypes
-    if _HIP is None:
-        _HIP = ctypes.CDLL("libamdhip64.so.7")   # the runtime torch already loaded (same soname)
-        _HIP.hipEventRecordWithFlags.restype = ctypes.c_int
-        _HIP.hipEventRecordWithFlags.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
-    stream = stream or torch.cuda.current_stream()
-    if event.cuda_event == 0:   # torch creates the HIP event lazily on its first record: record it once
-        raise RuntimeError("graph_event_record: record the event once outside the capture first")
-    rc = _HIP.hipEventRecordWithFlags(ctypes.c_void_p(event.cuda_event), ctypes.c_void_p(stream.cuda_stream), 1)
-    if rc != 0:
-        raise RuntimeError(f"hipEventRecordWithFlags failed: {rc}")
+class DecoderStamps:
+    """In-kernel timestamps of the decoder's per-step kernel groups (SatPolicy.stamps through
+    SatDecoderDims.policy): the library gives group g (diagnostics.GROUPS order) at step t the slot
+    g * (T-1) + t of ``cap`` workgroups; captured into the decoder graphs, every replay rewrites them."""
+
+    def __init__(self, T, device, base=None, cap=1024):
+        import sat_amd
+        from sat_amd.diagnostics import GROUPS
+        self.groups, self.T1, self.cap = GROUPS, T - 1, cap
+        self.buf = torch.zeros(len(GROUPS) * self.T1, cap, 2, dtype=torch.int64, device=device)
+        self.policy = sat_amd.Policy()
+        if base is not None:
+            __import__("ctypes").pointer(self.policy)[0] = base
+        self.policy.stamps = self.buf.data_ptr()
+        self.policy.stamp_capacity = cap
+
+    def group_spans_us(self):
+        st, en = self.buf[..., 0], self.buf[..., 1]
+        valid = st > 0
+        big = torch.iinfo(torch.int64).max
+        lo = torch.where(valid, st, torch.full_like(st, big)).min(dim=1).values.tolist()
+        hi = torch.where(valid, en, torch.zeros_like(en)).max(dim=1).values.tolist()
+        out = {}
+        for gi, g in enumerate(self.groups):
+            v = [(hi[k] - lo[k]) / 100.0 for k in range(gi * self.T1, (gi + 1) * self.T1) if hi[k] > 0]
+            if v:
+                out[g] = v
+        return out
 
 
 def conv_launches(network, B, H=224, fused=True):
@@ -165,10 +216,32 @@ def conv_launches(network, B, H=224, fused=True):
     return out
 
 
-def trunk_roofline(enc, imgs, launches, reps=3):
-    """Per-launch HIP events around every conv of `reps` eager forwards (on the launch stream)
-    -> per-class average duration, the dominant class and its roofline, and the whole trunk's
-    measured conv time against its roofline floor."""
+CONV_KERNEL_NAMES = ("fast_gemm_kernel", "conv_pipe_kernel", "conv1x1_stream_kernel", "bottleneck_kernel",
+                     "conv_ws_kernel", "conv3x3_frag_kernel", "conv3x3_band_kernel", "conv1x1_frag_kernel")
+
+
+def instep_conv_durations(stamps, launches):
+    """Per conv launch (conv_launches() order), its in-step durations [us] from the encoder graphs'
+    in-kernel timestamps (LaunchStamps, the last replay of each graph in the timed region)."""
+    per = [[] for _ in launches]
+    for st in stamps:
+        spans = st.spans_us()
+        if len(spans) != len(launches):
+            return None
+        for i, us in enumerate(spans):
+            if us is not None:
+                per[i].append(us)
+    return per
+
+
+def trunk_roofline(enc, imgs, launches, instep=None, reps=3):
+    """The encoder trunk against its roofline.
+
+    Dominant launch class and its ``achieved`` / ``frac``: from the IN-STEP durations when given (every
+    conv kernel of the timed, overlapped steps timed by its own in-kernel timestamps, LaunchStamps):
+    the figure a rocprofv3 kernel trace of the same command averages.  Secondary figures: the class's
+    launches of an eager forward re-issued back to back into warm caches (``avg_launch_us_b2b``) and an
+    event pair around every launch of ``reps`` eager forwards (``avg_launch_us_eager_event_pairs``)."""
     enc.timing, enc.timing_args = [], []
     with torch.no_grad():
         for _ in range(reps):
@@ -182,21 +255,27 @@ def trunk_roofline(enc, imgs, launches, reps=3):
     for r in range(reps):
         for i in range(n):
             st, en = ev[r * n + i]
-            dur[i] += st.elapsed_time(en) / reps   # ms
+            dur[i] += st.elapsed_time(en) / reps * 1e3   # us
+    if instep is not None:
+        step_dur = [sum(v) / len(v) if v else dur[i] for i, v in enumerate(instep)]
+    else:
+        step_dur = dur
     cls = {}
-    for l, d in zip(launches, dur):
-        c = cls.setdefault(l["cls"], dict(n=0, ms=0.0, flops=l["flops"], bytes=l["bytes"], bound=l["bound"],
-                                          fused=l.get("fused", False)))
+    for l, d, de in zip(launches, step_dur, dur):
+        c = cls.setdefault(l["cls"], dict(n=0, us=0.0, us_eager=0.0, flops=l["flops"], bytes=l["bytes"],
+                                          bound=l["bound"], fused=l.get("fused", False)))
         c["n"] += 1
-        c["ms"] += d
-    name, dom = max(cls.items(), key=lambda kv: kv[1]["ms"])
-    avg_event_us = dom["ms"] / dom["n"] * 1e3
-    # the dominant class's launches of the last forward re-issued back to back (same inputs, 5 each)
-    # between two events: the per-launch average without an event pair around every kernel
-    from sat_amd import ops
+        c["us"] += d
+        c["us_eager"] += de
+    name, dom = max(cls.items(), key=lambda kv: kv[1]["us"])
     idx = [i for i, l in enumerate(launches) if l["cls"] == name]
+    avg_us = dom["us"] / dom["n"]
+    samples = sum(len(instep[i]) for i in idx) if instep is not None else 0
+    # the dominant class's launches of the last forward re-issued back to back (same inputs, 5 each)
+    from sat_amd import ops
     last = conv_args[(reps - 1) * n:]
     b2b = 5
+
     def launch(a):
         if a[0] == "fused":
             ops.bottleneck_fused(a[1], *a[2])
@@ -218,29 +297,37 @@ def trunk_roofline(enc, imgs, launches, reps=3):
                 launch(last[i])
         en.record()
     en.synchronize()
-    avg_s = st.elapsed_time(en) / (len(idx) * b2b) * 1e-3
-    if dom["bound"] == "hbm":
-        achieved, peak, unit = dom["bytes"] / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
-    else:
-        achieved, peak, unit = dom["flops"] / avg_s / 1e12, BF16_DENSE_PEAK_TFLOPS, "TFLOP/s"
+    b2b_us = st.elapsed_time(en) / (len(idx) * b2b) * 1e3
+
+    def rate(us):
+        if dom["bound"] == "hbm":
+            return dom["bytes"] / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s"
+        return dom["flops"] / (us * 1e-6) / 1e12, BF16_DENSE_PEAK_TFLOPS, "TFLOP/s"
+    achieved, peak, unit = rate(avg_us)
     floor_us = sum(max(l["flops"] / (BF16_DENSE_PEAK_TFLOPS * 1e12), l["bytes"] / (PEAK_HBM_ACHIEVABLE_GBS * 1e9))
                    for l in launches) * 1e6
-    trunk_us = sum(dur) * 1e3
+    trunk_us = sum(step_dur)
     kname = "bottleneck_kernel (csrc/convblock.hip), fused block" if dom.get("fused") else (
         "conv3x3_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c2frag" for i in idx)
         else "conv1x1_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c1frag" for i in idx)
         else "conv kernels, conv class")
+    timing = (f"avg_launch_us: in-step -- every launch of the class in the last replay of each encoder graph of "
+              f"the timed, overlapped region ({samples} launches), timed by the kernels' own first-start / last-end "
+              f"timestamps (LaunchStamps); avg_launch_us_b2b: the class re-issued back to back into warm caches; "
+              f"avg_launch_us_eager_event_pairs: an event pair around every launch of {reps} eager forwards"
+              if instep is not None else
+              "avg_launch_us: an event pair around every launch of three eager forwards (no graph timers)")
     return dict(kernel=f"{kname} {name} ({dom['n']} launches/forward)", cls=name,
                 bound=dom["bound"], achieved=round(achieved, 2), peak=peak, unit=unit,
-                frac=round(achieved / peak, 4), avg_launch_us=round(avg_s * 1e6, 2),
-                avg_launch_us_event_pairs=round(avg_event_us, 2),
-                timing="avg_launch_us: the class's launches re-issued back to back between two HIP events; "
-                       "event_pairs: an event pair around every launch of three eager forwards",
-                algorithmic_bytes_per_launch=dom["bytes"], algorithmic_flops_per_launch=dom["flops"]), \
-        dict(conv_us_per_forward=round(trunk_us, 1), roofline_floor_us=round(floor_us, 1),
-             frac_of_floor=round(floor_us / trunk_us, 4),
-             classes={k: dict(n=v["n"], us=round(v["ms"] * 1e3, 1)) for k, v in
-                      sorted(cls.items(), key=lambda kv: -kv[1]["ms"])})
+                frac=round(achieved / peak, 4), avg_launch_us=round(avg_us, 2),
+                avg_launch_us_b2b=round(b2b_us, 2), frac_b2b=round(rate(b2b_us)[0] / peak, 4),
+                avg_launch_us_eager_event_pairs=round(dom["us_eager"] / dom["n"], 2),
+                timing=timing, algorithmic_bytes_per_launch=dom["bytes"], algorithmic_flops_per_launch=dom["flops"]), \
+        dict(conv_us_per_forward=round(trunk_us, 1), conv_us_per_forward_eager=round(sum(dur), 1),
+             roofline_floor_us=round(floor_us, 1), frac_of_floor=round(floor_us / trunk_us, 4),
+             timing="in-step (graph event nodes) when available, else eager event pairs",
+             classes={k: dict(n=v["n"], us=round(v["us"], 1), us_eager=round(v["us_eager"], 1)) for k, v in
+                      sorted(cls.items(), key=lambda kv: -kv[1]["us"])})
 
 
 def pmc_traffic(network, cls):
@@ -319,31 +406,50 @@ def cpu_baseline(args):
                                          "parameters not frozen, encoder.py:13-17)"}}
 
 
-def decoder_step_roofline(dec, enc, imgs, caps, reps=20):
-    """The per-time-step decoder kernels (fused attention + LSTM step and the skinny per-step
-    GEMMs) timed live: each group of the middle step re-issued `reps` times between HIP events on
-    the launch stream (sat_decoder_step_bench); achieved = algorithmic bytes / time vs 8 TB/s."""
+def decoder_step_roofline(dec, enc, imgs, caps, instep=None, reps=20):
+    """The per-time-step decoder kernels (the fused attention + LSTM step of SURVEY 8(d) and the per-step
+    GEMMs) against 8 TB/s: algorithmic bytes per launch / time.  ``us``: in-step (every per-step launch of
+    the last replay of each decoder graph in the timed region, from the kernels' own timestamps,
+    DecoderStamps) when given; ``us_b2b``:
+    each group of the middle step re-issued ``reps`` times back to back between HIP events
+    (sat_decoder_step_bench)."""
     from sat_amd.diagnostics import FUSED, decoder_step_kernels
     with torch.no_grad():
         feats = enc(imgs)
-    times, by = decoder_step_kernels(dec, feats, caps, reps=reps)
+    times_b2b, by = decoder_step_kernels(dec, feats, caps, reps=reps)
+    times = dict(times_b2b)
+    n_samples = {}
+    if instep:
+        for g, v in instep.items():
+            if v:
+                times[g] = sum(v) / len(v)
+                n_samples[g] = len(v)
+
+    def frac(b, us):
+        return b / (us * 1e-6) / 1e9 / HBM_PEAK_GBS
     groups = {}
     for g, us in times.items():
         if us <= 0 or by[g] <= 0:
             continue
-        groups[g] = {"us": round(us, 2), "mb": round(by[g] / 1e6, 2), "gbs": round(by[g] / (us * 1e-6) / 1e9, 1),
-                     "frac": round(by[g] / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+        groups[g] = {"us": round(us, 2), "us_b2b": round(times_b2b[g], 2), "mb": round(by[g] / 1e6, 2),
+                     "gbs": round(by[g] / (us * 1e-6) / 1e9, 1), "frac": round(frac(by[g], us), 4),
+                     "in_step_launches": n_samples.get(g, 0)}
     f_by = sum(by[g] for g in FUSED if g in groups)
     f_us = sum(times[g] for g in FUSED if g in groups)
+    f_b2b = sum(times_b2b[g] for g in FUSED if g in groups)
     a_by = sum(by[g] for g in groups)
     a_us = sum(times[g] for g in groups)
-    return {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "timing": f"each group of step (T-1)/2 re-issued "
-            f"{reps}x back to back between HIP events", "groups": groups,
+    a_b2b = sum(times_b2b[g] for g in groups)
+    src = ("us: in-step (the per-step kernels of the timed region's decoder graphs, first-start to last-end "
+           "in-kernel timestamps); us_b2b: "
+           if instep else "us: ") + f"each group of step (T-1)/2 re-issued {reps}x back to back between HIP events"
+    return {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "timing": src, "groups": groups,
             "fused_attention_lstm": {"kernels": list(FUSED), "us_per_step": round(f_us, 2),
                                      "achieved": round(f_by / (f_us * 1e-6) / 1e9, 1),
-                                     "frac": round(f_by / (f_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)},
+                                     "frac": round(frac(f_by, f_us), 4), "us_per_step_b2b": round(f_b2b, 2),
+                                     "frac_b2b": round(frac(f_by, f_b2b), 4)},
             "all_step_kernels": {"us_per_step": round(a_us, 2), "achieved": round(a_by / (a_us * 1e-6) / 1e9, 1),
-                                 "frac": round(a_by / (a_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}}
+                                 "frac": round(frac(a_by, a_us), 4), "us_per_step_b2b": round(a_b2b, 2)}}
 
 
 def fp32_step(args, enc, dec, imgs, caps, pad_id, skip_ids, world):
@@ -451,6 +557,7 @@ def main():
     use_graph = not args.no_graph
     overlap = use_graph and not args.no_overlap
     g_encA = None
+    stamps_enc, stamps_dec = [], []   # in-kernel timestamps: LaunchStamps per encoder graph, DecoderStamps per pair
     if use_graph:
         # hipGraphs: the encoder trunk (so its kernels can be bracketed with events) and decoder
         # fwd + loss + BPTT.  Adam and the RCCL all-reduce run eagerly after replay (Adam's bias
@@ -464,6 +571,7 @@ def main():
         split = 0
         if overlap and args.network == "resnet152" and args.enc_split != "none":
             split = enc.stage_starts()[{"layer2": 1, "layer3": 2, "layer4": 3}[args.enc_split]]
+        stamp_enc = not args.no_step_stamps and not split
         g_encA = [torch.cuda.CUDAGraph() for _ in range(nbuf)] if split else None
         # one private memory pool per graph: no intermediate of one graph aliases another's
         g_enc = [torch.cuda.CUDAGraph() for _ in range(nbuf)]
@@ -480,14 +588,22 @@ def main():
                     with torch.no_grad():
                         feats_static.append(enc(mid, steps=(split, n_plan)))
             else:
+                if stamp_enc:   # every conv launch of this graph writes its in-kernel timestamps
+                    stamps_enc.append(LaunchStamps(len(conv_launches(args.network, B, fused=enc.fuse_blocks)), dev,
+                                                   base=policy))
+                    enc.launch_policy = stamps_enc[-1].next_policy
                 with torch.cuda.graph(g_enc[k]):
                     with torch.no_grad():
                         feats_static.append(enc(imgs))
+                enc.launch_policy = None
         # backward phase 1 (output head) and phase 2 (BPTT) as two graphs, the head bucket's all-reduce
         # (N > 1) issued between them; --bwd serial: one graph
         split_bwd = world > 1 or args.bwd == "split"
         dec.defer_recurrent_backward(split_bwd)
         for k in range(nbuf):
+            if not args.no_step_stamps:   # the per-step kernels of this graph pair write in-kernel timestamps
+                stamps_dec.append(DecoderStamps(args.seq, dev, base=policy))
+                dec.policy = stamps_dec[-1].policy
             opt.zero_grad(set_to_none=True)   # each capture overwrites the gradients (beta = 0)
             with torch.cuda.graph(g_dec[k]):
                 preds, alphas = dec(feats_static[k], caps)
@@ -499,6 +615,7 @@ def main():
             else:
                 g_rec[k] = None
             loss_static.append(loss_k)
+            dec.policy = policy
         dec.defer_recurrent_backward(False)
         torch.cuda.synchronize()
 
@@ -592,8 +709,15 @@ def main():
     enc_ms = sum(s.elapsed_time(e) for s, e in enc_events) if use_graph else None
     loss_v = loss.item()
     diag = rank == 0 and not args.no_diagnostics
-    roof, trunk = trunk_roofline(enc, imgs, launches) if diag else (None, None)
-    step_kernels = decoder_step_roofline(dec, enc, imgs, caps) if diag else None
+    instep_conv = instep_conv_durations(stamps_enc, launches) if stamps_enc else None
+    instep_dec = None
+    if stamps_dec:
+        instep_dec = {}
+        for sd in stamps_dec:
+            for g, v in sd.group_spans_us().items():
+                instep_dec.setdefault(g, []).extend(v)
+    roof, trunk = trunk_roofline(enc, imgs, launches, instep=instep_conv) if diag else (None, None)
+    step_kernels = decoder_step_roofline(dec, enc, imgs, caps, instep=instep_dec) if diag else None
     fp32_leg = fp32_step(args, enc, dec, imgs, caps, pad_id, skip_ids, world) if world == 1 and args.fp32_steps > 0 \
         else None
     if roof is not None:

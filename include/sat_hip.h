@@ -64,6 +64,12 @@ typedef struct {
   int attn_bwd;         /* attention backward per decoder step: 0 auto, 1 the two-launch form */
   int decoder_splits[4];/* split-K counts of the per-step bf16 decoder GEMMs -- h: [U; f_beta; W_hh] h, c: context
                          * part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic */
+  /* diagnostics (bench.py's in-step kernel timing): when non-null, every workgroup w < stamp_capacity of the
+   * call's launch writes {first-wave start, last-wave end} of the device's 100 MHz real-time counter to
+   * stamps[2 w], stamps[2 w + 1] (device memory); the launch's span = max(end) - min(start).  Captured
+   * into a hipGraph, every replay rewrites them. */
+  uint64_t* stamps;
+  int stamp_capacity;
 } SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),
@@ -152,7 +158,7 @@ int sat_bottleneck_fused_supported(int H, int W, int Cin, int Cmid, int dtype);
  * Bit-identical to the three sat_conv2d_nhwc launches it replaces. */
 int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int dtype, const void* x, const void* w1f,
                          const float* b1, const void* w2f, const float* b2, const void* w3f, const float* b3,
-                         void* y, void* stream);
+                         void* y, const SatPolicy* policy, void* stream);
 /* 1 if sat_conv3x3_frag runs this geometry (today: bf16, 14x14, C 256 -- the c2 of ResNet152's layer3
  * identity blocks), else 0. */
 int sat_conv3x3_frag_supported(int H, int W, int C, int dtype);
@@ -161,7 +167,7 @@ int sat_conv3x3_frag_supported(int H, int W, int C, int dtype);
  * streamed register-direct.  x, y NHWC [N,H,W,C] (x != y); wf: sat_mfma_frag_layout of the folded
  * [C][3*3*C] (tap-major) weight; b: fp32 bias.  Bit-identical to sat_conv2d_nhwc on the same operands. */
 int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const void* x, const void* wf, const float* b, void* y,
-                     void* stream);
+                     const SatPolicy* policy, void* stream);
 /* 1 if sat_conv1x1_frag runs this geometry (today: bf16, 14x14, Cin 1024, Cout 256 -- the c1 of ResNet152's
  * layer3 identity blocks), else 0. */
 int sat_conv1x1_frag_supported(int H, int W, int Cin, int Cout, int dtype);
@@ -170,7 +176,7 @@ int sat_conv1x1_frag_supported(int H, int W, int Cin, int Cout, int dtype);
  * [N,H,W,Cout] (x != y); wf: sat_mfma_frag_layout of the folded [Cout][Cin] weight.  Bit-identical to
  * sat_conv2d_nhwc. */
 int sat_conv1x1_frag(int N, int H, int W, int Cin, int Cout, int dtype, const void* x, const void* wf,
-                     const float* b, void* y, void* stream);
+                     const float* b, void* y, const SatPolicy* policy, void* stream);
 /* MaxPool2d (floor mode, -inf padding) on NHWC. */
 int sat_maxpool2d_nhwc(int N, int H, int W, int C, int k, int stride, int pad, int dtype,
                        const void* x, void* y, int OH, int OW, void* stream);

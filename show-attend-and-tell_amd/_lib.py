@@ -32,7 +32,7 @@ class SatPolicy(ctypes.Structure):
     """Per-call kernel selection (include/sat_hip.h SatPolicy); all zeros = the library's defaults."""
     _fields_ = [(n, c_int) for n in ("conv_pipe", "conv_stream", "conv3x3_ws", "skinny", "gemm_stages", "gemm_tile",
                                      "gemm_linear_order", "gemm_epilogue", "attn_bwd")] + \
-               [("decoder_splits", c_int * 4)]
+               [("decoder_splits", c_int * 4), ("stamps", c_void_p), ("stamp_capacity", c_int)]
 
     def __init__(self, **kw):
         splits = kw.pop("decoder_splits", None)
@@ -83,13 +83,14 @@ _SIGNATURES = [
     ("sat_mfma_frag_layout", c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p]),
     ("sat_bottleneck_fused_supported", c_int, [c_int, c_int, c_int, c_int, c_int]),
     ("sat_bottleneck_fused", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(SatPolicy),
+                                     c_void_p]),
     ("sat_conv3x3_frag_supported", c_int, [c_int, c_int, c_int, c_int]),
     ("sat_conv3x3_frag", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                                 c_void_p]),
+                                 ctypes.POINTER(SatPolicy), c_void_p]),
     ("sat_conv1x1_frag_supported", c_int, [c_int, c_int, c_int, c_int, c_int]),
     ("sat_conv1x1_frag", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                                 c_void_p]),
+                                 ctypes.POINTER(SatPolicy), c_void_p]),
     ("sat_maxpool2d_nhwc", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                    c_int, c_int, c_void_p]),
     ("sat_attention_forward", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -87,7 +87,7 @@ constexpr int ANW = 8, FU = 8;
 constexpr int FNW = 16, FDV = 2, FFU = 4;
 
 template <typename T, int CH>   // CH = e-chunks of 64 x 16 bytes per lane covering E
-__global__ __launch_bounds__(FNW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
+__device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   constexpr int VN = V16<T>::N;            // elements per 16-byte vector
   constexpr int COLS = 64 * VN * FDV;      // context columns of one workgroup
   __shared__ float s_alpha[kMaxL];
@@ -258,11 +258,18 @@ __global__ __launch_bounds__(FNW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
   }
 }
 
+template <typename T, int CH>   // CH = e-chunks of 64 x 16 bytes per lane covering E
+__global__ __launch_bounds__(FNW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
+  const uint64_t t0 = sat_stamp_begin(a.st);
+  attn_fwd_kernel_body<T, CH>(a);
+  sat_stamp_end(a.st, t0);
+}
+
 // grid (B, NS): dL/dcontext for the workgroup's D-slice is formed ONCE (thread per column: the
 // gated-context slabs, gate, context, head term; the gate gradient written on the way) into LDS,
 // then every wave dots it with its slots' annotation rows (requested at kernel entry).
 template <typename T>
-__global__ __launch_bounds__(ANW * 64) void attn_bwd1_kernel(AttnBwdArgs a) {
+__device__ __forceinline__ void attn_bwd1_kernel_body(AttnBwdArgs a) {
   constexpr int VD = V16<T>::N;
   constexpr int COLS = 64 * VD;
   __shared__ float s_dctx[COLS];
@@ -319,6 +326,13 @@ __global__ __launch_bounds__(ANW * 64) void attn_bwd1_kernel(AttnBwdArgs a) {
   }
 }
 
+template <typename T>
+__global__ __launch_bounds__(ANW * 64) void attn_bwd1_kernel(AttnBwdArgs a) {
+  const uint64_t t0 = sat_stamp_begin(a.st);
+  attn_bwd1_kernel_body<T>(a);
+  sat_stamp_end(a.st, t0);
+}
+
 // grid (B, E / 256): a workgroup of 8 waves per (row, 256-wide e-slice); lane owns 4 consecutive
 // e, waves take BFU slots each per batch, so a row's 49 slots are two batches of loads in flight.
 // The softmax backward (a few hundred flops per row) is recomputed by each slice.
@@ -331,7 +345,7 @@ __device__ __forceinline__ void load_e4(const T* p, bool ok, float* o) {
 }
 
 template <typename T>
-__global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
+__device__ __forceinline__ void attn_bwd2_kernel_body(AttnBwdArgs a, int NS) {
   __shared__ float s_de[kMaxL];
   __shared__ float s_red[BNW][BSLICE];
   __shared__ float s_tmp[BNW];
@@ -436,6 +450,13 @@ __global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int 
   }
 }
 
+template <typename T>
+__global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
+  const uint64_t t0 = sat_stamp_begin(a.st);
+  attn_bwd2_kernel_body<T>(a, NS);
+  sat_stamp_end(a.st, t0);
+}
+
 // One launch for the whole attention backward of a step (replaces attn_bwd1 + attn_bwd2): one
 // 16-wave workgroup per batch row b.  The two-launch form existed only because dL/dalpha needs a
 // reduction over D and the softmax / tanh backward needs all of it; with the whole row in one
@@ -454,7 +475,7 @@ __global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int 
 // >= L keeps a row's annotation rows in one batch of loads: 16 x 4 at D <= 1024 elements per 16 B,
 // 8 x 7 (256 VGPRs per lane) at ResNet152's D = 2048)
 template <typename T, int DCH, int ECH, int FBW, int FBU>
-__global__ __launch_bounds__(FBW * 64) void attn_bwd_fused_kernel(AttnBwdArgs a) {
+__device__ __forceinline__ void attn_bwd_fused_kernel_body(AttnBwdArgs a) {
   constexpr int VN = V16<T>::N;
   __shared__ float s_dctx[64 * VN * DCH];
   __shared__ float s_de[kMaxL];
@@ -648,6 +669,13 @@ __global__ __launch_bounds__(FBW * 64) void attn_bwd_fused_kernel(AttnBwdArgs a)
   }
 }
 
+template <typename T, int DCH, int ECH, int FBW, int FBU>
+__global__ __launch_bounds__(FBW * 64) void attn_bwd_fused_kernel(AttnBwdArgs a) {
+  const uint64_t t0 = sat_stamp_begin(a.st);
+  attn_bwd_fused_kernel_body<T, DCH, ECH, FBW, FBU>(a);
+  sat_stamp_end(a.st, t0);
+}
+
 // After the time loop: dWs[b,l,e] = sum over t = T1-1 .. 0 of de[b,t,l] v[e] (1 - tanh^2(Ws[b,l,e] +
 // uh[b,t,e])) -- the per-element expression and summation order of the per-step accumulation it
 // replaces, so the fp32 path is bit-identical to it.  A wave owns DWS_LG rows l of one batch row b
@@ -740,7 +768,9 @@ void launch_fwd(int ch, dim3 grid, hipStream_t s, const AttnFwdArgs& a) {
 
 }  // namespace
 
-int sat_attention_fwd_launch(const AttnFwdArgs& a, hipStream_t s) {
+int sat_attention_fwd_launch(const AttnFwdArgs& args, hipStream_t s) {
+  AttnFwdArgs a = args;
+  a.st = sat_launch_stamps();
   const int VD = a.dtype == SAT_BF16 ? 8 : 4;
   SAT_REQUIRE(a.L <= kMaxL && a.E % VD == 0 && a.E <= 1024);
   SAT_REQUIRE((a.uh_ld % 4) == 0 && (a.hg_splits <= 1 || a.hg_split_stride % 4 == 0));
@@ -783,7 +813,9 @@ bool launch_bwd_fused(const AttnBwdArgs& a, hipStream_t s) {
 
 }  // namespace
 
-int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s) {
+int sat_attention_bwd_launch(const AttnBwdArgs& args, hipStream_t s) {
+  AttnBwdArgs a = args;
+  a.st = sat_launch_stamps();
   const int VD = a.dtype == SAT_BF16 ? 8 : 4;
   SAT_REQUIRE(a.L <= kMaxL && a.E % VD == 0 && a.E <= 1024);
   SAT_REQUIRE(a.D % VD == 0);

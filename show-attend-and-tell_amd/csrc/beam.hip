@@ -245,6 +245,7 @@ extern "C" int sat_decoder_beam_search(const SatDecoderDims* dp, const SatDecode
   SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
   SAT_REQUIRE(beam_size <= max_step + 2);  // out_alphas holds (max_step + 2) * L floats
   SatPolicyScope scope(dp->policy);
+  SatStampScope no_stamps(nullptr, 0);
   const SatDecoderDims& d = *dp;
   const int R = beam_size, L = d.L, D = d.D, E = d.E, V = d.V;
   const size_t ts = d.dtype == SAT_BF16 ? 2 : 4;

@@ -43,6 +43,7 @@ struct WArgs {
   int N, H, W;                           // images, height, width (= output height, width)
   int items, items_per_img, tiles_x;     // items = N * (H / TR) * tiles_x
   unsigned x_bytes, y_bytes;
+  SatStamps st;                      // in-kernel launch timestamps (SatPolicy::stamps)
 };
 
 template <int N>
@@ -55,7 +56,7 @@ __device__ __forceinline__ void w_wait_barrier_n() {
 // 3x3 convs; 4 / 16 / 2: ResNet152's stem as a 4x4 conv over the 2x2 space-to-depth input);
 // TR x TW output pixels per item (TR * TW = 224); HP halo pixels, DMA rounds of 8 KB (16 B per lane)
 template <int KK, int C, int PADT, int TR, int TW, int NSTG, int ACT>
-__global__ __launch_bounds__(WS_NW * 64) void conv_ws_kernel(WArgs a) {
+__device__ __forceinline__ void conv_ws_kernel_body(const WArgs& a) {
   static_assert(TR * TW == 2 * WS_MB * 16, "224 pixels per item");
   static_assert(NSTG == 2 || NSTG == 3, "ring depth");
   static_assert(C == 64 || C == 16, "8 or 2 16-B chunks per pixel");
@@ -195,6 +196,13 @@ __global__ __launch_bounds__(WS_NW * 64) void conv_ws_kernel(WArgs a) {
   }
 }
 
+template <int KK, int C, int PADT, int TR, int TW, int NSTG, int ACT>
+__global__ __launch_bounds__(WS_NW * 64) void conv_ws_kernel(WArgs a) {
+  const uint64_t t0 = sat_stamp_begin(a.st);
+  conv_ws_kernel_body<KK, C, PADT, TR, TW, NSTG, ACT>(a);
+  sat_stamp_end(a.st, t0);
+}
+
 int g_ws_cus = 0;    // CU count (queried once)
 
 inline bool wal16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -241,6 +249,7 @@ int sat_conv3x3_ws_try(const SatGemm& g, hipStream_t s, int* err) {
   a.items_per_img = (cv.H / TR) * a.tiles_x;
   a.items = cv.N * a.items_per_img;
   a.x_bytes = (unsigned)xb; a.y_bytes = (unsigned)yb;
+  a.st = sat_launch_stamps();
   // the stem variant (72 KB of LDS, 108 VGPRs) fits two workgroups per CU
   const int slots = g_ws_cus * (stem ? 2 : 1);
   const int grid = a.items < slots ? a.items : slots;

@@ -60,6 +60,7 @@ struct KArgs {
   const float* b1; const float* b2; const float* b3;
   bf16* y;            // [N][IH][IW][CIN]
   unsigned x_bytes;
+  SatStamps st;                      // in-kernel launch timestamps (SatPolicy::stamps)
 };
 
 template <int N>
@@ -403,7 +404,9 @@ __device__ __forceinline__ void bottleneck_body(const KArgs& a) {
 
 template <int PF, int ABL>
 __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
+  const uint64_t t0 = sat_stamp_begin(a.st);
   bottleneck_body<14, 7, 1024, 256, PF, ABL>(a);
+  sat_stamp_end(a.st, t0);
 }
 
 // The bottleneck's c2 phase as a conv of its own (the layer3 blocks the trunk leaves unfused, so the
@@ -638,8 +641,11 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
 
 template <int PF>
 __global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
-                                                           const float* __restrict__ bias, bf16* __restrict__ y) {
+                                                           const float* __restrict__ bias, bf16* __restrict__ y,
+                                                           SatStamps st) {
+  const uint64_t t0 = sat_stamp_begin(st);
   conv3x3_band_body<28, 7, 128, 1, 1, PF>(x, wf, bias, y);
+  sat_stamp_end(st, t0);
 }
 
 
@@ -751,15 +757,20 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
 
 __global__ __launch_bounds__(512) void conv1x1_frag_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
-                                                           unsigned x_bytes) {
+                                                           unsigned x_bytes, SatStamps st) {
+  const uint64_t t0 = sat_stamp_begin(st);
   conv1x1_frag_body<14, 7, 1024, 256, 2>(x, wf, bias, y, x_bytes);
+  sat_stamp_end(st, t0);
 }
 
 
 template <int PF>
 __global__ __launch_bounds__(512) void conv3x3_frag_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
-                                                           const float* __restrict__ bias, bf16* __restrict__ y) {
+                                                           const float* __restrict__ bias, bf16* __restrict__ y,
+                                                           SatStamps st) {
+  const uint64_t t0 = sat_stamp_begin(st);
   conv3x3_frag_body<14, 7, 256, PF>(x, wf, bias, y);
+  sat_stamp_end(st, t0);
 }
 
 // [N][K] bf16 -> [N/16][K/32][64 lanes][8]: lane l = (fh << 4) | fr holds row 16 nb + fr, k 32 ks + 8 fh ..
@@ -794,8 +805,9 @@ extern "C" int sat_bottleneck_fused_supported(int H, int W, int Cin, int Cmid, i
 
 extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int dtype, const void* x, const void* w1f,
                                     const float* b1, const void* w2f, const float* b2, const void* w3f,
-                                    const float* b3, void* y, void* stream) {
+                                    const float* b3, void* y, const SatPolicy* policy, void* stream) {
   SAT_REQUIRE(N > 0 && x && w1f && w2f && w3f && b1 && b2 && b3 && y && x != y);
+  SatPolicyScope scope(policy);
   SAT_REQUIRE(sat_bottleneck_fused_supported(H, W, Cin, Cmid, dtype));
   auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
   SAT_REQUIRE(al(x, 16) && al(y, 16) && al(w1f, 16) && al(w2f, 16) && al(w3f, 16) && al(b1, 16) && al(b2, 16) &&
@@ -807,6 +819,7 @@ extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int 
   a.w1 = (const bf16*)w1f; a.w2 = (const bf16*)w2f; a.w3 = (const bf16*)w3f;
   a.b1 = b1; a.b2 = b2; a.b3 = b3;
   a.x_bytes = (unsigned)x_bytes;
+  a.st = sat_launch_stamps();
   hipLaunchKernelGGL((bottleneck_kernel<2, 0>), dim3(2 * N), dim3(512), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
@@ -816,8 +829,10 @@ extern "C" int sat_conv3x3_frag_supported(int H, int W, int C, int dtype) {
 }
 
 extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const void* x, const void* wf, const float* b,
-                                void* y, void* stream) {
+                                void* y, const SatPolicy* policy, void* stream) {
   SAT_REQUIRE(N > 0 && x && wf && b && y && x != y);
+  SatPolicyScope scope(policy);
+  const SatStamps st = sat_launch_stamps();
   SAT_REQUIRE(sat_conv3x3_frag_supported(H, W, C, dtype));
   auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
   SAT_REQUIRE(al(x, 16) && al(y, 16) && al(wf, 16) && al(b, 16));
@@ -825,9 +840,9 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   const bf16 *xp = (const bf16*)x, *wp = (const bf16*)wf;
   bf16* yp = (bf16*)y;
   if (H == 28)   // layer2 c2: 7-row bands, four workgroups per image
-    hipLaunchKernelGGL(conv3x3_band_kernel<2>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp);
+    hipLaunchKernelGGL(conv3x3_band_kernel<2>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp, st);
   else           // layer3 c2: half images, two workgroups per image
-    hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp);
+    hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp, st);
   return (int)hipGetLastError();
 }
 
@@ -836,14 +851,15 @@ extern "C" int sat_conv1x1_frag_supported(int H, int W, int Cin, int Cout, int d
 }
 
 extern "C" int sat_conv1x1_frag(int N, int H, int W, int Cin, int Cout, int dtype, const void* x, const void* wf,
-                                const float* b, void* y, void* stream) {
+                                const float* b, void* y, const SatPolicy* policy, void* stream) {
   SAT_REQUIRE(N > 0 && x && wf && b && y && x != y);
   SAT_REQUIRE(sat_conv1x1_frag_supported(H, W, Cin, Cout, dtype));
+  SatPolicyScope scope(policy);
   auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
   SAT_REQUIRE(al(x, 16) && al(y, 16) && al(wf, 16) && al(b, 16));
   const long x_bytes = 2L * N * H * W * Cin;
   SAT_REQUIRE(x_bytes < (1L << 31));
   hipLaunchKernelGGL(conv1x1_frag_kernel, dim3(2 * N), dim3(512), 0, (hipStream_t)stream, (const bf16*)x,
-                     (const bf16*)wf, b, (bf16*)y, (unsigned)x_bytes);
+                     (const bf16*)wf, b, (bf16*)y, (unsigned)x_bytes, sat_launch_stamps());
   return (int)hipGetLastError();
 }

@@ -54,6 +54,7 @@ struct FArgs {
   int xcd_remap;
   int partial; long split_stride;   // partial-output split-K: split s stores plain into C + s*split_stride
   int res_lds;             // fast_gemm_kernel<..., RL = true> epilogue (host-checked shape)
+  SatStamps st;                      // in-kernel launch timestamps (SatPolicy::stamps)
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -121,7 +122,7 @@ __device__ __forceinline__ void wait_vm_barrier() {
 // residual tile is DMA'd into the free ring stage during the last k-tile, added in the MFMA
 // accumulator layout (ds_read_b64_tr_b16), and the finished bf16 tile is staged for 16-B row stores.
 template <int BM, int BN, int WGM, int WGN, bool AT, bool BT, int NS, bool RL = false>
-__global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
+__device__ __forceinline__ void fast_gemm_kernel_body(const FArgs& a) {
   constexpr int NW = WGM * WGN;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int MI = WTM / 16, NJ = WTN / 16;
@@ -470,6 +471,13 @@ __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
   }   // !RL
 }
 
+template <int BM, int BN, int WGM, int WGN, bool AT, bool BT, int NS, bool RL = false>
+__global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
+  const uint64_t t0 = sat_stamp_begin(a.st);
+  fast_gemm_kernel_body<BM, BN, WGM, WGN, AT, BT, NS, RL>(a);
+  sat_stamp_end(a.st, t0);
+}
+
 __device__ __attribute__((aligned(16))) bf16 g_zero16[64];
 
 // tile configurations (ids of SatPolicy::gemm_tile)
@@ -604,6 +612,7 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
     a.stride = g.conv.stride; a.pad = g.conv.pad; a.OH = g.conv.OH; a.OW = g.conv.OW;
   }
   a.xcd_remap = pol.gemm_linear_order ? 0 : 1;
+  a.st = sat_launch_stamps();
   a.res_lds = res_lds && (tcfg == T128x128W8 || tcfg == T128x64W8) && !at && !bt && a.splitk == 1 && !partial &&
               a.c_bf16 && (!g.add1 || (a.add1_bf16 && g.ld_add1 % 8 == 0)) && g.N % bn == 0 && g.ldc % 8 == 0 &&
               al16(g.C) &&

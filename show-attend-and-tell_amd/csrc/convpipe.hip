@@ -58,6 +58,7 @@ struct PArgs {
   int xcd_remap;
   unsigned a_bytes, b_bytes;   // buffer-resource extents (offsets beyond them read zeros)
   int var;                     // experiment: bit 0 DMA after the first MFMA half, bit 1 split DMA, bit 2 no setprio
+  SatStamps st;                      // in-kernel launch timestamps (SatPolicy::stamps)
 };
 
 // s_waitcnt vmcnt(N) + raw s_barrier (never __syncthreads: its fence would drain the DMA ring)
@@ -88,7 +89,7 @@ __device__ __forceinline__ const void* psel(bool ok, const void* p, const void* 
 // ABL (diagnostics only, tools/pipe_ab.py): bit 0 = no MFMA, bit 1 = no in-loop DMA,
 // bit 2 = no in-loop fragment reads.
 template <int NW, int AM, int ACT, bool RES, int ABL, bool BUF>
-__global__ __launch_bounds__(NW * 64) void conv_pipe_kernel(PArgs a) {
+__device__ __forceinline__ void conv_pipe_kernel_body(const PArgs& a) {
   constexpr int WGM = NW == 8 ? 4 : 2;
   constexpr int WTM = PBM / WGM, MI = WTM / 16, NJ = 4;
   constexpr int P_AI = PBM / (8 * NW), P_BI = PBN / (8 * NW);   // 1 KiB DMAs per wave per stage
@@ -322,6 +323,13 @@ __global__ __launch_bounds__(NW * 64) void conv_pipe_kernel(PArgs a) {
   }
 }
 
+template <int NW, int AM, int ACT, bool RES, int ABL, bool BUF>
+__global__ __launch_bounds__(NW * 64) void conv_pipe_kernel(PArgs a) {
+  const uint64_t t0 = sat_stamp_begin(a.st);
+  conv_pipe_kernel_body<NW, AM, ACT, RES, ABL, BUF>(a);
+  sat_stamp_end(a.st, t0);
+}
+
 __device__ __attribute__((aligned(16))) bf16 g_pipe_zero16[64];
 
 // DMA placement (PArgs::var): A before / B after the first MFMA half (measured best of the variants)
@@ -395,6 +403,7 @@ int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err) {
   a.tiles_n = sat_cdiv(g.N, PBN);
   a.xcd_remap = 1;
   a.var = kPipeVar;
+  a.st = sat_launch_stamps();
   {
     const long a_bytes = conv ? 2L * g.conv.N * g.conv.H * g.conv.W * g.conv.C : 2L * ((long)(g.M - 1) * g.lda + g.K);
     const long b_bytes = 2L * ((long)(g.N - 1) * g.ldb + g.K);

@@ -48,6 +48,7 @@ struct SArgs {
   int slices, per_slice, items;      // N / 128, workgroups per slice, M-tiles
   int xcd_group;                     // 1: slice = (b / 8) % slices (one M-tile sequence per XCD)
   unsigned a_bytes;
+  SatStamps st;                      // in-kernel launch timestamps (SatPolicy::stamps)
 };
 
 template <int N>
@@ -70,7 +71,7 @@ __device__ __forceinline__ void s_wait_barrier(int n) {
 // KT = K / 32 k-steps, MB = 16-row m-blocks per item (MT = 16 * MB rows), NB = 16-column n-blocks
 // per wave (the workgroup's slice is 128 * NB columns)
 template <int KT, int MB, int NB, bool RES, int ACT, bool STRIDED>
-__global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
+__device__ __forceinline__ void conv1x1_stream_kernel_body(const SArgs& a) {
   constexpr int K = KT * 32, MT = MB * 16, ROWB = K * 2;
   constexpr int SN = S_BN * NB, RROWB = SN * 2;            // slice columns, residual row bytes
   constexpr int TILE = MT * ROWB;                           // A tile bytes
@@ -254,6 +255,13 @@ __global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
   }
 }
 
+template <int KT, int MB, int NB, bool RES, int ACT, bool STRIDED>
+__global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
+  const uint64_t t0 = sat_stamp_begin(a.st);
+  conv1x1_stream_kernel_body<KT, MB, NB, RES, ACT, STRIDED>(a);
+  sat_stamp_end(a.st, t0);
+}
+
 int g_stream_cus = 0;    // CU count (queried once)
 
 template <int KT, int MB, int NB, bool RES, bool STRIDED>
@@ -327,6 +335,7 @@ int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err) {
   a.slices = slices; a.per_slice = per_slice; a.items = items;
   a.xcd_group = (per_slice * slices) % (8 * slices) == 0 && per_slice % 8 == 0;
   a.a_bytes = (unsigned)a_bytes;
+  a.st = sat_launch_stamps();
   const dim3 grid(per_slice * slices);
   const bool res = g.add1 != nullptr;
   if (NB == 2) {

@@ -398,6 +398,19 @@ int bwd_dhgemm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s
                       c.W(c.lay.hcat_w + (long)(E + D) * E), E, w.dh_rec, E, s, nullptr, 0, sp.dh, (long)B * E);
 }
 
+// In-kernel timestamps of the per-step kernels (SatPolicy::stamps, bench.py's in-step figures): the
+// policy's buffer holds kStampGroups x (T-1) slots of stamp_capacity workgroups, group g (the
+// sat_decoder_step_bench order: h GEMM, attention fwd, context GEMM, LSTM fwd, LSTM bwd, d(gated
+// context) GEMM, attention bwd, dh GEMM) at step t in slot g * (T-1) + t; every other launch of the
+// decoder records nothing.
+constexpr int kStampGroups = 8;
+inline uint64_t* step_slot(const SatDecoderDims& d, int g, int t) {
+  const SatPolicy* p = d.policy;
+  if (!p || !p->stamps || p->stamp_capacity <= 0) return nullptr;
+  return p->stamps + ((long)g * (d.T - 1) + t) * 2L * p->stamp_capacity;
+}
+inline int stamp_cap(const SatDecoderDims& d) { return d.policy ? d.policy->stamp_capacity : 0; }
+
 int check_dims(const SatDecoderDims* d) {
   if (!d) return SAT_ERR_INVALID;
   if (d->B <= 0 || d->L <= 0 || d->D <= 0 || d->E <= 0 || d->V <= 0 || d->T < 3) return SAT_ERR_INVALID;
@@ -429,6 +442,7 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
   SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
   SAT_REQUIRE(!(dp->training && dp->has_dropout_mask) || dropout_mask);
   SatPolicyScope scope(dp->policy);
+  SatStampScope no_stamps(nullptr, 0);   // only the per-step groups below record timestamps
   const SatDecoderDims& d = *dp;
   WS w;
   SAT_REQUIRE(carve(d, nullptr, &w) <= workspace_bytes);
@@ -436,6 +450,7 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
   hipStream_t s = (hipStream_t)stream;
   Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D};
   const int B = d.B, L = d.L, D = d.D, E = d.E, T1 = d.T - 1;
+  const int scap = stamp_cap(d);
   const long HG = c.HG;
   const bool att = d.attention != 0;
   const Splits sp = splits_for(d);
@@ -486,12 +501,22 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
     if (!d.tf)
       SAT_CHECK((hipError_t)linear(c, B, 4 * E, E, c.at(w.emb_t, (long)t * E), (long)T1 * E, c.W(lay->wih), E + D,
                                    c.F(lay->bih), w.xg + (long)t * 4 * E, (long)T1 * 4 * E, SAT_F32, SAT_ACT_NONE, s));
-    SAT_CHECK((hipError_t)fwd_hgemm(c, w, sp, t, s));
+    {
+      SatStampScope st(step_slot(d, 0, t), scap);
+      SAT_CHECK((hipError_t)fwd_hgemm(c, w, sp, t, s));
+    }
     if (att) {
-      SAT_CHECK((hipError_t)fwd_attn(c, w, sp, io, t, s));
+      {
+        SatStampScope st(step_slot(d, 1, t), scap);
+        SAT_CHECK((hipError_t)fwd_attn(c, w, sp, io, t, s));
+      }
+      SatStampScope st(step_slot(d, 2, t), scap);
       SAT_CHECK((hipError_t)fwd_cgemm(c, w, sp, t, s));
     }
-    SAT_CHECK((hipError_t)fwd_lstm(c, w, sp, t, s));
+    {
+      SatStampScope st(step_slot(d, 3, t), scap);
+      SAT_CHECK((hipError_t)fwd_lstm(c, w, sp, t, s));
+    }
     if (!d.tf) {
       SAT_CHECK((hipError_t)head_forward(c, w, B, t, true, preds, dropout_mask, s));
       if (t + 1 < T1)   // greedy feedback: argmax -> next token + its embedding (decoder.py:131-133)
@@ -517,6 +542,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   SAT_REQUIRE((phase & 3) != 0 && phase >= 1 && phase <= 7);
   SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
   SatPolicyScope scope(dp->policy);
+  SatStampScope no_stamps(nullptr, 0);   // only the per-step groups of the BPTT loop record timestamps
   const SatDecoderDims& d = *dp;
   WS w;
   SAT_REQUIRE(carve(d, nullptr, &w) <= workspace_bytes);
@@ -524,6 +550,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   hipStream_t s = (hipStream_t)stream;
   Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D};
   const int B = d.B, L = d.L, D = d.D, E = d.E, V = d.V, T1 = d.T - 1;
+  const int scap = stamp_cap(d);
   const int R = (int)c.R;
   const int VP = head_ld(d);
   const long HG = c.HG;
@@ -596,11 +623,19 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   }
   const StepIO io{img_features, const_cast<float*>(alphas), d_alphas};
   for (int t = T1 - 1; t >= 0; --t) {
-    SAT_CHECK((hipError_t)bwd_lstm(c, w, sp, t, s));
+    {
+      SatStampScope st(step_slot(d, 4, t), scap);
+      SAT_CHECK((hipError_t)bwd_lstm(c, w, sp, t, s));
+    }
     if (att) {
-      SAT_CHECK((hipError_t)bwd_ggemm(c, w, sp, t, s));
+      {
+        SatStampScope st(step_slot(d, 5, t), scap);
+        SAT_CHECK((hipError_t)bwd_ggemm(c, w, sp, t, s));
+      }
+      SatStampScope st(step_slot(d, 6, t), scap);
       SAT_CHECK((hipError_t)bwd_attn(c, w, sp, io, t, s));
     }
+    SatStampScope st(step_slot(d, 7, t), scap);
     SAT_CHECK((hipError_t)bwd_dhgemm(c, w, sp, t, s));
   }
 
@@ -653,6 +688,7 @@ extern "C" int sat_decoder_step_bench(const SatDecoderDims* dp, const SatDecoder
   SAT_REQUIRE(lay && params && img_features && workspace && alphas && d_alphas && us_out && reps > 0);
   SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
   SatPolicyScope scope(dp->policy);
+  SatStampScope no_stamps(nullptr, 0);
   const SatDecoderDims& d = *dp;
   WS w;
   SAT_REQUIRE(carve(d, nullptr, &w) <= workspace_bytes);

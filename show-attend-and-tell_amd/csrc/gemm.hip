@@ -424,6 +424,23 @@ const SatPolicy k_default_policy{};
 }  // namespace
 
 const SatPolicy& sat_policy() { return t_policy ? *t_policy : k_default_policy; }
+
+namespace {
+thread_local SatStamps t_stamps{};
+thread_local bool t_stamps_set = false;
+}  // namespace
+SatStamps sat_launch_stamps() {
+  if (t_stamps_set) return t_stamps;
+  return SatStamps{sat_policy().stamps, sat_policy().stamp_capacity};
+}
+SatStampScope::SatStampScope(uint64_t* p, int cap) : prev(t_stamps), prev_set(t_stamps_set) {
+  t_stamps = SatStamps{p, cap};
+  t_stamps_set = true;
+}
+SatStampScope::~SatStampScope() {
+  t_stamps = prev;
+  t_stamps_set = prev_set;
+}
 SatPolicyScope::SatPolicyScope(const SatPolicy* p) : prev(t_policy) { t_policy = p; }
 SatPolicyScope::~SatPolicyScope() { t_policy = prev; }
 

@@ -17,7 +17,7 @@ inline int grid_for(long n) {
 // over its split-K slabs (4x the loads in flight of a unit-per-thread kernel: 9.5 -> 5.7 us per
 // step at B=128, E=512, 4 + 8 slabs), the cell update reads the four gates back from LDS.
 template <typename T>
-__global__ __launch_bounds__(256) void lstm_fwd_gp_kernel(LstmFwdArgs a) {
+__device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
   __shared__ float sg[4][64];
   const int E = a.E;
   const int q = threadIdx.x >> 6, u = threadIdx.x & 63;
@@ -51,10 +51,17 @@ __global__ __launch_bounds__(256) void lstm_fwd_gp_kernel(LstmFwdArgs a) {
   }
 }
 
+template <typename T>
+__global__ __launch_bounds__(256) void lstm_fwd_gp_kernel(LstmFwdArgs a) {
+  const uint64_t t0 = sat_stamp_begin(a.st);
+  lstm_fwd_gp_kernel_body<T>(a);
+  sat_stamp_end(a.st, t0);
+}
+
 // Gate-parallel backward (layout as lstm_fwd_gp_kernel): thread (q, u) loads gate q and the
 // slabs s = q, q+4, ... of the recurrent dh; the four partial sums meet in LDS in a fixed order.
 template <typename T>
-__global__ __launch_bounds__(256) void lstm_bwd_gp_kernel(LstmBwdArgs a) {
+__device__ __forceinline__ void lstm_bwd_gp_kernel_body(LstmBwdArgs a) {
   __shared__ float sg[4][64], sdh[4][64];
   const int E = a.E;
   const int q = threadIdx.x >> 6, u = threadIdx.x & 63;
@@ -98,6 +105,13 @@ __global__ __launch_bounds__(256) void lstm_bwd_gp_kernel(LstmBwdArgs a) {
     }
     __syncthreads();
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void lstm_bwd_gp_kernel(LstmBwdArgs a) {
+  const uint64_t t0 = sat_stamp_begin(a.st);
+  lstm_bwd_gp_kernel_body<T>(a);
+  sat_stamp_end(a.st, t0);
 }
 
 // d(tanh pre) for init_h / init_c: dpre[b, 0:E] = dh (1-h^2), dpre[b, E:2E] = dc (1-c^2)
@@ -266,13 +280,17 @@ __global__ void tokens_kernel(const int64_t* caps, int B, int T, int T1, int32_t
     else hipLaunchKernelGGL(KERNEL<float>, grid, dim3(256), 0, s, __VA_ARGS__);               \
   } while (0)
 
-int sat_lstm_fwd_launch(const LstmFwdArgs& a, hipStream_t s) {
+int sat_lstm_fwd_launch(const LstmFwdArgs& args, hipStream_t s) {
+  LstmFwdArgs a = args;
+  a.st = sat_launch_stamps();
   long blocks = ((long)a.B * a.E + 63) / 64;
   if (blocks > 4096) blocks = 4096;
   DISPATCH_T(a.dtype, lstm_fwd_gp_kernel, dim3((int)blocks), a);
   return (int)hipGetLastError();
 }
-int sat_lstm_bwd_launch(const LstmBwdArgs& a, hipStream_t s) {
+int sat_lstm_bwd_launch(const LstmBwdArgs& args, hipStream_t s) {
+  LstmBwdArgs a = args;
+  a.st = sat_launch_stamps();
   long blocks = ((long)a.B * a.E + 63) / 64;
   if (blocks > 4096) blocks = 4096;
   DISPATCH_T(a.dtype, lstm_bwd_gp_kernel, dim3((int)blocks), a);

@@ -37,6 +37,36 @@ struct SatPolicyScope {
   SatPolicyScope& operator=(const SatPolicyScope&) = delete;
 };
 
+// ---- in-kernel launch timestamps (SatPolicy::stamps) ---------------------------
+struct SatStamps {
+  uint64_t* p = nullptr;
+  int cap = 0;
+};
+// the stamp slots of the next launch: the innermost SatStampScope's (the decoder gives every per-step launch
+// its own slot and none to the rest: p = nullptr), else the call's SatPolicy
+SatStamps sat_launch_stamps();
+struct SatStampScope {
+  SatStamps prev;
+  bool prev_set;
+  SatStampScope(uint64_t* p, int cap);
+  ~SatStampScope();
+  SatStampScope(const SatStampScope&) = delete;
+  SatStampScope& operator=(const SatStampScope&) = delete;
+};
+__device__ __forceinline__ uint64_t sat_stamp_begin(const SatStamps& st) {
+  return st.p ? __builtin_amdgcn_s_memrealtime() : 0;
+}
+// every wave of the workgroup has finished its work (barrier), then one lane records {start, end}
+__device__ __forceinline__ void sat_stamp_end(const SatStamps& st, uint64_t t0) {
+  if (!st.p) return;   // uniform
+  __syncthreads();
+  const int w = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  if (threadIdx.x == 0 && w < st.cap) {
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    *(ulonglong2*)(st.p + 2 * (long)w) = make_ulonglong2(t0, t1);
+  }
+}
+
 // ---- scalar load/store helpers for the two storage dtypes -------------------
 __device__ __forceinline__ float ld_as_f32(const void* p, long i, int dt) {
   return dt == SAT_BF16 ? (float)((const bf16*)p)[i] : ((const float*)p)[i];

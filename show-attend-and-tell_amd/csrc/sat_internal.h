@@ -28,6 +28,7 @@ struct AttnFwdArgs {
   void* gated; long gated_ld;           // dtype gate*context (nullable)
   float* uh_save; long uh_save_ld;      // copy of U h + b (nullable)
   int hg_splits; long hg_split_stride;  // uh / gate_pre are sums of hg_splits partial slabs (0|1 = plain)
+  SatStamps st;                         // in-kernel launch timestamps (set by the launcher)
 };
 int sat_attention_fwd_launch(const AttnFwdArgs& a, hipStream_t s);
 
@@ -51,6 +52,7 @@ struct AttnBwdArgs {
   float* dbv_acc;                       // [B]    += dL/dv.bias
   float* part;                          // scratch [B, NS, L]
   int dg_splits; long dg_split_stride;  // d_gated = sum of dg_splits partial slabs (0|1 = plain)
+  SatStamps st;                         // in-kernel launch timestamps (set by the launcher)
 };
 int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s);
 // dL/dWs[b,l,:] = sum_t de[b,t,l] v (1 - tanh^2(Ws[b,l,:] + uh[b,t,:])), summed t = T1-1 .. 0 (the
@@ -73,6 +75,7 @@ struct LstmFwdArgs {
   void* h_next_in_t; long h_next_in_t_ld;  // dtype copy as next step's input (nullable)
   int h_splits; long h_split_stride;    // hpart = sum of h_splits slabs
   int c_splits; long c_split_stride;    // cpart = sum of c_splits slabs
+  SatStamps st;                         // in-kernel launch timestamps (set by the launcher)
 };
 int sat_lstm_fwd_launch(const LstmFwdArgs& a, hipStream_t s);
 
@@ -89,6 +92,7 @@ struct LstmBwdArgs {
   float* d_gates; long d_gates_ld;      // out fp32
   void* d_gates_t; long d_gates_t_ld;   // out dtype copy (nullable)
   int dh_splits; long dh_split_stride;  // dh_rec = sum of dh_splits slabs
+  SatStamps st;                         // in-kernel launch timestamps (set by the launcher)
 };
 int sat_lstm_bwd_launch(const LstmBwdArgs& a, hipStream_t s);
 

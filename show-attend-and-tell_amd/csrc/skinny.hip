@@ -33,10 +33,11 @@ struct SkArgs {
   const bf16* W; long ldw;
   float* C; long ldc; long split_stride;
   const float* bias;
+  SatStamps st;
 };
 
 template <int MB, int NW>
-__global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(SkArgs a) {
+__device__ __forceinline__ void skinny_gemm_kernel_body(SkArgs a) {
   __shared__ __attribute__((aligned(16))) float red[MB * 16 * SK_RLD];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -111,6 +112,13 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(SkArgs a) {
   }
 }
 
+template <int MB, int NW>
+__global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(SkArgs a) {
+  const uint64_t t0 = sat_stamp_begin(a.st);
+  skinny_gemm_kernel_body<MB, NW>(a);
+  sat_stamp_end(a.st, t0);
+}
+
 template <int MB>
 void launch_mb(int nw, dim3 grid, hipStream_t st, const SkArgs& a) {
   if (nw == 8) hipLaunchKernelGGL((skinny_gemm_kernel<MB, 8>), grid, dim3(512), 0, st, a);
@@ -148,6 +156,7 @@ int sat_skinny_try(const SatGemm& g, hipStream_t st, int* err) {
   a.W = (const bf16*)g.B; a.ldw = g.ldb;
   a.C = (float*)g.C; a.ldc = g.ldc; a.split_stride = S > 1 ? g.split_stride : 0;
   a.bias = g.bias;
+  a.st = sat_launch_stamps();
   const dim3 grid(g.N / SK_COLS, S);
   if (g.M <= 32) launch_mb<2>(nw, grid, st, a);
   else if (g.M <= 64) launch_mb<4>(nw, grid, st, a);

@@ -145,6 +145,9 @@ class Encoder(nn.Module):
         self.timing = None   # bench hook: list collecting (start, end) HIP events around every conv launch
         self.timing_args = None   # bench hook: list collecting every conv launch's arguments
         # (a fused bottleneck launch is recorded as ("fused", x, frags))
+        # bench hook: callable() -> the SatPolicy of the next conv launch (bench.py gives every launch its own
+        # in-kernel timestamp slots, SatPolicy.stamps); None = self.policy for every launch
+        self.launch_policy = None
         # identity-residual bottlenecks the fused kernel supports run as ONE launch
         # (sat_bottleneck_fused, csrc/convblock.hip); False = three conv launches (A/B, tests);
         # an int n fuses every n-th eligible block only (the unfused ones leave CUs to a decoder
@@ -161,31 +164,30 @@ class Encoder(nn.Module):
         # defaults): A/B measurements and tests only
         self.policy = None
 
-    def _conv(self, x, f, relu, residual=None, out_hw=None):
-        w, b, s, p = f
+    def _launch(self, record, fn, *args, **kw):
+        """One conv launch with the bench's hooks: its arguments recorded, an event pair around it,
+        the in-graph launch timer's marks."""
         if self.timing_args is not None:
-            self.timing_args.append((x, w, b, s, p, relu, residual, out_hw))
+            self.timing_args.append(record)
+        kw["policy"] = self.launch_policy() if self.launch_policy is not None else self.policy
         if self.timing is None:
-            return ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual, out_hw=out_hw, policy=self.policy)
-        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        st.record()
-        y = ops.conv2d_nhwc(x, w, b, s, p, relu, residual=residual, out_hw=out_hw, policy=self.policy)
-        en.record()
-        self.timing.append((st, en))
+            y = fn(*args, **kw)
+        else:
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st.record()
+            y = fn(*args, **kw)
+            en.record()
+            self.timing.append((st, en))
         return y
 
+    def _conv(self, x, f, relu, residual=None, out_hw=None):
+        w, b, s, p = f
+        return self._launch((x, w, b, s, p, relu, residual, out_hw), ops.conv2d_nhwc, x, w, b, s, p, relu,
+                            residual=residual, out_hw=out_hw)
+
     def _frag_conv(self, kind, fn, x, f, *extra):
-        """A half-image fragment-weight conv launch (csrc/convblock.hip), with the bench's timing hooks."""
-        if self.timing_args is not None:
-            self.timing_args.append((kind, x, f) + extra)
-        if self.timing is None:
-            return fn(x, f, *extra)
-        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        st.record()
-        y = fn(x, f, *extra)
-        en.record()
-        self.timing.append((st, en))
-        return y
+        """A half-image fragment-weight conv launch (csrc/convblock.hip), with the bench's hooks."""
+        return self._launch((kind, x, f) + extra, fn, x, f, *extra)
 
     # ---- plan: folded NHWC weights ------------------------------------------
     @torch.no_grad()
@@ -340,16 +342,7 @@ class Encoder(nn.Module):
         _, c1, c2, c3, ds, fused, c2f = step
         if (fused is not None and self.fuse_blocks is not False and self._fuse_this(self._plan, step)
                 and ops.bottleneck_fused_supported(y.shape[1], y.shape[2], y.shape[3], c1[0].shape[0], y.dtype)):
-            if self.timing_args is not None:
-                self.timing_args.append(("fused", y, fused))
-            if self.timing is None:
-                return ops.bottleneck_fused(y, *fused)
-            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            st.record()
-            out = ops.bottleneck_fused(y, *fused)
-            en.record()
-            self.timing.append((st, en))
-            return out
+            return self._launch(("fused", y, fused), ops.bottleneck_fused, y, *fused)
         if fused is not None and self.c1_frag and ops.conv1x1_frag_supported(y.shape[1], y.shape[2], y.shape[3],
                                                                            c1[0].shape[0], y.dtype):
             out = self._frag_conv("c1frag", ops.conv1x1_frag, y, fused[0])

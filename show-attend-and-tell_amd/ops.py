@@ -175,7 +175,7 @@ def bottleneck_fused_supported(H, W, Cin, Cmid, dtype):
     return bool(L.lib().sat_bottleneck_fused_supported(H, W, Cin, Cmid, L.dtype_code(dtype)))
 
 
-def bottleneck_fused(x, f1, f2, f3, out=None):
+def bottleneck_fused(x, f1, f2, f3, out=None, policy=None):
     """One identity-residual stride-1 bottleneck in one launch.  x NHWC [N,H,W,Cin]; f1/f2/f3 =
     (fragment-layout weight, fp32 bias) of the folded c1 / c2 / c3 (Encoder plan)."""
     L.require_device(x)
@@ -184,7 +184,7 @@ def bottleneck_fused(x, f1, f2, f3, out=None):
     y = out if out is not None else torch.empty_like(x)
     L.check(L.lib().sat_bottleneck_fused(N, H, W, C, Cmid, L.dtype_code(x.dtype), L.ptr(x), L.ptr(f1[0]),
                                          L.ptr(f1[1]), L.ptr(f2[0]), L.ptr(f2[1]), L.ptr(f3[0]), L.ptr(f3[1]),
-                                         L.ptr(y), L.stream_of(y)), "sat_bottleneck_fused")
+                                         L.ptr(y), L.policy_ptr(policy), L.stream_of(y)), "sat_bottleneck_fused")
     return y
 
 
@@ -192,7 +192,7 @@ def conv3x3_frag_supported(H, W, C, dtype):
     return bool(L.lib().sat_conv3x3_frag_supported(H, W, C, L.dtype_code(dtype)))
 
 
-def conv3x3_frag(x, f, out=None):
+def conv3x3_frag(x, f, out=None, policy=None):
     """relu(conv3x3(x, pad 1) + b) with f = (fragment-layout weight, fp32 bias) of a folded [C][3][3][C]
     conv (a layer3 bottleneck's c2).  x NHWC [N,H,W,C]; bit-identical to conv2d_nhwc."""
     L.require_device(x)
@@ -201,7 +201,7 @@ def conv3x3_frag(x, f, out=None):
     N, H, W, C = x.shape
     y = out if out is not None else torch.empty_like(x)
     L.check(L.lib().sat_conv3x3_frag(N, H, W, C, L.dtype_code(x.dtype), L.ptr(x), L.ptr(f[0]), L.ptr(f[1]),
-                                     L.ptr(y), L.stream_of(y)), "sat_conv3x3_frag")
+                                     L.ptr(y), L.policy_ptr(policy), L.stream_of(y)), "sat_conv3x3_frag")
     return y
 
 
@@ -209,7 +209,7 @@ def conv1x1_frag_supported(H, W, Cin, Cout, dtype):
     return bool(L.lib().sat_conv1x1_frag_supported(H, W, Cin, Cout, L.dtype_code(dtype)))
 
 
-def conv1x1_frag(x, f, out=None):
+def conv1x1_frag(x, f, out=None, policy=None):
     """relu(x . W^T + b) with f = (fragment-layout weight, fp32 bias) of a folded [Cout][Cin] 1x1 conv (a
     layer3 bottleneck's c1).  x NHWC [N,H,W,Cin]; bit-identical to conv2d_nhwc."""
     L.require_device(x)
@@ -219,7 +219,7 @@ def conv1x1_frag(x, f, out=None):
     Cout = f[1].shape[0]
     y = out if out is not None else torch.empty(N, H, W, Cout, dtype=x.dtype, device=x.device)
     L.check(L.lib().sat_conv1x1_frag(N, H, W, C, Cout, L.dtype_code(x.dtype), L.ptr(x), L.ptr(f[0]), L.ptr(f[1]),
-                                     L.ptr(y), L.stream_of(y)), "sat_conv1x1_frag")
+                                     L.ptr(y), L.policy_ptr(policy), L.stream_of(y)), "sat_conv1x1_frag")
     return y
 
 
