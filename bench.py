@@ -98,15 +98,18 @@ class LaunchStamps:
     ``cap`` workgroup slots {start, end} per launch, and one SatPolicy per launch pointing at its slice.
     Every workgroup of a launch records when its first wave started and its last wave finished (the
     device's 100 MHz real-time counter); the launch's span is max(end) - min(start) -- the kernel's own
-    duration, taken inside the timed, overlapped graph replays with no extra node, event or barrier in
-    the stream (every replay rewrites the slots; read after the timed region).  Event-record nodes
-    spliced into the graph between kernels cost ~3 us each and add that to every bracketed kernel
-    (tools/graph_event_probe.py), so in-step figures come from these stamps."""
+    duration inside the overlapped graph replays, with no extra node, event or barrier in the stream.
+    The slots' enable words are off during the timed region (a launch then pays one scalar load) and on
+    for a diagnostic phase of the same overlapped schedule right after it.  Event-record nodes spliced
+    into the graph between kernels cost ~3 us each and add that to every bracketed kernel
+    (tools/graph_event_probe.py); a rocprofv3 kernel trace all but serialises the two streams (6 % of
+    the busy time overlapped, profiles/r3_s6/), so neither gives in-step kernel durations."""
 
     def __init__(self, n_launches, device, base=None, cap=16384):
         import sat_amd
         self.n, self.cap = n_launches, cap
-        self.buf = torch.zeros(n_launches, cap, 2, dtype=torch.int64, device=device)
+        # per launch: a 16-B header (enable word) + cap workgroup records (SatPolicy.stamps)
+        self.buf = torch.zeros(n_launches, cap + 1, 2, dtype=torch.int64, device=device)
         self.pols = []
         for k in range(n_launches):
             pol = sat_amd.Policy()
@@ -123,9 +126,15 @@ class LaunchStamps:
         self.used += 1
         return self.pols[self.used - 1]
 
+    def enable(self, on):
+        """Switch the launches' timestamps on / off (their enable words; graph replays read them)."""
+        self.buf[:, 0, 0] = 1 if on else 0
+        if on:
+            self.buf[:, 1:].zero_()
+
     def spans_us(self):
         """Per launch (in launch order): max(end) - min(start) over its workgroups, microseconds."""
-        st, en = self.buf[:self.used, :, 0], self.buf[:self.used, :, 1]
+        st, en = self.buf[:self.used, 1:, 0], self.buf[:self.used, 1:, 1]
         valid = st > 0
         big = torch.iinfo(torch.int64).max
         lo = torch.where(valid, st, torch.full_like(st, big)).min(dim=1).values
@@ -142,15 +151,21 @@ class DecoderStamps:
         import sat_amd
         from sat_amd.diagnostics import GROUPS
         self.groups, self.T1, self.cap = GROUPS, T - 1, cap
-        self.buf = torch.zeros(len(GROUPS) * self.T1, cap, 2, dtype=torch.int64, device=device)
+        # slot g * (T-1) + t: a 16-B header (enable word) + cap workgroup records (decoder.hip step_slot)
+        self.buf = torch.zeros(len(GROUPS) * self.T1, cap + 1, 2, dtype=torch.int64, device=device)
         self.policy = sat_amd.Policy()
         if base is not None:
             __import__("ctypes").pointer(self.policy)[0] = base
         self.policy.stamps = self.buf.data_ptr()
         self.policy.stamp_capacity = cap
 
+    def enable(self, on):
+        self.buf[:, 0, 0] = 1 if on else 0
+        if on:
+            self.buf[:, 1:].zero_()
+
     def group_spans_us(self):
-        st, en = self.buf[..., 0], self.buf[..., 1]
+        st, en = self.buf[:, 1:, 0], self.buf[:, 1:, 1]
         valid = st > 0
         big = torch.iinfo(torch.int64).max
         lo = torch.where(valid, st, torch.full_like(st, big)).min(dim=1).values.tolist()
@@ -689,6 +704,8 @@ def main():
             opt.step()
         return loss
 
+    for st in stamps_enc + stamps_dec:   # timestamps off for the timed region
+        st.enable(False)
     run(2)   # replay warm-up
     enc_events.clear()
     torch.cuda.synchronize()
@@ -707,11 +724,25 @@ def main():
         elapsed = t.item()
     launches = conv_launches(args.network, B, fused=enc.fuse_blocks)
     enc_ms = sum(s.elapsed_time(e) for s, e in enc_events) if use_graph else None
+    diag_phase = None
+    if (stamps_enc or stamps_dec) and not args.no_diagnostics:
+        # diagnostic phase (every rank: the all-reduces are collective): the same overlapped schedule with
+        # the kernels' timestamps switched on
+        for st in stamps_enc + stamps_dec:
+            st.enable(True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        n_diag = max(4, min(20, args.steps))
+        run(n_diag)
+        torch.cuda.synchronize()
+        diag_phase = {"steps": n_diag, "ms_per_step": round(1000 * (time.perf_counter() - t1) / n_diag, 3)}
+        for st in stamps_enc + stamps_dec:
+            st.enable(False)
     loss_v = loss.item()
     diag = rank == 0 and not args.no_diagnostics
-    instep_conv = instep_conv_durations(stamps_enc, launches) if stamps_enc else None
+    instep_conv = instep_conv_durations(stamps_enc, launches) if diag_phase and stamps_enc else None
     instep_dec = None
-    if stamps_dec:
+    if diag_phase and stamps_dec:
         instep_dec = {}
         for sd in stamps_dec:
             for g, v in sd.group_spans_us().items():
@@ -752,6 +783,8 @@ def main():
                        "parallelism": f"dp{world}", "hip_graph": use_graph,
                        "encoder_decoder_overlap": overlap},
             "roofline": roof,
+            "diagnostic_phase": dict(diag_phase, note="after the timed region: the same overlapped graphs with the "
+                                     "kernels' in-kernel timestamps on (roofline in-step figures)") if diag_phase else None,
             "encoder_trunk": dict(trunk or {}, graph_ms_per_step=(round(enc_ms / args.steps, 3) if enc_ms else None),
                                   split_at=args.enc_split if g_encA is not None else None),
             "loss": round(loss_v, 4),

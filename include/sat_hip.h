@@ -64,10 +64,12 @@ typedef struct {
   int attn_bwd;         /* attention backward per decoder step: 0 auto, 1 the two-launch form */
   int decoder_splits[4];/* split-K counts of the per-step bf16 decoder GEMMs -- h: [U; f_beta; W_hh] h, c: context
                          * part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic */
-  /* diagnostics (bench.py's in-step kernel timing): when non-null, every workgroup w < stamp_capacity of the
-   * call's launch writes {first-wave start, last-wave end} of the device's 100 MHz real-time counter to
-   * stamps[2 w], stamps[2 w + 1] (device memory); the launch's span = max(end) - min(start).  Captured
-   * into a hipGraph, every replay rewrites them. */
+  /* diagnostics (bench.py's in-step kernel timing): a device buffer; when non-null and stamps[0] != 0 (the
+   * enable word, read by the kernels at every launch -- so a captured hipGraph can be replayed with stamps
+   * on or off), every workgroup w < stamp_capacity of the call's launch writes {first-wave start, last-wave
+   * end} of the device's 100 MHz real-time counter to stamps[2 + 2 w], stamps[3 + 2 w]; the launch's span
+   * = max(end) - min(start).  The decoder calls lay out kStampGroups x (T-1) such slots of
+   * 2 (stamp_capacity + 1) words, one per per-step kernel group and step (decoder.hip). */
   uint64_t* stamps;
   int stamp_capacity;
 } SatPolicy;

@@ -260,7 +260,7 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
 
 template <typename T, int CH>   // CH = e-chunks of 64 x 16 bytes per lane covering E
 __global__ __launch_bounds__(FNW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
-  const uint64_t t0 = sat_stamp_begin(a.st);
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
   attn_fwd_kernel_body<T, CH>(a);
   sat_stamp_end(a.st, t0);
 }
@@ -328,7 +328,7 @@ __device__ __forceinline__ void attn_bwd1_kernel_body(AttnBwdArgs a) {
 
 template <typename T>
 __global__ __launch_bounds__(ANW * 64) void attn_bwd1_kernel(AttnBwdArgs a) {
-  const uint64_t t0 = sat_stamp_begin(a.st);
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
   attn_bwd1_kernel_body<T>(a);
   sat_stamp_end(a.st, t0);
 }
@@ -452,43 +452,40 @@ __device__ __forceinline__ void attn_bwd2_kernel_body(AttnBwdArgs a, int NS) {
 
 template <typename T>
 __global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int NS) {
-  const uint64_t t0 = sat_stamp_begin(a.st);
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
   attn_bwd2_kernel_body<T>(a, NS);
   sat_stamp_end(a.st, t0);
 }
 
-// One launch for the whole attention backward of a step (replaces attn_bwd1 + attn_bwd2): one
-// 16-wave workgroup per batch row b.  The two-launch form existed only because dL/dalpha needs a
-// reduction over D and the softmax / tanh backward needs all of it; with the whole row in one
-// workgroup that reduction stays in LDS.  Everything the row needs from memory -- the first batch
-// of annotation rows a[b, l, :], the first rows of Ws[b], U h + b and v -- is requested at kernel
-// entry (issue order = order of first use), so a step is one dependent memory round trip plus
-// the LDS phases:
-//   A  thread per column d: dL/dcontext = dL/dgated * gate (+ head term) into LDS, the gate
-//      gradient written on the way;
-//   B  wave per slot l, lanes over d: dL/dalpha_l = <dL/dcontext, a[b,l,:]> (+ the loss term);
-//   C  softmax backward: de_l = alpha_l (dL/dalpha_l - sum_k alpha_k dL/dalpha_k);
-//   D  wave per slot l, lanes over e: tanh recomputed, dL/d(U h) and dL/dv (+ dL/dv.bias) folded
-//      over the waves in a fixed order.
-
-// DCH / ECH: 16-B chunks per lane covering D / E; FBW waves, FBU slots per wave per batch (FBW * FBU
-// >= L keeps a row's annotation rows in one batch of loads: 16 x 4 at D <= 1024 elements per 16 B,
-// 8 x 7 (256 VGPRs per lane) at ResNet152's D = 2048)
+// The attention backward of one step split over L: grid (B, NL), workgroup (b, c) owns the slots
+// l in [c LC, (c + 1) LC) of batch row b (LC = ceil(L / NL)), so a row's annotation rows a[b, l, :] and
+// Ws[b, l, :] are streamed by NL workgroups (at B = 128: 256 workgroups fill the chip, where one per row
+// left half of it idle).  The softmax backward needs sum_k alpha_k dL/dalpha_k over ALL slots; it is
+//   sum_k alpha_k (a_k . dctx + dalpha_ext_k) = ctx . dctx + sum_k alpha_k dalpha_ext_k
+// (ctx = sum_k alpha_k a_k is the saved pre-gate context), so no workgroup needs another's dL/dalpha.
+// Phases: A thread per column d: dL/dcontext (+ gate gradient, chunk 0 writes it) and ctx . dctx;
+// B wave per slot: dL/dalpha_l; C de_l = alpha_l (dL/dalpha_l - sum); D tanh backward of the chunk's
+// slots: partial dL/d(U h), dL/dv, dL/dv.bias.  With NL > 1 the partials meet in the last-arriving
+// workgroup of the row (agent-scope ticket; payload stored and loaded sc1, so no cache fence is needed:
+// MI355X_MICROARCH.md, visibility, first row of the sc1 table), summed in chunk order (deterministic).
 template <typename T, int DCH, int ECH, int FBW, int FBU>
-__device__ __forceinline__ void attn_bwd_fused_kernel_body(AttnBwdArgs a) {
+__device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   constexpr int VN = V16<T>::N;
+  constexpr int EC = 64 * VN * ECH;
   __shared__ float s_dctx[64 * VN * DCH];
   __shared__ float s_de[kMaxL];
-  __shared__ float s_red[FBW][64 * VN * ECH];
+  __shared__ float s_red[FBW][EC];
   __shared__ float s_tmp[FBW];
-  const int b = blockIdx.x;
+  __shared__ int s_last;
+  const int b = blockIdx.x, c = blockIdx.y, NL = gridDim.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = a.L, D = a.D, E = a.E;
+  const int LC = (L + NL - 1) / NL, l_beg = c * LC, l_end = min(L, l_beg + LC);
   const T* ab = (const T*)a.a + (long)b * L * D + lane * VN;
   const T* Ws = (const T*)a.Ws + (long)b * L * E + lane * VN;
   // ---- requests in order of first use ----
-  float dcol[(64 * VN * DCH + FBW * 64 - 1) / (FBW * 64)][4];   // dg, g, cx, dx of this thread's columns
   constexpr int CPT = (64 * VN * DCH + FBW * 64 - 1) / (FBW * 64);
+  float dcol[CPT][4];   // dg, g, cx, dx of this thread's columns
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
     const int d = k * FBW * 64 + tid;
@@ -505,22 +502,22 @@ __device__ __forceinline__ void attn_bwd_fused_kernel_body(AttnBwdArgs a) {
 #pragma unroll
   for (int u = 0; u < FBU; ++u)
 #pragma unroll
-    for (int c = 0; c < DCH; ++c) {
-      const int l = w + FBW * u, d = c * 64 * VN + lane * VN;
-      xa[u][c] = ld16(ab + (long)l * D + c * 64 * VN, l < L && d < D);
+    for (int q = 0; q < DCH; ++q) {
+      const int l = l_beg + w + FBW * u, d = q * 64 * VN + lane * VN;
+      xa[u][q] = ld16(ab + (long)l * D + q * 64 * VN, l < l_end && d < D);
     }
   uint4 xw[FBU][ECH];
 #pragma unroll
   for (int u = 0; u < FBU; ++u)
 #pragma unroll
-    for (int c = 0; c < ECH; ++c) {
-      const int l = w + FBW * u, e = c * 64 * VN + lane * VN;
-      xw[u][c] = ld16(Ws + (long)l * E + c * 64 * VN, l < L && e < E);
+    for (int q = 0; q < ECH; ++q) {
+      const int l = l_beg + w + FBW * u, e = q * 64 * VN + lane * VN;
+      xw[u][q] = ld16(Ws + (long)l * E + q * 64 * VN, l < l_end && e < E);
     }
   float uu[ECH][VN], vw[ECH][VN];
 #pragma unroll
-  for (int c = 0; c < ECH; ++c) {
-    const int e = c * 64 * VN + lane * VN;
+  for (int q = 0; q < ECH; ++q) {
+    const int e = q * 64 * VN + lane * VN;
 #pragma unroll
     for (int j = 0; j < VN; j += 4) {
       float4 u4 = make_float4(0.f, 0.f, 0.f, 0.f), v4 = u4;
@@ -528,11 +525,13 @@ __device__ __forceinline__ void attn_bwd_fused_kernel_body(AttnBwdArgs a) {
         u4 = *(const float4*)(a.uh + (long)b * a.uh_ld + e + j);
         v4 = *(const float4*)(a.v_w + e + j);
       }
-      uu[c][j] = u4.x; uu[c][j + 1] = u4.y; uu[c][j + 2] = u4.z; uu[c][j + 3] = u4.w;
-      vw[c][j] = v4.x; vw[c][j + 1] = v4.y; vw[c][j + 2] = v4.z; vw[c][j + 3] = v4.w;
+      uu[q][j] = u4.x; uu[q][j + 1] = u4.y; uu[q][j + 2] = u4.z; uu[q][j + 3] = u4.w;
+      vw[q][j] = v4.x; vw[q][j + 1] = v4.y; vw[q][j + 2] = v4.z; vw[q][j + 3] = v4.w;
     }
   }
-  // ---- A: dL/dcontext and the gate gradient (thread per column) ----
+  // ---- A: dL/dcontext, the gate gradient (chunk 0), ctx . dctx + sum_k alpha_k dalpha_ext_k ----
+  const float* alpha = a.alpha + (long)b * a.alpha_ld;
+  float loc = 0.f;
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
     const int d = k * FBW * 64 + tid;
@@ -541,138 +540,194 @@ __device__ __forceinline__ void attn_bwd_fused_kernel_body(AttnBwdArgs a) {
       if (d < D) {
         const float dg = dcol[k][0], g = dcol[k][1], cx = dcol[k][2], dx = dcol[k][3];
         dctx = dg * g + dx;
-        const float dgp = dg * cx * g * (1.f - g);
-        a.d_gpre[(long)b * a.d_gpre_ld + d] = dgp;
-        if (a.d_gpre_t) ((T*)a.d_gpre_t)[(long)b * a.d_gpre_ld + d] = (T)dgp;
+        loc += cx * dctx;
+        if (c == 0) {
+          const float dgp = dg * cx * g * (1.f - g);
+          a.d_gpre[(long)b * a.d_gpre_ld + d] = dgp;
+          if (a.d_gpre_t) ((T*)a.d_gpre_t)[(long)b * a.d_gpre_ld + d] = (T)dgp;
+        }
       }
       s_dctx[d] = dctx;
     }
   }
-  lds_barrier();   // the annotation / Ws rows stay in flight
-  float dctx[DCH][VN];
-#pragma unroll
-  for (int c = 0; c < DCH; ++c)
-#pragma unroll
-    for (int j = 0; j < VN; ++j) dctx[c][j] = s_dctx[c * 64 * VN + lane * VN + j];
-  // ---- B: dL/dalpha per slot ----
-  for (int l0 = w; l0 < L; l0 += FBW * FBU) {
-    if (l0 != w) {
-#pragma unroll
-      for (int u = 0; u < FBU; ++u)
-#pragma unroll
-        for (int c = 0; c < DCH; ++c) {
-          const int l = l0 + FBW * u, d = c * 64 * VN + lane * VN;
-          xa[u][c] = ld16(ab + (long)l * D + c * 64 * VN, l < L && d < D);
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < FBU; ++u) {
-      const int l = l0 + FBW * u;
-      if (l >= L) break;   // wave-uniform
-      float p = 0.f;
-#pragma unroll
-      for (int c = 0; c < DCH; ++c) {
-        const T* h = (const T*)&xa[u][c];
-#pragma unroll
-        for (int j = 0; j < VN; ++j) p += dctx[c][j] * (float)h[j];
-      }
-      p = wave_sum(p);
-      if (lane == 0) s_de[l] = p + (a.d_alpha_ext ? a.d_alpha_ext[(long)b * a.d_alpha_ext_ld + l] : 0.f);
-    }
-  }
-  __syncthreads();
-  // ---- C: softmax backward ----
-  const float* alpha = a.alpha + (long)b * a.alpha_ld;
-  float loc = 0.f;
-  for (int l = tid; l < L; l += FBW * 64) loc += alpha[l] * s_de[l];
+  if (a.d_alpha_ext)
+    for (int l = tid; l < L; l += FBW * 64) loc += alpha[l] * a.d_alpha_ext[(long)b * a.d_alpha_ext_ld + l];
   loc = wave_sum(loc);
   if (lane == 0) s_tmp[w] = loc;
-  __syncthreads();
+  lds_barrier();   // the annotation / Ws rows stay in flight
   float sad = 0.f;
 #pragma unroll
   for (int i = 0; i < FBW; i += 2) sad += s_tmp[i] + s_tmp[i + 1];
-  __syncthreads();
-  for (int l = tid; l < L; l += FBW * 64) {
-    const float de = alpha[l] * (s_de[l] - sad);
-    s_de[l] = de;
-    a.de_out[(long)b * a.de_ld + l] = de;
-  }
-  __syncthreads();
-  // ---- D: tanh backward over E ----
-  float duh[ECH][VN], dv[ECH][VN];
+  float dctx[DCH][VN];
 #pragma unroll
-  for (int c = 0; c < ECH; ++c)
+  for (int q = 0; q < DCH; ++q)
 #pragma unroll
-    for (int j = 0; j < VN; ++j) duh[c][j] = dv[c][j] = 0.f;
-  float dbv = 0.f;
-  for (int l0 = w; l0 < L; l0 += FBW * FBU) {
-    if (l0 != w) {
+    for (int j = 0; j < VN; ++j) dctx[q][j] = s_dctx[q * 64 * VN + lane * VN + j];
+  // ---- B + C: dL/dalpha and de per slot of the chunk ----
+  for (int l0 = l_beg + w; l0 < l_end; l0 += FBW * FBU) {
+    if (l0 != l_beg + w) {
 #pragma unroll
       for (int u = 0; u < FBU; ++u)
 #pragma unroll
-        for (int c = 0; c < ECH; ++c) {
-          const int l = l0 + FBW * u, e = c * 64 * VN + lane * VN;
-          xw[u][c] = ld16(Ws + (long)l * E + c * 64 * VN, l < L && e < E);
+        for (int q = 0; q < DCH; ++q) {
+          const int l = l0 + FBW * u, d = q * 64 * VN + lane * VN;
+          xa[u][q] = ld16(ab + (long)l * D + q * 64 * VN, l < l_end && d < D);
         }
     }
 #pragma unroll
     for (int u = 0; u < FBU; ++u) {
       const int l = l0 + FBW * u;
-      if (l >= L) break;   // wave-uniform
-      const float de = s_de[l];
+      if (l >= l_end) break;   // wave-uniform
+      float p = 0.f;
+#pragma unroll
+      for (int q = 0; q < DCH; ++q) {
+        const T* h = (const T*)&xa[u][q];
+#pragma unroll
+        for (int j = 0; j < VN; ++j) p += dctx[q][j] * (float)h[j];
+      }
+      p = wave_sum(p);
+      if (lane == 0) {
+        const float da = p + (a.d_alpha_ext ? a.d_alpha_ext[(long)b * a.d_alpha_ext_ld + l] : 0.f);
+        const float de = alpha[l] * (da - sad);
+        s_de[l - l_beg] = de;
+        a.de_out[(long)b * a.de_ld + l] = de;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- D: tanh backward over E for the chunk's slots ----
+  float duh[ECH][VN], dv[ECH][VN];
+#pragma unroll
+  for (int q = 0; q < ECH; ++q)
+#pragma unroll
+    for (int j = 0; j < VN; ++j) duh[q][j] = dv[q][j] = 0.f;
+  float dbv = 0.f;
+  for (int l0 = l_beg + w; l0 < l_end; l0 += FBW * FBU) {
+    if (l0 != l_beg + w) {
+#pragma unroll
+      for (int u = 0; u < FBU; ++u)
+#pragma unroll
+        for (int q = 0; q < ECH; ++q) {
+          const int l = l0 + FBW * u, e = q * 64 * VN + lane * VN;
+          xw[u][q] = ld16(Ws + (long)l * E + q * 64 * VN, l < l_end && e < E);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < FBU; ++u) {
+      const int l = l0 + FBW * u;
+      if (l >= l_end) break;   // wave-uniform
+      const float de = s_de[l - l_beg];
       dbv += de;
 #pragma unroll
-      for (int c = 0; c < ECH; ++c) {
-        const T* h = (const T*)&xw[u][c];
+      for (int q = 0; q < ECH; ++q) {
+        const T* h = (const T*)&xw[u][q];
 #pragma unroll
         for (int j = 0; j < VN; ++j) {
-          const float t = tanh_t<T>((float)h[j] + uu[c][j]);
-          duh[c][j] += de * vw[c][j] * (1.f - t * t);
-          dv[c][j] += de * t;
+          const float t = tanh_t<T>((float)h[j] + uu[q][j]);
+          duh[q][j] += de * vw[q][j] * (1.f - t * t);
+          dv[q][j] += de * t;
         }
       }
     }
   }
-  // fold the waves in a fixed order: dL/d(U h), then dL/dv
-  constexpr int EC = 64 * VN * ECH;
+  // fold the waves in a fixed order: dL/d(U h) into registers of threads e < E, then dL/dv
 #pragma unroll
-  for (int c = 0; c < ECH; ++c)
+  for (int q = 0; q < ECH; ++q)
 #pragma unroll
-    for (int j = 0; j < VN; ++j) s_red[w][c * 64 * VN + lane * VN + j] = duh[c][j];
+    for (int j = 0; j < VN; ++j) s_red[w][q * 64 * VN + lane * VN + j] = duh[q][j];
   __syncthreads();
-  for (int e = tid; e < EC && e < E; e += FBW * 64) {
-    float v = 0.f;
+  constexpr int EPT = (EC + FBW * 64 - 1) / (FBW * 64);   // folded columns per thread
+  float fu[EPT], fv[EPT];
 #pragma unroll
-    for (int i = 0; i < FBW; i += 2) v += s_red[i][e] + s_red[i + 1][e];
-    a.d_uh[(long)b * a.d_uh_ld + e] = v;
-    if (a.d_uh_t) ((T*)a.d_uh_t)[(long)b * a.d_uh_ld + e] = (T)v;
+  for (int k = 0; k < EPT; ++k) {
+    const int e = k * FBW * 64 + tid;
+    float v = 0.f;
+    if (e < EC && e < E) {
+#pragma unroll
+      for (int i = 0; i < FBW; i += 2) v += s_red[i][e] + s_red[i + 1][e];
+    }
+    fu[k] = v;
   }
   __syncthreads();
 #pragma unroll
-  for (int c = 0; c < ECH; ++c)
+  for (int q = 0; q < ECH; ++q)
 #pragma unroll
-    for (int j = 0; j < VN; ++j) s_red[w][c * 64 * VN + lane * VN + j] = dv[c][j];
+    for (int j = 0; j < VN; ++j) s_red[w][q * 64 * VN + lane * VN + j] = dv[q][j];
   dbv = wave_sum(dbv);
   if (lane == 0) s_tmp[w] = dbv;
   __syncthreads();
-  for (int e = tid; e < EC && e < E; e += FBW * 64) {
-    float v = 0.f;
 #pragma unroll
-    for (int i = 0; i < FBW; i += 2) v += s_red[i][e] + s_red[i + 1][e];
-    a.dv_acc[(long)b * E + e] += v;
+  for (int k = 0; k < EPT; ++k) {
+    const int e = k * FBW * 64 + tid;
+    float v = 0.f;
+    if (e < EC && e < E) {
+#pragma unroll
+      for (int i = 0; i < FBW; i += 2) v += s_red[i][e] + s_red[i + 1][e];
+    }
+    fv[k] = v;
+  }
+  float fb = 0.f;
+#pragma unroll
+  for (int i = 0; i < FBW; i += 2) fb += s_tmp[i] + s_tmp[i + 1];
+  if (NL == 1) {   // the whole row here: write directly
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int e = k * FBW * 64 + tid;
+      if (e < EC && e < E) {
+        a.d_uh[(long)b * a.d_uh_ld + e] = fu[k];
+        if (a.d_uh_t) ((T*)a.d_uh_t)[(long)b * a.d_uh_ld + e] = (T)fu[k];
+        a.dv_acc[(long)b * E + e] += fv[k];
+      }
+    }
+    if (tid == 0) a.dbv_acc[b] += fb;
+    return;
+  }
+  // ---- E: partials of the chunk -> the row's last-arriving workgroup ----
+  unsigned* pp = (unsigned*)a.part + (long)(b * NL + c) * (2 * E + 1);
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = k * FBW * 64 + tid;
+    if (e < EC && e < E) {
+      __hip_atomic_store(pp + e, __float_as_uint(fu[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(pp + E + e, __float_as_uint(fv[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (tid == 0) __hip_atomic_store(pp + 2 * E, __float_as_uint(fb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its sc1 stores are done
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(a.ticket + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (unsigned)(NL - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;   // workgroup-uniform
+  const unsigned* rp = (const unsigned*)a.part + (long)b * NL * (2 * E + 1);
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = k * FBW * 64 + tid;
+    if (e < EC && e < E) {
+      float su = 0.f, sv = 0.f;
+      for (int q = 0; q < NL; ++q) {   // chunk order: the same sums whichever workgroup arrives last
+        su += __uint_as_float(__hip_atomic_load(rp + (long)q * (2 * E + 1) + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        sv += __uint_as_float(__hip_atomic_load(rp + (long)q * (2 * E + 1) + E + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+      a.d_uh[(long)b * a.d_uh_ld + e] = su;
+      if (a.d_uh_t) ((T*)a.d_uh_t)[(long)b * a.d_uh_ld + e] = (T)su;
+      a.dv_acc[(long)b * E + e] += sv;
+    }
   }
   if (tid == 0) {
-    float v = 0.f;
-#pragma unroll
-    for (int i = 0; i < FBW; i += 2) v += s_tmp[i] + s_tmp[i + 1];
-    a.dbv_acc[b] += v;
+    float sb = 0.f;
+    for (int q = 0; q < NL; ++q)
+      sb += __uint_as_float(__hip_atomic_load(rp + (long)q * (2 * E + 1) + 2 * E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    a.dbv_acc[b] += sb;
+    __hip_atomic_store(a.ticket + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // ready for the next step
   }
 }
-
 template <typename T, int DCH, int ECH, int FBW, int FBU>
-__global__ __launch_bounds__(FBW * 64) void attn_bwd_fused_kernel(AttnBwdArgs a) {
-  const uint64_t t0 = sat_stamp_begin(a.st);
-  attn_bwd_fused_kernel_body<T, DCH, ECH, FBW, FBU>(a);
+__global__ __launch_bounds__(FBW * 64) void attn_bwd_split_kernel(AttnBwdArgs a) {
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
+  attn_bwd_split_kernel_body<T, DCH, ECH, FBW, FBU>(a);
   sat_stamp_end(a.st, t0);
 }
 
@@ -784,29 +839,35 @@ int sat_attention_fwd_launch(const AttnFwdArgs& args, hipStream_t s) {
 
 namespace {
 
+template <typename T, int DCH, int ECH>
+void launch_bwd_split_e(int nl, hipStream_t s, const AttnBwdArgs& a) {
+  constexpr int FBU = DCH >= 8 ? 2 : 4;
+  hipLaunchKernelGGL((attn_bwd_split_kernel<T, DCH, ECH, 8, FBU>), dim3(a.B, nl), dim3(8 * 64), 0, s, a);
+}
 template <typename T, int DCH>
-bool launch_bwd_fused_e(int ech, hipStream_t s, const AttnBwdArgs& a) {
-  constexpr int NW = DCH >= 4 ? 8 : 16, NU = DCH >= 4 ? 7 : 4;
-  if (ech == 1) {
-    hipLaunchKernelGGL((attn_bwd_fused_kernel<T, DCH, 1, NW, NU>), dim3(a.B), dim3(NW * 64), 0, s, a);
-    return true;
+bool launch_bwd_split_d(int ech, int nl, hipStream_t s, const AttnBwdArgs& a) {
+  switch (ech) {
+    case 1: launch_bwd_split_e<T, DCH, 1>(nl, s, a); return true;
+    case 2: launch_bwd_split_e<T, DCH, 2>(nl, s, a); return true;
+    default: break;
   }
-  if constexpr (sizeof(T) == 4 || DCH == 1) {   // bf16 with DCH >= 2 and ECH = 2 spills: two-launch form
-    if (ech == 2) {
-      hipLaunchKernelGGL((attn_bwd_fused_kernel<T, DCH, 2, NW, NU>), dim3(a.B), dim3(NW * 64), 0, s, a);
-      return true;
-    }
+  if constexpr (sizeof(T) == 4) {
+    if (ech == 3) { launch_bwd_split_e<T, DCH, 3>(nl, s, a); return true; }
+    if (ech == 4) { launch_bwd_split_e<T, DCH, 4>(nl, s, a); return true; }
   }
   return false;
 }
 template <typename T>
-bool launch_bwd_fused(const AttnBwdArgs& a, hipStream_t s) {
+bool launch_bwd_split(const AttnBwdArgs& a, hipStream_t s) {
   constexpr int VN = V16<T>::N;
   const int dch = sat_cdiv(a.D, 64 * VN), ech = sat_cdiv(a.E, 64 * VN);
+  const int nl = sat_attention_bwd_chunks(a.B, a.L);
+  if (nl > 1 && (!a.part || !a.ticket)) return false;
   switch (dch) {
-    case 1: return launch_bwd_fused_e<T, 1>(ech, s, a);
-    case 2: return launch_bwd_fused_e<T, 2>(ech, s, a);
-    case 4: return launch_bwd_fused_e<T, 4>(ech, s, a);
+    case 1: return launch_bwd_split_d<T, 1>(ech, nl, s, a);
+    case 2: return launch_bwd_split_d<T, 2>(ech, nl, s, a);
+    case 3: case 4: return launch_bwd_split_d<T, 4>(ech, nl, s, a);
+    case 5: case 6: case 7: case 8: return launch_bwd_split_d<T, 8>(ech, nl, s, a);
     default: return false;
   }
 }
@@ -820,7 +881,7 @@ int sat_attention_bwd_launch(const AttnBwdArgs& args, hipStream_t s) {
   SAT_REQUIRE(a.L <= kMaxL && a.E % VD == 0 && a.E <= 1024);
   SAT_REQUIRE(a.D % VD == 0);
   if (sat_policy().attn_bwd != 1 && (a.uh_ld % 4) == 0 && (a.E % 4) == 0) {
-    const bool ok = a.dtype == SAT_BF16 ? launch_bwd_fused<bf16>(a, s) : launch_bwd_fused<float>(a, s);
+    const bool ok = a.dtype == SAT_BF16 ? launch_bwd_split<bf16>(a, s) : launch_bwd_split<float>(a, s);
     if (ok) return (int)hipGetLastError();
   }
   const int NS = sat_cdiv(a.D, 64 * VD);
@@ -849,9 +910,20 @@ int sat_attention_dws_launch(const void* Ws, const float* uh_all, const float* d
   return (int)hipGetLastError();
 }
 
-size_t sat_attention_part_floats(int B, int L, int D, int dtype) {
+int sat_attention_bwd_chunks(int B, int L) {
+  // ~256 workgroups at least 4 slots deep: B = 128 -> 2 chunks, B = 64 -> 4, small test batches more
+  int nl = sat_cdiv(256, B);
+  const int by_l = sat_cdiv(L, 4);
+  if (nl > by_l) nl = by_l;
+  if (nl > 16) nl = 16;
+  return nl < 1 ? 1 : nl;
+}
+
+size_t sat_attention_part_floats(int B, int L, int D, int E, int dtype) {
   const int VD = dtype == SAT_BF16 ? 8 : 4;
-  return (size_t)B * sat_cdiv(D, 64 * VD) * L;
+  const size_t two_launch = (size_t)B * sat_cdiv(D, 64 * VD) * L;
+  const size_t split = (size_t)B * sat_attention_bwd_chunks(B, L) * (2 * E + 1);
+  return two_launch > split ? two_launch : split;
 }
 
 // Standalone Attention.forward (attention.py:14-21): two GEMMs + the fused kernel.

@@ -198,7 +198,7 @@ __device__ __forceinline__ void conv_ws_kernel_body(const WArgs& a) {
 
 template <int KK, int C, int PADT, int TR, int TW, int NSTG, int ACT>
 __global__ __launch_bounds__(WS_NW * 64) void conv_ws_kernel(WArgs a) {
-  const uint64_t t0 = sat_stamp_begin(a.st);
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
   conv_ws_kernel_body<KK, C, PADT, TR, TW, NSTG, ACT>(a);
   sat_stamp_end(a.st, t0);
 }

@@ -404,7 +404,7 @@ __device__ __forceinline__ void bottleneck_body(const KArgs& a) {
 
 template <int PF, int ABL>
 __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
-  const uint64_t t0 = sat_stamp_begin(a.st);
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
   bottleneck_body<14, 7, 1024, 256, PF, ABL>(a);
   sat_stamp_end(a.st, t0);
 }
@@ -643,7 +643,7 @@ template <int PF>
 __global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
                                                            SatStamps st) {
-  const uint64_t t0 = sat_stamp_begin(st);
+  const SatStampT0 t0 = sat_stamp_begin(st);
   conv3x3_band_body<28, 7, 128, 1, 1, PF>(x, wf, bias, y);
   sat_stamp_end(st, t0);
 }
@@ -758,7 +758,7 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
 __global__ __launch_bounds__(512) void conv1x1_frag_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
                                                            unsigned x_bytes, SatStamps st) {
-  const uint64_t t0 = sat_stamp_begin(st);
+  const SatStampT0 t0 = sat_stamp_begin(st);
   conv1x1_frag_body<14, 7, 1024, 256, 2>(x, wf, bias, y, x_bytes);
   sat_stamp_end(st, t0);
 }
@@ -768,7 +768,7 @@ template <int PF>
 __global__ __launch_bounds__(512) void conv3x3_frag_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
                                                            SatStamps st) {
-  const uint64_t t0 = sat_stamp_begin(st);
+  const SatStampT0 t0 = sat_stamp_begin(st);
   conv3x3_frag_body<14, 7, 256, PF>(x, wf, bias, y);
   sat_stamp_end(st, t0);
 }

@@ -473,7 +473,7 @@ __device__ __forceinline__ void fast_gemm_kernel_body(const FArgs& a) {
 
 template <int BM, int BN, int WGM, int WGN, bool AT, bool BT, int NS, bool RL = false>
 __global__ __launch_bounds__(WGM * WGN * 64) void fast_gemm_kernel(FArgs a) {
-  const uint64_t t0 = sat_stamp_begin(a.st);
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
   fast_gemm_kernel_body<BM, BN, WGM, WGN, AT, BT, NS, RL>(a);
   sat_stamp_end(a.st, t0);
 }

@@ -325,7 +325,7 @@ __device__ __forceinline__ void conv_pipe_kernel_body(const PArgs& a) {
 
 template <int NW, int AM, int ACT, bool RES, int ABL, bool BUF>
 __global__ __launch_bounds__(NW * 64) void conv_pipe_kernel(PArgs a) {
-  const uint64_t t0 = sat_stamp_begin(a.st);
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
   conv_pipe_kernel_body<NW, AM, ACT, RES, ABL, BUF>(a);
   sat_stamp_end(a.st, t0);
 }

@@ -257,7 +257,7 @@ __device__ __forceinline__ void conv1x1_stream_kernel_body(const SArgs& a) {
 
 template <int KT, int MB, int NB, bool RES, int ACT, bool STRIDED>
 __global__ __launch_bounds__(S_NW * 64) void conv1x1_stream_kernel(SArgs a) {
-  const uint64_t t0 = sat_stamp_begin(a.st);
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
   conv1x1_stream_kernel_body<KT, MB, NB, RES, ACT, STRIDED>(a);
   sat_stamp_end(a.st, t0);
 }

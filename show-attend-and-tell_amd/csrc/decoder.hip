@@ -34,6 +34,7 @@ struct WS {
   void *dpre_t, *dfh_t, *dfz_t, *dhg_t, *dWs_t, *dpre0_t;
   float *dcomb, *dhd, *dctx_head, *dhg, *dgated, *dh_rec, *dc, *dWs_acc, *dv_acc, *dbv_acc, *part, *demb, *dpre0,
       *colsum, *de_all;
+  unsigned* ticket;
 };
 
 // split counts of the per-step skinny GEMMs (M = B rows).  bf16: the LDS-DMA kernel (128 x 64
@@ -139,7 +140,8 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   c.take(w->dWs_acc, B * L * E * f); c.take(w->dWs_t, B * L * E * ts);
   c.take(w->dv_acc, B * E * f); c.take(w->dbv_acc, B * f);
   c.take(w->de_all, R * L * f);
-  c.take(w->part, sat_attention_part_floats(d.B, d.L, d.D, d.dtype) * f);
+  c.take(w->part, sat_attention_part_floats(d.B, d.L, d.D, d.E, d.dtype) * f);
+  c.take(w->ticket, B * 4);
   c.take(w->demb, R * E * f);
   c.take(w->dpre0, B * 2 * E * f); c.take(w->dpre0_t, B * 2 * E * ts);
   size_t maxN = V > HG ? V : HG;
@@ -382,6 +384,7 @@ int bwd_attn(const Ctx& c, const WS& w, const Splits& sp, const StepIO& io, int 
   a.d_uh = w.dhg + (long)t * HG; a.d_uh_ld = T1 * HG; a.d_uh_t = c.at(w.dhg_t, (long)t * HG);
   a.d_gpre = w.dhg + (long)t * HG + E; a.d_gpre_ld = T1 * HG; a.d_gpre_t = c.at(w.dhg_t, (long)t * HG + E);
   a.de_out = w.de_all + (long)t * L; a.de_ld = T1 * L; a.dv_acc = w.dv_acc; a.dbv_acc = w.dbv_acc; a.part = w.part;
+  a.ticket = w.ticket;
   a.dg_splits = sp.g; a.dg_split_stride = (long)B * D;
   return sat_attention_bwd_launch(a, s);
 }
@@ -399,7 +402,7 @@ int bwd_dhgemm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s
 }
 
 // In-kernel timestamps of the per-step kernels (SatPolicy::stamps, bench.py's in-step figures): the
-// policy's buffer holds kStampGroups x (T-1) slots of stamp_capacity workgroups, group g (the
+// policy's buffer holds kStampGroups x (T-1) slots (a 16-B header + stamp_capacity records), group g (the
 // sat_decoder_step_bench order: h GEMM, attention fwd, context GEMM, LSTM fwd, LSTM bwd, d(gated
 // context) GEMM, attention bwd, dh GEMM) at step t in slot g * (T-1) + t; every other launch of the
 // decoder records nothing.
@@ -407,7 +410,7 @@ constexpr int kStampGroups = 8;
 inline uint64_t* step_slot(const SatDecoderDims& d, int g, int t) {
   const SatPolicy* p = d.policy;
   if (!p || !p->stamps || p->stamp_capacity <= 0) return nullptr;
-  return p->stamps + ((long)g * (d.T - 1) + t) * 2L * p->stamp_capacity;
+  return p->stamps + ((long)g * (d.T - 1) + t) * 2L * (p->stamp_capacity + 1);   // slot: header + records
 }
 inline int stamp_cap(const SatDecoderDims& d) { return d.policy ? d.policy->stamp_capacity : 0; }
 
@@ -620,6 +623,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   if (att) {
     SAT_CHECK((hipError_t)sat_zero_rows(w.dv_acc, (long)B * E, 1, (long)B * E, s));
     SAT_CHECK((hipError_t)sat_zero_rows(w.dbv_acc, B, 1, B, s));
+    SAT_CHECK((hipError_t)sat_zero_rows((float*)w.ticket, B, 1, B, s));   // split attention backward tickets
   }
   const StepIO io{img_features, const_cast<float*>(alphas), d_alphas};
   for (int t = T1 - 1; t >= 0; --t) {

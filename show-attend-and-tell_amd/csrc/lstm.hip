@@ -53,7 +53,7 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
 
 template <typename T>
 __global__ __launch_bounds__(256) void lstm_fwd_gp_kernel(LstmFwdArgs a) {
-  const uint64_t t0 = sat_stamp_begin(a.st);
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
   lstm_fwd_gp_kernel_body<T>(a);
   sat_stamp_end(a.st, t0);
 }
@@ -109,7 +109,7 @@ __device__ __forceinline__ void lstm_bwd_gp_kernel_body(LstmBwdArgs a) {
 
 template <typename T>
 __global__ __launch_bounds__(256) void lstm_bwd_gp_kernel(LstmBwdArgs a) {
-  const uint64_t t0 = sat_stamp_begin(a.st);
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
   lstm_bwd_gp_kernel_body<T>(a);
   sat_stamp_end(a.st, t0);
 }

@@ -38,10 +38,33 @@ struct SatPolicyScope {
 };
 
 // ---- in-kernel launch timestamps (SatPolicy::stamps) ---------------------------
+// A launch's stamp slot: p[0] = enable word (written by the host side between replays: a captured graph
+// keeps its slots, so its stamps can be switched on for a diagnostic phase and off for the timed one),
+// p[1] unused, then {start, end} of workgroup w at p[2 + 2 w], p[3 + 2 w] for w < cap.  Disabled, a
+// launch costs one scalar load of the enable word per workgroup.
 struct SatStamps {
   uint64_t* p = nullptr;
   int cap = 0;
 };
+struct SatStampT0 {
+  uint64_t t0;
+  bool on;
+};
+__device__ __forceinline__ SatStampT0 sat_stamp_begin(const SatStamps& st) {
+  if (!st.p || st.p[0] == 0) return SatStampT0{0, false};   // uniform
+  return SatStampT0{__builtin_amdgcn_s_memrealtime(), true};
+}
+// every wave of the workgroup has finished its work (barrier), then one lane records {start, end}
+__device__ __forceinline__ void sat_stamp_end(const SatStamps& st, SatStampT0 t) {
+  if (!t.on) return;   // uniform
+  __syncthreads();
+  const int w = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  if (threadIdx.x == 0 && w < st.cap) {
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    *(ulonglong2*)(st.p + 2 + 2 * (long)w) = make_ulonglong2(t.t0, t1);
+  }
+}
+
 // the stamp slots of the next launch: the innermost SatStampScope's (the decoder gives every per-step launch
 // its own slot and none to the rest: p = nullptr), else the call's SatPolicy
 SatStamps sat_launch_stamps();
@@ -53,20 +76,6 @@ struct SatStampScope {
   SatStampScope(const SatStampScope&) = delete;
   SatStampScope& operator=(const SatStampScope&) = delete;
 };
-__device__ __forceinline__ uint64_t sat_stamp_begin(const SatStamps& st) {
-  return st.p ? __builtin_amdgcn_s_memrealtime() : 0;
-}
-// every wave of the workgroup has finished its work (barrier), then one lane records {start, end}
-__device__ __forceinline__ void sat_stamp_end(const SatStamps& st, uint64_t t0) {
-  if (!st.p) return;   // uniform
-  __syncthreads();
-  const int w = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-  if (threadIdx.x == 0 && w < st.cap) {
-    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-    *(ulonglong2*)(st.p + 2 * (long)w) = make_ulonglong2(t0, t1);
-  }
-}
-
 // ---- scalar load/store helpers for the two storage dtypes -------------------
 __device__ __forceinline__ float ld_as_f32(const void* p, long i, int dt) {
   return dt == SAT_BF16 ? (float)((const bf16*)p)[i] : ((const float*)p)[i];

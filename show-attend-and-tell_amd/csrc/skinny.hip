@@ -114,7 +114,7 @@ __device__ __forceinline__ void skinny_gemm_kernel_body(SkArgs a) {
 
 template <int MB, int NW>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(SkArgs a) {
-  const uint64_t t0 = sat_stamp_begin(a.st);
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
   skinny_gemm_kernel_body<MB, NW>(a);
   sat_stamp_end(a.st, t0);
 }

@@ -1,12 +1,12 @@
 # in-step stamps vs rocprof on the same bench command
 set -u
-OUT=gpurun_out/r3_s5; mkdir -p $OUT; export TMPDIR=/tmp
+OUT=gpurun_out/r3_s7; mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 300 python bench.py --steps 100 --no-cpu-baseline --fp32-steps 0 > $OUT/bench.log 2>&1 || { tail -30 $OUT/bench.log; exit 1; }
 timeout -k 10 300 python bench.py --steps 100 --no-cpu-baseline --fp32-steps 0 --no-step-stamps --no-diagnostics > $OUT/bench_nostamp.log 2>&1 || { tail -30 $OUT/bench_nostamp.log; exit 1; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 100 --warmup 1 --no-cpu-baseline --fp32-steps 0 --no-diagnostics > $OUT/prof.log 2>&1 || { tail -30 $OUT/prof.log; exit 1; }
 python - <<'PY'
 import json, glob, csv
-out = "gpurun_out/r3_s5"
+out = "gpurun_out/r3_s7"
 for f in ("bench", "bench_nostamp"):
     d = json.loads([l for l in open(f"{out}/{f}.log") if l.startswith("{")][-1])
     r = d.get("roofline") or {}
