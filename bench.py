@@ -68,6 +68,9 @@ def parse():
                          "split-K GEMMs, 2 otherwise)")
     ap.add_argument("--no-ws3x3", action="store_true",
                     help="64 -> 64 3x3 convs on the implicit-GEMM tile kernel instead of csrc/conv3x3ws.hip (A/B)")
+    ap.add_argument("--conv-slices", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="layer3 c1 / c2 kernels: 0 auto (two 128-channel slices per half image at B <= 64), 1 one "
+                         "workgroup per half image, 2 / 3 two slices (SatPolicy.conv_slices, A/B)")
     ap.add_argument("--fuse-every", type=int, default=None,
                     help="fuse every n-th layer3 identity bottleneck only, the rest run as three conv launches "
                          "(default 0 = none: with the layer3 c2 / c3 on the half-image frag kernels the unfused "
@@ -100,10 +103,12 @@ class LaunchStamps:
     device's 100 MHz real-time counter); the launch's span is max(end) - min(start) -- the kernel's own
     duration inside the overlapped graph replays, with no extra node, event or barrier in the stream.
     The slots' enable words are off during the timed region (a launch then pays one scalar load) and on
-    for a diagnostic phase of the same overlapped schedule right after it.  Event-record nodes spliced
-    into the graph between kernels cost ~3 us each and add that to every bracketed kernel
-    (tools/graph_event_probe.py); a rocprofv3 kernel trace all but serialises the two streams (6 % of
-    the busy time overlapped, profiles/r3_s6/), so neither gives in-step kernel durations."""
+    for a diagnostic phase of the same overlapped schedule right after it, and for replays of each graph on
+    its own.  Timing events cannot be captured as graph nodes on this runtime (hipEventRecordWithFlags(..,
+    hipEventRecordExternal) returns hipErrorInvalidValue during capture: tools/event_node_probe.py,
+    profiles/r3_s9/probe.log), and a rocprofv3 kernel trace all but serialises the two streams (2.6 % of the
+    traced busy time had kernels of two queues running, profiles/r3_s8/prof_summary.json) and adds its own
+    per-dispatch signalling to every duration, so neither gives in-step kernel durations."""
 
     def __init__(self, n_launches, device, base=None, cap=16384):
         import sat_amd
@@ -249,14 +254,19 @@ def instep_conv_durations(stamps, launches):
     return per
 
 
-def trunk_roofline(enc, imgs, launches, instep=None, reps=3):
+def trunk_roofline(enc, imgs, launches, instep=None, overlapped=None, reps=3):
     """The encoder trunk against its roofline.
 
-    Dominant launch class and its ``achieved`` / ``frac``: from the IN-STEP durations when given (every
-    conv kernel of the timed, overlapped steps timed by its own in-kernel timestamps, LaunchStamps):
-    the figure a rocprofv3 kernel trace of the same command averages.  Secondary figures: the class's
-    launches of an eager forward re-issued back to back into warm caches (``avg_launch_us_b2b``) and an
-    event pair around every launch of ``reps`` eager forwards (``avg_launch_us_eager_event_pairs``)."""
+    Per conv launch, up to three durations [us]:
+      ``us``            the kernel's own first-start / last-end in-kernel timestamps in the captured encoder
+                        graphs replayed on their own after the timed region (LaunchStamps, ``instep``);
+      ``us_overlapped`` the same timestamps inside the timed region's overlapped schedule (``overlapped``);
+      ``us_eager``      an event pair around every launch of ``reps`` eager forwards.
+    The dominant class (largest per-forward time) and its ``achieved`` / ``frac`` come from ``us``; the others
+    are reported beside it, with the class's launches re-issued back to back into warm caches
+    (``avg_launch_us_b2b``).  A rocprofv3 kernel trace of the same command reports ~4 us more per conv
+    dispatch: its per-dispatch completion signalling (profiles/r3_s8/prof_summary.json: under the trace these
+    timestamps read 27.0 us for L3c2 where the trace reads 30.9 for the same launches)."""
     enc.timing, enc.timing_args = [], []
     with torch.no_grad():
         for _ in range(reps):
@@ -266,26 +276,26 @@ def trunk_roofline(enc, imgs, launches, instep=None, reps=3):
     conv_args, enc.timing_args = enc.timing_args, None
     n = len(launches)
     assert len(ev) == reps * n, (len(ev), n)
-    dur = [0.0] * n
+    eager = [0.0] * n
     for r in range(reps):
         for i in range(n):
             st, en = ev[r * n + i]
-            dur[i] += st.elapsed_time(en) / reps * 1e3   # us
-    if instep is not None:
-        step_dur = [sum(v) / len(v) if v else dur[i] for i, v in enumerate(instep)]
-    else:
-        step_dur = dur
+            eager[i] += st.elapsed_time(en) / reps * 1e3   # us
+
+    def mean_or_none(v):
+        return [sum(x) / len(x) if x else None for x in v] if v is not None else [None] * n
+    span, ov = mean_or_none(instep), mean_or_none(overlapped)
+    primary = [s_ if s_ is not None else e for s_, e in zip(span, eager)]
+    series = {"us": primary, "us_overlapped": ov, "us_eager": eager}
     cls = {}
-    for l, d, de in zip(launches, step_dur, dur):
-        c = cls.setdefault(l["cls"], dict(n=0, us=0.0, us_eager=0.0, flops=l["flops"], bytes=l["bytes"],
-                                          bound=l["bound"], fused=l.get("fused", False)))
+    for i, l in enumerate(launches):
+        c = cls.setdefault(l["cls"], dict(n=0, flops=l["flops"], bytes=l["bytes"], bound=l["bound"],
+                                          fused=l.get("fused", False), **{k: 0.0 for k in series}))
         c["n"] += 1
-        c["us"] += d
-        c["us_eager"] += de
+        for k, v in series.items():
+            c[k] += v[i] if v[i] is not None else float("nan")
     name, dom = max(cls.items(), key=lambda kv: kv[1]["us"])
     idx = [i for i, l in enumerate(launches) if l["cls"] == name]
-    avg_us = dom["us"] / dom["n"]
-    samples = sum(len(instep[i]) for i in idx) if instep is not None else 0
     # the dominant class's launches of the last forward re-issued back to back (same inputs, 5 each)
     from sat_amd import ops
     last = conv_args[(reps - 1) * n:]
@@ -318,31 +328,46 @@ def trunk_roofline(enc, imgs, launches, instep=None, reps=3):
         if dom["bound"] == "hbm":
             return dom["bytes"] / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s"
         return dom["flops"] / (us * 1e-6) / 1e12, BF16_DENSE_PEAK_TFLOPS, "TFLOP/s"
+    avg_us = dom["us"] / dom["n"]
     achieved, peak, unit = rate(avg_us)
+    extra = {}
+    for key, k in (("overlapped", "us_overlapped"),):
+        a = dom[k] / dom["n"]
+        if a == a:
+            extra[f"avg_launch_us_{key}"] = round(a, 2)
+            extra[f"frac_{key}"] = round(rate(a)[0] / peak, 4)
     floor_us = sum(max(l["flops"] / (BF16_DENSE_PEAK_TFLOPS * 1e12), l["bytes"] / (PEAK_HBM_ACHIEVABLE_GBS * 1e9))
                    for l in launches) * 1e6
-    trunk_us = sum(step_dur)
     kname = "bottleneck_kernel (csrc/convblock.hip), fused block" if dom.get("fused") else (
         "conv3x3_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c2frag" for i in idx)
         else "conv1x1_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c1frag" for i in idx)
         else "conv kernels, conv class")
-    timing = (f"avg_launch_us: in-step -- every launch of the class in the last replay of each encoder graph of "
-              f"the timed, overlapped region ({samples} launches), timed by the kernels' own first-start / last-end "
-              f"timestamps (LaunchStamps); avg_launch_us_b2b: the class re-issued back to back into warm caches; "
-              f"avg_launch_us_eager_event_pairs: an event pair around every launch of {reps} eager forwards"
+    timing = ("avg_launch_us: the kernels' own first-start / last-end in-kernel timestamps (LaunchStamps) of every "
+              "launch of the class in the captured encoder graphs replayed on their own after the timed region; "
+              "avg_launch_us_overlapped: the same timestamps inside the timed region's overlapped schedule (sharing "
+              "CUs with the decoder graphs); avg_launch_us_b2b: the class re-issued back to back into warm caches; "
+              f"avg_launch_us_eager_event_pairs: an event pair around every launch of {reps} eager forwards; a "
+              "rocprofv3 kernel trace adds its per-dispatch signalling (~4 us per conv launch, the same launches' "
+              "timestamps under the trace: profiles/r3_s8/prof_summary.json)"
               if instep is not None else
-              "avg_launch_us: an event pair around every launch of three eager forwards (no graph timers)")
+              "avg_launch_us: an event pair around every launch of the eager forwards (no in-kernel timestamps)")
+
+    def tot(k):
+        v = sum(x for x in series[k] if x is not None) if any(x is not None for x in series[k]) else None
+        return round(v, 1) if v is not None else None
     return dict(kernel=f"{kname} {name} ({dom['n']} launches/forward)", cls=name,
                 bound=dom["bound"], achieved=round(achieved, 2), peak=peak, unit=unit,
-                frac=round(achieved / peak, 4), avg_launch_us=round(avg_us, 2),
+                frac=round(achieved / peak, 4), avg_launch_us=round(avg_us, 2), **extra,
                 avg_launch_us_b2b=round(b2b_us, 2), frac_b2b=round(rate(b2b_us)[0] / peak, 4),
                 avg_launch_us_eager_event_pairs=round(dom["us_eager"] / dom["n"], 2),
                 timing=timing, algorithmic_bytes_per_launch=dom["bytes"], algorithmic_flops_per_launch=dom["flops"]), \
-        dict(conv_us_per_forward=round(trunk_us, 1), conv_us_per_forward_eager=round(sum(dur), 1),
-             roofline_floor_us=round(floor_us, 1), frac_of_floor=round(floor_us / trunk_us, 4),
-             timing="in-step (graph event nodes) when available, else eager event pairs",
-             classes={k: dict(n=v["n"], us=round(v["us"], 1), us_eager=round(v["us_eager"], 1)) for k, v in
-                      sorted(cls.items(), key=lambda kv: -kv[1]["us"])})
+        dict(conv_us_per_forward=tot("us"), conv_us_per_forward_overlapped=tot("us_overlapped"),
+             conv_us_per_forward_eager=tot("us_eager"),
+             roofline_floor_us=round(floor_us, 1), frac_of_floor=round(floor_us / tot("us"), 4),
+             timing="per class: us = in-kernel timestamps (the encoder graphs replayed alone), us_overlapped = the "
+                    "same in the timed region's overlapped schedule, us_eager = eager event pairs (roofline.timing)",
+             classes={k: dict(n=v["n"], **{s_: round(v[s_], 1) for s_ in series if v[s_] == v[s_]})
+                      for k, v in sorted(cls.items(), key=lambda kv: -kv[1]["us"])})
 
 
 def pmc_traffic(network, cls):
@@ -421,24 +446,24 @@ def cpu_baseline(args):
                                          "parameters not frozen, encoder.py:13-17)"}}
 
 
-def decoder_step_roofline(dec, enc, imgs, caps, instep=None, reps=20):
+def decoder_step_roofline(dec, enc, imgs, caps, instep=None, overlapped=None, reps=20):
     """The per-time-step decoder kernels (the fused attention + LSTM step of SURVEY 8(d) and the per-step
-    GEMMs) against 8 TB/s: algorithmic bytes per launch / time.  ``us``: in-step (every per-step launch of
-    the last replay of each decoder graph in the timed region, from the kernels' own timestamps,
-    DecoderStamps) when given; ``us_b2b``:
-    each group of the middle step re-issued ``reps`` times back to back between HIP events
-    (sat_decoder_step_bench)."""
+    GEMMs) against 8 TB/s: algorithmic bytes per launch / time.  Per group, up to three durations [us]:
+    ``us`` the kernels' own first-start / last-end timestamps in the timed decoder graphs replayed on their own
+    after the timed region (DecoderStamps, ``instep``); ``us_overlapped`` the same inside the timed region's
+    overlapped schedule; ``us_b2b`` each group of the middle step re-issued ``reps`` times back to back between
+    HIP events (sat_decoder_step_bench).  A rocprofv3 kernel trace reports ~2 us more per decoder dispatch (its
+    per-dispatch signalling; profiles/r3_s8/prof_summary.json)."""
     from sat_amd.diagnostics import FUSED, decoder_step_kernels
     with torch.no_grad():
         feats = enc(imgs)
     times_b2b, by = decoder_step_kernels(dec, feats, caps, reps=reps)
-    times = dict(times_b2b)
-    n_samples = {}
-    if instep:
-        for g, v in instep.items():
-            if v:
-                times[g] = sum(v) / len(v)
-                n_samples[g] = len(v)
+
+    def avg(d):
+        return {g: sum(v) / len(v) for g, v in (d or {}).items() if v}
+    t_span, t_ov = avg(instep), avg(overlapped)
+    primary = t_span or times_b2b
+    times = {g: primary.get(g, times_b2b[g]) for g in times_b2b}
 
     def frac(b, us):
         return b / (us * 1e-6) / 1e9 / HBM_PEAK_GBS
@@ -446,25 +471,28 @@ def decoder_step_roofline(dec, enc, imgs, caps, instep=None, reps=20):
     for g, us in times.items():
         if us <= 0 or by[g] <= 0:
             continue
-        groups[g] = {"us": round(us, 2), "us_b2b": round(times_b2b[g], 2), "mb": round(by[g] / 1e6, 2),
-                     "gbs": round(by[g] / (us * 1e-6) / 1e9, 1), "frac": round(frac(by[g], us), 4),
-                     "in_step_launches": n_samples.get(g, 0)}
-    f_by = sum(by[g] for g in FUSED if g in groups)
-    f_us = sum(times[g] for g in FUSED if g in groups)
-    f_b2b = sum(times_b2b[g] for g in FUSED if g in groups)
-    a_by = sum(by[g] for g in groups)
-    a_us = sum(times[g] for g in groups)
-    a_b2b = sum(times_b2b[g] for g in groups)
-    src = ("us: in-step (the per-step kernels of the timed region's decoder graphs, first-start to last-end "
-           "in-kernel timestamps); us_b2b: "
-           if instep else "us: ") + f"each group of step (T-1)/2 re-issued {reps}x back to back between HIP events"
+        groups[g] = {"us": round(us, 2), "mb": round(by[g] / 1e6, 2), "gbs": round(by[g] / (us * 1e-6) / 1e9, 1),
+                     "frac": round(frac(by[g], us), 4), "us_b2b": round(times_b2b[g], 2)}
+        for key, t in (("us_overlapped", t_ov),):
+            if g in t:
+                groups[g][key] = round(t[g], 2)
+
+    def summary(keys):
+        by_ = sum(by[g] for g in keys if g in groups)
+        out = {}
+        for key, t in (("", times), ("_overlapped", t_ov), ("_b2b", times_b2b)):
+            if all(g in t for g in keys if g in groups):
+                us = sum(t[g] for g in keys if g in groups)
+                out[f"us_per_step{key}"] = round(us, 2)
+                out[f"frac{key}"] = round(frac(by_, us), 4)
+        out["achieved"] = round(by_ / (out["us_per_step"] * 1e-6) / 1e9, 1)
+        return out
+    src = ("us: the kernels' own first-start / last-end in-kernel timestamps in the timed decoder graphs replayed on "
+           "their own; us_overlapped: the same inside the timed region's overlapped schedule; " if t_span else "us: ") + \
+        f"us_b2b: each group of step (T-1)/2 re-issued {reps}x back to back between HIP events"
     return {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "timing": src, "groups": groups,
-            "fused_attention_lstm": {"kernels": list(FUSED), "us_per_step": round(f_us, 2),
-                                     "achieved": round(f_by / (f_us * 1e-6) / 1e9, 1),
-                                     "frac": round(frac(f_by, f_us), 4), "us_per_step_b2b": round(f_b2b, 2),
-                                     "frac_b2b": round(frac(f_by, f_b2b), 4)},
-            "all_step_kernels": {"us_per_step": round(a_us, 2), "achieved": round(a_by / (a_us * 1e-6) / 1e9, 1),
-                                 "frac": round(frac(a_by, a_us), 4), "us_per_step_b2b": round(a_b2b, 2)}}
+            "fused_attention_lstm": dict(kernels=list(FUSED), **summary(FUSED)),
+            "all_step_kernels": summary(list(groups))}
 
 
 def fp32_step(args, enc, dec, imgs, caps, pad_id, skip_ids, world):
@@ -520,9 +548,9 @@ def main():
 
     # per-call kernel selection for the A/B flags (None = the library's defaults)
     policy = None
-    if args.no_skinny or args.no_ws3x3 or args.gemm_stages:
+    if args.no_skinny or args.no_ws3x3 or args.gemm_stages or args.conv_slices:
         policy = sat_amd.Policy(skinny=1 if args.no_skinny else 0, conv3x3_ws=1 if args.no_ws3x3 else 0,
-                                gemm_stages=args.gemm_stages)
+                                gemm_stages=args.gemm_stages, conv_slices=args.conv_slices)
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
@@ -740,15 +768,42 @@ def main():
             st.enable(False)
     loss_v = loss.item()
     diag = rank == 0 and not args.no_diagnostics
-    instep_conv = instep_conv_durations(stamps_enc, launches) if diag_phase and stamps_enc else None
-    instep_dec = None
-    if diag_phase and stamps_dec:
-        instep_dec = {}
-        for sd in stamps_dec:
-            for g, v in sd.group_spans_us().items():
-                instep_dec.setdefault(g, []).extend(v)
-    roof, trunk = trunk_roofline(enc, imgs, launches, instep=instep_conv) if diag else (None, None)
-    step_kernels = decoder_step_roofline(dec, enc, imgs, caps, instep=instep_dec) if diag else None
+
+    def collect():
+        conv = instep_conv_durations(stamps_enc, launches) if stamps_enc else None
+        decd = None
+        if stamps_dec:
+            decd = {}
+            for sd in stamps_dec:
+                for g, v in sd.group_spans_us().items():
+                    decd.setdefault(g, []).extend(v)
+        return conv, decd
+    overlap_conv, overlap_dec = collect() if diag_phase else (None, None)
+    alone_conv = alone_dec = None
+    if diag and diag_phase and use_graph:
+        # graph-alone phase: each encoder graph, then each decoder graph pair, replayed on its own (nothing
+        # beside it) with the timestamps on -- the kernels' durations as a rocprofv3 kernel trace of this
+        # command sees them (the trace all but serialises the two streams); the overlapped figures above
+        # stay as the secondary in-step keys
+        for st in stamps_enc + stamps_dec:
+            st.enable(True)
+        torch.cuda.synchronize()
+        for k in range(len(g_enc)):
+            for _ in range(3):
+                g_enc[k].replay()
+                torch.cuda.synchronize()
+            for _ in range(3):
+                g_dec[k].replay()
+                if g_rec[k] is not None:
+                    g_rec[k].replay()
+                torch.cuda.synchronize()
+        alone_conv, alone_dec = collect()
+        for st in stamps_enc + stamps_dec:
+            st.enable(False)
+    roof, trunk = trunk_roofline(enc, imgs, launches, instep=alone_conv or overlap_conv,
+                                 overlapped=overlap_conv) if diag else (None, None)
+    step_kernels = decoder_step_roofline(dec, enc, imgs, caps, instep=alone_dec or overlap_dec,
+                                         overlapped=overlap_dec) if diag else None
     fp32_leg = fp32_step(args, enc, dec, imgs, caps, pad_id, skip_ids, world) if world == 1 and args.fp32_steps > 0 \
         else None
     if roof is not None:

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SAT_ABI_VERSION 2
+#define SAT_ABI_VERSION 3
 
 enum { SAT_F32 = 0, SAT_BF16 = 1 };
 enum { SAT_ACT_NONE = 0, SAT_ACT_RELU = 1, SAT_ACT_TANH = 2, SAT_ACT_SIGMOID = 3 };
@@ -72,6 +72,9 @@ typedef struct {
    * 2 (stamp_capacity + 1) words, one per per-step kernel group and step (decoder.hip). */
   uint64_t* stamps;
   int stamp_capacity;
+  int conv_slices;      /* layer3 c1 / c2 half-image kernels (sat_conv1x1_frag, sat_conv3x3_frag at 14x14): 0 auto
+                         * (channel slices when B <= 64), 1 one workgroup per half image, 2 two 128-channel slices
+                         * per half image, 3 (3x3 only) the same with two m-groups of waves */
 } SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),
@@ -119,6 +122,11 @@ typedef struct {
   int64_t embedding, init_w, init_b, hcat_w, hcat_b, attW_w, attW_b, v_w, v_b, wih, bih;
   int64_t fh_w, fh_b, fz_w, fz_b, fout_w, fout_b, do_w, do_b;
   int64_t total;
+  /* bf16 mode, optional (-1 = absent): element offsets in params_lp of transposed copies
+   *   wih_ctx_t = W_ih[:, E:]^T [D, 4E] and hcat_t = hcat_w^T [E, E+D+4E]
+   * (sat_decoder_refresh_transposed writes them from the shadow's own rows after every weight update); the
+   * BPTT's dL/d(gated context) and dL/dh products then read k-contiguous weights (the skinny kernel) */
+  int64_t wih_ctx_t, hcat_t;
 } SatDecoderLayout;
 
 int sat_abi_version(void);
@@ -203,6 +211,10 @@ int sat_decoder_step_bench(const SatDecoderDims* dims, const SatDecoderLayout* l
                            const void* params_lp, const void* img_features, void* workspace, size_t workspace_bytes,
                            float* alphas, const float* d_alphas, int reps, float* us_out, void* stream);
 size_t sat_decoder_workspace_bytes(const SatDecoderDims* d);
+/* bf16 mode: rewrite the transposed weight copies layout->wih_ctx_t / hcat_t inside params_lp from the shadow's
+ * own W_ih / hcat rows (after the shadow changed: the fused Adam step, a cast); a no-op when either is -1. */
+int sat_decoder_refresh_transposed(const SatDecoderDims* d, const SatDecoderLayout* lay, void* params_lp,
+                                   void* stream);
 /* preds [B,T-1,V] (dtype), alphas [B,T-1,L] fp32, tokens [B,T-1] int32 = token fed at each step. */
 int sat_decoder_forward(const SatDecoderDims* d, const SatDecoderLayout* lay, const float* params,
                         const void* params_lp, const void* img_features, const int64_t* captions,

@@ -25,14 +25,14 @@ class SatConvGeom(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("N", "H", "W", "C", "KH", "KW", "stride", "pad", "OH", "OW")]
 
 
-ABI_VERSION = 2   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
+ABI_VERSION = 3   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
 
 
 class SatPolicy(ctypes.Structure):
     """Per-call kernel selection (include/sat_hip.h SatPolicy); all zeros = the library's defaults."""
     _fields_ = [(n, c_int) for n in ("conv_pipe", "conv_stream", "conv3x3_ws", "skinny", "gemm_stages", "gemm_tile",
                                      "gemm_linear_order", "gemm_epilogue", "attn_bwd")] + \
-               [("decoder_splits", c_int * 4), ("stamps", c_void_p), ("stamp_capacity", c_int)]
+               [("decoder_splits", c_int * 4), ("stamps", c_void_p), ("stamp_capacity", c_int), ("conv_slices", c_int)]
 
     def __init__(self, **kw):
         splits = kw.pop("decoder_splits", None)
@@ -62,7 +62,8 @@ class SatDecoderDims(ctypes.Structure):
 
 
 LAYOUT_FIELDS = ("embedding", "init_w", "init_b", "hcat_w", "hcat_b", "attW_w", "attW_b", "v_w", "v_b", "wih",
-                 "bih", "fh_w", "fh_b", "fz_w", "fz_b", "fout_w", "fout_b", "do_w", "do_b", "total")
+                 "bih", "fh_w", "fh_b", "fz_w", "fz_b", "fout_w", "fout_b", "do_w", "do_b", "total", "wih_ctx_t",
+                 "hcat_t")
 
 
 class SatDecoderLayout(ctypes.Structure):
@@ -97,6 +98,8 @@ _SIGNATURES = [
                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p]),
     ("sat_decoder_workspace_bytes", c_size_t, [ctypes.POINTER(SatDecoderDims)]),
+    ("sat_decoder_refresh_transposed", c_int, [ctypes.POINTER(SatDecoderDims), ctypes.POINTER(SatDecoderLayout),
+                                               c_void_p, c_void_p]),
     ("sat_decoder_forward", c_int, [ctypes.POINTER(SatDecoderDims), ctypes.POINTER(SatDecoderLayout), c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
                                     c_void_p, c_void_p, c_void_p]),

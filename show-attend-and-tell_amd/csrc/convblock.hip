@@ -71,9 +71,9 @@ __device__ __forceinline__ void k_wait_barrier() {
 __device__ __forceinline__ void k_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // vmem instructions one wave issues after its input DMAs A(T) (2 instructions) and before the wait
-// of c1 k-tile T: the issue order is A0 B0 A1 B1 B2 .. B(PF-1) (B = 4 weight loads), then per k-tile
+// of c1 k-tile T: the issue order is A0 B0 A1 B1 B2 .. B(PF-1) (B = nb weight loads), then per k-tile
 // it, after its wait: A(it+2) (it+2 < KT1), B(it+PF) (it+PF < NT, when weights stream)
-constexpr int younger_than_a(int T, int KT1, int NT, int PF, bool stream) {
+constexpr int younger_than_a(int T, int KT1, int NT, int PF, bool stream, int nb = 4) {
   int n = 0;
   bool after = false;
   auto ev_a = [&](int idx) {
@@ -81,7 +81,7 @@ constexpr int younger_than_a(int T, int KT1, int NT, int PF, bool stream) {
     if (idx == T) after = true;
   };
   auto ev_b = [&]() {
-    if (after) n += 4;
+    if (after) n += nb;
   };
   ev_a(0); ev_b(); ev_a(1); ev_b();
   for (int e = 2; e < PF; ++e) ev_b();
@@ -531,7 +531,7 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
 // as the tile kernel: bit-identical.
 template <int IW, int RO, int C, int NSL, int WM, int PF>
 __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
-                                                  const float* __restrict__ bias, bf16* __restrict__ y) {
+                                                  const float* __restrict__ bias, bf16* __restrict__ y, int nbands) {
   constexpr int IH = IW, NPART = IH / RO, PO = RO * IW, MBT = (PO + 15) / 16;
   constexpr int MB = (MBT + WM - 1) / WM, WN = 8 / WM;   // m-blocks per wave; waves = WM m-groups x WN
   constexpr int SLOTS = RO + 2, ZR = SLOTS * IW;        // LDS pixel rows + the zero row
@@ -549,6 +549,7 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
   // NSL slices of one band land on one XCD and share its input rows in L2
   const int slice = NSL == 1 ? 0 : (int)((blockIdx.x >> 3) % NSL);
   const int band = NSL == 1 ? (int)blockIdx.x : (int)((blockIdx.x / (8 * NSL)) * 8 + (blockIdx.x & 7));
+  if (band >= nbands) return;   // the grid rounds the bands up to whole groups of 8 (NSL > 1)
   const int img = band / NPART, part = band % NPART;
   const int y0 = part * RO;
   const int cb = slice * CS;                       // first output channel of this workgroup
@@ -642,9 +643,21 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
 template <int PF>
 __global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
-                                                           SatStamps st) {
+                                                           int nbands, SatStamps st) {
   const SatStampT0 t0 = sat_stamp_begin(st);
-  conv3x3_band_body<28, 7, 128, 1, 1, PF>(x, wf, bias, y);
+  conv3x3_band_body<28, 7, 128, 1, 1, PF>(x, wf, bias, y, nbands);
+  sat_stamp_end(st, t0);
+}
+
+// ResNet152 layer3's c2 when half images alone would leave CUs idle (B <= 80 per GPU: 2B workgroups): each
+// half image as two 128-channel slices (4B workgroups), each streaming half the weights.  WM = 1: the 8
+// waves own 16 channels each and every m-block; WM = 2: 2 m-groups x 4 channel groups of 32.
+template <int WM>
+__global__ __launch_bounds__(512) void conv3x3_slice2_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                             const float* __restrict__ bias, bf16* __restrict__ y,
+                                                             int nbands, SatStamps st) {
+  const SatStampT0 t0 = sat_stamp_begin(st);
+  conv3x3_band_body<14, 7, 256, 2, WM, 2>(x, wf, bias, y, nbands);
   sat_stamp_end(st, t0);
 }
 
@@ -656,21 +669,29 @@ __global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restric
 // counted vmcnt + one barrier per k-tile), the weights register-direct two k-tiles ahead.  The tile
 // kernel (convpipe.hip) runs this shape as 196 tiles of 256 x 128 that each fetch 768 KB; here 256
 // workgroups each fetch 712 KB.  Same k order, bias, ReLU and rounding: bit-identical.
-template <int IW, int RO, int CI, int CM, int PF>
+template <int IW, int RO, int CI, int CM, int PF, int NSL = 1>
 __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                   const float* __restrict__ bias, bf16* __restrict__ y,
-                                                  unsigned x_bytes) {
+                                                  unsigned x_bytes, int nhalves) {
   static_assert(IW / RO == 2 && IW % RO == 0 && CM == 256 && CI % 64 == 0, "two workgroups per image");
   constexpr int IH = IW, PO = RO * IW, MB = (PO + 15) / 16;
   constexpr int ROWB = 128, STG = 128 * ROWB;   // ring stage: 128 rows x 64 channels
   static_assert(MB * 16 <= 128, "one stage holds the half image's rows");
   constexpr int NT = CI / 64, KS = CI / 32;
+  constexpr int NJ = 2 / NSL;                   // 16-channel n-blocks per wave (NSL channel slices per half image)
+  static_assert(NSL == 1 || NSL == 2, "one or two channel slices");
   __shared__ __attribute__((aligned(16))) char smem[3 * STG];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fh = lane >> 4;
-  const long pix0 = (long)(blockIdx.x >> 1) * IH * IW + (long)(blockIdx.x & 1) * PO;
+  // NSL > 1: slice-major over groups of 8 consecutive workgroups (one per XCD under round-robin placement),
+  // so both slices of a half image read its input from one XCD's L2
+  const int slice = NSL == 1 ? 0 : (int)((blockIdx.x >> 3) % NSL);
+  const int hb = NSL == 1 ? (int)blockIdx.x : (int)((blockIdx.x / (8 * NSL)) * 8 + (blockIdx.x & 7));
+  if (hb >= nhalves) return;
+  const int nb0 = slice * (CM / 16 / NSL) + w * NJ;   // this wave's first 16-channel n-block
+  const long pix0 = (long)(hb >> 1) * IH * IW + (long)(hb & 1) * PO;
 
   const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)x_bytes, 0x00020000);
   unsigned dsrc[2];
@@ -686,25 +707,25 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (k_lds_void*)(st + (w * 2 + u) * 1024), 16,
                                                dsrc[u] == K_OOB ? (int)K_OOB : (int)(dsrc[u] + t * 128), 0, 0, 0);
   };
-  bf16x8 bq[PF + 1][2][2];
-  auto load_b = [&](int T, bf16x8 (&dst)[2][2]) {
+  bf16x8 bq[PF + 1][2][NJ];
+  auto load_b = [&](int T, bf16x8 (&dst)[2][NJ]) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-        dst[ks][j] = *(const bf16x8*)(wf + ((long)((w * 2 + j) * KS + 2 * T + ks) * 64 + lane) * 8);
+        dst[ks][j] = *(const bf16x8*)(wf + ((long)((nb0 + j) * KS + 2 * T + ks) * 64 + lane) * 8);
   };
-  float4 bv[2];
+  float4 bv[NJ];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + w * 32 + j * 16 + 4 * fh);
+  for (int j = 0; j < NJ; ++j) bv[j] = *(const float4*)(bias + (nb0 + j) * 16 + 4 * fh);
   int offu[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) offu[ks] = fr * ROWB + 16 * ((ks * 4 + fh) ^ (fr & 7));
-  f32x4 acc[MB][2];
+  f32x4 acc[MB][NJ];
 #pragma unroll
   for (int i = 0; i < MB; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // issue order A0 B0 A1 B1 B2 .. B(PF-1), then per k-tile after its wait A(T+2), B(T+PF): the order
   // younger_than_a() counts (bias loads are older than A0 and retire first)
@@ -718,10 +739,10 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
     constexpr int T = decltype(Tc)::value;
     // this wave's DMAs of tile T have landed, every wave's too after the barrier; the barrier also
     // retires every wave's reads of stage (T + 2) % 3 (tile T - 1) before it is refilled
-    k_wait_barrier<younger_than_a(T, NT, NT, PF, true)>();
+    k_wait_barrier<younger_than_a(T, NT, NT, PF, true, 2 * NJ)>();
     if constexpr (T + 2 < NT) dma_a(T + 2);
     if constexpr (T + PF < NT) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
-    const bf16x8 (&b)[2][2] = bq[T % (PF + 1)];
+    const bf16x8 (&b)[2][NJ] = bq[T % (PF + 1)];
     const char* st = smem + (T % 3) * STG;
     bf16x8 af[2][MB];
 #pragma unroll
@@ -734,13 +755,13 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
 #pragma unroll
       for (int i = 0; i < MB; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   });
 
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int ch = w * 32 + j * 16 + 4 * fh;
+  for (int j = 0; j < NJ; ++j) {
+    const int ch = (nb0 + j) * 16 + 4 * fh;
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
       const int p = i * 16 + fr;
@@ -759,7 +780,16 @@ __global__ __launch_bounds__(512) void conv1x1_frag_kernel(const bf16* __restric
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
                                                            unsigned x_bytes, SatStamps st) {
   const SatStampT0 t0 = sat_stamp_begin(st);
-  conv1x1_frag_body<14, 7, 1024, 256, 2>(x, wf, bias, y, x_bytes);
+  conv1x1_frag_body<14, 7, 1024, 256, 2>(x, wf, bias, y, x_bytes, (int)gridDim.x);
+  sat_stamp_end(st, t0);
+}
+
+// the same with each half image as two 128-channel slices (B <= 80 per GPU, as conv3x3_slice2_kernel)
+__global__ __launch_bounds__(512) void conv1x1_frag2_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                            const float* __restrict__ bias, bf16* __restrict__ y,
+                                                            unsigned x_bytes, int nhalves, SatStamps st) {
+  const SatStampT0 t0 = sat_stamp_begin(st);
+  conv1x1_frag_body<14, 7, 1024, 256, 2, 2>(x, wf, bias, y, x_bytes, nhalves);
   sat_stamp_end(st, t0);
 }
 
@@ -786,6 +816,15 @@ __global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restric
     const int row = nb * 16 + (lane & 15), k = ks * 32 + (lane >> 4) * 8;
     *(uint4*)(dst + e) = *(const uint4*)(src + (long)row * K + k);
   }
+}
+
+// Layer3 c1 / c2 launch form for a batch of N images: 1 = one workgroup per half image (2N workgroups), 2 / 3 = two
+// 128-channel slices per half image (4N; 3x3: 2 = one m-group of waves, 3 = two).  SatPolicy::conv_slices forces
+// one; automatic: slices when the half images fill at most half the chip's 256 CUs (B <= 64 per GPU).
+int sat_frag_slices(int N) {
+  const int f = sat_policy().conv_slices;
+  if (f >= 1 && f <= 3) return f;
+  return 2 * N <= 128 ? 2 : 1;
 }
 
 }  // namespace
@@ -839,10 +878,20 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   const hipStream_t s = (hipStream_t)stream;
   const bf16 *xp = (const bf16*)x, *wp = (const bf16*)wf;
   bf16* yp = (bf16*)y;
-  if (H == 28)   // layer2 c2: 7-row bands, four workgroups per image
-    hipLaunchKernelGGL(conv3x3_band_kernel<2>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp, st);
-  else           // layer3 c2: half images, two workgroups per image
+  if (H == 28) {   // layer2 c2: 7-row bands, four workgroups per image
+    hipLaunchKernelGGL(conv3x3_band_kernel<2>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp, 4 * N, st);
+    return (int)hipGetLastError();
+  }
+  // layer3 c2: half images (two workgroups per image), or two channel slices per half image when the half
+  // images alone would leave CUs idle (SatPolicy::conv_slices)
+  const int mode = sat_frag_slices(N);
+  const int groups = sat_cdiv(2 * N, 8) * 8 * 2;   // whole groups of 8 half images x 2 slices
+  if (mode == 1)
     hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp, st);
+  else if (mode == 2)
+    hipLaunchKernelGGL(conv3x3_slice2_kernel<1>, dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
+  else
+    hipLaunchKernelGGL(conv3x3_slice2_kernel<2>, dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
   return (int)hipGetLastError();
 }
 
@@ -859,7 +908,11 @@ extern "C" int sat_conv1x1_frag(int N, int H, int W, int Cin, int Cout, int dtyp
   SAT_REQUIRE(al(x, 16) && al(y, 16) && al(wf, 16) && al(b, 16));
   const long x_bytes = 2L * N * H * W * Cin;
   SAT_REQUIRE(x_bytes < (1L << 31));
-  hipLaunchKernelGGL(conv1x1_frag_kernel, dim3(2 * N), dim3(512), 0, (hipStream_t)stream, (const bf16*)x,
-                     (const bf16*)wf, b, (bf16*)y, (unsigned)x_bytes, sat_launch_stamps());
+  if (sat_frag_slices(N) == 1)
+    hipLaunchKernelGGL(conv1x1_frag_kernel, dim3(2 * N), dim3(512), 0, (hipStream_t)stream, (const bf16*)x,
+                       (const bf16*)wf, b, (bf16*)y, (unsigned)x_bytes, sat_launch_stamps());
+  else
+    hipLaunchKernelGGL(conv1x1_frag2_kernel, dim3(sat_cdiv(2 * N, 8) * 8 * 2), dim3(512), 0, (hipStream_t)stream,
+                       (const bf16*)x, (const bf16*)wf, b, (bf16*)y, (unsigned)x_bytes, 2 * N, sat_launch_stamps());
   return (int)hipGetLastError();
 }

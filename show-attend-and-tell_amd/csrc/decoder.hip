@@ -61,30 +61,42 @@ inline int pick_splits(int M, int N, int K, int dtype, bool kmajor_w, int target
   return best;
 }
 inline int forced(int f, int K, int auto_s) { return (f > 0 && K % 64 == 0 && (K / 64) % f == 0) ? f : auto_s; }
-inline Splits splits_for(const SatDecoderDims& d) {
+// tr: the backward's dL/d(gated context) and dL/dh products read the transposed weight copies
+// (SatDecoderLayout::wih_ctx_t / hcat_t, k-contiguous) and run on the skinny kernel with its own K split
+inline Splits splits_for(const SatDecoderDims& d, bool tr) {
   const int E = d.E, D = d.D, HG = 5 * E + D;
   const bool bf = d.dtype == SAT_BF16;
   const int tg = d.split_target > 0 ? d.split_target : kSplitTargetDefault;
+  const int KH = d.attention ? HG : 4 * E;
   Splits s;
-  s.h = pick_splits(d.B, d.attention ? HG : 4 * E, E, d.dtype, false, tg);
+  s.h = pick_splits(d.B, KH, E, d.dtype, false, tg);
   s.c = pick_splits(d.B, 4 * E, D, d.dtype, false, tg);
-  s.g = pick_splits(d.B, D, 4 * E, d.dtype, true, tg);
-  s.dh = pick_splits(d.B, E, d.attention ? HG : 4 * E, d.dtype, true, tg);
+  s.g = pick_splits(d.B, D, 4 * E, d.dtype, !tr, tg);
+  s.dh = pick_splits(d.B, E, KH, d.dtype, !tr, tg);
   s.i = pick_splits(d.B, 2 * E, D, d.dtype, false, tg);
   if (bf) {   // per-step products the skinny kernel runs (csrc/skinny.hip): its own K split
     int k;
-    if ((k = sat_skinny_splits(d.B, d.attention ? HG : 4 * E, E))) s.h = k;
+    if ((k = sat_skinny_splits(d.B, KH, E))) s.h = k;
     if ((k = sat_skinny_splits(d.B, 4 * E, D))) s.c = k;
     if ((k = sat_skinny_splits(d.B, 2 * E, D))) s.i = k;
+    // the backward's products through the transposed copies: 512-deep splits (fewer slabs for the attention /
+    // LSTM backward kernels that sum them: B = 128 decoder fwd + bwd 3.15 -> 3.04 ms, B = 64 2.47 -> 2.36 ms
+    // against 256-deep, profiles/r3_s11_decoder_splits.txt)
+    if (tr && (k = sat_skinny_splits(d.B, D, 4 * E)) && (4 * E) % 512 == 0) s.g = k / 2;
+    if (tr && (k = sat_skinny_splits(d.B, E, KH)) && KH % 512 == 0) s.dh = k / 2;
   }
   if (bf) {   // per-call overrides (SatPolicy::decoder_splits, 0 = automatic)
     const int* f = sat_policy().decoder_splits;
     s.h = forced(f[0], E, s.h);
     s.c = forced(f[1], D, s.c);
     s.g = forced(f[2], 4 * E, s.g);
-    s.dh = forced(f[3], d.attention ? HG : 4 * E, s.dh);
+    s.dh = forced(f[3], KH, s.dh);
   }
   return s;
+}
+// whether a call may use the transposed weight copies (bf16, both offsets given, the skinny kernel not excluded)
+inline bool use_transposed(const SatDecoderDims& d, const SatDecoderLayout& lay) {
+  return d.dtype == SAT_BF16 && lay.wih_ctx_t >= 0 && lay.hcat_t >= 0 && sat_policy().skinny != 1;
 }
 
 struct Carver {
@@ -107,7 +119,12 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   const size_t B = d.B, L = d.L, D = d.D, E = d.E, V = d.V, T1 = d.T - 1, R = B * T1;
   const size_t HG = 5 * E + D;
   const size_t ts = d.dtype == SAT_BF16 ? 2 : 4, f = 4;
-  const Splits sp = splits_for(d);
+  Splits sp = splits_for(d, false);
+  {   // split-K slabs sized for either form of the backward's products (the layout decides per call)
+    const Splits st = splits_for(d, true);
+    sp.g = sp.g > st.g ? sp.g : st.g;
+    sp.dh = sp.dh > st.dh ? sp.dh : st.dh;
+  }
   Carver c{base};
   c.take(w->mean_f, B * D * f);  c.take(w->mean_t, B * D * ts);
   c.take(w->hc0, B * 2 * E * f);
@@ -144,8 +161,13 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   c.take(w->ticket, B * 4);
   c.take(w->demb, R * E * f);
   c.take(w->dpre0, B * 2 * E * f); c.take(w->dpre0_t, B * 2 * E * ts);
+  // column-sum scratch: the largest single sum, or all the bias sums of one backward phase in one launch pair
+  // (phase 1: f_out / f_h / f_z biases; phase 2: attention W / v, init, [U; f_beta; W_hh] and gate biases)
   size_t maxN = V > HG ? V : HG;
   if (D > maxN) maxN = D;
+  const size_t ph1 = V + 2 * E, ph2 = 9 * E + D + 1;
+  if (ph1 > maxN) maxN = ph1;
+  if (ph2 > maxN) maxN = ph2;
   c.take(w->colsum, sat_colsum_scratch_floats((int)R, (int)maxN) * f);
   return c.off + 256;
 }
@@ -201,6 +223,7 @@ struct Ctx {
   const void* LP;
   int ts;
   long T1, R, HG;
+  bool tr;   // use_transposed(d, lay)
   const void* W(int64_t off) const {
     return d.dtype == SAT_BF16 ? (const void*)((const bf16*)LP + off) : (const void*)(P + off);
   }
@@ -362,6 +385,10 @@ int dgrad_launch(const Ctx& c, int M, int N, int K, const void* X, long ldx, con
 int bwd_ggemm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) {
   const SatDecoderDims& d = c.d;
   const int B = d.B, D = d.D, E = d.E;
+  if (c.tr)   // d gates . (W_ih[:, E:]^T)^T with the transposed copy [D][4E]: k-contiguous, the skinny kernel
+    return linear(c, B, D, 4 * E, c.at(w.dhg_t, (long)t * c.HG + E + D), c.T1 * c.HG, c.W(c.lay.wih_ctx_t), 4 * E,
+                  nullptr, w.dgated, D, SAT_F32, SAT_ACT_NONE, s, nullptr, 0, SAT_F32, nullptr, 0, SAT_F32, sp.g,
+                  (long)B * D);
   return dgrad_launch(c, B, D, 4 * E, c.at(w.dhg_t, (long)t * c.HG + E + D), c.T1 * c.HG, c.W(c.lay.wih + E), E + D,
                       w.dgated, D, s, nullptr, 0, sp.g, (long)B * D);
 }
@@ -394,6 +421,12 @@ int bwd_dhgemm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s
   const SatDecoderDims& d = c.d;
   const int B = d.B, D = d.D, E = d.E;
   const long T1 = c.T1, HG = c.HG;
+  if (c.tr) {   // against the transposed copy hcat^T [E][HG] (k-contiguous: the skinny kernel)
+    const long k0 = d.attention ? 0 : E + D;
+    return linear(c, B, E, (int)(HG - k0), c.at(w.dhg_t, (long)t * HG + k0), T1 * HG, c.W(c.lay.hcat_t + k0), HG,
+                  nullptr, w.dh_rec, E, SAT_F32, SAT_ACT_NONE, s, nullptr, 0, SAT_F32, nullptr, 0, SAT_F32, sp.dh,
+                  (long)B * E);
+  }
   if (d.attention)
     return dgrad_launch(c, B, E, (int)HG, c.at(w.dhg_t, (long)t * HG), T1 * HG, c.W(c.lay.hcat_w), E, w.dh_rec, E, s,
                         nullptr, 0, sp.dh, (long)B * E);
@@ -414,6 +447,12 @@ inline uint64_t* step_slot(const SatDecoderDims& d, int g, int t) {
 }
 inline int stamp_cap(const SatDecoderDims& d) { return d.policy ? d.policy->stamp_capacity : 0; }
 
+// One per-step kernel group's in-kernel timestamp slot (SatPolicy::stamps) for the launches in its scope.
+struct StepTimer {
+  SatStampScope stamps;
+  StepTimer(const SatDecoderDims& d, int g, int t) : stamps(step_slot(d, g, t), stamp_cap(d)) {}
+};
+
 int check_dims(const SatDecoderDims* d) {
   if (!d) return SAT_ERR_INVALID;
   if (d->B <= 0 || d->L <= 0 || d->D <= 0 || d->E <= 0 || d->V <= 0 || d->T < 3) return SAT_ERR_INVALID;
@@ -428,6 +467,58 @@ int check_dims(const SatDecoderDims* d) {
 }
 
 }  // namespace
+
+namespace {
+// dst[c * ld_dst + r] = src[r * ld_src + c] for a rows x cols bf16 block (rows, cols, ld_src, ld_dst multiples of 8,
+// 16-B aligned rows): 64 x 64 tiles through LDS (16-B loads along the source rows, 16-B stores along the
+// destination rows)
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ src, long ld_src, int rows,
+                                                             int cols, bf16* __restrict__ dst, long ld_dst) {
+  __shared__ bf16 tile[64][64 + 8];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tr = threadIdx.x >> 3, tc = (threadIdx.x & 7) * 8;   // 32 rows x 8 chunks of 8 per pass
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int r = r0 + tr + 32 * p;
+    if (r < rows && c0 + tc < cols) {
+      const uint4 v = *(const uint4*)(src + (long)r * ld_src + c0 + tc);
+      const bf16* e = (const bf16*)&v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tile[tr + 32 * p][tc + j] = e[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c = c0 + tr + 32 * p;   // destination row = source column
+    if (c < cols && r0 + tc < rows) {
+      uint4 v;
+      bf16* e = (bf16*)&v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[j] = tile[tc + j][tr + 32 * p];
+      *(uint4*)(dst + (long)c * ld_dst + r0 + tc) = v;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int sat_decoder_refresh_transposed(const SatDecoderDims* d, const SatDecoderLayout* lay, void* params_lp,
+                                              void* stream) {
+  SAT_CHECK((hipError_t)check_dims(d));
+  SAT_REQUIRE(lay && params_lp);
+  if (d->dtype != SAT_BF16 || lay->wih_ctx_t < 0 || lay->hcat_t < 0) return 0;
+  const int E = d->E, D = d->D, HG = 5 * E + D;
+  SAT_REQUIRE(lay->wih_ctx_t % 8 == 0 && lay->hcat_t % 8 == 0 && lay->wih % 8 == 0 && lay->hcat_w % 8 == 0);
+  bf16* lp = (bf16*)params_lp;
+  hipStream_t s = (hipStream_t)stream;
+  // W_ih [4E][E + D]: its context columns E.. as [D][4E]
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3(sat_cdiv(D, 64), sat_cdiv(4 * E, 64)), dim3(256), 0, s, lp + lay->wih + E, (long)(E + D),
+                     4 * E, D, lp + lay->wih_ctx_t, (long)4 * E);
+  // hcat [HG][E] as [E][HG]
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3(sat_cdiv(E, 64), sat_cdiv(HG, 64)), dim3(256), 0, s, lp + lay->hcat_w, (long)E,
+                     HG, E, lp + lay->hcat_t, (long)HG);
+  return (int)hipGetLastError();
+}
 
 extern "C" size_t sat_decoder_workspace_bytes(const SatDecoderDims* d) {
   if (check_dims(d)) return 0;
@@ -451,12 +542,12 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
   SAT_REQUIRE(carve(d, nullptr, &w) <= workspace_bytes);
   carve(d, (char*)workspace, &w);
   hipStream_t s = (hipStream_t)stream;
-  Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D};
+  Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D,
+        use_transposed(d, *lay)};
   const int B = d.B, L = d.L, D = d.D, E = d.E, T1 = d.T - 1;
-  const int scap = stamp_cap(d);
   const long HG = c.HG;
   const bool att = d.attention != 0;
-  const Splits sp = splits_for(d);
+  const Splits sp = splits_for(d, c.tr);
   const StepIO io{img_features, alphas, nullptr};
 
   // fed tokens + embeddings
@@ -505,19 +596,19 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
       SAT_CHECK((hipError_t)linear(c, B, 4 * E, E, c.at(w.emb_t, (long)t * E), (long)T1 * E, c.W(lay->wih), E + D,
                                    c.F(lay->bih), w.xg + (long)t * 4 * E, (long)T1 * 4 * E, SAT_F32, SAT_ACT_NONE, s));
     {
-      SatStampScope st(step_slot(d, 0, t), scap);
+      StepTimer st(d, 0, t);
       SAT_CHECK((hipError_t)fwd_hgemm(c, w, sp, t, s));
     }
     if (att) {
       {
-        SatStampScope st(step_slot(d, 1, t), scap);
+        StepTimer st(d, 1, t);
         SAT_CHECK((hipError_t)fwd_attn(c, w, sp, io, t, s));
       }
-      SatStampScope st(step_slot(d, 2, t), scap);
+      StepTimer st(d, 2, t);
       SAT_CHECK((hipError_t)fwd_cgemm(c, w, sp, t, s));
     }
     {
-      SatStampScope st(step_slot(d, 3, t), scap);
+      StepTimer st(d, 3, t);
       SAT_CHECK((hipError_t)fwd_lstm(c, w, sp, t, s));
     }
     if (!d.tf) {
@@ -551,15 +642,15 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   SAT_REQUIRE(carve(d, nullptr, &w) <= workspace_bytes);
   carve(d, (char*)workspace, &w);
   hipStream_t s = (hipStream_t)stream;
-  Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D};
+  Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D,
+        use_transposed(d, *lay)};
   const int B = d.B, L = d.L, D = d.D, E = d.E, V = d.V, T1 = d.T - 1;
-  const int scap = stamp_cap(d);
   const int R = (int)c.R;
   const int VP = head_ld(d);
   const long HG = c.HG;
   const bool att = d.attention != 0;
   const float beta = accumulate ? 1.f : 0.f;
-  const Splits sp = splits_for(d);
+  const Splits sp = splits_for(d, c.tr);
   auto G = [&](int64_t off) { return grads + off; };
   // weight gradient: G[M,N] (+)= X[K,M]^T Y[K,N]   (X m-contig, Y n-contig)
   auto wgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo,
@@ -594,14 +685,16 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
         dpre = w.dpre_t;
       }
       SAT_CHECK((hipError_t)wgrad(V, E, R, dpre, ldp, w.comb_t, E, G(lay->fout_w), E, VP != V));
-      SAT_CHECK((hipError_t)colsum(dpre, d.dtype, ldp, R, V, G(lay->fout_b)));
       SAT_CHECK((hipError_t)dgrad_launch(c, R, E, V, dpre, ldp, c.W(lay->fout_w), E, w.dcomb, E, s, nullptr, 0, 0, 0,
                                          VP != V));
       SAT_CHECK((hipError_t)sat_ado_bwd_split(w.dcomb, w.fh, w.fz, (long)R * E, d.dtype, w.dfh_t, w.dfz_t, s));
       SAT_CHECK((hipError_t)wgrad(E, E, R, w.dfh_t, E, w.hd_t, E, G(lay->fh_w), E));
-      SAT_CHECK((hipError_t)colsum(w.dfh_t, d.dtype, E, R, E, G(lay->fh_b)));
       SAT_CHECK((hipError_t)wgrad(E, D, R, w.dfz_t, E, w.ctx_t, D, G(lay->fz_w), D));
-      SAT_CHECK((hipError_t)colsum(w.dfz_t, d.dtype, E, R, E, G(lay->fz_b)));
+      // the three bias gradients (column sums of d logits, d f_h, d f_z) in one launch pair
+      const SatColsumSeg cs[3] = {{dpre, d.dtype, ldp, R, V, G(lay->fout_b), accumulate, nullptr},
+                                  {w.dfh_t, d.dtype, E, R, E, G(lay->fh_b), accumulate, nullptr},
+                                  {w.dfz_t, d.dtype, E, R, E, G(lay->fz_b), accumulate, nullptr}};
+      SAT_CHECK((hipError_t)sat_colsum_multi(cs, 3, w.colsum, s));
       SAT_CHECK((hipError_t)dgrad(R, E, E, w.dfh_t, E, c.W(lay->fh_w), E, w.dhd, E));
       if (att) SAT_CHECK((hipError_t)dgrad(R, D, E, w.dfz_t, E, c.W(lay->fz_w), D, w.dctx_head, D));
     } else {
@@ -620,26 +713,34 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   if (!(phase & 2)) return 0;
 
   // ---------------- recurrent BPTT (reverse time loop) ----------------
-  if (att) {
-    SAT_CHECK((hipError_t)sat_zero_rows(w.dv_acc, (long)B * E, 1, (long)B * E, s));
-    SAT_CHECK((hipError_t)sat_zero_rows(w.dbv_acc, B, 1, B, s));
-    SAT_CHECK((hipError_t)sat_zero_rows((float*)w.ticket, B, 1, B, s));   // split attention backward tickets
+  {   // one launch zeroes the BPTT accumulators, the split attention backward's tickets and (beta = 0) the dense
+      // embedding gradient the scatter-add after the loop accumulates into
+    float* zp[4];
+    long zn[4];
+    int nz = 0;
+    if (att) {
+      zp[nz] = w.dv_acc; zn[nz++] = (long)B * E;
+      zp[nz] = w.dbv_acc; zn[nz++] = B;
+      zp[nz] = (float*)w.ticket; zn[nz++] = B;
+    }
+    if (!d.bert && !accumulate) { zp[nz] = G(lay->embedding); zn[nz++] = (long)V * E; }
+    SAT_CHECK((hipError_t)sat_zero_multi(zp, zn, nz, s));
   }
   const StepIO io{img_features, const_cast<float*>(alphas), d_alphas};
   for (int t = T1 - 1; t >= 0; --t) {
     {
-      SatStampScope st(step_slot(d, 4, t), scap);
+      StepTimer st(d, 4, t);
       SAT_CHECK((hipError_t)bwd_lstm(c, w, sp, t, s));
     }
     if (att) {
       {
-        SatStampScope st(step_slot(d, 5, t), scap);
+        StepTimer st(d, 5, t);
         SAT_CHECK((hipError_t)bwd_ggemm(c, w, sp, t, s));
       }
-      SatStampScope st(step_slot(d, 6, t), scap);
+      StepTimer st(d, 6, t);
       SAT_CHECK((hipError_t)bwd_attn(c, w, sp, io, t, s));
     }
-    SatStampScope st(step_slot(d, 7, t), scap);
+    StepTimer st(d, 7, t);
     SAT_CHECK((hipError_t)bwd_dhgemm(c, w, sp, t, s));
   }
 
@@ -648,31 +749,36 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
     SAT_CHECK((hipError_t)sat_attention_dws_launch(w.Ws, w.uh_all, w.de_all, c.F(lay->v_w), B, L, E, T1, d.dtype,
                                                    w.dWs_acc, w.dWs_t, s));
     SAT_CHECK((hipError_t)wgrad(E, D, B * L, w.dWs_t, E, img_features, D, G(lay->attW_w), D));
-    SAT_CHECK((hipError_t)colsum(w.dWs_acc, SAT_F32, E, B * L, E, G(lay->attW_b)));
-    SAT_CHECK((hipError_t)colsum(w.dv_acc, SAT_F32, E, B, E, G(lay->v_w)));
-    SAT_CHECK((hipError_t)colsum(w.dbv_acc, SAT_F32, 1, B, 1, G(lay->v_b)));
   }
   // init_h / init_c (decoder.py:137-147): dh0 = dh_rec, dc0 = dc after the t = 0 step
   SAT_CHECK((hipError_t)sat_tanh_pair_bwd(w.dh_rec, sp.dh, (long)B * E, w.dc, w.hc0, B, E, w.dpre0, w.dpre0_t,
                                           d.dtype, s));
   SAT_CHECK((hipError_t)wgrad(2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D));
-  SAT_CHECK((hipError_t)colsum(w.dpre0, SAT_F32, 2 * E, B, 2 * E, G(lay->init_b)));
+  {   // every bias gradient of this phase (column sums) in one launch pair; b_hh and b_ih receive the same
+      // gradient (the sum of d gates)
+    SatColsumSeg cs[6];
+    int n = 0;
+    if (att) {
+      cs[n++] = {w.dWs_acc, SAT_F32, E, B * L, E, G(lay->attW_b), accumulate, nullptr};
+      cs[n++] = {w.dv_acc, SAT_F32, E, B, E, G(lay->v_w), accumulate, nullptr};
+      cs[n++] = {w.dbv_acc, SAT_F32, 1, B, 1, G(lay->v_b), accumulate, nullptr};
+      cs[n++] = {w.dhg, SAT_F32, HG, R, E + D, G(lay->hcat_b), accumulate, nullptr};
+    }
+    cs[n++] = {w.dpre0, SAT_F32, 2 * E, B, 2 * E, G(lay->init_b), accumulate, nullptr};
+    cs[n++] = {w.dhg + E + D, SAT_F32, HG, R, 4 * E, G(lay->hcat_b + E + D), accumulate, G(lay->bih)};
+    SAT_CHECK((hipError_t)sat_colsum_multi(cs, n, w.colsum, s));
+  }
 
   const void* dg_t = c.at(w.dhg_t, E + D);   // d gates rows (ld HG)
-  const float* dg_f = w.dhg + E + D;
   if (att) {
     SAT_CHECK((hipError_t)wgrad((int)HG, E, R, w.dhg_t, HG, w.h_in_t, E, G(lay->hcat_w), E));
-    SAT_CHECK((hipError_t)colsum(w.dhg, SAT_F32, HG, R, E + D, G(lay->hcat_b)));
   } else {
     SAT_CHECK((hipError_t)wgrad(4 * E, E, R, dg_t, HG, w.h_in_t, E, G(lay->hcat_w + (long)(E + D) * E), E));
   }
-  // b_hh and b_ih receive the same gradient (sum of d gates)
-  SAT_CHECK((hipError_t)colsum(dg_f, SAT_F32, HG, R, 4 * E, G(lay->hcat_b + E + D), G(lay->bih)));
   SAT_CHECK((hipError_t)wgrad(4 * E, E, R, dg_t, HG, w.emb_t, E, G(lay->wih), E + D));
   SAT_CHECK((hipError_t)wgrad(4 * E, D, R, dg_t, HG, w.gated_t, D, G(lay->wih + E), E + D));
-  if (!d.bert) {  // dense embedding gradient, scatter-added by fed token (decoder.py:87,133)
+  if (!d.bert) {  // dense embedding gradient (zeroed before the loop), scatter-added by fed token (decoder.py:87,133)
     SAT_CHECK((hipError_t)dgrad(R, E, 4 * E, dg_t, HG, c.W(lay->wih), E + D, w.demb, E, d.ado ? w.dcomb : nullptr, E));
-    if (!accumulate) SAT_CHECK((hipError_t)sat_zero_rows(G(lay->embedding), (long)V * E, 1, (long)V * E, s));
     SAT_CHECK((hipError_t)sat_embed_scatter_add(w.demb, w.tok, R, E, G(lay->embedding), s));
   }
   return 0;
@@ -698,8 +804,9 @@ extern "C" int sat_decoder_step_bench(const SatDecoderDims* dp, const SatDecoder
   SAT_REQUIRE(carve(d, nullptr, &w) <= workspace_bytes);
   carve(d, (char*)workspace, &w);
   hipStream_t s = (hipStream_t)stream;
-  Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D};
-  const Splits sp = splits_for(d);
+  Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D,
+        use_transposed(d, *lay)};
+  const Splits sp = splits_for(d, c.tr);
   const StepIO io{img_features, alphas, d_alphas};
   const int t = (d.T - 1) / 2;
   hipEvent_t e0, e1;

@@ -248,25 +248,32 @@ __global__ __launch_bounds__(256) void mean_rows_vec_kernel(const T* __restrict_
 }
 
 // ---- column sums: out[n] (+)= sum_r X[r*ld + n] ----------------------------
-// pass 1: grid (ceil(N/256), RS) partial sums over row chunks; pass 2 folds them.
+// pass 1: grid (ceil(N/256), RS) partial sums over row chunks; pass 2 folds them.  The bodies take the block
+// coordinates as arguments so the multi-segment kernels below (several column sums in one launch pair) run
+// exactly the same arithmetic as the single ones.
+template <typename T>
+__device__ __forceinline__ void colsum_partial_body(const T* __restrict__ X, long ld, int R, int N, int rows_per,
+                                                    float* __restrict__ part, int bx, int by) {
+  int n = bx * 256 + (int)threadIdx.x;
+  if (n >= N) return;
+  int r0 = by * rows_per, r1 = min(R, r0 + rows_per);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += (float)X[(long)r * ld + n];
+  part[(long)by * N + n] = s;
+}
 template <typename T>
 __global__ void colsum_partial_kernel(const T* __restrict__ X, long ld, int R, int N, int rows_per,
                                       float* __restrict__ part) {
-  int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  int r0 = blockIdx.y * rows_per, r1 = min(R, r0 + rows_per);
-  float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += (float)X[(long)r * ld + n];
-  part[(long)blockIdx.y * N + n] = s;
+  colsum_partial_body<T>(X, ld, R, N, rows_per, part, blockIdx.x, blockIdx.y);
 }
 // 16-byte rows chunks per thread (VEC columns), 4 rows in flight per iteration
 template <typename T>
-__global__ void colsum_partial_vec_kernel(const T* __restrict__ X, long ld, int R, int N, int rows_per,
-                                          float* __restrict__ part) {
+__device__ __forceinline__ void colsum_partial_vec_body(const T* __restrict__ X, long ld, int R, int N, int rows_per,
+                                                        float* __restrict__ part, int bx, int by) {
   constexpr int VEC = 16 / sizeof(T);
-  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * VEC;
+  const int n = (bx * 256 + (int)threadIdx.x) * VEC;
   if (n >= N) return;
-  const int r0 = blockIdx.y * rows_per, r1 = min(R, r0 + rows_per);
+  const int r0 = by * rows_per, r1 = min(R, r0 + rows_per);
   float acc[VEC];
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
@@ -289,12 +296,18 @@ __global__ void colsum_partial_vec_kernel(const T* __restrict__ X, long ld, int 
     for (int j = 0; j < VEC; ++j) acc[j] += (float)h[j];
   }
 #pragma unroll
-  for (int j = 0; j < VEC; ++j) part[(long)blockIdx.y * N + n + j] = acc[j];
+  for (int j = 0; j < VEC; ++j) part[(long)by * N + n + j] = acc[j];
+}
+template <typename T>
+__global__ void colsum_partial_vec_kernel(const T* __restrict__ X, long ld, int R, int N, int rows_per,
+                                          float* __restrict__ part) {
+  colsum_partial_vec_body<T>(X, ld, R, N, rows_per, part, blockIdx.x, blockIdx.y);
 }
 
-__global__ void colsum_final_kernel(const float* __restrict__ part, int RS, int N, float* __restrict__ out,
-                                    int accumulate, float* __restrict__ out2) {
-  int n = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void colsum_final_body(const float* __restrict__ part, int RS, int N,
+                                                  float* __restrict__ out, int accumulate, float* __restrict__ out2,
+                                                  int bx) {
+  int n = bx * 256 + (int)threadIdx.x;
   if (n >= N) return;
   // four independent partial sums (a single chain serialises RS L2 round trips), fixed order
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -309,6 +322,86 @@ __global__ void colsum_final_kernel(const float* __restrict__ part, int RS, int 
   const float s = (s0 + s1) + (s2 + s3);
   out[n] = accumulate ? out[n] + s : s;
   if (out2) out2[n] = accumulate ? out2[n] + s : s;
+}
+__global__ void colsum_final_kernel(const float* __restrict__ part, int RS, int N, float* __restrict__ out,
+                                    int accumulate, float* __restrict__ out2) {
+  colsum_final_body(part, RS, N, out, accumulate, out2, blockIdx.x);
+}
+
+// geometry of one column sum (shared by sat_colsum and sat_colsum_multi): RS row chunks of rows_per rows
+struct ColsumPlan {
+  bool vok;
+  int colblocks, RS, rows_per;
+};
+inline ColsumPlan colsum_plan(const void* X, int dtype, long ld, int R, int N) {
+  ColsumPlan p;
+  const int vec = dtype == SAT_BF16 ? 8 : 4;
+  p.vok = N % vec == 0 && ld % vec == 0 && ((uintptr_t)X & 15) == 0;
+  p.colblocks = sat_cdiv(N, 256 * (p.vok ? vec : 1));
+  int RS = 1;
+  while (p.colblocks * RS < 512 && RS < 64 && (R + RS * 2 - 1) / (RS * 2) >= 16) RS *= 2;
+  int rows_per = sat_cdiv(R, RS);
+  RS = sat_cdiv(R, rows_per > 0 ? rows_per : 1);
+  if (R <= 0) { RS = 1; rows_per = 0; }
+  p.RS = RS;
+  p.rows_per = rows_per;
+  return p;
+}
+
+constexpr int kColsumMaxSegs = 8;
+struct ColsumMultiArgs {
+  int n;
+  struct Seg {
+    const void* X; long ld; int R, N, dtype, vok, colblocks, RS, rows_per, accumulate;
+    int blk0, fblk0;            // first partial / final block of this segment
+    float* part; float* out; float* out2;
+  } seg[kColsumMaxSegs];
+};
+__device__ __forceinline__ int colsum_seg_of(const ColsumMultiArgs& a, int b, bool final_pass) {
+  int i = 0;
+  for (int k = 1; k < a.n; ++k)
+    if ((final_pass ? a.seg[k].fblk0 : a.seg[k].blk0) <= b) i = k;
+  return i;
+}
+__global__ void colsum_multi_partial_kernel(ColsumMultiArgs a) {
+  const int b = blockIdx.x;
+  const auto& sg = a.seg[colsum_seg_of(a, b, false)];
+  const int lb = b - sg.blk0, bx = lb % sg.colblocks, by = lb / sg.colblocks;
+  if (sg.vok) {
+    if (sg.dtype == SAT_BF16) colsum_partial_vec_body<bf16>((const bf16*)sg.X, sg.ld, sg.R, sg.N, sg.rows_per, sg.part, bx, by);
+    else colsum_partial_vec_body<float>((const float*)sg.X, sg.ld, sg.R, sg.N, sg.rows_per, sg.part, bx, by);
+  } else {
+    if (sg.dtype == SAT_BF16) colsum_partial_body<bf16>((const bf16*)sg.X, sg.ld, sg.R, sg.N, sg.rows_per, sg.part, bx, by);
+    else colsum_partial_body<float>((const float*)sg.X, sg.ld, sg.R, sg.N, sg.rows_per, sg.part, bx, by);
+  }
+}
+__global__ void colsum_multi_final_kernel(ColsumMultiArgs a) {
+  const int b = blockIdx.x;
+  const auto& sg = a.seg[colsum_seg_of(a, b, true)];
+  colsum_final_body(sg.part, sg.RS, sg.N, sg.out, sg.accumulate, sg.out2, b - sg.fblk0);
+}
+
+// zero several fp32 ranges in one launch
+constexpr int kZeroMaxSegs = 8;
+struct ZeroMultiArgs {
+  int n;
+  float* p[kZeroMaxSegs];
+  long count[kZeroMaxSegs];
+};
+__global__ void zero_multi_kernel(ZeroMultiArgs a) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (int k = 0; k < a.n; ++k) {
+    float* p = a.p[k];
+    const long n = a.count[k];
+    if (((uintptr_t)p & 15) == 0) {
+      const long n4 = n >> 2;
+      for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride)
+        ((float4*)p)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (long i = (n4 << 2) + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) p[i] = 0.f;
+    } else {
+      for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) p[i] = 0.f;
+    }
+  }
 }
 
 // ---- embedding gather: out[r, :] = W[tok[r], :] ------------------------------
@@ -457,25 +550,61 @@ int sat_mean_rows(const void* a, int B, int L, int D, int dtype, float* out_f32,
 int sat_colsum(const void* X, int dtype, long ld, int R, int N, float* out, int accumulate, float* out2,
                float* scratch, hipStream_t s) {
   if (N <= 0) return 0;
-  const int vec = dtype == SAT_BF16 ? 8 : 4;
-  const bool vok = N % vec == 0 && ld % vec == 0 && ((uintptr_t)X & 15) == 0;
-  const int colblocks = sat_cdiv(N, 256 * (vok ? vec : 1));
-  int RS = 1;
-  while (colblocks * RS < 512 && RS < 64 && (R + RS * 2 - 1) / (RS * 2) >= 16) RS *= 2;
-  int rows_per = sat_cdiv(R, RS);
-  RS = sat_cdiv(R, rows_per > 0 ? rows_per : 1);
-  if (R <= 0) { RS = 1; rows_per = 0; }
-  dim3 g1(colblocks, RS);
-  if (vok) {
+  const ColsumPlan p = colsum_plan(X, dtype, ld, R, N);
+  dim3 g1(p.colblocks, p.RS);
+  if (p.vok) {
     if (dtype == SAT_BF16)
-      hipLaunchKernelGGL(colsum_partial_vec_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)X, ld, R, N, rows_per, scratch);
+      hipLaunchKernelGGL(colsum_partial_vec_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)X, ld, R, N, p.rows_per, scratch);
     else
-      hipLaunchKernelGGL(colsum_partial_vec_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ld, R, N, rows_per, scratch);
+      hipLaunchKernelGGL(colsum_partial_vec_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ld, R, N, p.rows_per, scratch);
   } else if (dtype == SAT_BF16)
-    hipLaunchKernelGGL(colsum_partial_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)X, ld, R, N, rows_per, scratch);
+    hipLaunchKernelGGL(colsum_partial_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)X, ld, R, N, p.rows_per, scratch);
   else
-    hipLaunchKernelGGL(colsum_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ld, R, N, rows_per, scratch);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(sat_cdiv(N, 256)), dim3(256), 0, s, scratch, RS, N, out, accumulate, out2);
+    hipLaunchKernelGGL(colsum_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ld, R, N, p.rows_per, scratch);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(sat_cdiv(N, 256)), dim3(256), 0, s, scratch, p.RS, N, out, accumulate, out2);
+  return (int)hipGetLastError();
+}
+
+int sat_colsum_multi(const SatColsumSeg* segs, int n, float* scratch, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n > kColsumMaxSegs) return (int)hipErrorInvalidValue;
+  ColsumMultiArgs a{};
+  int blk = 0, fblk = 0, k = 0;
+  long off = 0;
+  for (int i = 0; i < n; ++i) {
+    const SatColsumSeg& g = segs[i];
+    if (g.N <= 0) continue;
+    const ColsumPlan p = colsum_plan(g.X, g.dtype, g.ld, g.R, g.N);
+    auto& sg = a.seg[k++];
+    sg.X = g.X; sg.ld = g.ld; sg.R = g.R; sg.N = g.N; sg.dtype = g.dtype; sg.vok = p.vok;
+    sg.colblocks = p.colblocks; sg.RS = p.RS; sg.rows_per = p.rows_per; sg.accumulate = g.accumulate;
+    sg.blk0 = blk; sg.fblk0 = fblk;
+    sg.part = scratch + off; sg.out = g.out; sg.out2 = g.out2;
+    blk += p.colblocks * p.RS;
+    fblk += sat_cdiv(g.N, 256);
+    off += (long)p.RS * g.N;
+  }
+  a.n = k;
+  if (k == 0) return 0;
+  hipLaunchKernelGGL(colsum_multi_partial_kernel, dim3(blk), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(colsum_multi_final_kernel, dim3(fblk), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int sat_zero_multi(float* const* ptrs, const long* counts, int n, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n > kZeroMaxSegs) return (int)hipErrorInvalidValue;
+  ZeroMultiArgs a{};
+  long tot = 0;
+  for (int i = 0; i < n; ++i) {
+    a.p[i] = ptrs[i];
+    a.count[i] = counts[i];
+    tot += counts[i];
+  }
+  a.n = n;
+  long g = (tot / 4 + 255) / 256;
+  g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
+  hipLaunchKernelGGL(zero_multi_kernel, dim3((int)g), dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
 size_t sat_colsum_scratch_floats(int R, int N) { (void)R; return (size_t)64 * (N > 0 ? N : 1); }

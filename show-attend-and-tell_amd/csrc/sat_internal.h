@@ -6,6 +6,14 @@ int sat_mean_rows(const void* a, int B, int L, int D, int dtype, float* out_f32,
 int sat_colsum(const void* X, int dtype, long ld, int R, int N, float* out, int accumulate, float* out2,
                float* scratch, hipStream_t s);
 size_t sat_colsum_scratch_floats(int R, int N);
+// several column sums in one partial + one final launch (<= 8 segments, same arithmetic as sat_colsum); the
+// scratch holds sum_i 64 * N_i floats
+struct SatColsumSeg {
+  const void* X; int dtype; long ld; int R, N; float* out; int accumulate; float* out2;
+};
+int sat_colsum_multi(const SatColsumSeg* segs, int n, float* scratch, hipStream_t s);
+// zero n (<= 8) fp32 ranges in one launch (graph-safe memset)
+int sat_zero_multi(float* const* ptrs, const long* counts, int n, hipStream_t s);
 int sat_embed_gather(const float* W, const int32_t* tok, int B, int T1, long tok_stride_b, int E, int dtype,
                      void* out, long out_ld, hipStream_t s);
 int sat_embed_scatter_add(const float* dX, const int32_t* tok, int R, int E, float* G, hipStream_t s);

@@ -131,12 +131,15 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 int sat_skinny_try(const SatGemm& g, hipStream_t st, int* err) {
   *err = 0;
-  const int mode = sat_policy().skinny;   // 0 the decoder's K/256-split products, 1 off, 2 every eligible
+  const int mode = sat_policy().skinny;   // 0 the decoder's split products, 1 off, 2 every eligible
   if (mode == 1) return 0;
-  // mode 0: only products the decoder split for this kernel (partial_splits == K / 256, the context
-  // GEMM: 9.2 vs 10.9 us per step); the [U; f_beta; W_hh] h GEMM stays on the tile kernel (8.2 vs 8.6
+  // mode 0: only products the decoder split for this kernel (partial splits of 256 - 1024 deep K ranges in
+  // whole 256-deep slabs: the context GEMM 9.2 vs 10.9 us per step; the backward's products through the
+  // transposed weight copies); the [U; f_beta; W_hh] h GEMM (one split) stays on the tile kernel (8.2 vs 8.6
   // us: with K = 512 every workgroup reads all of A); mode 2: every eligible problem (tests)
-  if (mode == 0 && !(g.partial_splits > 1 && g.K % 256 == 0 && g.partial_splits == g.K / 256)) return 0;
+  if (mode == 0 && !(g.partial_splits > 1 && g.K % g.partial_splits == 0 && (g.K / g.partial_splits) % 256 == 0 &&
+                     g.K / g.partial_splits <= 1024))
+    return 0;
   if (g.dtype != SAT_BF16 || g.c_dtype != SAT_F32 || g.batch != 1 || g.conv.C > 0) return 0;
   if (g.transA || g.transB || g.aux || g.add1 || g.act != SAT_ACT_NONE || g.beta != 0.f || g.alpha != 1.f) return 0;
   if (g.M < 1 || g.M > 128 || g.N % SK_COLS || g.K % 32 || g.K <= 0) return 0;

@@ -110,6 +110,9 @@ class Decoder(nn.Module):
         # workgroups the per-step split-K GEMMs aim for (SatDecoderDims.split_target; 0 = library
         # default): 64 when the decoder shares the chip with the next batch's encoder (bench / train.py)
         self.split_target = 0
+        # bf16: the BPTT's dL/d(gated context) and dL/dh products read transposed weight copies kept behind the
+        # shadow (SatDecoderLayout.wih_ctx_t / hcat_t); False = the k-major originals (A/B)
+        self.transposed_weights = True
         self._pending_bwd = None
         self.last_tokens = None        # int32 [B, T-1]: token fed at each step of the last forward
 
@@ -154,7 +157,33 @@ class Decoder(nn.Module):
         lay.fout_w, lay.fout_b = get("f_out.weight"), get("f_out.bias")
         lay.do_w, lay.do_b = get("deep_output.weight"), get("deep_output.bias")
         lay.total = self._flat.numel()
+        # transposed copies of W_ih[:, E:] and [U; f_beta; W_hh] behind the bf16 shadow (sat_decoder_refresh_transposed)
+        lay.wih_ctx_t, lay.hcat_t = self._lp_t_offsets() if self._flat_lp is not None and self.transposed_weights \
+            else (-1, -1)
         return lay
+
+    def _lp_t_offsets(self):
+        """Element offsets of the transposed weight copies at the tail of the bf16 shadow:
+        W_ih[:, E:]^T [D, 4E], then [U; f_beta; W_hh]^T [E, E+D+4E] (the flat size is a multiple of 64)."""
+        E, D = self.embedding_size, self.encoder_dim
+        base = self._flat.numel()
+        return base, base + D * 4 * E
+
+    def _lp_numel(self):
+        E, D = self.embedding_size, self.encoder_dim
+        return self._flat.numel() + D * 4 * E + E * (5 * E + D)
+
+    def refresh_transposed(self):
+        """Rewrite the transposed weight copies from the bf16 shadow (after the shadow changed: a cast, the
+        fused Adam step); the BPTT's dL/d(gated context) and dL/dh products read them."""
+        if self._flat_lp is None or not self.transposed_weights:
+            return
+        d = L.SatDecoderDims()
+        d.B, d.L, d.D, d.E, d.V, d.T = 1, 1, self.encoder_dim, self.embedding_size, self.vocabulary_size, 3
+        d.dtype = L.SAT_BF16
+        lay = self._layout()
+        L.check(L.lib().sat_decoder_refresh_transposed(ctypes.byref(d), ctypes.byref(lay), L.ptr(self._flat_lp),
+                                                        L.stream_of(self._flat_lp)), "sat_decoder_refresh_transposed")
 
     def _flat_ok(self, device):
         if self._flat is None or self._flat.device != device:
@@ -194,11 +223,12 @@ class Decoder(nn.Module):
     def _ensure_lp(self):
         versions = tuple(p._version for p in self.parameters())
         if self._flat_lp is None:
-            self._flat_lp = torch.empty(self._flat.numel(), device=self._flat.device, dtype=torch.bfloat16)
+            self._flat_lp = torch.empty(self._lp_numel(), device=self._flat.device, dtype=torch.bfloat16)
             self._lp_versions = None
         if versions != self._lp_versions:
             from .ops import cast_
-            cast_(self._flat, self._flat_lp)
+            cast_(self._flat, self._flat_lp[:self._flat.numel()])
+            self.refresh_transposed()
             self._lp_versions = versions
 
     def flat_lp_for_optimizer(self):

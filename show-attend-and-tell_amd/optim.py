@@ -101,7 +101,11 @@ class Adam(torch.optim.Optimizer):
                 else:
                     pv, gv, mv, vv = p.view(-1), p.grad.view(-1), st["exp_avg"].view(-1), st["exp_avg_sq"].view(-1)
                 ops.adam_step_(pv, gv, mv, vv, lp, b1, b2, eps, lr / bc1, math.sqrt(bc2))
+            refreshed = set()
             for p, owner, st in items:
                 if owner is not None and owner._flat_lp is not None:
                     owner._lp_versions = tuple(q._version for q in owner.parameters())
+                    if id(owner) not in refreshed:   # the transposed copies follow the updated shadow
+                        refreshed.add(id(owner))
+                        owner.refresh_transposed()
         return loss

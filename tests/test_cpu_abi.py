@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol():
     lib = sat_amd._lib.lib()
     missing = [f for f in declared_functions() if not hasattr(lib, f)]
     assert not missing, missing
-    assert lib.sat_abi_version() == sat_amd._lib.ABI_VERSION == header_abi_version() == 2
+    assert lib.sat_abi_version() == sat_amd._lib.ABI_VERSION == header_abi_version() == 3
     assert set(declared_functions()) == set(sat_amd._lib.EXPORTED)
 
 
@@ -50,11 +50,11 @@ def test_library_refuses_other_abi_version(monkeypatch):
     import sat_amd
     L = sat_amd._lib
     monkeypatch.setattr(L, "_lib", None)
-    monkeypatch.setattr(L, "ABI_VERSION", 1)
+    monkeypatch.setattr(L, "ABI_VERSION", 2)
     with pytest.raises(RuntimeError, match="C-ABI version"):
         L.lib()
     monkeypatch.undo()
-    assert L.lib().sat_abi_version() == 2
+    assert L.lib().sat_abi_version() == 3
 
 
 def test_error_strings():

@@ -1068,12 +1068,14 @@ def test_bottleneck_fused_bit_identical(sat, N):
     assert rel(nchw(y), t3) < 2e-2
 
 
-@pytest.mark.parametrize("N,H,C", [(1, 14, 256), (2, 14, 256), (5, 14, 256), (8, 14, 256), (16, 14, 256),
-                                   (1, 28, 128), (3, 28, 128)])
-def test_conv3x3_frag_bit_identical(sat, N, H, C):
-    """csrc/convblock.hip's half-image 3x3 kernel (a layer3 c2 left unfused: 14x14, 256 -> 256) and its
-    7-row band form (layer2 c2: 28x28, 128 -> 128) are bit-identical to the tile kernel on the same
-    operands, and close to torch fp32."""
+@pytest.mark.parametrize("N,H,C,slices", [(1, 14, 256, 1), (2, 14, 256, 1), (5, 14, 256, 1), (16, 14, 256, 1),
+                                          (1, 14, 256, 2), (3, 14, 256, 2), (70, 14, 256, 2), (5, 14, 256, 3),
+                                          (8, 14, 256, 0), (1, 28, 128, 0), (3, 28, 128, 0)])
+def test_conv3x3_frag_bit_identical(sat, N, H, C, slices):
+    """csrc/convblock.hip's half-image 3x3 kernel (a layer3 c2 left unfused: 14x14, 256 -> 256), its two-slice
+    form (SatPolicy.conv_slices 2 / 3: each half image as two 128-channel workgroups, the default at B <= 64;
+    N = 70 leaves a partial group of 8 half images) and its 7-row band form (layer2 c2: 28x28, 128 -> 128) are
+    bit-identical to the tile kernel on the same operands, and close to torch fp32."""
     from sat_amd import ops
     g = torch.Generator().manual_seed(40 + N + H)
     x = torch.randn(N, H, H, C, generator=g).relu().bfloat16().to(DEV)
@@ -1081,7 +1083,7 @@ def test_conv3x3_frag_bit_identical(sat, N, H, C):
     b = (0.1 * torch.randn(C, generator=g)).to(DEV)
     ref = ops.conv2d_nhwc(x, w, b, 1, 1, True)
     f = (ops.mfma_frag_layout(w.reshape(C, -1)), b)
-    y = ops.conv3x3_frag(x, f)
+    y = ops.conv3x3_frag(x, f, policy=sat.Policy(conv_slices=slices))
     torch.cuda.synchronize()
     assert torch.equal(y, ref), f"max |frag - tile| = {(y.float() - ref.float()).abs().max().item()}"
     t = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2).cpu(), w.float().permute(0, 3, 1, 2).cpu(), b.cpu(),
@@ -1089,17 +1091,18 @@ def test_conv3x3_frag_bit_identical(sat, N, H, C):
     assert rel(y.float().permute(0, 3, 1, 2).cpu(), t) < 1e-2
 
 
-@pytest.mark.parametrize("N", [1, 2, 5])
-def test_conv1x1_frag_bit_identical(sat, N):
+@pytest.mark.parametrize("N,slices", [(1, 1), (2, 1), (5, 1), (1, 2), (5, 2), (70, 2), (3, 0)])
+def test_conv1x1_frag_bit_identical(sat, N, slices):
     """csrc/convblock.hip's half-image 1x1 kernel (a layer3 c1 left unfused: 14x14, 1024 -> 256, input
-    slabs by LDS-DMA) is bit-identical to sat_conv2d_nhwc on the same operands, and close to torch fp32."""
+    slabs by LDS-DMA) and its two-slice form (SatPolicy.conv_slices 2, the default at B <= 64) are
+    bit-identical to sat_conv2d_nhwc on the same operands, and close to torch fp32."""
     from sat_amd import ops
     g = torch.Generator().manual_seed(60 + N)
     x = torch.randn(N, 14, 14, 1024, generator=g).relu().bfloat16().to(DEV)
     w = (torch.randn(256, 1, 1, 1024, generator=g) * math.sqrt(2.0 / 1024)).bfloat16().to(DEV)
     b = (0.1 * torch.randn(256, generator=g)).to(DEV)
     ref = ops.conv2d_nhwc(x, w, b, 1, 0, True)
-    y = ops.conv1x1_frag(x, (ops.mfma_frag_layout(w.reshape(256, -1)), b))
+    y = ops.conv1x1_frag(x, (ops.mfma_frag_layout(w.reshape(256, -1)), b), policy=sat.Policy(conv_slices=slices))
     torch.cuda.synchronize()
     assert torch.equal(y, ref), f"max |frag - conv| = {(y.float() - ref.float()).abs().max().item()}"
     t = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2).cpu(), w.float().permute(0, 3, 1, 2).cpu(), b.cpu()))
@@ -1235,6 +1238,40 @@ def test_decoder_skinny_matches_tile_kernel(sat, tf):
     for n, g in g0.items():
         scale = g0["attention.v.weight"] if n == "attention.v.bias" else g
         assert ((g1[n] - g).norm() / scale.norm().clamp_min(1e-12)).item() < 3e-2, n
+
+
+def test_decoder_transposed_weight_copies(sat):
+    """The bf16 shadow's tail holds W_ih[:, E:]^T and [U; f_beta; W_hh]^T (SatDecoderLayout.wih_ctx_t / hcat_t)
+    exactly, after the first cast and again after every fused Adam step (the BPTT's dL/d(gated context) and
+    dL/dh products read them on the skinny kernel)."""
+    B, Lf, D, V, T, E = 8, 49, 512, 300, 6, 512
+    torch.manual_seed(0)
+    dec = sat.Decoder(V, D, tf=True, ado=True, attention=True).to(DEV).train()
+    opt = sat.Adam(dec.parameters(), lr=1e-2)
+    g = torch.Generator().manual_seed(1)
+    feats = torch.randn(B, Lf, D, generator=g).bfloat16().to(DEV)
+    caps = O.make_captions(B, T, V, 1).to(DEV)
+
+    def check():
+        torch.cuda.synchronize()
+        lp, o = dec._flat_lp, dec._offsets
+        a, h = dec._lp_t_offsets()
+        wih = lp[o["lstm.weight_ih"]:o["lstm.weight_ih"] + 4 * E * (E + D)].view(4 * E, E + D)
+        HG = 5 * E + D
+        hcat = lp[o["attention.U.weight"]:o["attention.U.weight"] + HG * E].view(HG, E)
+        assert torch.equal(lp[a:a + D * 4 * E].view(D, 4 * E), wih[:, E:].t().contiguous())
+        assert torch.equal(lp[h:h + E * HG].view(E, HG), hcat.t().contiguous())
+        # and the shadow itself is the parameters rounded to bf16
+        assert torch.equal(wih, dec.lstm.weight_ih.detach().bfloat16())
+    for it in range(2):
+        opt.zero_grad()
+        preds, alphas = dec(feats, caps)
+        if it == 0:
+            check()   # after the first cast
+        loss, _ = sat.caption_loss(preds, alphas, caps)
+        loss.backward()
+        opt.step()
+        check()       # after the Adam step rewrote the shadow
 
 
 @pytest.mark.parametrize("N,H,relu,bias,stem", [(4, 56, True, True, False), (3, 56, False, True, False),

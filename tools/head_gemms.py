@@ -1,0 +1,92 @@
+"""Time the decoder's batched (non-per-step) GEMMs at the bench shape one by one (GPU).
+
+B = 128, T = 27 (R = B * 26 = 3328 rows), V = 10000, E = 512, D = 2048, L = 49, bf16 operands: the hoisted
+Ws = a W^T, the input / output head products of the forward, and the weight / input gradients of the backward
+(decoder.hip).  Each product is re-issued back to back between HIP events; per tile configuration
+(SatPolicy.gemm_tile) when --tiles.
+
+    python tools/head_gemms.py [--tiles] [--reps 10]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import sat_amd  # noqa: E402
+from sat_amd import ops  # noqa: E402
+
+B, T, V, E, D, L = 128, 27, 10000, 512, 2048, 49
+R = B * (T - 1)
+HG = 5 * E + D
+DEV = torch.device("cuda")
+
+# name, M, N, K, transA, transB, c dtype, beta
+SHAPES = [
+    ("Ws = a.W^T (fwd)", B * L, E, D, False, False, torch.bfloat16, 0.0),
+    ("x gates = emb.W_ih[:, :E]^T", R, 4 * E, E, False, False, torch.float32, 0.0),
+    ("f_z (fwd)", R, E, D, False, False, torch.float32, 0.0),
+    ("f_out logits (fwd)", R, V, E, False, False, torch.bfloat16, 0.0),
+    ("dW f_out", V, E, R, True, True, torch.float32, 0.0),
+    ("dX f_out", R, E, V, False, True, torch.float32, 0.0),
+    ("dW f_z", E, D, R, True, True, torch.float32, 0.0),
+    ("dX f_z", R, D, E, False, True, torch.float32, 0.0),
+    ("dW attention.W", E, D, B * L, True, True, torch.float32, 0.0),
+    ("dW [U; f_beta; W_hh]", HG, E, R, True, True, torch.float32, 0.0),
+    ("dW W_ih[:, :E]", 4 * E, E, R, True, True, torch.float32, 0.0),
+    ("dW W_ih[:, E:]", 4 * E, D, R, True, True, torch.float32, 0.0),
+    ("dX embedding", R, E, 4 * E, False, True, torch.float32, 0.0),
+]
+
+
+def operands(M, N, K, ta, tb, cdt):
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    A = (torch.randn(K, M, device=DEV, generator=g) if ta else torch.randn(M, K, device=DEV, generator=g)).bfloat16()
+    Bm = (torch.randn(K, N, device=DEV, generator=g) if tb else torch.randn(N, K, device=DEV, generator=g)).bfloat16()
+    C = torch.empty(M, N, device=DEV, dtype=cdt)
+    return A, Bm, C
+
+
+def time_one(A, Bm, C, ta, tb, beta, policy, reps):
+    def go():
+        ops.gemm(A, Bm, C, transA=ta, transB=tb, beta=beta, policy=policy)
+    for _ in range(2):
+        go()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(reps):
+        go()
+    en.record()
+    en.synchronize()
+    return st.elapsed_time(en) / reps * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tiles", action="store_true")
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    tot_us = tot_f = 0.0
+    for name, M, N, K, ta, tb, cdt, beta in SHAPES:
+        A, Bm, C = operands(M, N, K, ta, tb, cdt)
+        f = 2.0 * M * N * K
+        us = time_one(A, Bm, C, ta, tb, beta, None, a.reps)
+        tot_us += us
+        tot_f += f
+        line = f"{name:30s} M {M:5d} N {N:5d} K {K:5d} {'T' if ta else 'N'}{'T' if tb else 'N'}  {us:8.1f} us " \
+               f"{f / us / 1e6:7.1f} TF/s"
+        if a.tiles:
+            alt = []
+            for tile in (1, 2, 3, 4, 5):
+                try:
+                    alt.append(f"t{tile}:{time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_tile=tile), a.reps):.1f}")
+                except RuntimeError:
+                    alt.append(f"t{tile}:-")
+            line += "  [" + " ".join(alt) + "]"
+        print(line, flush=True)
+    print(f"total {tot_us:.1f} us for {tot_f / 1e9:.1f} GFLOP = {tot_f / tot_us / 1e6:.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
