@@ -51,6 +51,9 @@ def parse():
                     help="graph + overlap (ResNet152): the encoder runs as two graphs split at this stage; the "
                          "decoder of batch i runs beside batch i+1's first part only, the second part (the fused, "
                          "chip-filling layer3 blocks) starts when that decoder is done")
+    ap.add_argument("--enc-start", choices=["decoder", "phase2"], default="decoder",
+                    help="graph + overlap: batch i+1's encoder starts beside batch i's whole decoder (decoder), or "
+                         "only once its forward + head backward graph is done, beside the BPTT graph and Adam (phase2)")
     ap.add_argument("--split-target", type=int, default=None,
                     help="graph + overlap: workgroups the decoder's per-step split-K GEMMs aim for (default: "
                          "64 with ResNet152 features, 128 with VGG19's: profiles/r2_s54_sched.txt)")
@@ -68,9 +71,12 @@ def parse():
                          "split-K GEMMs, 2 otherwise)")
     ap.add_argument("--no-ws3x3", action="store_true",
                     help="64 -> 64 3x3 convs on the implicit-GEMM tile kernel instead of csrc/conv3x3ws.hip (A/B)")
-    ap.add_argument("--conv-slices", type=int, default=0, choices=[0, 1, 2, 3],
+    ap.add_argument("--conv-slices", type=int, default=0, choices=[0, 1, 2, 3, 4, 5],
                     help="layer3 c1 / c2 kernels: 0 auto (two 128-channel slices per half image at B <= 64), 1 one "
                          "workgroup per half image, 2 / 3 two slices (SatPolicy.conv_slices, A/B)")
+    ap.add_argument("--policy", default="",
+                    help="extra SatPolicy fields for every encoder / decoder call, e.g. attn_bwd_chunks=1,gemm_stages=3 "
+                         "(A/B; include/sat_hip.h)")
     ap.add_argument("--fuse-every", type=int, default=None,
                     help="fuse every n-th layer3 identity bottleneck only, the rest run as three conv launches "
                          "(default 0 = none: with the layer3 c2 / c3 on the half-image frag kernels the unfused "
@@ -145,6 +151,15 @@ class LaunchStamps:
         lo = torch.where(valid, st, torch.full_like(st, big)).min(dim=1).values
         hi = torch.where(valid, en, torch.zeros_like(en)).max(dim=1).values
         return [((h - l) / 100.0 if h > 0 else None) for l, h in zip(lo.tolist(), hi.tolist())]   # 100 MHz ticks
+
+    def intervals_us(self):
+        """Per launch: first start of the NEXT launch minus its own first start (its span plus the boundary after
+        it -- the launch's share of the stream), microseconds; None for the last launch."""
+        st = self.buf[:self.used, 1:, 0]
+        big = torch.iinfo(torch.int64).max
+        lo = torch.where(st > 0, st, torch.full_like(st, big)).min(dim=1).values.tolist()
+        return [((lo[i + 1] - lo[i]) / 100.0 if lo[i] < big and lo[i + 1] < big else None) for i in range(len(lo) - 1)] \
+            + [None]
 
 
 class DecoderStamps:
@@ -240,12 +255,13 @@ CONV_KERNEL_NAMES = ("fast_gemm_kernel", "conv_pipe_kernel", "conv1x1_stream_ker
                      "conv_ws_kernel", "conv3x3_frag_kernel", "conv3x3_band_kernel", "conv1x1_frag_kernel")
 
 
-def instep_conv_durations(stamps, launches):
+def instep_conv_durations(stamps, launches, intervals=False):
     """Per conv launch (conv_launches() order), its in-step durations [us] from the encoder graphs'
-    in-kernel timestamps (LaunchStamps, the last replay of each graph in the timed region)."""
+    in-kernel timestamps (LaunchStamps, the last replay of each graph); intervals: launch-start to next
+    launch-start instead of the span."""
     per = [[] for _ in launches]
     for st in stamps:
-        spans = st.spans_us()
+        spans = st.intervals_us() if intervals else st.spans_us()
         if len(spans) != len(launches):
             return None
         for i, us in enumerate(spans):
@@ -254,7 +270,7 @@ def instep_conv_durations(stamps, launches):
     return per
 
 
-def trunk_roofline(enc, imgs, launches, instep=None, overlapped=None, reps=3):
+def trunk_roofline(enc, imgs, launches, instep=None, overlapped=None, intervals=None, reps=3):
     """The encoder trunk against its roofline.
 
     Per conv launch, up to three durations [us]:
@@ -284,9 +300,9 @@ def trunk_roofline(enc, imgs, launches, instep=None, overlapped=None, reps=3):
 
     def mean_or_none(v):
         return [sum(x) / len(x) if x else None for x in v] if v is not None else [None] * n
-    span, ov = mean_or_none(instep), mean_or_none(overlapped)
+    span, ov, itv = mean_or_none(instep), mean_or_none(overlapped), mean_or_none(intervals)
     primary = [s_ if s_ is not None else e for s_, e in zip(span, eager)]
-    series = {"us": primary, "us_overlapped": ov, "us_eager": eager}
+    series = {"us": primary, "us_overlapped": ov, "us_eager": eager, "us_interval": itv}
     cls = {}
     for i, l in enumerate(launches):
         c = cls.setdefault(l["cls"], dict(n=0, flops=l["flops"], bytes=l["bytes"], bound=l["bound"],
@@ -331,7 +347,7 @@ def trunk_roofline(enc, imgs, launches, instep=None, overlapped=None, reps=3):
     avg_us = dom["us"] / dom["n"]
     achieved, peak, unit = rate(avg_us)
     extra = {}
-    for key, k in (("overlapped", "us_overlapped"),):
+    for key, k in (("overlapped", "us_overlapped"), ("interval", "us_interval")):
         a = dom[k] / dom["n"]
         if a == a:
             extra[f"avg_launch_us_{key}"] = round(a, 2)
@@ -346,9 +362,11 @@ def trunk_roofline(enc, imgs, launches, instep=None, overlapped=None, reps=3):
               "launch of the class in the captured encoder graphs replayed on their own after the timed region; "
               "avg_launch_us_overlapped: the same timestamps inside the timed region's overlapped schedule (sharing "
               "CUs with the decoder graphs); avg_launch_us_b2b: the class re-issued back to back into warm caches; "
-              f"avg_launch_us_eager_event_pairs: an event pair around every launch of {reps} eager forwards; a "
-              "rocprofv3 kernel trace adds its per-dispatch signalling (~4 us per conv launch, the same launches' "
-              "timestamps under the trace: profiles/r3_s8/prof_summary.json)"
+              f"avg_launch_us_eager_event_pairs: an event pair around every launch of {reps} eager forwards; "
+              "avg_launch_us_interval: first start of the launch to first start of the next one in the graphs "
+              "replayed alone (span + the boundary after it: the launch's share of the stream, the figure closest to "
+              "a rocprofv3 kernel trace's per-dispatch duration, which adds its own signalling: "
+              "profiles/r3_s8/prof_summary.json)"
               if instep is not None else
               "avg_launch_us: an event pair around every launch of the eager forwards (no in-kernel timestamps)")
 
@@ -548,9 +566,10 @@ def main():
 
     # per-call kernel selection for the A/B flags (None = the library's defaults)
     policy = None
-    if args.no_skinny or args.no_ws3x3 or args.gemm_stages or args.conv_slices:
+    extra = {k: int(v) for k, v in (kv.split("=") for kv in args.policy.split(",") if kv)}
+    if args.no_skinny or args.no_ws3x3 or args.gemm_stages or args.conv_slices or extra:
         policy = sat_amd.Policy(skinny=1 if args.no_skinny else 0, conv3x3_ws=1 if args.no_ws3x3 else 0,
-                                gemm_stages=args.gemm_stages, conv_slices=args.conv_slices)
+                                gemm_stages=args.gemm_stages, conv_slices=args.conv_slices, **extra)
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
@@ -675,6 +694,7 @@ def main():
         s_enc = torch.cuda.Stream() if overlap else s_main
     ev_enc = [torch.cuda.Event() for _ in range(2)]
     ev_dec = [torch.cuda.Event() for _ in range(2)]
+    ev_ph1 = torch.cuda.Event()   # --enc-start phase2: the decoder's forward + head backward graph is done
 
     def replay_encoder(k, wait_dec, dec_ev=None):
         """Batch k's encoder on s_enc.  wait_dec: feature buffer k was last read by the decoder two
@@ -683,6 +703,8 @@ def main():
         with torch.cuda.stream(s_enc):
             if wait_dec:
                 s_enc.wait_event(ev_dec[k])
+            if args.enc_start == "phase2" and dec_ev is not None:
+                s_enc.wait_event(ev_ph1)
             if g_encA is not None:   # encoder time = the two parts' own spans (not the wait between)
                 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 st.record(s_enc)
@@ -708,6 +730,8 @@ def main():
                 k = i % len(g_enc)
                 s_main.wait_event(ev_enc[k])
                 g_dec[k].replay()
+                if args.enc_start == "phase2":
+                    ev_ph1.record(s_main)
                 # DP: the output-head bucket is final after phase 1 -> its all-reduce runs on RCCL's
                 # stream beside the BPTT graph; the rest follows phase 2
                 w1 = allreduce_bucket_async(dec, 1) if world > 1 else None
@@ -779,7 +803,7 @@ def main():
                     decd.setdefault(g, []).extend(v)
         return conv, decd
     overlap_conv, overlap_dec = collect() if diag_phase else (None, None)
-    alone_conv = alone_dec = None
+    alone_conv = alone_dec = alone_intervals = None
     if diag and diag_phase and use_graph:
         # graph-alone phase: each encoder graph, then each decoder graph pair, replayed on its own (nothing
         # beside it) with the timestamps on -- the kernels' durations as a rocprofv3 kernel trace of this
@@ -798,10 +822,11 @@ def main():
                     g_rec[k].replay()
                 torch.cuda.synchronize()
         alone_conv, alone_dec = collect()
+        alone_intervals = instep_conv_durations(stamps_enc, launches, intervals=True) if stamps_enc else None
         for st in stamps_enc + stamps_dec:
             st.enable(False)
     roof, trunk = trunk_roofline(enc, imgs, launches, instep=alone_conv or overlap_conv,
-                                 overlapped=overlap_conv) if diag else (None, None)
+                                 overlapped=overlap_conv, intervals=alone_intervals) if diag else (None, None)
     step_kernels = decoder_step_roofline(dec, enc, imgs, caps, instep=alone_dec or overlap_dec,
                                          overlapped=overlap_dec) if diag else None
     fp32_leg = fp32_step(args, enc, dec, imgs, caps, pad_id, skip_ids, world) if world == 1 and args.fp32_steps > 0 \

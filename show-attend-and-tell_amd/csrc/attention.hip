@@ -84,9 +84,11 @@ constexpr int ANW = 8, FU = 8;
 // wave-uniform test), and everything the epilogue needs from HBM (gate pre-activation slabs) is
 // requested at kernel entry with the first annotation rows, so a step is one dependent memory
 // round trip plus the score / softmax / context phases.
-constexpr int FNW = 16, FDV = 2, FFU = 4;
+constexpr int FNW = 16, FFU = 4;
 
-template <typename T, int CH>   // CH = e-chunks of 64 x 16 bytes per lane covering E
+// FDV: 16-byte context vectors per lane (2: a workgroup owns 1024 bf16 columns; 1: 512, twice the workgroups for
+// small batches -- the score pass is recomputed per slice, the context sums are the same per column)
+template <typename T, int CH, int FDV>   // CH = e-chunks of 64 x 16 bytes per lane covering E
 __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   constexpr int VN = V16<T>::N;            // elements per 16-byte vector
   constexpr int COLS = 64 * VN * FDV;      // context columns of one workgroup
@@ -258,10 +260,10 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   }
 }
 
-template <typename T, int CH>   // CH = e-chunks of 64 x 16 bytes per lane covering E
+template <typename T, int CH, int FDV>   // CH = e-chunks of 64 x 16 bytes per lane covering E
 __global__ __launch_bounds__(FNW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
   const SatStampT0 t0 = sat_stamp_begin(a.st);
-  attn_fwd_kernel_body<T, CH>(a);
+  attn_fwd_kernel_body<T, CH, FDV>(a);
   sat_stamp_end(a.st, t0);
 }
 
@@ -814,11 +816,11 @@ inline int e_chunks(int E, int VN) {
   return c <= 1 ? 1 : (c <= 2 ? 2 : 4);
 }
 
-template <typename T>
+template <typename T, int FDV>
 void launch_fwd(int ch, dim3 grid, hipStream_t s, const AttnFwdArgs& a) {
-  if (ch == 1) hipLaunchKernelGGL((attn_fwd_kernel<T, 1>), grid, dim3(FNW * 64), 0, s, a);
-  else if (ch == 2) hipLaunchKernelGGL((attn_fwd_kernel<T, 2>), grid, dim3(FNW * 64), 0, s, a);
-  else hipLaunchKernelGGL((attn_fwd_kernel<T, 4>), grid, dim3(FNW * 64), 0, s, a);
+  if (ch == 1) hipLaunchKernelGGL((attn_fwd_kernel<T, 1, FDV>), grid, dim3(FNW * 64), 0, s, a);
+  else if (ch == 2) hipLaunchKernelGGL((attn_fwd_kernel<T, 2, FDV>), grid, dim3(FNW * 64), 0, s, a);
+  else hipLaunchKernelGGL((attn_fwd_kernel<T, 4, FDV>), grid, dim3(FNW * 64), 0, s, a);
 }
 
 }  // namespace
@@ -830,10 +832,17 @@ int sat_attention_fwd_launch(const AttnFwdArgs& args, hipStream_t s) {
   SAT_REQUIRE(a.L <= kMaxL && a.E % VD == 0 && a.E <= 1024);
   SAT_REQUIRE((a.uh_ld % 4) == 0 && (a.hg_splits <= 1 || a.hg_split_stride % 4 == 0));
   SAT_REQUIRE(a.D % VD == 0);
-  const int NS = sat_cdiv(a.D, 64 * VD * FDV);
+  // bf16: 1024-column slices by default; 512-column ones (twice the workgroups, SatPolicy::attn_fwd = 2) measured
+  // no faster at B = 64 (7.82 vs 7.79 us per step) and slower at B = 128 (15.2 vs 10.3 us): profiles/r3_s14/
+  const bool narrow = a.dtype == SAT_BF16 && sat_policy().attn_fwd == 2;
+  const int NS = sat_cdiv(a.D, 64 * VD * (narrow ? 1 : 2));
   dim3 grid(a.B, NS);
-  if (a.dtype == SAT_BF16) launch_fwd<bf16>(e_chunks(a.E, 8), grid, s, a);
-  else launch_fwd<float>(e_chunks(a.E, 4), grid, s, a);
+  if (a.dtype == SAT_BF16) {
+    if (narrow) launch_fwd<bf16, 1>(e_chunks(a.E, 8), grid, s, a);
+    else launch_fwd<bf16, 2>(e_chunks(a.E, 8), grid, s, a);
+  } else {
+    launch_fwd<float, 2>(e_chunks(a.E, 4), grid, s, a);
+  }
   return (int)hipGetLastError();
 }
 
@@ -911,6 +920,8 @@ int sat_attention_dws_launch(const void* Ws, const float* uh_all, const float* d
 }
 
 int sat_attention_bwd_chunks(int B, int L) {
+  const int f = sat_policy().attn_bwd_chunks;   // forced (A/B), clamped to the slots
+  if (f > 0) return f < L ? (f < 16 ? f : 16) : (L < 16 ? L : 16);
   // ~256 workgroups at least 4 slots deep: B = 128 -> 2 chunks, B = 64 -> 4, small test batches more
   int nl = sat_cdiv(256, B);
   const int by_l = sat_cdiv(L, 4);

@@ -652,12 +652,12 @@ __global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restric
 // ResNet152 layer3's c2 when half images alone would leave CUs idle (B <= 80 per GPU: 2B workgroups): each
 // half image as two 128-channel slices (4B workgroups), each streaming half the weights.  WM = 1: the 8
 // waves own 16 channels each and every m-block; WM = 2: 2 m-groups x 4 channel groups of 32.
-template <int WM>
+template <int WM, int PF>
 __global__ __launch_bounds__(512) void conv3x3_slice2_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                              const float* __restrict__ bias, bf16* __restrict__ y,
                                                              int nbands, SatStamps st) {
   const SatStampT0 t0 = sat_stamp_begin(st);
-  conv3x3_band_body<14, 7, 256, 2, WM, 2>(x, wf, bias, y, nbands);
+  conv3x3_band_body<14, 7, 256, 2, WM, PF>(x, wf, bias, y, nbands);
   sat_stamp_end(st, t0);
 }
 
@@ -818,12 +818,13 @@ __global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restric
   }
 }
 
-// Layer3 c1 / c2 launch form for a batch of N images: 1 = one workgroup per half image (2N workgroups), 2 / 3 = two
-// 128-channel slices per half image (4N; 3x3: 2 = one m-group of waves, 3 = two).  SatPolicy::conv_slices forces
+// Layer3 c1 / c2 launch form for a batch of N images: 1 = one workgroup per half image (2N workgroups), 2 - 5 = two
+// 128-channel slices per half image (4N; 3x3: 2 = one m-group of waves, 3 = two, 4 / 5 = one with the weights
+// prefetched 3 / 4 k-tiles ahead instead of 2).  SatPolicy::conv_slices forces
 // one; automatic: slices when the half images fill at most half the chip's 256 CUs (B <= 64 per GPU).
 int sat_frag_slices(int N) {
   const int f = sat_policy().conv_slices;
-  if (f >= 1 && f <= 3) return f;
+  if (f >= 1 && f <= 5) return f;
   return 2 * N <= 128 ? 2 : 1;
 }
 
@@ -889,9 +890,13 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   if (mode == 1)
     hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp, st);
   else if (mode == 2)
-    hipLaunchKernelGGL(conv3x3_slice2_kernel<1>, dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
+    hipLaunchKernelGGL((conv3x3_slice2_kernel<1, 2>), dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
+  else if (mode == 3)
+    hipLaunchKernelGGL((conv3x3_slice2_kernel<2, 2>), dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
+  else if (mode == 4)
+    hipLaunchKernelGGL((conv3x3_slice2_kernel<1, 3>), dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
   else
-    hipLaunchKernelGGL(conv3x3_slice2_kernel<2>, dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
+    hipLaunchKernelGGL((conv3x3_slice2_kernel<1, 4>), dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
   return (int)hipGetLastError();
 }
 

@@ -551,11 +551,13 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   int splitk = 1;
   const bool can_split = g.c_dtype == SAT_F32 && g.act == SAT_ACT_NONE && !g.add1 && (g.beta == 0.f || g.beta == 1.f) && !conv;
   if (g.beta != 0.f && !(can_split && g.beta == 1.f)) return 0;
+  // workgroups the atomic split-K aims for (SatPolicy::gemm_split_wgs; 0 = 320, split when tiles < half of it)
+  const int split_wgs = pol.gemm_split_wgs > 0 ? pol.gemm_split_wgs : 320;
   if (partial) {
     splitk = 1;
-  } else if (tiles < 160) {
+  } else if (tiles < split_wgs / 2) {
     if (can_split && g.K >= 1024) {
-      splitk = (int)((320 + tiles - 1) / tiles);
+      splitk = (int)((split_wgs + tiles - 1) / tiles);
       const int by_k = g.K / 256;
       if (splitk > by_k) splitk = by_k;
       if (splitk > 16) splitk = 16;

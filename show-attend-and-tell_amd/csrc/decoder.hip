@@ -77,7 +77,9 @@ inline Splits splits_for(const SatDecoderDims& d, bool tr) {
   if (bf) {   // per-step products the skinny kernel runs (csrc/skinny.hip): its own K split
     int k;
     if ((k = sat_skinny_splits(d.B, KH, E))) s.h = k;
-    if ((k = sat_skinny_splits(d.B, 4 * E, D))) s.c = k;
+    // the context GEMM in 512-deep splits (fewer slabs for the LSTM forward to sum: decoder fwd + bwd 3.05 ->
+    // 3.00 ms at B = 128 against 256-deep, profiles/r3_s13/splits128.log)
+    if ((k = sat_skinny_splits(d.B, 4 * E, D))) s.c = D % 512 == 0 ? k / 2 : k;
     if ((k = sat_skinny_splits(d.B, 2 * E, D))) s.i = k;
     // the backward's products through the transposed copies: 512-deep splits (fewer slabs for the attention /
     // LSTM backward kernels that sum them: B = 128 decoder fwd + bwd 3.15 -> 3.04 ms, B = 64 2.47 -> 2.36 ms

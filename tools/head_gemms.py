@@ -22,12 +22,13 @@ R = B * (T - 1)
 HG = 5 * E + D
 DEV = torch.device("cuda")
 
-# name, M, N, K, transA, transB, c dtype, beta
+RELU = sat_amd._lib.ACT_RELU
+# name, M, N, K, transA, transB, c dtype, beta[, act]
 SHAPES = [
     ("Ws = a.W^T (fwd)", B * L, E, D, False, False, torch.bfloat16, 0.0),
     ("x gates = emb.W_ih[:, :E]^T", R, 4 * E, E, False, False, torch.float32, 0.0),
-    ("f_z (fwd)", R, E, D, False, False, torch.float32, 0.0),
-    ("f_out logits (fwd)", R, V, E, False, False, torch.bfloat16, 0.0),
+    ("f_z (fwd, ReLU)", R, E, D, False, False, torch.float32, 0.0, RELU),
+    ("f_out logits (fwd, ReLU)", R, V, E, False, False, torch.bfloat16, 0.0, RELU),
     ("dW f_out", V, E, R, True, True, torch.float32, 0.0),
     ("dX f_out", R, E, V, False, True, torch.float32, 0.0),
     ("dW f_z", E, D, R, True, True, torch.float32, 0.0),
@@ -48,9 +49,9 @@ def operands(M, N, K, ta, tb, cdt):
     return A, Bm, C
 
 
-def time_one(A, Bm, C, ta, tb, beta, policy, reps):
+def time_one(A, Bm, C, ta, tb, beta, policy, reps, act=0):
     def go():
-        ops.gemm(A, Bm, C, transA=ta, transB=tb, beta=beta, policy=policy)
+        ops.gemm(A, Bm, C, transA=ta, transB=tb, beta=beta, act=act, policy=policy)
     for _ in range(2):
         go()
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -65,13 +66,15 @@ def time_one(A, Bm, C, ta, tb, beta, policy, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", action="store_true")
+    ap.add_argument("--split", action="store_true", help="also the atomic split-K aimed at 512 / 768 / 1024 workgroups")
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
     tot_us = tot_f = 0.0
-    for name, M, N, K, ta, tb, cdt, beta in SHAPES:
+    for name, M, N, K, ta, tb, cdt, beta, *rest in SHAPES:
+        act = rest[0] if rest else 0
         A, Bm, C = operands(M, N, K, ta, tb, cdt)
         f = 2.0 * M * N * K
-        us = time_one(A, Bm, C, ta, tb, beta, None, a.reps)
+        us = time_one(A, Bm, C, ta, tb, beta, None, a.reps, act)
         tot_us += us
         tot_f += f
         line = f"{name:30s} M {M:5d} N {N:5d} K {K:5d} {'T' if ta else 'N'}{'T' if tb else 'N'}  {us:8.1f} us " \
@@ -80,9 +83,13 @@ def main():
             alt = []
             for tile in (1, 2, 3, 4, 5):
                 try:
-                    alt.append(f"t{tile}:{time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_tile=tile), a.reps):.1f}")
+                    alt.append(f"t{tile}:{time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_tile=tile), a.reps, act):.1f}")
                 except RuntimeError:
                     alt.append(f"t{tile}:-")
+            line += "  [" + " ".join(alt) + "]"
+        if a.split:
+            alt = [f"w{wgs}:{time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_split_wgs=wgs), a.reps, act):.1f}"
+                   for wgs in (512, 768, 1024)]
             line += "  [" + " ".join(alt) + "]"
         print(line, flush=True)
     print(f"total {tot_us:.1f} us for {tot_f / 1e9:.1f} GFLOP = {tot_f / tot_us / 1e6:.1f} TF/s", flush=True)
