@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--bwd", choices=["serial", "split"], default="split",
                     help="N = 1 decoder backward structure: one graph in order (serial), or two graphs as at N > 1 "
                          "(split)")
+    ap.add_argument("--no-transposed", action="store_true",
+                    help="BPTT input-gradient products on the k-major weights instead of the transposed copies (A/B)")
     ap.add_argument("--no-skinny", action="store_true",
                     help="per-step decoder GEMMs on the LDS-DMA tile kernel instead of csrc/skinny.hip (A/B)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -71,7 +73,7 @@ def parse():
                          "split-K GEMMs, 2 otherwise)")
     ap.add_argument("--no-ws3x3", action="store_true",
                     help="64 -> 64 3x3 convs on the implicit-GEMM tile kernel instead of csrc/conv3x3ws.hip (A/B)")
-    ap.add_argument("--conv-slices", type=int, default=0, choices=[0, 1, 2, 3, 4, 5],
+    ap.add_argument("--conv-slices", type=int, default=0, choices=[0, 1, 2, 3, 4, 5, 6, 7],
                     help="layer3 c1 / c2 kernels: 0 auto (two 128-channel slices per half image at B <= 64), 1 one "
                          "workgroup per half image, 2 / 3 two slices (SatPolicy.conv_slices, A/B)")
     ap.add_argument("--policy", default="",
@@ -566,10 +568,11 @@ def main():
 
     # per-call kernel selection for the A/B flags (None = the library's defaults)
     policy = None
-    extra = {k: int(v) for k, v in (kv.split("=") for kv in args.policy.split(",") if kv)}
-    if args.no_skinny or args.no_ws3x3 or args.gemm_stages or args.conv_slices or extra:
-        policy = sat_amd.Policy(skinny=1 if args.no_skinny else 0, conv3x3_ws=1 if args.no_ws3x3 else 0,
-                                gemm_stages=args.gemm_stages, conv_slices=args.conv_slices, **extra)
+    extra = dict(skinny=1 if args.no_skinny else 0, conv3x3_ws=1 if args.no_ws3x3 else 0,
+                 gemm_stages=args.gemm_stages, conv_slices=args.conv_slices)
+    extra.update({k: int(v) for k, v in (kv.split("=") for kv in args.policy.split(",") if kv)})
+    if any(extra.values()):
+        policy = sat_amd.Policy(**extra)
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream
     D = 2048 if args.network == "resnet152" else 512
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
@@ -584,6 +587,7 @@ def main():
     dec = sat_amd.Decoder(args.vocab, D, tf=not args.no_tf, ado=not args.bert, bert=args.bert,
                           attention=True).to(dev).train()
     dec.policy = policy
+    dec.transposed_weights = not args.no_transposed
     if not args.no_graph and not args.no_overlap:
         # the decoder shares the chip with the next batch's encoder: fewer split-K workgroups
         dec.split_target = args.split_target

@@ -784,6 +784,17 @@ __global__ __launch_bounds__(512) void conv1x1_frag_kernel(const bf16* __restric
   sat_stamp_end(st, t0);
 }
 
+// whole 14x14 images as NSL = 4 channel slices of 64 (N x 4 workgroups, each streaming a quarter of the weights for
+// 196 output pixels), WM m-groups of waves (SatPolicy::conv_slices 6: WM = 4, 7: WM = 2; experiments for B <= 64)
+template <int WM>
+__global__ __launch_bounds__(512) void conv3x3_img4_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                           const float* __restrict__ bias, bf16* __restrict__ y,
+                                                           int nbands, SatStamps st) {
+  const SatStampT0 t0 = sat_stamp_begin(st);
+  conv3x3_band_body<14, 14, 256, 4, WM, 2>(x, wf, bias, y, nbands);
+  sat_stamp_end(st, t0);
+}
+
 // the same with each half image as two 128-channel slices (B <= 80 per GPU, as conv3x3_slice2_kernel)
 __global__ __launch_bounds__(512) void conv1x1_frag2_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                             const float* __restrict__ bias, bf16* __restrict__ y,
@@ -820,11 +831,11 @@ __global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restric
 
 // Layer3 c1 / c2 launch form for a batch of N images: 1 = one workgroup per half image (2N workgroups), 2 - 5 = two
 // 128-channel slices per half image (4N; 3x3: 2 = one m-group of waves, 3 = two, 4 / 5 = one with the weights
-// prefetched 3 / 4 k-tiles ahead instead of 2).  SatPolicy::conv_slices forces
+// prefetched 3 / 4 k-tiles ahead instead of 2; 6 / 7 (3x3) = whole images as four 64-channel slices).  SatPolicy::conv_slices forces
 // one; automatic: slices when the half images fill at most half the chip's 256 CUs (B <= 64 per GPU).
 int sat_frag_slices(int N) {
   const int f = sat_policy().conv_slices;
-  if (f >= 1 && f <= 5) return f;
+  if (f >= 1 && f <= 7) return f;
   return 2 * N <= 128 ? 2 : 1;
 }
 
@@ -895,8 +906,12 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
     hipLaunchKernelGGL((conv3x3_slice2_kernel<2, 2>), dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
   else if (mode == 4)
     hipLaunchKernelGGL((conv3x3_slice2_kernel<1, 3>), dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
-  else
+  else if (mode == 5)
     hipLaunchKernelGGL((conv3x3_slice2_kernel<1, 4>), dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
+  else if (mode == 6)
+    hipLaunchKernelGGL((conv3x3_img4_kernel<4>), dim3(sat_cdiv(N, 8) * 8 * 4), dim3(512), 0, s, xp, wp, b, yp, N, st);
+  else
+    hipLaunchKernelGGL((conv3x3_img4_kernel<2>), dim3(sat_cdiv(N, 8) * 8 * 4), dim3(512), 0, s, xp, wp, b, yp, N, st);
   return (int)hipGetLastError();
 }
 

@@ -159,7 +159,7 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   c.take(w->dWs_acc, B * L * E * f); c.take(w->dWs_t, B * L * E * ts);
   c.take(w->dv_acc, B * E * f); c.take(w->dbv_acc, B * f);
   c.take(w->de_all, R * L * f);
-  c.take(w->part, sat_attention_part_floats(d.B, d.L, d.D, d.E, d.dtype) * f);
+  c.take(w->part, sat_attention_part_floats(d.B, d.L, d.D, d.E, d.dtype, d.split_target) * f);
   c.take(w->ticket, B * 4);
   c.take(w->demb, R * E * f);
   c.take(w->dpre0, B * 2 * E * f); c.take(w->dpre0_t, B * 2 * E * ts);
@@ -415,6 +415,7 @@ int bwd_attn(const Ctx& c, const WS& w, const Splits& sp, const StepIO& io, int 
   a.de_out = w.de_all + (long)t * L; a.de_ld = T1 * L; a.dv_acc = w.dv_acc; a.dbv_acc = w.dbv_acc; a.part = w.part;
   a.ticket = w.ticket;
   a.dg_splits = sp.g; a.dg_split_stride = (long)B * D;
+  a.wg_target = d.split_target;   // beside the encoder: fewer workgroups (sat_attention_bwd_chunks)
   return sat_attention_bwd_launch(a, s);
 }
 

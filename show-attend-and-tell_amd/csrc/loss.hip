@@ -46,6 +46,18 @@ __device__ __forceinline__ void online_add(float& m, float& se, float x) {
   else se += expf(x - m);
 }
 
+// row r's statistics: log-sum-exp, CE term (the last step is never scored), top-1 / top-5 hits (C = number of
+// logits ranked above the target), non-pad flag
+__device__ __forceinline__ void write_row_stats(float* stats, int r, int T1, int t, float lse, float xt, float C,
+                                                bool nonpad) {
+  float* st = stats + (long)r * kStat;
+  st[0] = lse;
+  st[1] = (t < T1 - 1) ? lse - xt : 0.f;
+  st[2] = (nonpad && C < 1.f) ? 1.f : 0.f;
+  st[3] = (nonpad && C < 5.f) ? 1.f : 0.f;
+  st[4] = nonpad ? 1.f : 0.f;
+}
+
 template <typename TT>
 __global__ __launch_bounds__(256) void loss_rows_kernel(const TT* __restrict__ preds, const int64_t* __restrict__ caps,
                                                         int B, int T, int V, int pad_id, float* __restrict__ stats) {
@@ -58,6 +70,54 @@ __global__ __launch_bounds__(256) void loss_rows_kernel(const TT* __restrict__ p
   const float xt = (tgt >= 0 && tgt < V) ? (float)x[tgt] : 0.f;
   float m = -INFINITY, se = 0.f, cnt = 0.f;
   constexpr int VEC = 16 / sizeof(TT);
+  constexpr int RV = 12;   // register-resident row: up to RV 16-byte vectors per thread (V <= 24576 bf16 / 12288 fp32)
+  if (V % VEC == 0 && V / VEC <= RV * 256) {
+    // the whole row in registers (every load requested up front), then two passes over registers: the
+    // thread max, the block max, then one v_exp per element against it (the online form paid a branch and
+    // up to two exps per element: VALU-bound at V = 10000, 36 us per 3328 rows)
+    const int NV = V / VEC;
+    uint4 u[RV];
+#pragma unroll
+    for (int k = 0; k < RV; ++k) {
+      const int c = threadIdx.x + k * 256;
+      u[k] = c < NV ? *(const uint4*)(x + (long)c * VEC) : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int k = 0; k < RV; ++k) {
+      const int c = threadIdx.x + k * 256;
+      if (c < NV) {
+        const TT* h = (const TT*)&u[k];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const float xv = (float)h[j];
+          m = fmaxf(m, xv);
+          cnt += (xv > xt || (xv == xt && c * VEC + j < tgt)) ? 1.f : 0.f;
+        }
+      }
+    }
+    const float M = block_max(m, red_m);
+#pragma unroll
+    for (int k = 0; k < RV; ++k) {
+      const int c = threadIdx.x + k * 256;
+      if (c < NV) {
+        const TT* h = (const TT*)&u[k];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) se += __expf((float)h[j] - M);
+      }
+    }
+    // the block's sums in a fixed order (wave shuffle tree, then the 4 waves in order)
+    se = wave_sum(se);
+    cnt = wave_sum(cnt);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) { red_s[w] = se; red_c[w] = cnt; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float S = (red_s[0] + red_s[1]) + (red_s[2] + red_s[3]);
+      const float C = (red_c[0] + red_c[1]) + (red_c[2] + red_c[3]);
+      write_row_stats(stats, r, T1, t, M + logf(S), xt, C, tgt != pad_id);
+    }
+    return;
+  }
   if (V % VEC == 0) {
     // LU vectors per thread in flight (the per-thread order c = tid, tid + 256, .. is unchanged)
     constexpr int LU = 4;
@@ -110,14 +170,7 @@ __global__ __launch_bounds__(256) void loss_rows_kernel(const TT* __restrict__ p
       M = nm;
       C += red_c[i];
     }
-    const float lse = M + logf(S);
-    const bool nonpad = tgt != pad_id;
-    float* st = stats + (long)r * kStat;
-    st[0] = lse;
-    st[1] = (t < T1 - 1) ? lse - xt : 0.f;
-    st[2] = (nonpad && C < 1.f) ? 1.f : 0.f;
-    st[3] = (nonpad && C < 5.f) ? 1.f : 0.f;
-    st[4] = nonpad ? 1.f : 0.f;
+    write_row_stats(stats, r, T1, t, M + logf(S), xt, C, tgt != pad_id);
   }
 }
 

@@ -280,19 +280,24 @@ __global__ void tokens_kernel(const int64_t* caps, int B, int T, int T1, int32_t
     else hipLaunchKernelGGL(KERNEL<float>, grid, dim3(256), 0, s, __VA_ARGS__);               \
   } while (0)
 
+// blocks of 64 units (256 threads) for B x E units: one per 64 units, capped at 4096 or at SatPolicy::lstm_blocks
+// (A/B: fewer resident waves beside a concurrent encoder; the kernels stride over the rest)
+inline long lstm_blocks(int B, int E) {
+  long blocks = ((long)B * E + 63) / 64;
+  const int cap = sat_policy().lstm_blocks > 0 ? sat_policy().lstm_blocks : 4096;
+  return blocks > cap ? cap : blocks;
+}
 int sat_lstm_fwd_launch(const LstmFwdArgs& args, hipStream_t s) {
   LstmFwdArgs a = args;
   a.st = sat_launch_stamps();
-  long blocks = ((long)a.B * a.E + 63) / 64;
-  if (blocks > 4096) blocks = 4096;
+  const long blocks = lstm_blocks(a.B, a.E);
   DISPATCH_T(a.dtype, lstm_fwd_gp_kernel, dim3((int)blocks), a);
   return (int)hipGetLastError();
 }
 int sat_lstm_bwd_launch(const LstmBwdArgs& args, hipStream_t s) {
   LstmBwdArgs a = args;
   a.st = sat_launch_stamps();
-  long blocks = ((long)a.B * a.E + 63) / 64;
-  if (blocks > 4096) blocks = 4096;
+  const long blocks = lstm_blocks(a.B, a.E);
   DISPATCH_T(a.dtype, lstm_bwd_gp_kernel, dim3((int)blocks), a);
   return (int)hipGetLastError();
 }

@@ -61,6 +61,7 @@ struct AttnBwdArgs {
   float* part;                          // scratch: [B, NS, L] (two-launch form) | [B, NL, 2E+1] (split form)
   unsigned* ticket;                     // [B] arrival counters of the split form (zero between launches)
   int dg_splits; long dg_split_stride;  // d_gated = sum of dg_splits partial slabs (0|1 = plain)
+  int wg_target;                        // workgroups the split form aims for (0 = 256; the decoder's split target)
   SatStamps st;                         // in-kernel launch timestamps (set by the launcher)
 };
 int sat_attention_bwd_launch(const AttnBwdArgs& a, hipStream_t s);
@@ -125,9 +126,10 @@ int sat_zero_rows(float* p, long ld, long rows, long cols, hipStream_t s);   // 
 int sat_broadcast_rows(const void* src, int B, int D, int T1, int dtype, void* dst, hipStream_t s);
 int sat_row_sum_accumulate(const float* X, int R, int N, float* out, hipStream_t s);
 int sat_tokens_from_captions(const int64_t* caps, int B, int T, int T1, int32_t* tok, hipStream_t s);
-size_t sat_attention_part_floats(int B, int L, int D, int E, int dtype);
-// chunks of L one batch row's attention backward is split over (sat_attention_bwd_launch)
-int sat_attention_bwd_chunks(int B, int L);
+size_t sat_attention_part_floats(int B, int L, int D, int E, int dtype, int wg_target);
+// chunks of L one batch row's attention backward is split over (sat_attention_bwd_launch), aiming for wg_target
+// workgroups (0 = 256)
+int sat_attention_bwd_chunks(int B, int L, int wg_target);
 
 // sum of `n` partial slabs (n <= 1: plain read).  Three independent accumulators keep several
 // slab loads in flight (a single running sum serialises one L2 round trip per slab).
