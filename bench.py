@@ -73,12 +73,12 @@ def parse():
                          "split-K GEMMs, 2 otherwise)")
     ap.add_argument("--no-ws3x3", action="store_true",
                     help="64 -> 64 3x3 convs on the implicit-GEMM tile kernel instead of csrc/conv3x3ws.hip (A/B)")
-    ap.add_argument("--conv-slices", type=int, default=0, choices=[0, 1, 2, 3, 4, 5, 6, 7],
+    ap.add_argument("--conv-slices", type=int, default=0, choices=[0, 1, 2],
                     help="layer3 c1 / c2 kernels: 0 auto (two 128-channel slices per half image at B <= 64), 1 one "
-                         "workgroup per half image, 2 / 3 two slices (SatPolicy.conv_slices, A/B)")
+                         "workgroup per half image, 2 two slices (SatPolicy.conv_slices, A/B)")
     ap.add_argument("--policy", default="",
                     help="extra SatPolicy fields for every encoder / decoder call, e.g. attn_bwd_chunks=1,gemm_stages=3 "
-                         "(A/B; include/sat_hip.h)")
+                         "or decoder_splits=2.0.0.0 (A/B; include/sat_hip.h)")
     ap.add_argument("--fuse-every", type=int, default=None,
                     help="fuse every n-th layer3 identity bottleneck only, the rest run as three conv launches "
                          "(default 0 = none: with the layer3 c2 / c3 on the half-image frag kernels the unfused "
@@ -570,7 +570,9 @@ def main():
     policy = None
     extra = dict(skinny=1 if args.no_skinny else 0, conv3x3_ws=1 if args.no_ws3x3 else 0,
                  gemm_stages=args.gemm_stages, conv_slices=args.conv_slices)
-    extra.update({k: int(v) for k, v in (kv.split("=") for kv in args.policy.split(",") if kv)})
+    for kv in (x for x in args.policy.split(",") if x):
+        k, v = kv.split("=")
+        extra[k] = [int(t) for t in v.split(".")] if "." in v else int(v)   # decoder_splits=2.0.0.0
     if any(extra.values()):
         policy = sat_amd.Policy(**extra)
     torch.manual_seed(42 + rank)   # train.py:452 seed; per-rank data stream

@@ -62,9 +62,6 @@ typedef struct {
   int gemm_epilogue;    /* bf16-output epilogue of 128-row tiles: 0 bf16 LDS epilogue for every eligible launch,
                          * 1 for residual launches only, 2 fp32 tile staged in LDS */
   int attn_bwd;         /* attention backward per decoder step: 0 auto, 1 the two-launch form */
-  int attn_fwd;         /* bf16 attention forward: 0 / 1 1024-column slices per 16-wave workgroup, 2 512-column slices
-                         * (twice the workgroups; bit-identical: the same per-column sums), 3 1024-column slices per
-                         * 8-wave workgroup (8 slots per wave: half the resident waves) */
   int attn_bwd_chunks;  /* split attention backward: slot chunks per batch row (0 auto: ~256 workgroups) */
   int gemm_split_wgs;   /* bf16 tile GEMM, fp32 output: workgroups an atomic split-K aims for (0 = 320; problems with
                          * fewer than half as many tiles and K >= 1024 are split) */
@@ -81,9 +78,7 @@ typedef struct {
   int stamp_capacity;
   int conv_slices;      /* layer3 c1 / c2 half-image kernels (sat_conv1x1_frag, sat_conv3x3_frag at 14x14): 0 auto
                          * (channel slices when B <= 64), 1 one workgroup per half image, 2 two 128-channel slices
-                         * per half image, 3 (3x3 only) the same with two m-groups of waves, 4 / 5 (3x3 only) one
-                         * m-group with weights prefetched 3 / 4 k-tiles ahead, 6 / 7 (3x3 only) whole images as four
-                         * 64-channel slices with 4 / 2 m-groups */
+                         * per half image */
 } SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),

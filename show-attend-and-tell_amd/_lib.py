@@ -31,7 +31,7 @@ ABI_VERSION = 3   # include/sat_hip.h SAT_ABI_VERSION: the library must match th
 class SatPolicy(ctypes.Structure):
     """Per-call kernel selection (include/sat_hip.h SatPolicy); all zeros = the library's defaults."""
     _fields_ = [(n, c_int) for n in ("conv_pipe", "conv_stream", "conv3x3_ws", "skinny", "gemm_stages", "gemm_tile",
-                                     "gemm_linear_order", "gemm_epilogue", "attn_bwd", "attn_fwd",
+                                     "gemm_linear_order", "gemm_epilogue", "attn_bwd",
                                      "attn_bwd_chunks", "gemm_split_wgs", "lstm_blocks")] + \
                [("decoder_splits", c_int * 4), ("stamps", c_void_p), ("stamp_capacity", c_int), ("conv_slices", c_int)]
 

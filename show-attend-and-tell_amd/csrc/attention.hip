@@ -84,18 +84,20 @@ constexpr int ANW = 8, FU = 8;
 // wave-uniform test), and everything the epilogue needs from HBM (gate pre-activation slabs) is
 // requested at kernel entry with the first annotation rows, so a step is one dependent memory
 // round trip plus the score / softmax / context phases.
-constexpr int FNW = 16, FFU = 4;
+constexpr int FNW = 16, FFU = 4;   // the default shape: 16 waves x 4 slots per batch of loads
 
-// FDV: 16-byte context vectors per lane (2: a workgroup owns 1024 bf16 columns; 1: 512, twice the workgroups for
-// small batches -- the score pass is recomputed per slice, the context sums are the same per column)
-template <typename T, int CH, int FDV>   // CH = e-chunks of 64 x 16 bytes per lane covering E
+// FDV: 16-byte context vectors per lane (2: a workgroup owns 1024 bf16 / 512 fp32 columns)
+// NW waves, FU slots per wave per batch of loads (16 x 4: every slot of L = 49 in one batch).
+template <typename T, int CH, int FDV, int NW = FNW, int FU = FFU>   // CH = e-chunks of 64 x 16 bytes per lane covering E
 __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   constexpr int VN = V16<T>::N;            // elements per 16-byte vector
   constexpr int COLS = 64 * VN * FDV;      // context columns of one workgroup
+  constexpr int NT = NW * 64, CPT = (COLS + NT - 1) / NT;   // output columns per thread
+  static_assert(NW % 8 == 0, "waves fold through 8 LDS rows");
   __shared__ float s_alpha[kMaxL];
-  // the 16 waves' context partials fold through 8 LDS rows in two rounds (36 KB of LDS instead of 68:
-  // the kernel then fits beside a 98-122 KB encoder workgroup on the same CU)
-  __shared__ float s_red[FNW / 2][COLS];
+  // the waves' context partials fold through 8 LDS rows in NW / 8 rounds (36 KB of LDS instead of 68 at 16
+  // waves: the kernel then fits beside a 98-122 KB encoder workgroup on the same CU)
+  __shared__ float s_red[8][COLS];
   const int b = blockIdx.x, s = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = a.L, D = a.D, E = a.E;
@@ -107,12 +109,12 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   // Issue order = order of first use (vmcnt retires loads in order): the first batch of score
   // rows, then U h + b and v, then the context rows and the gate pre-activation, which stay in
   // flight while the scores and the softmax are computed.
-  uint4 xv[FFU][CH];
+  uint4 xv[FU][CH];
 #pragma unroll
-  for (int u = 0; u < FFU; ++u)
+  for (int u = 0; u < FU; ++u)
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-      const int l = w + FNW * u, e = c * 64 * VN + lane * VN;
+      const int l = w + NW * u, e = c * 64 * VN + lane * VN;
       xv[u][c] = ld16(Ws + (long)l * E + e, l < L && e < E);
     }
 
@@ -134,31 +136,35 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   }
 
   // context rows of the first batch and the epilogue's gate pre-activation (this thread's column)
-  uint4 xa[FFU][FDV];
+  uint4 xa[FU][FDV];
 #pragma unroll
-  for (int u = 0; u < FFU; ++u)
+  for (int u = 0; u < FU; ++u)
 #pragma unroll
     for (int v = 0; v < FDV; ++v)
-      xa[u][v] = ld16(ab + (long)(w + FNW * u) * D + v * 64 * VN, w + FNW * u < L && c0 + v * 64 * VN + lane * VN < D);
-  const int dout = c0 + tid;
-  const bool out_ok = tid < COLS && dout < D;
-  float gpre = 0.f;
-  if (a.gate_pre && out_ok) gpre = sum_parts(a.gate_pre, (long)b * a.gate_ld + dout, a.hg_splits, a.hg_split_stride);
+      xa[u][v] = ld16(ab + (long)(w + NW * u) * D + v * 64 * VN, w + NW * u < L && c0 + v * 64 * VN + lane * VN < D);
+  float gpre[CPT];
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int col = k * NT + tid, dout = c0 + col;
+    gpre[k] = 0.f;
+    if (a.gate_pre && col < COLS && dout < D)
+      gpre[k] = sum_parts(a.gate_pre, (long)b * a.gate_ld + dout, a.hg_splits, a.hg_split_stride);
+  }
 
   const float bv = a.v_b[0];
-  for (int l0 = w; l0 < L; l0 += FNW * FFU) {
+  for (int l0 = w; l0 < L; l0 += NW * FU) {
     if (l0 != w) {
 #pragma unroll
-      for (int u = 0; u < FFU; ++u)
+      for (int u = 0; u < FU; ++u)
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
-          const int l = l0 + FNW * u, e = c * 64 * VN + lane * VN;
+          const int l = l0 + NW * u, e = c * 64 * VN + lane * VN;
           xv[u][c] = ld16(Ws + (long)l * E + e, l < L && e < E);
         }
     }
 #pragma unroll
-    for (int u = 0; u < FFU; ++u) {
-      const int l = l0 + FNW * u;
+    for (int u = 0; u < FU; ++u) {
+      const int l = l0 + NW * u;
       if (l >= L) break;   // wave-uniform
       float acc = 0.f;
 #pragma unroll
@@ -208,18 +214,18 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   for (int v = 0; v < FDV; ++v)
 #pragma unroll
     for (int j = 0; j < VN; ++j) part[v][j] = 0.f;
-  for (int l0 = w; l0 < L; l0 += FNW * FFU) {
+  for (int l0 = w; l0 < L; l0 += NW * FU) {
     if (l0 != w) {
 #pragma unroll
-      for (int u = 0; u < FFU; ++u)
+      for (int u = 0; u < FU; ++u)
 #pragma unroll
         for (int v = 0; v < FDV; ++v)
-          xa[u][v] = ld16(ab + (long)(l0 + FNW * u) * D + v * 64 * VN,
-                          l0 + FNW * u < L && c0 + v * 64 * VN + lane * VN < D);
+          xa[u][v] = ld16(ab + (long)(l0 + NW * u) * D + v * 64 * VN,
+                          l0 + NW * u < L && c0 + v * 64 * VN + lane * VN < D);
     }
 #pragma unroll
-    for (int u = 0; u < FFU; ++u) {
-      const int l = l0 + FNW * u;
+    for (int u = 0; u < FU; ++u) {
+      const int l = l0 + NW * u;
       if (l < L) {
         const float al = s_alpha[l];
 #pragma unroll
@@ -231,11 +237,13 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
       }
     }
   }
-  // fixed summation order over the wave partials: c = sum over q = 0, 2, .., 14 of (p_q + p_(q+1)),
-  // waves 0-7 first, then waves 8-15 through the same 8 rows
-  float c = 0.f;
+  // fixed summation order over the wave partials: c = sum over q = 0, 2, .., 6 of (p_q + p_(q+1)) per round of
+  // 8 waves, waves 0-7 first, then waves 8-15 through the same 8 rows
+  float cacc[CPT];
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  for (int k = 0; k < CPT; ++k) cacc[k] = 0.f;
+#pragma unroll
+  for (int half = 0; half < NW / 8; ++half) {
     if ((w >> 3) == half) {
 #pragma unroll
       for (int v = 0; v < FDV; ++v)
@@ -243,27 +251,36 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
         for (int j = 0; j < VN; ++j) s_red[w & 7][v * 64 * VN + lane * VN + j] = part[v][j];
     }
     __syncthreads();
-    if (out_ok) {
 #pragma unroll
-      for (int q = 0; q < FNW / 2; q += 2) c += s_red[q][tid] + s_red[q + 1][tid];
+    for (int k = 0; k < CPT; ++k) {
+      const int col = k * NT + tid;
+      if (col < COLS && c0 + col < D) {
+#pragma unroll
+        for (int q = 0; q < 8; q += 2) cacc[k] += s_red[q][col] + s_red[q + 1][col];
+      }
     }
-    if (half == 0) __syncthreads();
+    if (half + 1 < NW / 8) __syncthreads();
   }
-  if (out_ok) {
-    a.ctx[(long)b * a.ctx_ld + dout] = c;
-    if (a.ctx_t) ((T*)a.ctx_t)[(long)b * a.ctx_t_ld + dout] = (T)c;
-    if (a.gate_pre) {
-      const float g = 1.0f / (1.0f + expf(-gpre));
-      if (a.gate) a.gate[(long)b * a.gate_out_ld + dout] = g;
-      if (a.gated) ((T*)a.gated)[(long)b * a.gated_ld + dout] = (T)(g * c);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int col = k * NT + tid, dout = c0 + col;
+    if (col < COLS && dout < D) {
+      const float c = cacc[k];
+      a.ctx[(long)b * a.ctx_ld + dout] = c;
+      if (a.ctx_t) ((T*)a.ctx_t)[(long)b * a.ctx_t_ld + dout] = (T)c;
+      if (a.gate_pre) {
+        const float g = 1.0f / (1.0f + expf(-gpre[k]));
+        if (a.gate) a.gate[(long)b * a.gate_out_ld + dout] = g;
+        if (a.gated) ((T*)a.gated)[(long)b * a.gated_ld + dout] = (T)(g * c);
+      }
     }
   }
 }
 
-template <typename T, int CH, int FDV>   // CH = e-chunks of 64 x 16 bytes per lane covering E
-__global__ __launch_bounds__(FNW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
+template <typename T, int CH, int FDV, int NW = FNW, int FU = FFU>   // CH = e-chunks of 64 x 16 bytes per lane covering E
+__global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
   const SatStampT0 t0 = sat_stamp_begin(a.st);
-  attn_fwd_kernel_body<T, CH, FDV>(a);
+  attn_fwd_kernel_body<T, CH, FDV, NW, FU>(a);
   sat_stamp_end(a.st, t0);
 }
 
@@ -816,11 +833,11 @@ inline int e_chunks(int E, int VN) {
   return c <= 1 ? 1 : (c <= 2 ? 2 : 4);
 }
 
-template <typename T, int FDV>
+template <typename T, int FDV, int NW = FNW, int FU = FFU>
 void launch_fwd(int ch, dim3 grid, hipStream_t s, const AttnFwdArgs& a) {
-  if (ch == 1) hipLaunchKernelGGL((attn_fwd_kernel<T, 1, FDV>), grid, dim3(FNW * 64), 0, s, a);
-  else if (ch == 2) hipLaunchKernelGGL((attn_fwd_kernel<T, 2, FDV>), grid, dim3(FNW * 64), 0, s, a);
-  else hipLaunchKernelGGL((attn_fwd_kernel<T, 4, FDV>), grid, dim3(FNW * 64), 0, s, a);
+  if (ch == 1) hipLaunchKernelGGL((attn_fwd_kernel<T, 1, FDV, NW, FU>), grid, dim3(NW * 64), 0, s, a);
+  else if (ch == 2) hipLaunchKernelGGL((attn_fwd_kernel<T, 2, FDV, NW, FU>), grid, dim3(NW * 64), 0, s, a);
+  else hipLaunchKernelGGL((attn_fwd_kernel<T, 4, FDV, NW, FU>), grid, dim3(NW * 64), 0, s, a);
 }
 
 }  // namespace
@@ -834,12 +851,13 @@ int sat_attention_fwd_launch(const AttnFwdArgs& args, hipStream_t s) {
   SAT_REQUIRE(a.D % VD == 0);
   // bf16: 1024-column slices by default; 512-column ones (twice the workgroups, SatPolicy::attn_fwd = 2) measured
   // no faster at B = 64 (7.82 vs 7.79 us per step) and slower at B = 128 (15.2 vs 10.3 us): profiles/r3_s14/
-  const bool narrow = a.dtype == SAT_BF16 && sat_policy().attn_fwd == 2;
-  const int NS = sat_cdiv(a.D, 64 * VD * (narrow ? 1 : 2));
+  // one workgroup of 16 waves per (row, 1024 bf16 columns).  Measured and removed (profiles/r3_s14, r3_s19): 512-column
+  // slices (twice the workgroups; bit-identical) -- no faster at B = 64, 15.2 vs 10.3 us per step at B = 128; 8 waves
+  // x 8 slots per workgroup (half the resident waves) -- 6.61-6.66 vs 6.57-6.58 ms per overlapped step
+  const int NS = sat_cdiv(a.D, 64 * VD * 2);
   dim3 grid(a.B, NS);
   if (a.dtype == SAT_BF16) {
-    if (narrow) launch_fwd<bf16, 1>(e_chunks(a.E, 8), grid, s, a);
-    else launch_fwd<bf16, 2>(e_chunks(a.E, 8), grid, s, a);
+    launch_fwd<bf16, 2>(e_chunks(a.E, 8), grid, s, a);
   } else {
     launch_fwd<float, 2>(e_chunks(a.E, 4), grid, s, a);
   }
@@ -870,7 +888,7 @@ template <typename T>
 bool launch_bwd_split(const AttnBwdArgs& a, hipStream_t s) {
   constexpr int VN = V16<T>::N;
   const int dch = sat_cdiv(a.D, 64 * VN), ech = sat_cdiv(a.E, 64 * VN);
-  const int nl = sat_attention_bwd_chunks(a.B, a.L);
+  const int nl = sat_attention_bwd_chunks(a.B, a.L, a.wg_target);
   if (nl > 1 && (!a.part || !a.ticket)) return false;
   switch (dch) {
     case 1: return launch_bwd_split_d<T, 1>(ech, nl, s, a);
@@ -919,21 +937,29 @@ int sat_attention_dws_launch(const void* Ws, const float* uh_all, const float* d
   return (int)hipGetLastError();
 }
 
-int sat_attention_bwd_chunks(int B, int L) {
+int sat_attention_bwd_chunks(int B, int L, int wg_target) {
   const int f = sat_policy().attn_bwd_chunks;   // forced (A/B), clamped to the slots
   if (f > 0) return f < L ? (f < 16 ? f : 16) : (L < 16 ? L : 16);
-  // ~256 workgroups at least 4 slots deep: B = 128 -> 2 chunks, B = 64 -> 4, small test batches more
-  int nl = sat_cdiv(256, B);
+  // alone: ~256 workgroups at least 4 slots deep (B = 128 -> 2 chunks, B = 64 -> 4, small test batches more);
+  // beside the encoder (the decoder's split target: 64 with ResNet152 features, 128 with VGG19's): ~target
+  // workgroups but at most 128 slots each -- one workgroup per row at L = 49 (fewer resident waves for the conv
+  // kernels sharing the CUs: 6.69 -> 6.59 ms per overlapped step), two at L = 196 (10.90 vs 11.3 ms with one:
+  // profiles/r3_s17/)
+  int nl = sat_cdiv(wg_target > 0 ? wg_target : 256, B);
+  if (wg_target > 0) {
+    const int by_depth = sat_cdiv(L, 128);
+    if (nl < by_depth) nl = by_depth;
+  }
   const int by_l = sat_cdiv(L, 4);
   if (nl > by_l) nl = by_l;
   if (nl > 16) nl = 16;
   return nl < 1 ? 1 : nl;
 }
 
-size_t sat_attention_part_floats(int B, int L, int D, int E, int dtype) {
+size_t sat_attention_part_floats(int B, int L, int D, int E, int dtype, int wg_target) {
   const int VD = dtype == SAT_BF16 ? 8 : 4;
   const size_t two_launch = (size_t)B * sat_cdiv(D, 64 * VD) * L;
-  const size_t split = (size_t)B * sat_attention_bwd_chunks(B, L) * (2 * E + 1);
+  const size_t split = (size_t)B * sat_attention_bwd_chunks(B, L, wg_target) * (2 * E + 1);
   return two_launch > split ? two_launch : split;
 }
 

@@ -649,15 +649,15 @@ __global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restric
   sat_stamp_end(st, t0);
 }
 
-// ResNet152 layer3's c2 when half images alone would leave CUs idle (B <= 80 per GPU: 2B workgroups): each
-// half image as two 128-channel slices (4B workgroups), each streaming half the weights.  WM = 1: the 8
-// waves own 16 channels each and every m-block; WM = 2: 2 m-groups x 4 channel groups of 32.
-template <int WM, int PF>
+// ResNet152 layer3's c2 when half images alone would leave CUs idle (B <= 64 per GPU: 2B workgroups): each half image
+// as two 128-channel slices (4B workgroups), each streaming half the weights; the 8 waves own 16 channels each and
+// every m-block.  Measured and removed (profiles/r3_s13, r3_s14, r3_s16): two m-groups of waves, weights 3 / 4
+// k-tiles ahead, whole images as four 64-channel slices -- all within noise of this form.
 __global__ __launch_bounds__(512) void conv3x3_slice2_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                              const float* __restrict__ bias, bf16* __restrict__ y,
                                                              int nbands, SatStamps st) {
   const SatStampT0 t0 = sat_stamp_begin(st);
-  conv3x3_band_body<14, 7, 256, 2, WM, PF>(x, wf, bias, y, nbands);
+  conv3x3_band_body<14, 7, 256, 2, 1, 2>(x, wf, bias, y, nbands);
   sat_stamp_end(st, t0);
 }
 
@@ -784,17 +784,6 @@ __global__ __launch_bounds__(512) void conv1x1_frag_kernel(const bf16* __restric
   sat_stamp_end(st, t0);
 }
 
-// whole 14x14 images as NSL = 4 channel slices of 64 (N x 4 workgroups, each streaming a quarter of the weights for
-// 196 output pixels), WM m-groups of waves (SatPolicy::conv_slices 6: WM = 4, 7: WM = 2; experiments for B <= 64)
-template <int WM>
-__global__ __launch_bounds__(512) void conv3x3_img4_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
-                                                           const float* __restrict__ bias, bf16* __restrict__ y,
-                                                           int nbands, SatStamps st) {
-  const SatStampT0 t0 = sat_stamp_begin(st);
-  conv3x3_band_body<14, 14, 256, 4, WM, 2>(x, wf, bias, y, nbands);
-  sat_stamp_end(st, t0);
-}
-
 // the same with each half image as two 128-channel slices (B <= 80 per GPU, as conv3x3_slice2_kernel)
 __global__ __launch_bounds__(512) void conv1x1_frag2_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                             const float* __restrict__ bias, bf16* __restrict__ y,
@@ -829,13 +818,12 @@ __global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restric
   }
 }
 
-// Layer3 c1 / c2 launch form for a batch of N images: 1 = one workgroup per half image (2N workgroups), 2 - 5 = two
-// 128-channel slices per half image (4N; 3x3: 2 = one m-group of waves, 3 = two, 4 / 5 = one with the weights
-// prefetched 3 / 4 k-tiles ahead instead of 2; 6 / 7 (3x3) = whole images as four 64-channel slices).  SatPolicy::conv_slices forces
+// Layer3 c1 / c2 launch form for a batch of N images: 1 = one workgroup per half image (2N workgroups), 2 = two
+// 128-channel slices per half image (4N).  SatPolicy::conv_slices forces
 // one; automatic: slices when the half images fill at most half the chip's 256 CUs (B <= 64 per GPU).
 int sat_frag_slices(int N) {
   const int f = sat_policy().conv_slices;
-  if (f >= 1 && f <= 7) return f;
+  if (f == 1 || f == 2) return f;
   return 2 * N <= 128 ? 2 : 1;
 }
 
@@ -900,18 +888,8 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   const int groups = sat_cdiv(2 * N, 8) * 8 * 2;   // whole groups of 8 half images x 2 slices
   if (mode == 1)
     hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp, st);
-  else if (mode == 2)
-    hipLaunchKernelGGL((conv3x3_slice2_kernel<1, 2>), dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
-  else if (mode == 3)
-    hipLaunchKernelGGL((conv3x3_slice2_kernel<2, 2>), dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
-  else if (mode == 4)
-    hipLaunchKernelGGL((conv3x3_slice2_kernel<1, 3>), dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
-  else if (mode == 5)
-    hipLaunchKernelGGL((conv3x3_slice2_kernel<1, 4>), dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
-  else if (mode == 6)
-    hipLaunchKernelGGL((conv3x3_img4_kernel<4>), dim3(sat_cdiv(N, 8) * 8 * 4), dim3(512), 0, s, xp, wp, b, yp, N, st);
   else
-    hipLaunchKernelGGL((conv3x3_img4_kernel<2>), dim3(sat_cdiv(N, 8) * 8 * 4), dim3(512), 0, s, xp, wp, b, yp, N, st);
+    hipLaunchKernelGGL(conv3x3_slice2_kernel, dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
   return (int)hipGetLastError();
 }
 

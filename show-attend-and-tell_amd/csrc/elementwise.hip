@@ -510,17 +510,43 @@ __global__ __launch_bounds__(256) void argmax_kernel(const T* __restrict__ X, lo
 }
 
 // ---- Adam (torch.optim.Adam single-tensor algorithm) ------------------------
+// torch's single-tensor Adam arithmetic for one element (exp_avg.lerp_(grad, 1-beta1): the weight < 0.5
+// branch of at::lerp; exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1-beta2); addcdiv_ with the bias corrections)
+__device__ __forceinline__ void adam_elem(float& pi, float gi, float& mi, float& vi, float w1, float b2, float eps,
+                                          float step_size, float bc2_sqrt) {
+  mi = mi + w1 * (gi - mi);
+  vi = vi * b2 + (1.f - b2) * gi * gi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  pi = pi + (-step_size) * (mi / denom);
+}
+// 16-byte vectors of 4 elements where the range is 16-B aligned (the decoder's flat parameter groups are
+// 64-element aligned), the scalar form for the tail / unaligned ranges: the same per-element arithmetic
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, bf16* __restrict__ p_lp, long n, float b1, float b2, float eps,
                             float step_size, float bc2_sqrt) {
   const float w1 = 1.f - b1;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float gi = g[i], mi = m[i], vi = v[i];
-    // exp_avg.lerp_(grad, 1-beta1): weight < 0.5 branch of at::lerp
-    mi = mi + w1 * (gi - mi);
-    vi = vi * b2 + (1.f - b2) * gi * gi;
-    float denom = sqrtf(vi) / bc2_sqrt + eps;
-    float pi = p[i] + (-step_size) * (mi / denom);
+  const long stride = (long)gridDim.x * blockDim.x;
+  const bool vec = ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0) &&
+                   (((uintptr_t)p_lp & 7) == 0);
+  const long n4 = vec ? n >> 2 : 0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = ((float4*)p)[i], mm = ((float4*)m)[i], vv = ((float4*)v)[i];
+    const float4 gg = ((const float4*)g)[i];
+    adam_elem(pp.x, gg.x, mm.x, vv.x, w1, b2, eps, step_size, bc2_sqrt);
+    adam_elem(pp.y, gg.y, mm.y, vv.y, w1, b2, eps, step_size, bc2_sqrt);
+    adam_elem(pp.z, gg.z, mm.z, vv.z, w1, b2, eps, step_size, bc2_sqrt);
+    adam_elem(pp.w, gg.w, mm.w, vv.w, w1, b2, eps, step_size, bc2_sqrt);
+    ((float4*)p)[i] = pp; ((float4*)m)[i] = mm; ((float4*)v)[i] = vv;
+    if (p_lp) {
+      uint2 o;
+      bf16* ob = (bf16*)&o;
+      ob[0] = (bf16)pp.x; ob[1] = (bf16)pp.y; ob[2] = (bf16)pp.z; ob[3] = (bf16)pp.w;
+      ((uint2*)p_lp)[i] = o;
+    }
+  }
+  for (long i = (n4 << 2) + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    adam_elem(pi, g[i], mi, vi, w1, b2, eps, step_size, bc2_sqrt);
     m[i] = mi; v[i] = vi; p[i] = pi;
     if (p_lp) p_lp[i] = (bf16)pi;
   }
@@ -722,7 +748,7 @@ extern "C" int sat_adam_step(float* param, const float* grad, float* exp_avg, fl
                              float bias_correction2_sqrt, void* stream) {
   SAT_REQUIRE(param && grad && exp_avg && exp_avg_sq && n >= 0);
   if (n == 0) return 0;
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
                      exp_avg_sq, (bf16*)param_lp, (long)n, beta1, beta2, eps, step_size, bias_correction2_sqrt);
   return (int)hipGetLastError();
 }

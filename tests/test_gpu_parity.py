@@ -1069,11 +1069,11 @@ def test_bottleneck_fused_bit_identical(sat, N):
 
 
 @pytest.mark.parametrize("N,H,C,slices", [(1, 14, 256, 1), (2, 14, 256, 1), (5, 14, 256, 1), (16, 14, 256, 1),
-                                          (1, 14, 256, 2), (3, 14, 256, 2), (70, 14, 256, 2), (5, 14, 256, 3), (3, 14, 256, 4), (3, 14, 256, 5),
+                                          (1, 14, 256, 2), (3, 14, 256, 2), (70, 14, 256, 2),
                                           (8, 14, 256, 0), (1, 28, 128, 0), (3, 28, 128, 0)])
 def test_conv3x3_frag_bit_identical(sat, N, H, C, slices):
     """csrc/convblock.hip's half-image 3x3 kernel (a layer3 c2 left unfused: 14x14, 256 -> 256), its two-slice
-    form (SatPolicy.conv_slices 2 / 3: each half image as two 128-channel workgroups, the default at B <= 64;
+    form (SatPolicy.conv_slices 2: each half image as two 128-channel workgroups, the default at B <= 64;
     N = 70 leaves a partial group of 8 half images) and its 7-row band form (layer2 c2: 28x28, 128 -> 128) are
     bit-identical to the tile kernel on the same operands, and close to torch fp32."""
     from sat_amd import ops
@@ -1238,27 +1238,6 @@ def test_decoder_skinny_matches_tile_kernel(sat, tf):
     for n, g in g0.items():
         scale = g0["attention.v.weight"] if n == "attention.v.bias" else g
         assert ((g1[n] - g).norm() / scale.norm().clamp_min(1e-12)).item() < 3e-2, n
-
-
-@pytest.mark.parametrize("B", [8, 64])
-def test_attention_forward_slices_bit_identical(sat, B):
-    """attn_fwd_kernel with 512-column slices (twice the workgroups; the default when B x D / 1024 < 256) and with
-    1024-column slices (SatPolicy.attn_fwd 2 / 1): the same per-column sums, so the whole bf16 decoder forward is
-    bit-identical."""
-    Lf, D, V, T = 49, 2048, 500, 8
-    outs = []
-    for mode in (1, 2):
-        torch.manual_seed(0)
-        dec = sat.Decoder(V, D, tf=True, ado=True, attention=True).to(DEV).eval()
-        dec.policy = sat.Policy(attn_fwd=mode)
-        g = torch.Generator().manual_seed(2)
-        feats = torch.randn(B, Lf, D, generator=g).bfloat16().to(DEV)
-        caps = O.make_captions(B, T, V, 1).to(DEV)
-        with torch.no_grad():
-            preds, alphas = dec(feats, caps)
-        torch.cuda.synchronize()
-        outs.append((preds.float().cpu(), alphas.cpu()))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
 def test_decoder_transposed_weight_copies(sat):

@@ -3,7 +3,7 @@ copies (Decoder.transposed_weights) on the bench workload (L=49, D=2048, E=512, 
 one process: per configuration the per-step kernel groups (diagnostics.decoder_step_kernels, back to back) and the
 decoder fwd + loss + bwd time (events, split target 64 as in the overlapped bench).
 
-    CONFIGS="tr:h,c,g,dh[:attn_fwd:attn_bwd_chunks];..." B=128 python tools/bench_decoder_splits.py
+    CONFIGS="tr:h,c,g,dh[:attn_bwd_chunks];..." B=128 python tools/bench_decoder_splits.py
 """
 import os
 import statistics
@@ -24,9 +24,9 @@ dec.split_target = 64
 feats = torch.randn(B, L, D, device=dev).bfloat16()
 caps = synthetic_captions(B, T, V, generator=torch.Generator().manual_seed(1), device=dev)
 CONFIGS = []
-for c in os.environ.get("CONFIGS", "0:0,0,0,0;1:0,0,0,0;1:0,0,0,0:2:0;1:0,0,0,0:0:4;1:0,0,0,0:2:4").split(";"):
-    f = c.split(":") + ["0", "0"]
-    CONFIGS.append((int(f[0]), tuple(int(v) for v in f[1].split(",")), int(f[2]), int(f[3])))
+for c in os.environ.get("CONFIGS", "0:0,0,0,0;1:0,0,0,0;1:0,0,0,0:1;1:0,0,0,0:2").split(";"):
+    f = c.split(":") + ["0"]
+    CONFIGS.append((int(f[0]), tuple(int(v) for v in f[1].split(",")), int(f[2])))
 
 
 def step():
@@ -38,7 +38,7 @@ def step():
 def configure(cfg):
     dec.transposed_weights = bool(cfg[0])
     dec._lp_versions = None   # re-cast the shadow (and refresh the transposed copies when on)
-    dec.policy = sat_amd.Policy(decoder_splits=cfg[1], attn_fwd=cfg[2], attn_bwd_chunks=cfg[3])
+    dec.policy = sat_amd.Policy(decoder_splits=cfg[1], attn_bwd_chunks=cfg[2])
 
 
 times = {c: [] for c in CONFIGS}
@@ -59,5 +59,5 @@ for rnd in range(3):
             groups[cfg] = decoder_step_kernels(dec, feats, caps, reps=20)[0]
 for cfg in CONFIGS:
     g = groups[cfg]
-    print(f"transposed={cfg[0]} splits h,c,g,dh={cfg[1]} attn_fwd={cfg[2]} bwd_chunks={cfg[3]}: fwd+bwd {statistics.median(times[cfg]):.3f} ms; per step "
+    print(f"transposed={cfg[0]} splits h,c,g,dh={cfg[1]} bwd_chunks={cfg[2]}: fwd+bwd {statistics.median(times[cfg]):.3f} ms; per step "
           f"{sum(g.values()):.1f} us: " + " ".join(f"{k} {v:.2f}" for k, v in g.items()), flush=True)
