@@ -79,6 +79,12 @@ def parse():
     ap.add_argument("--policy", default="",
                     help="extra SatPolicy fields for every encoder / decoder call, e.g. attn_bwd_chunks=1,gemm_stages=3 "
                          "or decoder_splits=2.0.0.0 (A/B; include/sat_hip.h)")
+    ap.add_argument("--c2-frag-sizes", default="7,14,28",
+                    help="spatial sizes whose stride-1 3x3 convs run on the staged-input kernels (sat_conv3x3_frag); "
+                         "the others on the tile kernel (A/B)")
+    ap.add_argument("--fuse-layer2", action="store_true",
+                    help="layer2's identity bottlenecks as one fused band-kernel launch each instead of three conv "
+                         "launches (A/B: profiles/r3_s22)")
     ap.add_argument("--fuse-every", type=int, default=None,
                     help="fuse every n-th layer3 identity bottleneck only, the rest run as three conv launches "
                          "(default 0 = none: with the layer3 c2 / c3 on the half-image frag kernels the unfused "
@@ -200,7 +206,7 @@ class DecoderStamps:
         return out
 
 
-def conv_launches(network, B, H=224, fused=True):
+def conv_launches(network, B, H=224, fused=True, fused2=False):
     """Every conv launch of one encoder forward, in launch order (encoder.py forward: per
     bottleneck c1, c2, downsample, c3, or ONE fused launch for the identity blocks the fused
     bottleneck kernel runs), with its algorithmic work: FLOPs = 2*M*N*K (real Cin=3 for the first
@@ -233,6 +239,9 @@ def conv_launches(network, B, H=224, fused=True):
                 oh = h // s
                 if fused and bi > 0 and (h, cin, pl) == (14, 1024, 256) \
                         and (fused is True or (bi - 1) % int(fused) == 0):   # sat_bottleneck_fused_supported
+                    add_block(f"L{li + 1}block(fused)", B * h * h, cin, pl)
+                    continue
+                if fused2 and bi > 0 and (h, cin, pl) == (28, 512, 128):   # layer2's band form
                     add_block(f"L{li + 1}block(fused)", B * h * h, cin, pl)
                     continue
                 add(f"L{li + 1}c1", B * h * h, pl, cin, B * h * h * cin)
@@ -582,6 +591,8 @@ def main():
         args.fuse_every = 0   # profiles/r2_s62: none fused 6.79 ms, every 3rd 7.15, every block 7.48
     if args.split_target is None:
         args.split_target = 128 if args.network == "vgg19" else 64
+    enc.fuse_layer2 = args.fuse_layer2
+    enc.c2_frag_sizes = tuple(int(v) for v in args.c2_frag_sizes.split(",") if v)
     enc.fuse_blocks = (False if args.no_fuse_blocks or args.fuse_every == 0 else
                        (True if args.fuse_every == 1 else args.fuse_every))
     enc.policy = policy
@@ -657,7 +668,7 @@ def main():
                         feats_static.append(enc(mid, steps=(split, n_plan)))
             else:
                 if stamp_enc:   # every conv launch of this graph writes its in-kernel timestamps
-                    stamps_enc.append(LaunchStamps(len(conv_launches(args.network, B, fused=enc.fuse_blocks)), dev,
+                    stamps_enc.append(LaunchStamps(len(conv_launches(args.network, B, fused=enc.fuse_blocks, fused2=enc.fuse_layer2)), dev,
                                                    base=policy))
                     enc.launch_policy = stamps_enc[-1].next_policy
                 with torch.cuda.graph(g_enc[k]):
@@ -780,7 +791,7 @@ def main():
         t = torch.tensor([elapsed], device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    launches = conv_launches(args.network, B, fused=enc.fuse_blocks)
+    launches = conv_launches(args.network, B, fused=enc.fuse_blocks, fused2=enc.fuse_layer2)
     enc_ms = sum(s.elapsed_time(e) for s, e in enc_events) if use_graph else None
     diag_phase = None
     if (stamps_enc or stamps_dec) and not args.no_diagnostics:

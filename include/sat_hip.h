@@ -78,7 +78,8 @@ typedef struct {
   int stamp_capacity;
   int conv_slices;      /* layer3 c1 / c2 half-image kernels (sat_conv1x1_frag, sat_conv3x3_frag at 14x14): 0 auto
                          * (channel slices when B <= 64), 1 one workgroup per half image, 2 two 128-channel slices
-                         * per half image */
+                         * per half image; sat_conv3x3_frag at 7x7: 0 auto (two images per workgroup when B > 64),
+                         * 1 two images, 2 one image per workgroup */
 } SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),
@@ -173,12 +174,12 @@ int sat_bottleneck_fused_supported(int H, int W, int Cin, int Cmid, int dtype);
 int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int dtype, const void* x, const void* w1f,
                          const float* b1, const void* w2f, const float* b2, const void* w3f, const float* b3,
                          void* y, const SatPolicy* policy, void* stream);
-/* 1 if sat_conv3x3_frag runs this geometry (today: bf16, 14x14, C 256 -- the c2 of ResNet152's layer3
- * identity blocks), else 0. */
+/* 1 if sat_conv3x3_frag runs this geometry (bf16: 14x14 C 256, 28x28 C 128, 7x7 C 512 -- the c2 of ResNet152's
+ * layer3 / layer2 / layer4 identity blocks), else 0. */
 int sat_conv3x3_frag_supported(int H, int W, int C, int dtype);
 /* 3x3 / stride 1 / pad 1 conv C -> C + folded bias + ReLU (a bottleneck's c2, encoder.py:13-17 through
- * torchvision), one workgroup per half image with its input rows staged once in LDS and the weights
- * streamed register-direct.  x, y NHWC [N,H,W,C] (x != y); wf: sat_mfma_frag_layout of the folded
+ * torchvision), one workgroup per half image (14x14), 7-row band (28x28) or one / two whole images x a
+ * 128-channel slice (7x7) with its input rows staged once in LDS and the weights streamed register-direct.  x, y NHWC [N,H,W,C] (x != y); wf: sat_mfma_frag_layout of the folded
  * [C][3*3*C] (tap-major) weight; b: fp32 bias.  Bit-identical to sat_conv2d_nhwc on the same operands. */
 int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const void* x, const void* wf, const float* b, void* y,
                      const SatPolicy* policy, void* stream);

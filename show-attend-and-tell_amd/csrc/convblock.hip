@@ -70,14 +70,14 @@ __device__ __forceinline__ void k_wait_barrier() {
 }
 __device__ __forceinline__ void k_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// vmem instructions one wave issues after its input DMAs A(T) (2 instructions) and before the wait
+// vmem instructions one wave issues after its input DMAs A(T) (na instructions) and before the wait
 // of c1 k-tile T: the issue order is A0 B0 A1 B1 B2 .. B(PF-1) (B = nb weight loads), then per k-tile
 // it, after its wait: A(it+2) (it+2 < KT1), B(it+PF) (it+PF < NT, when weights stream)
-constexpr int younger_than_a(int T, int KT1, int NT, int PF, bool stream, int nb = 4) {
+constexpr int younger_than_a(int T, int KT1, int NT, int PF, bool stream, int nb = 4, int na = 2) {
   int n = 0;
   bool after = false;
   auto ev_a = [&](int idx) {
-    if (after) n += 2;
+    if (after) n += na;
     if (idx == T) after = true;
   };
   auto ev_b = [&]() {
@@ -409,6 +409,217 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
   sat_stamp_end(a.st, t0);
 }
 
+// The fused block for ResNet152's layer2 identity bottlenecks (28 x 28, 512 -> 128 -> 128 -> 512): one
+// workgroup per band of RO = 7 output rows (four per image, 512 for B = 128), 8 waves.  Three launches
+// move each block's two 12.8 MB intermediates through HBM and stream ~98 us at B = 128; here they stay
+// in LDS:
+//   * c1 (1x1, 512 -> 128) runs over the band's 9 slot rows (image rows y0 - 1 .. y0 + 7; slots outside
+//     the image read zeros through the DMA's out-of-range path and are never read back), its input
+//     through a 3-stage LDS-DMA ring of 256-row x 64-channel slabs (4 DMAs per wave per k-tile), its
+//     bf16 output to X1 (two 64-channel planes of 253 rows: 252 slot pixels + the zero row);
+//   * c2 (3x3, 128 -> 128) reads X1 with the band kernel's per-lane tap shifts (taps in the padding read
+//     the zero row) and writes X2 (208 rows, aliasing the dead ring);
+//   * c3 (1x1, 128 -> 512) in four 128-channel chunks reads X2, adds bias + the residual (the block's own
+//     input rows) in fp32, applies ReLU, rounds once and stores.
+// Every wave owns one 16-channel n-block per phase (per chunk in c3) and every m-block; weights stream
+// register-direct from the fragment layout two k-tiles ahead across phase boundaries (544 KB per
+// workgroup for 196 outputs).  LDS: 64,768 B (X1) + 98,304 B (ring / X2) = 163,072 of 163,840.
+// Each conv sums K in the unfused kernels' order: bit-identical to the three launches.
+template <int IW, int RO, int CIN, int CMID, int PF>
+__device__ __forceinline__ void block_band_body(const KArgs& a) {
+  constexpr int IH = IW, NPART = IH / RO, PO = RO * IW;
+  constexpr int SLOTS = RO + 2, P1 = SLOTS * IW;           // c1 pixels (slot rows) = 252
+  constexpr int MB1 = (P1 + 15) / 16, MB2 = (PO + 15) / 16;   // 16, 13
+  constexpr int ROWB = 128, NPL = CMID / 64;
+  constexpr int X1PL = (P1 + 1) * ROWB, X2PL = MB2 * 16 * ROWB;
+  constexpr int STG = MB1 * 16 * ROWB, NA = MB1 * 16 / 64;   // ring stage bytes; DMAs per wave per k-tile
+  constexpr int X1 = 0, RING = NPL * X1PL, X2 = RING;
+  constexpr int LDS = RING + 3 * STG;
+  static_assert(IH % RO == 0 && CMID == 128 && CIN % 128 == 0 && MB1 * 16 == 8 * 8 * NA, "band shapes");
+  static_assert(NPL * X2PL <= 3 * STG && LDS <= 163840, "LDS budget");
+  constexpr int KT1 = CIN / 64, KT2 = 9 * CMID / 64, NCK = CIN / 128, KT3C = CMID / 64;
+  constexpr int NT = KT1 + KT2 + NCK * KT3C;
+  constexpr int KS1 = CIN / 32, KS2 = 9 * CMID / 32, KS3 = CMID / 32;
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fh = lane >> 4;
+  const int img = blockIdx.x / NPART, part = blockIdx.x % NPART;
+  const int y0 = part * RO;
+  const int s_lo = y0 == 0 ? 1 : 0, s_hi = y0 + RO == IH ? RO : RO + 1;   // slots inside the image
+  const long pix_img = (long)img * IH * IW;
+
+  // ---- c1 input ring: k-tile t = channels 64t .. 64t+63 of LDS row r = slot pixel r (slot r / IW) ----
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, (int)a.x_bytes, 0x00020000);
+  unsigned dsrc[NA];
+#pragma unroll
+  for (int u = 0; u < NA; ++u) {
+    const int d = w * NA + u, r = d * 8 + (lane >> 3), c = (lane & 7) ^ (lane >> 3), s = r / IW;
+    const bool ok = r < P1 && s >= s_lo && s <= s_hi;
+    dsrc[u] = ok ? (unsigned)(((pix_img + (long)(y0 - 1) * IW + r) * CIN + 8 * c) * 2) : K_OOB;
+  }
+  auto dma_a = [&](int t) {
+    char* st = smem + RING + (t % 3) * STG;
+#pragma unroll
+    for (int u = 0; u < NA; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (k_lds_void*)(st + (w * NA + u) * 1024), 16,
+                                               dsrc[u] == K_OOB ? (int)K_OOB : (int)(dsrc[u] + t * 128), 0, 0, 0);
+  };
+
+  // ---- weight fragments of k-tile T: this wave's n-block of the phase (c3: of chunk ck), both 32-k halves ----
+  bf16x8 bq[PF + 1][2];
+  auto load_b = [&](int T, bf16x8 (&dst)[2]) {
+    const bf16* base;
+    int nb, ks0, KS;
+    if (T < KT1) { base = a.w1; nb = w; ks0 = 2 * T; KS = KS1; }
+    else if (T < KT1 + KT2) { base = a.w2; nb = w; ks0 = 2 * (T - KT1); KS = KS2; }
+    else { const int t = T - KT1 - KT2; base = a.w3; nb = (t / KT3C) * 8 + w; ks0 = 2 * (t % KT3C); KS = KS3; }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) dst[ks] = *(const bf16x8*)(base + ((long)(nb * KS + ks0 + ks) * 64 + lane) * 8);
+  };
+
+  int offu[2];   // unshifted rows (ring, X2): row i*16 + fr at i * 16 * ROWB + offu
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) offu[ks] = fr * ROWB + 16 * ((ks * 4 + fh) ^ (fr & 7));
+  int offs[MB2][2];   // c2: output pixel p = i*16 + fr under tap (dh, dw) reads X1 slot row py + 1 + dh
+  auto tap_offsets = [&](int tap) {
+    const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+#pragma unroll
+    for (int i = 0; i < MB2; ++i) {
+      const int p = i * 16 + fr, py = p / IW, pxx = p - py * IW;
+      const bool ok = p < PO && (unsigned)(y0 + py + dh) < (unsigned)IH && (unsigned)(pxx + dw) < (unsigned)IW;
+      const int q = ok ? (py + 1 + dh) * IW + pxx + dw : P1;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) offs[i][ks] = q * ROWB + 16 * ((ks * 4 + fh) ^ (q & 7));
+    }
+  };
+
+  f32x4 acc[MB1];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < MB1; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  // one 64-deep k-tile over MB m-blocks, one 32-deep half at a time (MB fragments live at once)
+  auto tile_u = [&](auto MBc, const char* base, const bf16x8 (&b)[2]) {
+    constexpr int MB = decltype(MBc)::value;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[MB];
+#pragma unroll
+      for (int i = 0; i < MB; ++i) af[i] = *(const bf16x8*)(base + i * 16 * ROWB + offu[ks]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MB; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks], af[i], acc[i], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+  auto tile_s = [&](const char* base, const bf16x8 (&b)[2]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[MB2];
+#pragma unroll
+      for (int i = 0; i < MB2; ++i) af[i] = *(const bf16x8*)(base + offs[i][ks]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MB2; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks], af[i], acc[i], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+  // epilogue into an LDS plane image: the lane holds channels 16w + 4fh .. +3 of row i*16 + fr
+  auto store_planes = [&](auto MBc, int region, int plane_bytes, int rows, const float4& bv) {
+    constexpr int MB = decltype(MBc)::value;
+    const int plane = w >> 2, c = (w & 3) * 2 + (fh >> 1);
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int r = i * 16 + fr;
+      u32x2 o;
+      bf16* ob = (bf16*)&o;
+      ob[0] = (bf16)fmaxf(acc[i][0] + bv.x, 0.f);
+      ob[1] = (bf16)fmaxf(acc[i][1] + bv.y, 0.f);
+      ob[2] = (bf16)fmaxf(acc[i][2] + bv.z, 0.f);
+      ob[3] = (bf16)fmaxf(acc[i][3] + bv.w, 0.f);
+      if (r < rows) *(u32x2*)(smem + region + plane * plane_bytes + r * ROWB + 16 * (c ^ (r & 7)) + 8 * (fh & 1)) = o;
+    }
+  };
+
+  // ---- prologue: biases (older than every DMA), A0 B0 A1 B1 .. B(PF-1) ----
+  const float4 bias1 = *(const float4*)(a.b1 + w * 16 + 4 * fh);
+  const float4 bias2 = *(const float4*)(a.b2 + w * 16 + 4 * fh);
+  float4 bias3;
+  if (tid < 8) *(uint4*)(smem + X1 + (tid >> 2) * X1PL + P1 * ROWB + (tid & 3) * 32) = make_uint4(0, 0, 0, 0);
+  if (tid < 8) *(uint4*)(smem + X1 + (tid >> 2) * X1PL + P1 * ROWB + (tid & 3) * 32 + 16) = make_uint4(0, 0, 0, 0);
+  dma_a(0);
+  load_b(0, bq[0]);
+  dma_a(1);
+  load_b(1, bq[1]);
+  static_for<PF - 2>([&](auto e) { load_b(2 + decltype(e)::value, bq[2 + decltype(e)::value]); });
+  zero_acc();
+  u32x2 resv[MB2];
+
+  static_for<NT>([&](auto Tc) {
+    constexpr int T = decltype(Tc)::value;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (T < KT1) {
+      // this wave's DMAs of tile T have landed (every wave's after the barrier, which also retires every
+      // wave's reads of stage (T + 2) % 3 before it is refilled)
+      k_wait_barrier<younger_than_a(T, KT1, NT, PF, true, 2, NA)>();
+      if constexpr (T + 2 < KT1) dma_a(T + 2);
+    }
+    if constexpr (T + PF < NT) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
+    const bf16x8 (&b)[2] = bq[T % (PF + 1)];
+    if constexpr (T < KT1) {
+      tile_u(std::integral_constant<int, MB1>{}, smem + RING + (T % 3) * STG, b);
+      if constexpr (T == KT1 - 1) {   // c1 epilogue -> X1 (slot pixels 0 .. P1 - 1)
+        store_planes(std::integral_constant<int, MB1>{}, X1, X1PL, P1, bias1);
+        zero_acc();
+        k_lds_barrier();
+      }
+    } else if constexpr (T < KT1 + KT2) {
+      constexpr int t = T - KT1, pl = t % NPL;
+      if constexpr (pl == 0) tap_offsets(t / NPL);
+      tile_s(smem + X1 + pl * X1PL, b);
+      if constexpr (t == KT2 - 1) {   // c2 epilogue -> X2 (the ring is dead: every wave passed c1's barrier)
+        store_planes(std::integral_constant<int, MB2>{}, X2, X2PL, MB2 * 16, bias2);
+        zero_acc();
+        k_lds_barrier();
+      }
+    } else {
+      constexpr int t = T - KT1 - KT2, ck = t / KT3C, kt = t % KT3C;
+      const int ch = ck * 128 + w * 16 + 4 * fh;
+      if constexpr (kt == 0) {   // residual rows + bias of this chunk, for its epilogue
+        bias3 = *(const float4*)(a.b3 + ch);
+#pragma unroll
+        for (int i = 0; i < MB2; ++i) {   // rows past PO load a valid row (never stored): no branch
+          const int p = min(i * 16 + fr, PO - 1);
+          resv[i] = *(const u32x2*)(a.x + (pix_img + (long)y0 * IW + p) * CIN + ch);
+        }
+      }
+      tile_u(std::integral_constant<int, MB2>{}, smem + X2 + kt * X2PL, b);
+      if constexpr (kt == KT3C - 1) {   // c3 epilogue: bias, fp32 residual add, ReLU, one rounding
+#pragma unroll
+        for (int i = 0; i < MB2; ++i) {
+          const int p = i * 16 + fr;
+          const bf16* rh = (const bf16*)&resv[i];
+          const float v[4] = {acc[i][0] + bias3.x, acc[i][1] + bias3.y, acc[i][2] + bias3.z, acc[i][3] + bias3.w};
+          u32x2 o;
+          bf16* ob = (bf16*)&o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ob[e] = (bf16)fmaxf(v[e] + (float)rh[e], 0.f);
+          if (p < PO) *(u32x2*)(a.y + (pix_img + (long)y0 * IW + p) * CIN + ch) = o;
+        }
+        zero_acc();
+      }
+    }
+  });
+}
+
+__global__ __launch_bounds__(512) void block_band_kernel(KArgs a) {
+  const SatStampT0 t0 = sat_stamp_begin(a.st);
+  block_band_body<28, 7, 512, 128, 2>(a);
+  sat_stamp_end(a.st, t0);
+}
+
 // The bottleneck's c2 phase as a conv of its own (the layer3 blocks the trunk leaves unfused, so the
 // decoder running beside the encoder finds CUs between launches): y = relu(conv3x3(x) + b) for
 // x, y [N][IW][IW][C].  The 256 x 128 tile kernel (convpipe.hip) runs this shape as 196 tiles on 256
@@ -649,6 +860,124 @@ __global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restric
   sat_stamp_end(st, t0);
 }
 
+// The same idea for images small enough to stage whole (ResNet152 layer4's stride-1 c2: 7 x 7, 512 -> 512): a
+// workgroup takes G consecutive images (G * 49 pixels, their rows contiguous in memory and in LDS, plus the zero
+// row) and one of NSL output-channel slices; taps outside an image read the zero row.  The tile kernel runs this
+// shape as 98 tiles of 256 x 128 on 256 CUs (each fetching a 2.4 MB im2col A tile and a 1.2 MB weight panel);
+// here G = 2, NSL = 4 gives 256 workgroups that each stage 100 KB of input once and stream a 1.18 MB weight
+// slice for 98 x 128 outputs.  G = 1 at B <= 64 per GPU.  Same k order, bias, ReLU and rounding: bit-identical.
+template <int IW, int C, int G, int NSL, int PF>
+__device__ __forceinline__ void conv3x3_img_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                 const float* __restrict__ bias, bf16* __restrict__ y, int nimg) {
+  constexpr int IH = IW, PI = IH * IW, P = G * PI, MB = (P + 15) / 16, ZR = P;
+  constexpr int ROWB = 128, XPL = (P + 1) * ROWB, NPL = C / 64, NJ = C / (16 * 8 * NSL), CS = C / NSL;
+  constexpr int NT = 9 * C / 64, KS = 9 * C / 32, CPP = C / 8;
+  constexpr int PER_T = (P * CPP + 511) / 512;
+  static_assert(NJ >= 1 && C % (128 * NSL) == 0 && NPL * XPL <= 163840, "16-channel n-blocks per wave, LDS");
+  __shared__ __attribute__((aligned(16))) char smem[NPL * XPL];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fh = lane >> 4;
+  // slice-major over groups of 8 consecutive workgroups (one per XCD under round-robin placement): the NSL
+  // slices of one image group land on one XCD and share its input rows in L2
+  const int slice = NSL == 1 ? 0 : (int)((blockIdx.x >> 3) % NSL);
+  const int grp = NSL == 1 ? (int)blockIdx.x : (int)((blockIdx.x / (8 * NSL)) * 8 + (blockIdx.x & 7));
+  const int ngrp = (nimg + G - 1) / G;
+  if (grp >= ngrp) return;   // the grid rounds the groups up to whole groups of 8
+  const int img0 = grp * G, nv = min(G, nimg - img0) * PI;   // valid pixels of this group
+  const int cb = slice * CS;
+  const unsigned lane_b = (unsigned)lane * 16;
+
+  uint4 xin[PER_T];
+  const uint4* xs = (const uint4*)(x + (long)img0 * PI * C);
+#pragma unroll
+  for (int u = 0; u < PER_T; ++u) xin[u] = xs[min(u * 512 + tid, nv * CPP - 1)];
+  float4 bv[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) bv[j] = *(const float4*)(bias + cb + (w * NJ + j) * 16 + 4 * fh);
+  bf16x8 bq[PF + 1][2][NJ];
+  auto load_b = [&](int T, bf16x8 (&dst)[2][NJ]) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        dst[ks][j] = *(const bf16x8*)((const char*)wf + (size_t)((cb / 16 + w * NJ + j) * KS + 2 * T + ks) * 1024 + lane_b);
+  };
+  static_for<PF>([&](auto e) { load_b(decltype(e)::value, bq[decltype(e)::value]); });
+#pragma unroll
+  for (int u = 0; u < PER_T; ++u) {
+    const int q = u * 512 + tid, r = q / CPP, c = q % CPP;
+    if (q < P * CPP) *(uint4*)(smem + (c >> 3) * XPL + r * ROWB + 16 * ((c & 7) ^ (r & 7))) = xin[u];
+  }
+  if (tid < NPL * 8) *(uint4*)(smem + (tid >> 3) * XPL + ZR * ROWB + (tid & 7) * 16) = make_uint4(0, 0, 0, 0);
+  k_lds_barrier();
+
+  int offs[MB][2];
+  auto tap_offsets = [&](int tap) {
+    const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int p = i * 16 + fr, g = p / PI, qq = p - g * PI, py = qq / IW, pxx = qq - py * IW;
+      const bool ok = p < P && (unsigned)(py + dh) < (unsigned)IH && (unsigned)(pxx + dw) < (unsigned)IW;
+      const int q = ok ? p + dh * IW + dw : ZR;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) offs[i][ks] = q * ROWB + 16 * ((ks * 4 + fh) ^ (q & 7));
+    }
+  };
+  f32x4 acc[MB][NJ];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  static_for<NT>([&](auto Tc) {
+    constexpr int T = decltype(Tc)::value, pl = T % NPL;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (T + PF < NT) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
+    if constexpr (pl == 0) tap_offsets(T / NPL);
+    const bf16x8 (&b)[2][NJ] = bq[T % (PF + 1)];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[MB];
+#pragma unroll
+      for (int i = 0; i < MB; ++i) af[i] = *(const bf16x8*)(smem + pl * XPL + offs[i][ks]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  });
+
+  char* y_s = (char*)(y + (long)img0 * PI * C + cb + w * NJ * 16);
+  const unsigned row_b = (unsigned)(fr * C + 4 * fh) * 2;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int p = i * 16 + fr;
+      u32x2 o;
+      bf16* ob = (bf16*)&o;
+      ob[0] = (bf16)fmaxf(acc[i][j][0] + bv[j].x, 0.f);
+      ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
+      ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
+      ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
+      if (p < nv) *(u32x2*)(y_s + (size_t)(i * 16 * C + j * 16) * 2 + row_b) = o;
+    }
+  }
+}
+
+template <int G>
+__global__ __launch_bounds__(512) void conv3x3_img_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                          const float* __restrict__ bias, bf16* __restrict__ y,
+                                                          int nimg, SatStamps st) {
+  const SatStampT0 t0 = sat_stamp_begin(st);
+  conv3x3_img_body<7, 512, G, 4, 2>(x, wf, bias, y, nimg);
+  sat_stamp_end(st, t0);
+}
+
 // ResNet152 layer3's c2 when half images alone would leave CUs idle (B <= 64 per GPU: 2B workgroups): each half image
 // as two 128-channel slices (4B workgroups), each streaming half the weights; the 8 waves own 16 channels each and
 // every m-block.  Measured and removed (profiles/r3_s13, r3_s14, r3_s16): two m-groups of waves, weights 3 / 4
@@ -839,7 +1168,8 @@ extern "C" int sat_mfma_frag_layout(int N, int K, const void* src, void* dst, vo
 }
 
 extern "C" int sat_bottleneck_fused_supported(int H, int W, int Cin, int Cmid, int dtype) {
-  return dtype == SAT_BF16 && H == 14 && W == 14 && Cin == 1024 && Cmid == 256;
+  return dtype == SAT_BF16 && ((H == 14 && W == 14 && Cin == 1024 && Cmid == 256) ||
+                               (H == 28 && W == 28 && Cin == 512 && Cmid == 128));
 }
 
 extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int dtype, const void* x, const void* w1f,
@@ -859,12 +1189,16 @@ extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int 
   a.b1 = b1; a.b2 = b2; a.b3 = b3;
   a.x_bytes = (unsigned)x_bytes;
   a.st = sat_launch_stamps();
-  hipLaunchKernelGGL((bottleneck_kernel<2, 0>), dim3(2 * N), dim3(512), 0, (hipStream_t)stream, a);
+  if (H == 28)   // layer2: 7-row bands, four workgroups per image
+    hipLaunchKernelGGL(block_band_kernel, dim3(4 * N), dim3(512), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL((bottleneck_kernel<2, 0>), dim3(2 * N), dim3(512), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 
 extern "C" int sat_conv3x3_frag_supported(int H, int W, int C, int dtype) {
-  return dtype == SAT_BF16 && ((H == 14 && W == 14 && C == 256) || (H == 28 && W == 28 && C == 128));
+  return dtype == SAT_BF16 && ((H == 14 && W == 14 && C == 256) || (H == 28 && W == 28 && C == 128) ||
+                               (H == 7 && W == 7 && C == 512));
 }
 
 extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const void* x, const void* wf, const float* b,
@@ -878,6 +1212,15 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   const hipStream_t s = (hipStream_t)stream;
   const bf16 *xp = (const bf16*)x, *wp = (const bf16*)wf;
   bf16* yp = (bf16*)y;
+  if (H == 7) {   // layer4 c2: whole images, two per workgroup (one at B <= 64), four 128-channel slices
+    const int G = (sat_policy().conv_slices == 1 || (sat_policy().conv_slices != 2 && N > 64)) ? 2 : 1;
+    const int groups = sat_cdiv(sat_cdiv(N, G), 8) * 8 * 4;
+    if (G == 2)
+      hipLaunchKernelGGL(conv3x3_img_kernel<2>, dim3(groups), dim3(512), 0, s, xp, wp, b, yp, N, st);
+    else
+      hipLaunchKernelGGL(conv3x3_img_kernel<1>, dim3(groups), dim3(512), 0, s, xp, wp, b, yp, N, st);
+    return (int)hipGetLastError();
+  }
   if (H == 28) {   // layer2 c2: 7-row bands, four workgroups per image
     hipLaunchKernelGGL(conv3x3_band_kernel<2>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp, 4 * N, st);
     return (int)hipGetLastError();

@@ -153,10 +153,17 @@ class Encoder(nn.Module):
         # an int n fuses every n-th eligible block only (the unfused ones leave CUs to a decoder
         # running beside the encoder: bench.py --fuse-every)
         self.fuse_blocks = True
+        # layer2's identity bottlenecks (28 x 28, 512 -> 128) as ONE launch each (the band form of
+        # sat_bottleneck_fused); independent of fuse_blocks, which governs the 14 x 14 layer3 blocks.  Off: at
+        # B = 128 the fused band kernel is no faster than the three launches (112 vs 106 us; B = 64: 51 vs 60)
+        # and its 159 KB of LDS per CU slow the overlapped train step (profiles/r3_s22)
+        self.fuse_layer2 = False
         # the c2 of an identity block left unfused runs on the half-image conv kernel
         # (sat_conv3x3_frag: input rows staged once in LDS, fragment-layout weights); False = the
         # tile kernel (A/B, tests)
         self.c2_frag = True
+        # ... at these spatial sizes (layer4 7, layer3 14, layer2 28); A/B: bench.py --c2-frag-sizes
+        self.c2_frag_sizes = (7, 14, 28)
         # ... its c1 on the half-image 1x1 kernel (sat_conv1x1_frag: input slabs by LDS-DMA, weights
         # register-direct)
         self.c1_frag = True
@@ -317,11 +324,17 @@ class Encoder(nn.Module):
             y = ops.nchw_to_nhwc(x, IN_PAD, dtype)
         return self._run_plan(y, plan, stop)
 
+    @staticmethod
+    def _block_cin(step):
+        return step[1][0].shape[3]   # c1's folded weight [Cout, 1, 1, Cin]
+
     def _fuse_this(self, plan, step):
+        if self._block_cin(step) == 512:
+            return bool(self.fuse_layer2)
         f = self.fuse_blocks
         if f is True or f is False:
             return f
-        elig = [s for s in plan if s[0] == "block" and s[5] is not None]
+        elig = [s for s in plan if s[0] == "block" and s[5] is not None and self._block_cin(s) != 512]
         return next(i for i, s in enumerate(elig) if s is step) % int(f) == 0
 
     def _run_plan(self, y, plan, stop):
@@ -340,7 +353,7 @@ class Encoder(nn.Module):
         if step[0] == "pool":
             return ops.maxpool2d_nhwc(y, step[1], step[2], step[3])
         _, c1, c2, c3, ds, fused, c2f = step
-        if (fused is not None and self.fuse_blocks is not False and self._fuse_this(self._plan, step)
+        if (fused is not None and self._fuse_this(self._plan, step)
                 and ops.bottleneck_fused_supported(y.shape[1], y.shape[2], y.shape[3], c1[0].shape[0], y.dtype)):
             return self._launch(("fused", y, fused), ops.bottleneck_fused, y, *fused)
         if fused is not None and self.c1_frag and ops.conv1x1_frag_supported(y.shape[1], y.shape[2], y.shape[3],
@@ -348,7 +361,8 @@ class Encoder(nn.Module):
             out = self._frag_conv("c1frag", ops.conv1x1_frag, y, fused[0])
         else:
             out = self._conv(y, c1, True)
-        if c2f is not None and self.c2_frag and ops.conv3x3_frag_supported(out.shape[1], out.shape[2], out.shape[3],
+        if c2f is not None and self.c2_frag and out.shape[1] in self.c2_frag_sizes \
+                and ops.conv3x3_frag_supported(out.shape[1], out.shape[2], out.shape[3],
                                                                          out.dtype):
             out = self._frag_conv("c2frag", ops.conv3x3_frag, out, c2f)
         else:

@@ -34,16 +34,25 @@ def test_no_tf_mode(monkeypatch):
     assert a.no_tf and a.vocab == 10000 and a.seq == 27
 
 
-@pytest.mark.parametrize("network,fused,n", [("resnet152", False, 155), ("resnet152", True, 155 - 2 * 35),
-                                             ("vgg19", True, 16)])
-def test_conv_launch_inventory(network, fused, n):
-    launches = bench.conv_launches(network, 1, fused=fused)
+@pytest.mark.parametrize("network,fused,fused2,n", [("resnet152", False, False, 155),
+                                                    ("resnet152", True, False, 155 - 2 * 35),
+                                                    ("resnet152", False, True, 155 - 2 * 7),
+                                                    ("resnet152", True, True, 155 - 2 * 42),
+                                                    ("vgg19", True, True, 16)])
+def test_conv_launch_inventory(network, fused, fused2, n):
+    launches = bench.conv_launches(network, 1, fused=fused, fused2=fused2)
     assert len(launches) == n
     blocks = [l for l in launches if l.get("fused")]
-    assert len(blocks) == (35 if fused and network == "resnet152" else 0)
-    if blocks:   # one layer3 block = c1 + c2 + c3 of the unfused inventory
-        un = {l["cls"].split()[0]: l["flops"] for l in bench.conv_launches(network, 1, fused=False)}
-        assert abs(blocks[0]["flops"] - (un["L3c1"] + un["L3c2"] + un["L3c3+res"])) < 1
+    nb3, nb2 = (35 if fused else 0), (7 if fused2 else 0)
+    assert len(blocks) == (nb3 + nb2 if network == "resnet152" else 0)
+    un = {l["cls"].split()[0]: l["flops"] for l in bench.conv_launches(network, 1, fused=False, fused2=False)}
+    if network != "resnet152":
+        return
+    for li, nb in ((2, nb2), (3, nb3)):   # one fused block = c1 + c2 + c3 of the unfused inventory
+        mine = [b for b in blocks if b["cls"].startswith(f"L{li}block")]
+        assert len(mine) == nb
+        if mine:
+            assert abs(mine[0]["flops"] - (un[f"L{li}c1"] + un[f"L{li}c2"] + un[f"L{li}c3+res"])) < 1
 
 
 def test_bert_synthetic_captions_layout():

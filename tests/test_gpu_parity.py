@@ -1034,23 +1034,25 @@ def test_mfma_frag_layout_exact(sat):
     assert torch.equal(ops.mfma_frag_layout(w.to(DEV)).cpu(), ref)
 
 
-def _bottleneck_operands(N, seed):
+def _bottleneck_operands(N, seed, H=14, C=1024, M=256):
     g = torch.Generator().manual_seed(seed)
-    x = torch.randn(N, 14, 14, 1024, generator=g).relu().bfloat16()   # a block input is post-ReLU
+    x = torch.randn(N, H, H, C, generator=g).relu().bfloat16()   # a block input is post-ReLU
 
     def conv(cout, cin, k):
         w = (torch.randn(cout, k, k, cin, generator=g) * math.sqrt(2.0 / (k * k * cin))).bfloat16()
         return w.to(DEV), (0.1 * torch.randn(cout, generator=g)).to(DEV)
-    return x.to(DEV), (conv(256, 1024, 1), conv(256, 256, 3), conv(1024, 256, 1))
+    return x.to(DEV), (conv(M, C, 1), conv(M, M, 3), conv(C, M, 1))
 
 
-@pytest.mark.parametrize("N", [1, 3])
-def test_bottleneck_fused_bit_identical(sat, N):
-    """csrc/convblock.hip runs a ResNet152 layer3 identity bottleneck (14x14, 1024 -> 256 -> 1024) as one
-    launch: bit-identical to the three conv launches it replaces (same fp32 sums, bias, ReLU and
-    residual order, one bf16 rounding per conv) and close to torch fp32 on the same bf16 operands."""
+@pytest.mark.parametrize("N,H,C,M", [(1, 14, 1024, 256), (3, 14, 1024, 256), (1, 28, 512, 128), (3, 28, 512, 128),
+                                     (9, 28, 512, 128)])
+def test_bottleneck_fused_bit_identical(sat, N, H, C, M):
+    """csrc/convblock.hip runs a ResNet152 layer3 identity bottleneck (14x14, 1024 -> 256 -> 1024: half images)
+    and a layer2 one (28x28, 512 -> 128 -> 512: 7-row bands, four per image) as one launch: bit-identical to the
+    three conv launches it replaces (same fp32 sums, bias, ReLU and residual order, one bf16 rounding per conv)
+    and close to torch fp32 on the same bf16 operands."""
     from sat_amd import ops
-    xd, ((w1, b1), (w2, b2), (w3, b3)) = _bottleneck_operands(N, 10 + N)
+    xd, ((w1, b1), (w2, b2), (w3, b3)) = _bottleneck_operands(N, 10 + N, H, C, M)
     y1 = ops.conv2d_nhwc(xd, w1, b1, 1, 0, True)
     y2 = ops.conv2d_nhwc(y1, w2, b2, 1, 1, True)
     ref = ops.conv2d_nhwc(y2, w3, b3, 1, 0, True, residual=xd)
@@ -1070,12 +1072,15 @@ def test_bottleneck_fused_bit_identical(sat, N):
 
 @pytest.mark.parametrize("N,H,C,slices", [(1, 14, 256, 1), (2, 14, 256, 1), (5, 14, 256, 1), (16, 14, 256, 1),
                                           (1, 14, 256, 2), (3, 14, 256, 2), (70, 14, 256, 2),
-                                          (8, 14, 256, 0), (1, 28, 128, 0), (3, 28, 128, 0)])
+                                          (8, 14, 256, 0), (1, 28, 128, 0), (3, 28, 128, 0),
+                                          (1, 7, 512, 0), (3, 7, 512, 1), (4, 7, 512, 1), (17, 7, 512, 2),
+                                          (70, 7, 512, 0)])
 def test_conv3x3_frag_bit_identical(sat, N, H, C, slices):
     """csrc/convblock.hip's half-image 3x3 kernel (a layer3 c2 left unfused: 14x14, 256 -> 256), its two-slice
     form (SatPolicy.conv_slices 2: each half image as two 128-channel workgroups, the default at B <= 64;
-    N = 70 leaves a partial group of 8 half images) and its 7-row band form (layer2 c2: 28x28, 128 -> 128) are
-    bit-identical to the tile kernel on the same operands, and close to torch fp32."""
+    N = 70 leaves a partial group of 8 half images), its 7-row band form (layer2 c2: 28x28, 128 -> 128) and its
+    whole-image form (layer4 c2: 7x7, 512 -> 512, one or two images x four 128-channel slices per workgroup; odd N
+    leaves a one-image group) are bit-identical to the tile kernel on the same operands, and close to torch fp32."""
     from sat_amd import ops
     g = torch.Generator().manual_seed(40 + N + H)
     x = torch.randn(N, H, H, C, generator=g).relu().bfloat16().to(DEV)
@@ -1117,7 +1122,7 @@ def test_encoder_c2_frag_equal_tile(sat):
     enc = sat.Encoder("resnet152", dtype=torch.bfloat16)
     enc.load_state_dict(p, strict=True)
     enc = enc.to(DEV).eval()
-    enc.fuse_blocks = False
+    enc.fuse_blocks = enc.fuse_layer2 = False
     x = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(7)).to(DEV)
     with torch.no_grad():
         enc.c1_frag, enc.c2_frag = True, True
@@ -1131,7 +1136,8 @@ def test_encoder_c2_frag_equal_tile(sat):
 
 
 def test_encoder_fused_blocks_equal_unfused(sat):
-    """ResNet152 trunk at 224 x 224: the fused layer3 blocks change no output bit."""
+    """ResNet152 trunk at 224 x 224: the fused layer3 and layer2 blocks change no output bit (each kind alone
+    and both)."""
     torch.manual_seed(0)
     p = O.make_resnet152_params(4)
     enc = sat.Encoder("resnet152", dtype=torch.bfloat16)
@@ -1139,12 +1145,19 @@ def test_encoder_fused_blocks_equal_unfused(sat):
     enc = enc.to(DEV).eval()
     x = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(6)).to(DEV)
     plan = enc.compiled_plan(x.device, torch.bfloat16)
-    assert sum(1 for s in plan if s[0] == "block" and s[5] is not None) == 35
+    assert sum(1 for s in plan if s[0] == "block" and s[5] is not None) == 35 + 7
     with torch.no_grad():
+        enc.fuse_blocks = enc.fuse_layer2 = True
         y_f = enc(x)
         enc.fuse_blocks = False
+        y_2 = enc(x)            # layer2 fused only
+        enc.fuse_layer2 = False
         y_u = enc(x)
+        enc.fuse_blocks = True
+        y_3 = enc(x)            # layer3 fused only
     assert torch.equal(y_f, y_u)
+    assert torch.equal(y_2, y_u)
+    assert torch.equal(y_3, y_u)
 
 
 @pytest.mark.parametrize("dtype,D,bert", [(torch.bfloat16, 2048, False), (torch.float32, 512, False),
