@@ -740,16 +740,17 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
 // workgroup, two 128-channel slices: each workgroup streams half the weights -- 0.59 MB -- for 196 output
 // pixels, where the half-image kernel streams all 1.18 MB for 98).  Same k order, bias, ReLU and rounding
 // as the tile kernel: bit-identical.
-template <int IW, int RO, int C, int NSL, int WM, int PF>
+template <int IW, int RO, int C, int NSL, int WM, int PF, int NWV = 8>
 __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                   const float* __restrict__ bias, bf16* __restrict__ y, int nbands) {
   constexpr int IH = IW, NPART = IH / RO, PO = RO * IW, MBT = (PO + 15) / 16;
-  constexpr int MB = (MBT + WM - 1) / WM, WN = 8 / WM;   // m-blocks per wave; waves = WM m-groups x WN
+  constexpr int MB = (MBT + WM - 1) / WM, WN = NWV / WM;   // m-blocks per wave; NWV waves = WM m-groups x WN
   constexpr int SLOTS = RO + 2, ZR = SLOTS * IW;        // LDS pixel rows + the zero row
   constexpr int ROWB = 128, XPL = (ZR + 1) * ROWB, NPL = C / 64, NJ = C / (16 * WN * NSL), CS = C / NSL;
   constexpr int NT = 9 * C / 64, KS = 9 * C / 32, CPP = C / 8;   // CPP: 16-B chunks per pixel
-  constexpr int PER_T = (ZR * CPP + 511) / 512;
-  static_assert(IH % RO == 0 && C % (16 * WN * NSL) == 0 && NJ >= 1 && 8 % WM == 0, "whole bands, 16-channel n-blocks per wave");
+  constexpr int NTH = NWV * 64, PER_T = (ZR * CPP + NTH - 1) / NTH;
+  static_assert(IH % RO == 0 && C % (16 * WN * NSL) == 0 && NJ >= 1 && NWV % WM == 0 && NPL * 8 <= NTH,
+                "whole bands, 16-channel n-blocks per wave");
   __shared__ __attribute__((aligned(16))) char smem[NPL * XPL];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -773,7 +774,7 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
   uint4 xin[PER_T];
   const uint4* xs = (const uint4*)(x + (pix_img + (long)(y0 - 1 + s_lo) * IW) * C);
 #pragma unroll
-  for (int u = 0; u < PER_T; ++u) xin[u] = xs[min(u * 512 + tid, nchunk - 1)];
+  for (int u = 0; u < PER_T; ++u) xin[u] = xs[min(u * NTH + tid, nchunk - 1)];
   float4 bv[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) bv[j] = *(const float4*)(bias + cb + (wn * NJ + j) * 16 + 4 * fh);
@@ -789,7 +790,7 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
   static_for<PF>([&](auto e) { load_b(decltype(e)::value, bq[decltype(e)::value]); });
 #pragma unroll
   for (int u = 0; u < PER_T; ++u) {
-    const int q = u * 512 + tid, r = s_lo * IW + q / CPP, c = q % CPP;
+    const int q = u * NTH + tid, r = s_lo * IW + q / CPP, c = q % CPP;
     if (q < nchunk) *(uint4*)(smem + (c >> 3) * XPL + r * ROWB + 16 * ((c & 7) ^ (r & 7))) = xin[u];
   }
   if (tid < NPL * 8) *(uint4*)(smem + (tid >> 3) * XPL + ZR * ROWB + (tid & 7) * 16) = make_uint4(0, 0, 0, 0);
@@ -979,14 +980,16 @@ __global__ __launch_bounds__(512) void conv3x3_img_kernel(const bf16* __restrict
 }
 
 // ResNet152 layer3's c2 when half images alone would leave CUs idle (B <= 64 per GPU: 2B workgroups): each half image
-// as two 128-channel slices (4B workgroups), each streaming half the weights; the 8 waves own 16 channels each and
-// every m-block.  Measured and removed (profiles/r3_s13, r3_s14, r3_s16): two m-groups of waves, weights 3 / 4
-// k-tiles ahead, whole images as four 64-channel slices -- all within noise of this form.
-__global__ __launch_bounds__(512) void conv3x3_slice2_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+// as two 128-channel slices (4B workgroups), each streaming half the weights, with four waves that own 32 channels
+// each and every m-block (each A fragment feeds two MFMAs; two workgroups fit a CU): 18.5 vs 19.4 us and 4.37 vs
+// 4.42-4.44 ms per B = 64 step against eight waves of 16 channels (profiles/r3_s24).  Measured and removed: the
+// same four-wave form over whole images (31.5 vs 29.3 us at B = 128), and (profiles/r3_s13, r3_s14, r3_s16) two
+// m-groups of waves, weights 3 / 4 k-tiles ahead, whole images as four 64-channel slices -- all within noise.
+__global__ __launch_bounds__(256) void conv3x3_slice2_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                              const float* __restrict__ bias, bf16* __restrict__ y,
                                                              int nbands, SatStamps st) {
   const SatStampT0 t0 = sat_stamp_begin(st);
-  conv3x3_band_body<14, 7, 256, 2, 1, 2>(x, wf, bias, y, nbands);
+  conv3x3_band_body<14, 7, 256, 2, 1, 2, 4>(x, wf, bias, y, nbands);
   sat_stamp_end(st, t0);
 }
 
@@ -1232,7 +1235,7 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   if (mode == 1)
     hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp, st);
   else
-    hipLaunchKernelGGL(conv3x3_slice2_kernel, dim3(groups), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
+    hipLaunchKernelGGL(conv3x3_slice2_kernel, dim3(groups), dim3(256), 0, s, xp, wp, b, yp, 2 * N, st);
   return (int)hipGetLastError();
 }
 
