@@ -68,6 +68,8 @@ def main():
     ap.add_argument("--tiles", action="store_true")
     ap.add_argument("--split", action="store_true", help="also the atomic split-K aimed at 512 / 768 / 1024 workgroups")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--torch", action="store_true",
+                    help="calibration: torch.matmul (hipBLASLt) of the same bf16 operands, bf16 output")
     a = ap.parse_args()
     tot_us = tot_f = 0.0
     for name, M, N, K, ta, tb, cdt, beta, *rest in SHAPES:
@@ -87,6 +89,22 @@ def main():
                 except RuntimeError:
                     alt.append(f"t{tile}:-")
             line += "  [" + " ".join(alt) + "]"
+        if a.torch:
+            At = A.t() if ta else A          # [M, K] view
+            Bt = Bm if tb else Bm.t()        # [K, N] view
+            out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+
+            def mm():
+                torch.matmul(At, Bt, out=out)
+            for _ in range(2):
+                mm()
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st.record()
+            for _ in range(a.reps):
+                mm()
+            en.record()
+            en.synchronize()
+            line += f"  [hipBLASLt {st.elapsed_time(en) / a.reps * 1e3:.1f} us]"
         if a.split:
             alt = [f"w{wgs}:{time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_split_wgs=wgs), a.reps, act):.1f}"
                    for wgs in (512, 768, 1024)]
