@@ -54,6 +54,10 @@ def parse():
     ap.add_argument("--enc-start", choices=["decoder", "phase2"], default="decoder",
                     help="graph + overlap: batch i+1's encoder starts beside batch i's whole decoder (decoder), or "
                          "only once its forward + head backward graph is done, beside the BPTT graph and Adam (phase2)")
+    ap.add_argument("--feature-buffers", type=int, default=3, choices=[2, 3, 4],
+                    help="graph + overlap: encoder output buffers (and graph sets) in flight; the next batch's encoder waits "
+                         "for the decoder that last read its buffer (3: B = 64 4.08-4.11 vs 4.15 ms with 2, B = 128 "
+                         "within noise; profiles/r3_s31)")
     ap.add_argument("--split-target", type=int, default=None,
                     help="graph + overlap: workgroups the decoder's per-step split-K GEMMs aim for (default: "
                          "64 with ResNet152 features, 128 with VGG19's: profiles/r2_s54_sched.txt)")
@@ -601,6 +605,7 @@ def main():
                           attention=True).to(dev).train()
     dec.policy = policy
     dec.transposed_weights = not args.no_transposed
+    dec.record_tokens = False      # the fed-token record is a diagnostic output, not part of the step
     if not args.no_graph and not args.no_overlap:
         # the decoder shares the chip with the next batch's encoder: fewer split-K workgroups
         dec.split_target = args.split_target
@@ -645,7 +650,7 @@ def main():
         # while the decoder of batch i, its all-reduce and Adam run on the main stream (the
         # encoder does not read any decoder parameter), so the latency-bound decoder kernels and
         # the gradient exchange share the chip with the conv trunk.
-        nbuf = 2 if overlap else 1
+        nbuf = args.feature_buffers if overlap else 1
         # encoder part A (plan[:split], beside the previous batch's decoder) and part B (plan[split:])
         split = 0
         if overlap and args.network == "resnet152" and args.enc_split != "none":
@@ -709,8 +714,10 @@ def main():
     else:
         s_main = torch.cuda.current_stream()
         s_enc = torch.cuda.Stream() if overlap else s_main
-    ev_enc = [torch.cuda.Event() for _ in range(2)]
-    ev_dec = [torch.cuda.Event() for _ in range(2)]
+    nb = len(g_enc) if use_graph else 1
+    ev_enc = [torch.cuda.Event() for _ in range(max(nb, 2))]
+    ev_dec = [torch.cuda.Event() for _ in range(max(nb, 2))]
+    dec_events = []   # (start, end) of each batch's decoder graphs on s_main (after its wait for the features)
     ev_ph1 = torch.cuda.Event()   # --enc-start phase2: the decoder's forward + head backward graph is done
 
     def replay_encoder(k, wait_dec, dec_ev=None):
@@ -746,6 +753,8 @@ def main():
             if use_graph:
                 k = i % len(g_enc)
                 s_main.wait_event(ev_enc[k])
+                d_st, d_en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                d_st.record(s_main)
                 g_dec[k].replay()
                 if args.enc_start == "phase2":
                     ev_ph1.record(s_main)
@@ -755,11 +764,13 @@ def main():
                 if g_rec[k] is not None:
                     g_rec[k].replay()
                 w2 = allreduce_bucket_async(dec, 2) if world > 1 else None
+                d_en.record(s_main)
+                dec_events.append((d_st, d_en))
                 ev_dec[k].record(s_main)
                 loss = loss_static[k]
                 if i + 1 < n:
-                    if overlap:
-                        replay_encoder((i + 1) % 2, i >= 1, ev_dec[k])
+                    if overlap:   # buffer (i + 1) % nb was last read by batch i + 1 - nb's decoder
+                        replay_encoder((i + 1) % nb, i >= nb - 1, ev_dec[k])
                     else:
                         replay_encoder(0, False)
                 if world > 1:
@@ -777,6 +788,7 @@ def main():
         st.enable(False)
     run(2)   # replay warm-up
     enc_events.clear()
+    dec_events.clear()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -793,6 +805,7 @@ def main():
         elapsed = t.item()
     launches = conv_launches(args.network, B, fused=enc.fuse_blocks, fused2=enc.fuse_layer2)
     enc_ms = sum(s.elapsed_time(e) for s, e in enc_events) if use_graph else None
+    dec_ms = sum(s.elapsed_time(e) for s, e in dec_events) if use_graph and dec_events else None
     diag_phase = None
     if (stamps_enc or stamps_dec) and not args.no_diagnostics:
         # diagnostic phase (every rank: the all-reduces are collective): the same overlapped schedule with
@@ -882,6 +895,7 @@ def main():
             "roofline": roof,
             "diagnostic_phase": dict(diag_phase, note="after the timed region: the same overlapped graphs with the "
                                      "kernels' in-kernel timestamps on (roofline in-step figures)") if diag_phase else None,
+            "decoder_graphs_ms_per_step": round(dec_ms / args.steps, 3) if dec_ms else None,
             "encoder_trunk": dict(trunk or {}, graph_ms_per_step=(round(enc_ms / args.steps, 3) if enc_ms else None),
                                   split_at=args.enc_split if g_encA is not None else None),
             "loss": round(loss_v, 4),

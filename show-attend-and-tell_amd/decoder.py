@@ -115,6 +115,7 @@ class Decoder(nn.Module):
         self.transposed_weights = True
         self._pending_bwd = None
         self.last_tokens = None        # int32 [B, T-1]: token fed at each step of the last forward
+        self.record_tokens = True      # False: last_tokens stays None (training loops: no copy launch per step)
 
     # ------------------------------------------------------------------ layout
     def _groups(self):
@@ -419,7 +420,7 @@ class _DecoderFn(torch.autograd.Function):
         B, T1 = dims.B, dims.T - 1
         preds = torch.empty(B, T1, dims.V, device=dev, dtype=feats.dtype)
         alphas = torch.empty(B, T1, dims.L, device=dev, dtype=torch.float32)
-        tokens = torch.empty(B, T1, device=dev, dtype=torch.int32)
+        tokens = torch.empty(B, T1, device=dev, dtype=torch.int32) if dec.record_tokens else None
         mask = None
         if dims.has_dropout_mask:
             mask = dec.dropout_mask.to(device=dev, dtype=torch.uint8).contiguous()

@@ -40,8 +40,7 @@ class _CaptionLossFn(torch.autograd.Function):
         ctx.save_for_backward(preds_c, caps)
         ctx.ws, ctx.dims, ctx.alpha_c = ws, (B, T, V, Lf), float(alpha_c)
         ctx.relu = bool(getattr(preds, "_sat_relu_logits", False))   # set by sat_amd.Decoder (ado)
-        loss = out[0].clone()
-        metrics = out[1:7].clone()
+        loss, metrics = out[0], out[1:7]   # views of the kernel's output (no copy launches in the step)
         ctx.mark_non_differentiable(metrics)
         return loss, metrics
 

@@ -361,6 +361,7 @@ def main(argv=None):
             print(json.dumps(rec), flush=True)
 
     encoder, decoder, word_dict, dt = build(args, device)
+    decoder.record_tokens = False   # no fed-token record per training step
     if not args.no_overlap:   # the decoder shares the chip with the next batch's encoder (bench.py defaults)
         decoder.split_target = 128 if args.network == "vgg19" else 64
         # no layer3 block fused: the unfused c2 / c3 half-image kernels leave CUs to the decoder
