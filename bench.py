@@ -196,6 +196,43 @@ class DecoderStamps:
         if on:
             self.buf[:, 1:].zero_()
 
+    def _lo_hi(self):
+        st, en = self.buf[:, 1:, 0], self.buf[:, 1:, 1]
+        valid = st > 0
+        big = torch.iinfo(torch.int64).max
+        lo = torch.where(valid, st, torch.full_like(st, big)).min(dim=1).values.tolist()
+        hi = torch.where(valid, en, torch.zeros_like(en)).max(dim=1).values.tolist()
+        return lo, hi
+
+    def chain_us(self):
+        """Per time step of the forward (h_gemm .. lstm_fwd) and of the BPTT (lstm_bwd .. dh_gemm): the mean
+        interval from one step's first kernel start to the next step's, beside the mean sum of the step's kernel
+        spans -- the difference is what the dependent launches cost between kernels."""
+        lo, hi = self._lo_hi()
+        T1, gi = self.T1, {g: i for i, g in enumerate(self.groups)}
+
+        def span(g, t):
+            k = gi[g] * T1 + t
+            return (hi[k] - lo[k]) / 100.0 if hi[k] > 0 else None
+
+        def start(g, t):
+            k = gi[g] * T1 + t
+            return lo[k] if hi[k] > 0 else None
+        out = {}
+        for name, groups, order in (("fwd", self.groups[:4], range(T1)), ("bwd", self.groups[4:], range(T1 - 1, -1, -1))):
+            order = list(order)
+            iv, ks = [], []
+            for a, b in zip(order, order[1:]):
+                sa, sb = start(groups[0], a), start(groups[0], b)
+                spans = [span(g, a) for g in groups]
+                if sa is not None and sb is not None and all(v is not None for v in spans):
+                    iv.append((sb - sa) / 100.0)
+                    ks.append(sum(spans))
+            if iv:
+                out[f"{name}_step_interval_us"] = round(sum(iv) / len(iv), 2)
+                out[f"{name}_step_kernels_us"] = round(sum(ks) / len(ks), 2)
+        return out
+
     def group_spans_us(self):
         st, en = self.buf[:, 1:, 0], self.buf[:, 1:, 1]
         valid = st > 0
@@ -832,7 +869,14 @@ def main():
                 for g, v in sd.group_spans_us().items():
                     decd.setdefault(g, []).extend(v)
         return conv, decd
+
+    def chains():   # the per-step chain figures, averaged over the graph sets
+        cs = [sd.chain_us() for sd in stamps_dec]
+        keys = {k for c in cs for k in c}
+        return {k: round(sum(c[k] for c in cs if k in c) / sum(1 for c in cs if k in c), 2) for k in sorted(keys)}
     overlap_conv, overlap_dec = collect() if diag_phase else (None, None)
+    chain_overlapped = chains() if diag_phase and stamps_dec else None
+    chain_alone = None
     alone_conv = alone_dec = alone_intervals = None
     if diag and diag_phase and use_graph:
         # graph-alone phase: each encoder graph, then each decoder graph pair, replayed on its own (nothing
@@ -852,6 +896,7 @@ def main():
                     g_rec[k].replay()
                 torch.cuda.synchronize()
         alone_conv, alone_dec = collect()
+        chain_alone = chains() if stamps_dec else None
         alone_intervals = instep_conv_durations(stamps_enc, launches, intervals=True) if stamps_enc else None
         for st in stamps_enc + stamps_dec:
             st.enable(False)
@@ -859,6 +904,10 @@ def main():
                                  overlapped=overlap_conv, intervals=alone_intervals) if diag else (None, None)
     step_kernels = decoder_step_roofline(dec, enc, imgs, caps, instep=alone_dec or overlap_dec,
                                          overlapped=overlap_dec) if diag else None
+    if step_kernels is not None and (chain_alone or chain_overlapped):
+        step_kernels["step_chain"] = dict(alone=chain_alone, overlapped=chain_overlapped,
+                                          note="per time step: first-kernel start to the next step's first-kernel "
+                                               "start (interval) beside the sum of the step's four kernel spans")
     fp32_leg = fp32_step(args, enc, dec, imgs, caps, pad_id, skip_ids, world) if world == 1 and args.fp32_steps > 0 \
         else None
     if roof is not None:

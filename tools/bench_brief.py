@@ -22,3 +22,7 @@ for f in sys.argv[1:]:
             print("   ", g, v)
         print("  fused", ds["fused_attention_lstm"])
         print("  all", ds["all_step_kernels"])
+        if ds.get("step_chain"):
+            print("  chain", {k: v for k, v in ds["step_chain"].items() if k != "note"})
+    if d.get("decoder_graphs_ms_per_step"):
+        print("  decoder graphs ms/step", d["decoder_graphs_ms_per_step"])
