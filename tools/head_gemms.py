@@ -66,7 +66,8 @@ def time_one(A, Bm, C, ta, tb, beta, policy, reps, act=0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", action="store_true")
-    ap.add_argument("--split", action="store_true", help="also the atomic split-K aimed at 512 / 768 / 1024 workgroups")
+    ap.add_argument("--split", action="store_true", help="also the atomic split-K aimed at other workgroup counts")
+    ap.add_argument("--split-wgs", default="512,768,1024", help="--split: the SatPolicy.gemm_split_wgs values")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--torch", action="store_true",
                     help="calibration: torch.matmul (hipBLASLt) of the same bf16 operands, bf16 output")
@@ -107,7 +108,7 @@ def main():
             line += f"  [hipBLASLt {st.elapsed_time(en) / a.reps * 1e3:.1f} us]"
         if a.split:
             alt = [f"w{wgs}:{time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_split_wgs=wgs), a.reps, act):.1f}"
-                   for wgs in (512, 768, 1024)]
+                   for wgs in [int(v) for v in a.split_wgs.split(",")]]
             line += "  [" + " ".join(alt) + "]"
         print(line, flush=True)
     print(f"total {tot_us:.1f} us for {tot_f / 1e9:.1f} GFLOP = {tot_f / tot_us / 1e6:.1f} TF/s", flush=True)
