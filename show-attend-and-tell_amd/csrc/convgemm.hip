@@ -518,6 +518,20 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 }  // namespace
 
 // Returns 1 if the problem was handled by the fast path, 0 if the caller should use the generic kernel.
+// the atomic split-K decision of sat_fast_gemm_try for a plain bf16 product with fp32 output (the decoder's
+// weight gradients), so a caller can zero several such targets in one launch and set SatGemm::c_zeroed
+int sat_gemm_splits_atomically(const SatGemm& g) {
+  if (g.dtype != SAT_BF16 || g.c_dtype != SAT_F32 || g.act != SAT_ACT_NONE || g.add1 || g.beta != 0.f ||
+      g.conv.C > 0 || g.partial_splits > 1 || g.K < 1024)
+    return 0;
+  const SatPolicy& pol = sat_policy();
+  const bool tr = g.transA || g.transB;
+  const int tcfg = (!tr && g.N <= 64) ? T128x64W8 : T128x128W8;
+  const long tiles = (long)sat_cdiv(g.M, tile_bm(tcfg)) * sat_cdiv(g.N, tile_bn(tcfg));
+  const int split_wgs = pol.gemm_split_wgs > 0 ? pol.gemm_split_wgs : 320;
+  return tiles < split_wgs / 2 ? 1 : 0;
+}
+
 int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   *err = 0;
   if (g.dtype != SAT_BF16 || g.batch != 1 || g.aux) return 0;
@@ -597,7 +611,7 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
     if (a.splitk == 1) {   // beta == 1, single split: still accumulate atomically
       a.splitk = 2; a.kchunk = sat_cdiv(g.K, BK) * BK;   // split 1 has an empty K range and adds 0
     }
-    if (g.beta == 0.f) {
+    if (g.beta == 0.f && !g.c_zeroed) {
       SAT_CHECK((hipError_t)sat_zero_rows((float*)g.C, g.ldc, g.M, g.N, s));
     }
   }

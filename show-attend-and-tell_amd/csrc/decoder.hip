@@ -656,15 +656,28 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   const Splits sp = splits_for(d, c.tr);
   auto G = [&](int64_t off) { return grads + off; };
   // weight gradient: G[M,N] (+)= X[K,M]^T Y[K,N]   (X m-contig, Y n-contig)
-  auto wgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo,
-                   int a_tail = 0) {
+  auto wg = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo,
+                int a_tail = 0) {
     SatGemm g;
     g.a_tail = a_tail;
     g.M = M; g.N = N; g.K = K; g.dtype = d.dtype;
     g.A = X; g.lda = ldx; g.transA = 1;
     g.B = Y; g.ldb = ldy; g.transB = 1;
     g.C = out; g.ldc = ldo; g.c_dtype = SAT_F32; g.beta = beta;
-    return sat_gemm_launch(g, s);
+    return g;
+  };
+  auto wgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo,
+                   int a_tail = 0) {
+    return sat_gemm_launch(wg(M, N, K, X, ldx, Y, ldy, out, ldo, a_tail), s);
+  };
+  // the targets of this phase's weight-gradient products that run as atomic split-K (beta = 0): marked zeroed
+  // and appended to one zeroing launch instead of a zeroing pass per product
+  auto prezero = [&](SatGemm* const* gs, int n, SatZeroSeg* seg, int& nseg) {
+    for (int i = 0; i < n; ++i)
+      if (!accumulate && sat_gemm_splits_atomically(*gs[i])) {
+        seg[nseg++] = SatZeroSeg{(float*)gs[i]->C, gs[i]->M, gs[i]->N, gs[i]->ldc};
+        gs[i]->c_zeroed = 1;
+      }
   };
   auto dgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Wt, long ldw, float* out, long ldo,
                    const float* add1 = nullptr, long ld_add1 = 0) {
@@ -687,12 +700,22 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
         SAT_CHECK((hipError_t)sat_relu_mask_mul(d_preds, preds, (long)R * V, d.dtype, w.dpre_t, s));
         dpre = w.dpre_t;
       }
-      SAT_CHECK((hipError_t)wgrad(V, E, R, dpre, ldp, w.comb_t, E, G(lay->fout_w), E, VP != V));
+      SatGemm gfo = wg(V, E, R, dpre, ldp, w.comb_t, E, G(lay->fout_w), E, VP != V);
+      SatGemm gfh = wg(E, E, R, w.dfh_t, E, w.hd_t, E, G(lay->fh_w), E);
+      SatGemm gfz = wg(E, D, R, w.dfz_t, E, w.ctx_t, D, G(lay->fz_w), D);
+      {
+        SatGemm* gs[3] = {&gfo, &gfh, &gfz};
+        SatZeroSeg seg[3];
+        int nseg = 0;
+        prezero(gs, 3, seg, nseg);
+        SAT_CHECK((hipError_t)sat_zero_segs(seg, nseg, s));
+      }
+      SAT_CHECK((hipError_t)sat_gemm_launch(gfo, s));
       SAT_CHECK((hipError_t)dgrad_launch(c, R, E, V, dpre, ldp, c.W(lay->fout_w), E, w.dcomb, E, s, nullptr, 0, 0, 0,
                                          VP != V));
       SAT_CHECK((hipError_t)sat_ado_bwd_split(w.dcomb, w.fh, w.fz, (long)R * E, d.dtype, w.dfh_t, w.dfz_t, s));
-      SAT_CHECK((hipError_t)wgrad(E, E, R, w.dfh_t, E, w.hd_t, E, G(lay->fh_w), E));
-      SAT_CHECK((hipError_t)wgrad(E, D, R, w.dfz_t, E, w.ctx_t, D, G(lay->fz_w), D));
+      SAT_CHECK((hipError_t)sat_gemm_launch(gfh, s));
+      SAT_CHECK((hipError_t)sat_gemm_launch(gfz, s));
       // the three bias gradients (column sums of d logits, d f_h, d f_z) in one launch pair
       const SatColsumSeg cs[3] = {{dpre, d.dtype, ldp, R, V, G(lay->fout_b), accumulate, nullptr},
                                   {w.dfh_t, d.dtype, E, R, E, G(lay->fh_b), accumulate, nullptr},
@@ -716,18 +739,27 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   if (!(phase & 2)) return 0;
 
   // ---------------- recurrent BPTT (reverse time loop) ----------------
-  {   // one launch zeroes the BPTT accumulators, the split attention backward's tickets and (beta = 0) the dense
-      // embedding gradient the scatter-add after the loop accumulates into
-    float* zp[4];
-    long zn[4];
+  // this phase's weight-gradient products (launched after the loop)
+  const void* dg_t = c.at(w.dhg_t, E + D);   // d gates rows (ld HG)
+  SatGemm g_attw = wg(E, D, B * L, w.dWs_t, E, img_features, D, G(lay->attW_w), D);
+  SatGemm g_init = wg(2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D);
+  SatGemm g_hcat = att ? wg((int)HG, E, R, w.dhg_t, HG, w.h_in_t, E, G(lay->hcat_w), E)
+                       : wg(4 * E, E, R, dg_t, HG, w.h_in_t, E, G(lay->hcat_w + (long)(E + D) * E), E);
+  SatGemm g_wihx = wg(4 * E, E, R, dg_t, HG, w.emb_t, E, G(lay->wih), E + D);
+  SatGemm g_wihc = wg(4 * E, D, R, dg_t, HG, w.gated_t, D, G(lay->wih + E), E + D);
+  {   // one launch zeroes the BPTT accumulators, the split attention backward's tickets, (beta = 0) the dense
+      // embedding gradient the scatter-add after the loop accumulates into, and the atomic split-K targets
+    SatZeroSeg seg[12];
     int nz = 0;
     if (att) {
-      zp[nz] = w.dv_acc; zn[nz++] = (long)B * E;
-      zp[nz] = w.dbv_acc; zn[nz++] = B;
-      zp[nz] = (float*)w.ticket; zn[nz++] = B;
+      seg[nz++] = SatZeroSeg{w.dv_acc, 1, (long)B * E, (long)B * E};
+      seg[nz++] = SatZeroSeg{w.dbv_acc, 1, B, B};
+      seg[nz++] = SatZeroSeg{(float*)w.ticket, 1, B, B};
     }
-    if (!d.bert && !accumulate) { zp[nz] = G(lay->embedding); zn[nz++] = (long)V * E; }
-    SAT_CHECK((hipError_t)sat_zero_multi(zp, zn, nz, s));
+    if (!d.bert && !accumulate) seg[nz++] = SatZeroSeg{G(lay->embedding), 1, (long)V * E, (long)V * E};
+    SatGemm* gs[5] = {&g_hcat, &g_wihx, &g_wihc, &g_init, &g_attw};
+    prezero(gs, att ? 5 : 4, seg, nz);
+    SAT_CHECK((hipError_t)sat_zero_segs(seg, nz, s));
   }
   const StepIO io{img_features, const_cast<float*>(alphas), d_alphas};
   for (int t = T1 - 1; t >= 0; --t) {
@@ -751,12 +783,12 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   if (att) {
     SAT_CHECK((hipError_t)sat_attention_dws_launch(w.Ws, w.uh_all, w.de_all, c.F(lay->v_w), B, L, E, T1, d.dtype,
                                                    w.dWs_acc, w.dWs_t, s));
-    SAT_CHECK((hipError_t)wgrad(E, D, B * L, w.dWs_t, E, img_features, D, G(lay->attW_w), D));
+    SAT_CHECK((hipError_t)sat_gemm_launch(g_attw, s));
   }
   // init_h / init_c (decoder.py:137-147): dh0 = dh_rec, dc0 = dc after the t = 0 step
   SAT_CHECK((hipError_t)sat_tanh_pair_bwd(w.dh_rec, sp.dh, (long)B * E, w.dc, w.hc0, B, E, w.dpre0, w.dpre0_t,
                                           d.dtype, s));
-  SAT_CHECK((hipError_t)wgrad(2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D));
+  SAT_CHECK((hipError_t)sat_gemm_launch(g_init, s));
   {   // every bias gradient of this phase (column sums) in one launch pair; b_hh and b_ih receive the same
       // gradient (the sum of d gates)
     SatColsumSeg cs[6];
@@ -772,14 +804,9 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
     SAT_CHECK((hipError_t)sat_colsum_multi(cs, n, w.colsum, s));
   }
 
-  const void* dg_t = c.at(w.dhg_t, E + D);   // d gates rows (ld HG)
-  if (att) {
-    SAT_CHECK((hipError_t)wgrad((int)HG, E, R, w.dhg_t, HG, w.h_in_t, E, G(lay->hcat_w), E));
-  } else {
-    SAT_CHECK((hipError_t)wgrad(4 * E, E, R, dg_t, HG, w.h_in_t, E, G(lay->hcat_w + (long)(E + D) * E), E));
-  }
-  SAT_CHECK((hipError_t)wgrad(4 * E, E, R, dg_t, HG, w.emb_t, E, G(lay->wih), E + D));
-  SAT_CHECK((hipError_t)wgrad(4 * E, D, R, dg_t, HG, w.gated_t, D, G(lay->wih + E), E + D));
+  SAT_CHECK((hipError_t)sat_gemm_launch(g_hcat, s));
+  SAT_CHECK((hipError_t)sat_gemm_launch(g_wihx, s));
+  SAT_CHECK((hipError_t)sat_gemm_launch(g_wihc, s));
   if (!d.bert) {  // dense embedding gradient (zeroed before the loop), scatter-added by fed token (decoder.py:87,133)
     SAT_CHECK((hipError_t)dgrad(R, E, 4 * E, dg_t, HG, c.W(lay->wih), E + D, w.demb, E, d.ado ? w.dcomb : nullptr, E));
     SAT_CHECK((hipError_t)sat_embed_scatter_add(w.demb, w.tok, R, E, G(lay->embedding), s));

@@ -381,25 +381,29 @@ __global__ void colsum_multi_final_kernel(ColsumMultiArgs a) {
   colsum_final_body(sg.part, sg.RS, sg.N, sg.out, sg.accumulate, sg.out2, b - sg.fblk0);
 }
 
-// zero several fp32 ranges in one launch
-constexpr int kZeroMaxSegs = 8;
+// zero several fp32 row blocks (rows x cols at a row stride ld; contiguous ranges as one row) in one launch
+constexpr int kZeroMaxSegs = 12;
 struct ZeroMultiArgs {
   int n;
   float* p[kZeroMaxSegs];
-  long count[kZeroMaxSegs];
+  long rows[kZeroMaxSegs], cols[kZeroMaxSegs], ld[kZeroMaxSegs];
 };
 __global__ void zero_multi_kernel(ZeroMultiArgs a) {
   const long stride = (long)gridDim.x * blockDim.x;
   for (int k = 0; k < a.n; ++k) {
     float* p = a.p[k];
-    const long n = a.count[k];
-    if (((uintptr_t)p & 15) == 0) {
-      const long n4 = n >> 2;
-      for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride)
-        ((float4*)p)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (long i = (n4 << 2) + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) p[i] = 0.f;
+    const long R = a.rows[k], C = a.cols[k], ld = a.ld[k];
+    if (((uintptr_t)p & 15) == 0 && C % 4 == 0 && ld % 4 == 0) {
+      const long c4 = C >> 2, n4 = R * c4;
+      for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const long r = i / c4;
+        *(float4*)(p + r * ld + 4 * (i - r * c4)) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     } else {
-      for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) p[i] = 0.f;
+      for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < R * C; i += stride) {
+        const long r = i / C;
+        p[r * ld + (i - r * C)] = 0.f;
+      }
     }
   }
 }
@@ -617,21 +621,27 @@ int sat_colsum_multi(const SatColsumSeg* segs, int n, float* scratch, hipStream_
   return (int)hipGetLastError();
 }
 
-int sat_zero_multi(float* const* ptrs, const long* counts, int n, hipStream_t s) {
+int sat_zero_segs(const SatZeroSeg* seg, int n, hipStream_t s) {
   if (n <= 0) return 0;
   if (n > kZeroMaxSegs) return (int)hipErrorInvalidValue;
   ZeroMultiArgs a{};
   long tot = 0;
   for (int i = 0; i < n; ++i) {
-    a.p[i] = ptrs[i];
-    a.count[i] = counts[i];
-    tot += counts[i];
+    a.p[i] = seg[i].p;
+    a.rows[i] = seg[i].rows; a.cols[i] = seg[i].cols; a.ld[i] = seg[i].ld;
+    tot += seg[i].rows * seg[i].cols;
   }
   a.n = n;
   long g = (tot / 4 + 255) / 256;
   g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
   hipLaunchKernelGGL(zero_multi_kernel, dim3((int)g), dim3(256), 0, s, a);
   return (int)hipGetLastError();
+}
+int sat_zero_multi(float* const* ptrs, const long* counts, int n, hipStream_t s) {
+  if (n > kZeroMaxSegs) return (int)hipErrorInvalidValue;
+  SatZeroSeg seg[kZeroMaxSegs];
+  for (int i = 0; i < n; ++i) seg[i] = SatZeroSeg{ptrs[i], 1, counts[i], counts[i]};
+  return sat_zero_segs(seg, n, s);
 }
 size_t sat_colsum_scratch_floats(int R, int N) { (void)R; return (size_t)64 * (N > 0 ? N : 1); }
 

@@ -133,6 +133,8 @@ struct SatGemm {
   // A's contiguous dimension (M when transA, else K) is readable -- zero-padded -- up to the next
   // multiple of 8, so the 16-B DMA paths may take M % 8 / K % 8 != 0 (the decoder's padded d logits)
   int a_tail = 0;
+  // beta = 0 and the caller has already zeroed C: an atomic split-K launch skips its own zeroing pass
+  int c_zeroed = 0;
 };
 
 int sat_gemm_launch(const SatGemm& g, hipStream_t s);

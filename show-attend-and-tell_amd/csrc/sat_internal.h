@@ -14,6 +14,15 @@ struct SatColsumSeg {
 int sat_colsum_multi(const SatColsumSeg* segs, int n, float* scratch, hipStream_t s);
 // zero n (<= 8) fp32 ranges in one launch (graph-safe memset)
 int sat_zero_multi(float* const* ptrs, const long* counts, int n, hipStream_t s);
+// zero up to 12 fp32 row blocks (rows x cols at row stride ld) in one launch
+struct SatZeroSeg {
+  float* p;
+  long rows, cols, ld;
+};
+int sat_zero_segs(const SatZeroSeg* seg, int n, hipStream_t s);
+// 1 when sat_gemm_launch would run this problem as an atomic split-K (fp32 C accumulated by atomics: with
+// beta = 0 it zeroes C first unless SatGemm::c_zeroed says the caller already did)
+int sat_gemm_splits_atomically(const SatGemm& g);
 int sat_embed_gather(const float* W, const int32_t* tok, int B, int T1, long tok_stride_b, int E, int dtype,
                      void* out, long out_ld, hipStream_t s);
 int sat_embed_scatter_add(const float* dX, const int32_t* tok, int R, int E, float* G, hipStream_t s);
