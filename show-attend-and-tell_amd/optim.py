@@ -66,22 +66,28 @@ class Adam(torch.optim.Optimizer):
                 st = self._state_for(p, owner)
                 st["step"] += 1
                 items.append((p, owner, st))
-            # merge runs of params that are adjacent in one flat buffer (same step count)
+            # merge runs of params that are adjacent in one flat buffer (same step count); a run also spans the
+            # alignment padding between two parameter groups (< 64 floats holding no parameter: zero value,
+            # gradient and moments, which the update leaves at zero), so one launch covers a whole flat buffer
             runs = []
             for p, owner, st in sorted(items, key=lambda it: (id(it[1]), it[0].data_ptr())):
                 step = int(st["step"].item())
+                gap = (p.data_ptr() - runs[-1]["end_ptr"]) // 4 if runs else -1
+                padding_only = (runs and owner is not None and runs[-1]["owner"] is owner and 0 < gap < 64
+                                and not any(runs[-1]["end_off"] <= o < p._sat_offset for o in owner._offsets.values()))
                 contiguous_with_prev = (runs and owner is not None and runs[-1]["owner"] is owner
                                         and runs[-1]["step"] == step
-                                        and runs[-1]["end_ptr"] == p.data_ptr()
-                                        and runs[-1]["gend"] == p.grad.data_ptr()
-                                        and runs[-1]["mend"] == st["exp_avg"].data_ptr())
+                                        and (gap == 0 or padding_only)
+                                        and runs[-1]["gend"] + 4 * gap == p.grad.data_ptr()
+                                        and runs[-1]["mend"] + 4 * gap == st["exp_avg"].data_ptr())
                 if contiguous_with_prev:
                     r = runs[-1]
-                    r["n"] += p.numel()
+                    r["n"] += gap + p.numel()
                 else:
                     runs.append(dict(owner=owner, step=step, p=p, st=st, n=p.numel()))
                     r = runs[-1]
                 r["end_ptr"] = p.data_ptr() + 4 * p.numel()
+                r["end_off"] = (p._sat_offset + p.numel()) if owner is not None else 0
                 r["gend"] = p.grad.data_ptr() + 4 * p.numel()
                 r["mend"] = st["exp_avg"].data_ptr() + 4 * p.numel()
             for r in runs:

@@ -1315,3 +1315,33 @@ def test_conv3x3_ws_kernel(sat, N, H, relu, bias, stem):
         outs.append(y.cpu())
     assert ((outs[0].double() - ref).abs().max() / ref.abs().max()).item() < 8e-3
     assert torch.equal(outs[0], outs[1])
+
+
+def test_adam_flat_runs_match_torch_adam(sat):
+    """sat_amd.Adam merges the decoder's parameters into runs over its flat buffer (across the alignment padding
+    between parameter groups) and updates each run in one launch: three steps must equal torch.optim.Adam on
+    copies of the same parameters and gradients, and a parameter whose grad is None is skipped (left untouched
+    and without state), as torch skips it."""
+    torch.manual_seed(0)
+    dec = sat.Decoder(300, 64, tf=True, ado=True, attention=True).to(DEV)
+    dec._ensure_flat(torch.device(DEV))
+    params = dict(dec.named_parameters())
+    active = dec.active_param_names()
+    skip = "attention.v.bias" if "attention.v.bias" in active else active[len(active) // 2]
+    ref = {n: p.detach().clone().requires_grad_(True) for n, p in params.items()}
+    opt = sat.Adam(dec.parameters(), lr=1e-3)
+    ropt = torch.optim.Adam(list(ref.values()), lr=1e-3)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    for _ in range(3):
+        dec._attach_grads()
+        for n in active:
+            gr = torch.randn(params[n].shape, device=DEV, generator=g)
+            params[n].grad.copy_(gr)
+            ref[n].grad = gr.clone()
+        params[skip].grad = None   # its flat gradient region keeps the random values: a run over it would move it
+        ref[skip].grad = None
+        opt.step()
+        ropt.step()
+    torch.cuda.synchronize()
+    for n, p in params.items():
+        assert torch.allclose(p.detach(), ref[n].detach(), rtol=1e-5, atol=1e-6), n
