@@ -475,10 +475,20 @@ namespace {
 // dst[c * ld_dst + r] = src[r * ld_src + c] for a rows x cols bf16 block (rows, cols, ld_src, ld_dst multiples of 8,
 // 16-B aligned rows): 64 x 64 tiles through LDS (16-B loads along the source rows, 16-B stores along the
 // destination rows)
-__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ src, long ld_src, int rows,
-                                                             int cols, bf16* __restrict__ dst, long ld_dst) {
+// two blocks per launch (the refresh's W_ih context columns and [U; f_beta; W_hh]): workgroup i < nx0 * ny0 takes
+// tile (i % nx0, i / nx0) of block 0, the rest tiles of block 1
+struct TransposePair {
+  const bf16* src[2]; long ld_src[2]; int rows[2], cols[2]; bf16* dst[2]; long ld_dst[2]; int nx[2], ntiles0;
+};
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(TransposePair a) {
+  const int k = (int)blockIdx.x < a.ntiles0 ? 0 : 1;
+  const int i = (int)blockIdx.x - (k ? a.ntiles0 : 0);
+  const bf16* __restrict__ src = a.src[k];
+  bf16* __restrict__ dst = a.dst[k];
+  const long ld_src = a.ld_src[k], ld_dst = a.ld_dst[k];
+  const int rows = a.rows[k], cols = a.cols[k];
   __shared__ bf16 tile[64][64 + 8];
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int r0 = (i / a.nx[k]) * 64, c0 = (i % a.nx[k]) * 64;
   const int tr = threadIdx.x >> 3, tc = (threadIdx.x & 7) * 8;   // 32 rows x 8 chunks of 8 per pass
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
@@ -514,12 +524,16 @@ extern "C" int sat_decoder_refresh_transposed(const SatDecoderDims* d, const Sat
   SAT_REQUIRE(lay->wih_ctx_t % 8 == 0 && lay->hcat_t % 8 == 0 && lay->wih % 8 == 0 && lay->hcat_w % 8 == 0);
   bf16* lp = (bf16*)params_lp;
   hipStream_t s = (hipStream_t)stream;
-  // W_ih [4E][E + D]: its context columns E.. as [D][4E]
-  hipLaunchKernelGGL(transpose_bf16_kernel, dim3(sat_cdiv(D, 64), sat_cdiv(4 * E, 64)), dim3(256), 0, s, lp + lay->wih + E, (long)(E + D),
-                     4 * E, D, lp + lay->wih_ctx_t, (long)4 * E);
-  // hcat [HG][E] as [E][HG]
-  hipLaunchKernelGGL(transpose_bf16_kernel, dim3(sat_cdiv(E, 64), sat_cdiv(HG, 64)), dim3(256), 0, s, lp + lay->hcat_w, (long)E,
-                     HG, E, lp + lay->hcat_t, (long)HG);
+  // one launch: W_ih [4E][E + D]'s context columns E.. as [D][4E], and hcat [HG][E] as [E][HG]
+  TransposePair a{};
+  a.src[0] = lp + lay->wih + E; a.ld_src[0] = E + D; a.rows[0] = 4 * E; a.cols[0] = D;
+  a.dst[0] = lp + lay->wih_ctx_t; a.ld_dst[0] = 4L * E;
+  a.src[1] = lp + lay->hcat_w; a.ld_src[1] = E; a.rows[1] = (int)HG; a.cols[1] = E;
+  a.dst[1] = lp + lay->hcat_t; a.ld_dst[1] = HG;
+  for (int k = 0; k < 2; ++k) a.nx[k] = sat_cdiv(a.cols[k], 64);
+  a.ntiles0 = a.nx[0] * sat_cdiv(a.rows[0], 64);
+  const int ntiles = a.ntiles0 + a.nx[1] * sat_cdiv(a.rows[1], 64);
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3(ntiles), dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
 
@@ -555,8 +569,8 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
 
   // fed tokens + embeddings
   if (d.tf) {
-    SAT_CHECK((hipError_t)sat_tokens_from_captions(captions, B, d.T, T1, w.tok, s));
-    SAT_CHECK((hipError_t)sat_embed_gather(c.F(lay->embedding), w.tok, B, T1, T1, E, d.dtype, w.emb_t, E, s));
+    SAT_CHECK((hipError_t)sat_embed_gather_captions(c.F(lay->embedding), captions, B, d.T, E, d.dtype, w.emb_t, E,
+                                                    w.tok, s));
   } else {
     hipLaunchKernelGGL(start_tokens_kernel, dim3(sat_cdiv(B, 256)), dim3(256), 0, s, w.tok, B, T1, d.start_token);
     SAT_LAUNCH_CHECK();

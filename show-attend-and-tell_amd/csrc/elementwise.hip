@@ -422,6 +422,29 @@ __global__ void embed_gather_kernel(const float* __restrict__ W, const int32_t* 
   for (int e = threadIdx.x; e < E; e += blockDim.x) dst[e] = (T)src[e];
 }
 
+// teacher forcing: the fed tokens straight from the int64 captions (tok[b, t] = captions[b, t], t < T-1) and
+// their embedding rows in one launch
+template <typename OT>
+__global__ void embed_gather_captions_kernel(const float* __restrict__ W, const int64_t* __restrict__ caps, int R,
+                                             int T, int T1, int E, OT* __restrict__ out, long out_ld,
+                                             int32_t* __restrict__ tok) {
+  const int r = blockIdx.x;
+  if (r >= R) return;
+  const int b = r / T1, t = r - b * T1;
+  const int id = (int)caps[(long)b * T + t];
+  if (threadIdx.x == 0) tok[r] = id;
+  const float* src = W + (long)id * E;
+  OT* dst = out + (long)r * out_ld;
+  if ((E & 3) == 0 && ((uintptr_t)src & 15) == 0) {
+    for (int e = 4 * threadIdx.x; e < E; e += 4 * blockDim.x) {
+      const float4 v = *(const float4*)(src + e);
+      dst[e] = (OT)v.x; dst[e + 1] = (OT)v.y; dst[e + 2] = (OT)v.z; dst[e + 3] = (OT)v.w;
+    }
+  } else {
+    for (int e = threadIdx.x; e < E; e += blockDim.x) dst[e] = (OT)src[e];
+  }
+}
+
 // ---- embedding backward: G[tok[r], :] += dX[r, :] (fp32 atomics) -------------
 __global__ void embed_scatter_kernel(const float* __restrict__ dX, const int32_t* __restrict__ tok, int R, int E,
                                      float* __restrict__ G) {
@@ -655,6 +678,19 @@ int sat_embed_gather(const float* W, const int32_t* tok, int B, int T1, long tok
   else
     hipLaunchKernelGGL(embed_gather_kernel<float>, dim3(R), dim3(256), 0, s, W, tok, R, tok_stride_b, T1, E,
                        (float*)out, out_ld);
+  return (int)hipGetLastError();
+}
+
+int sat_embed_gather_captions(const float* W, const int64_t* caps, int B, int T, int E, int dtype, void* out,
+                              long out_ld, int32_t* tok, hipStream_t s) {
+  const int T1 = T - 1, R = B * T1;
+  if (R <= 0) return 0;
+  if (dtype == SAT_BF16)
+    hipLaunchKernelGGL(embed_gather_captions_kernel<bf16>, dim3(R), dim3(128), 0, s, W, caps, R, T, T1, E, (bf16*)out,
+                       out_ld, tok);
+  else
+    hipLaunchKernelGGL(embed_gather_captions_kernel<float>, dim3(R), dim3(128), 0, s, W, caps, R, T, T1, E,
+                       (float*)out, out_ld, tok);
   return (int)hipGetLastError();
 }
 

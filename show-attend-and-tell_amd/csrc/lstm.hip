@@ -264,14 +264,6 @@ __global__ void row_sum_acc_kernel(const float* X, int R, int N, float* out) {
   out[n] += s;
 }
 
-__global__ void tokens_kernel(const int64_t* caps, int B, int T, int T1, int32_t* tok) {
-  const int n = B * T1;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const int b = i / T1, t = i - b * T1;
-    tok[i] = (int32_t)caps[(long)b * T + t];
-  }
-}
-
 }  // namespace
 
 #define DISPATCH_T(dtype, KERNEL, grid, ...)                                                   \
@@ -373,9 +365,5 @@ int sat_broadcast_rows(const void* src, int B, int D, int T1, int dtype, void* d
 }
 int sat_row_sum_accumulate(const float* X, int R, int N, float* out, hipStream_t s) {
   hipLaunchKernelGGL(row_sum_acc_kernel, dim3(sat_cdiv(N, 256)), dim3(256), 0, s, X, R, N, out);
-  return (int)hipGetLastError();
-}
-int sat_tokens_from_captions(const int64_t* caps, int B, int T, int T1, int32_t* tok, hipStream_t s) {
-  hipLaunchKernelGGL(tokens_kernel, dim3(grid_for((long)B * T1)), dim3(256), 0, s, caps, B, T, T1, tok);
   return (int)hipGetLastError();
 }

@@ -26,6 +26,9 @@ int sat_gemm_splits_atomically(const SatGemm& g);
 int sat_embed_gather(const float* W, const int32_t* tok, int B, int T1, long tok_stride_b, int E, int dtype,
                      void* out, long out_ld, hipStream_t s);
 int sat_embed_scatter_add(const float* dX, const int32_t* tok, int R, int E, float* G, hipStream_t s);
+// teacher forcing: tok[b, t] = captions[b, t] (t < T-1) and their embedding rows, one launch
+int sat_embed_gather_captions(const float* W, const int64_t* caps, int B, int T, int E, int dtype, void* out,
+                              long out_ld, int32_t* tok, hipStream_t s);
 int sat_argmax_rows(const void* X, int dtype, long ld, int B, int V, int32_t* out, long out_stride,
                     const float* emb, int E, void* emb_out, long emb_ld, hipStream_t s);
 int sat_cast_launch(const void* x, int xd, void* y, int yd, long n, hipStream_t s);
@@ -134,7 +137,6 @@ int sat_fill_const(float* p, long n, float v, hipStream_t s);
 int sat_zero_rows(float* p, long ld, long rows, long cols, hipStream_t s);   // graph-safe memset
 int sat_broadcast_rows(const void* src, int B, int D, int T1, int dtype, void* dst, hipStream_t s);
 int sat_row_sum_accumulate(const float* X, int R, int N, float* out, hipStream_t s);
-int sat_tokens_from_captions(const int64_t* caps, int B, int T, int T1, int32_t* tok, hipStream_t s);
 size_t sat_attention_part_floats(int B, int L, int D, int E, int dtype, int wg_target);
 // chunks of L one batch row's attention backward is split over (sat_attention_bwd_launch), aiming for wg_target
 // workgroups (0 = 256)
