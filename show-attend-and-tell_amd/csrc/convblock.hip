@@ -882,6 +882,8 @@ __device__ __forceinline__ void conv3x3_img_body(const bf16* __restrict__ x, con
   const int fr = lane & 15, fh = lane >> 4;
   // slice-major over groups of 8 consecutive workgroups (one per XCD under round-robin placement): the NSL
   // slices of one image group land on one XCD and share its input rows in L2
+  // (measured and removed: each XCD owning one slice -- XCD x streams slice x % 4 only -- cuts the per-XCD weight
+  // refetch, 2.9x -> ~2.3x of the algorithmic bytes, but runs 34.3-35.4 vs 33.5 us: not HBM-bound, profiles/r3_s39)
   const int slice = NSL == 1 ? 0 : (int)((blockIdx.x >> 3) % NSL);
   const int grp = NSL == 1 ? (int)blockIdx.x : (int)((blockIdx.x / (8 * NSL)) * 8 + (blockIdx.x & 7));
   const int ngrp = (nimg + G - 1) / G;

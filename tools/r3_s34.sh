@@ -1,0 +1,15 @@
+set -u
+OUT=gpurun_out/r3_s34; mkdir -p $OUT; export TMPDIR=/tmp
+timeout -k 10 200 python tools/head_gemms.py --split --split-wgs 96,160,224,320 > $OUT/head_split.log 2>&1 || { tail -5 $OUT/head_split.log; exit 1; }
+cat $OUT/head_split.log
+ab() {  # label, args...
+  local label=$1; shift; i=$((i+1))
+  timeout -k 10 200 python bench.py --steps 150 --no-cpu-baseline --fp32-steps 0 --no-diagnostics "$@" > $OUT/ab_$i.log 2>&1 || { tail -5 $OUT/ab_$i.log; exit 1; }
+  echo "[$label] $(python -c "import json,sys; d=json.loads([l for l in open('$OUT/ab_$i.log') if l.startswith('{')][-1]); print(d['value'], d['ms_per_step'], 'enc', d['encoder_trunk']['graph_ms_per_step'], 'dec', d['decoder_graphs_ms_per_step'])")"
+}
+i=0
+for r in 1 2; do
+ab "cfg2"
+ab "cfg2 split160" --policy gemm_split_wgs=160
+ab "cfg2 split224" --policy gemm_split_wgs=224
+done
