@@ -986,7 +986,8 @@ __global__ __launch_bounds__(512) void conv3x3_img_kernel(const bf16* __restrict
 // each and every m-block (each A fragment feeds two MFMAs; two workgroups fit a CU): 18.5 vs 19.4 us and 4.37 vs
 // 4.42-4.44 ms per B = 64 step against eight waves of 16 channels (profiles/r3_s24); weights 3 or 4 k-tiles ahead:
 // 18.6-18.9 vs 18.6 us (r3_s29).  At B = 128 the half-image kernel on four waves of 64 channels (one wave per SIMD,
-// VGPRs left to decoder waves): 32.4 vs 29.1 us, step 6.66 vs 6.50 ms (r3_s32).  Measured and removed: the
+// VGPRs left to decoder waves): 32.4 vs 29.1 us, step 6.66 vs 6.50 ms (r3_s32).  At B = 64 four 64-channel slices
+// per half image (two workgroups per CU): 19.5-20.0 vs 18.3-18.5 us, step 4.23-4.25 vs 4.04-4.13 ms (r3_s40).  Measured and removed: the
 // same four-wave form over whole images (31.5 vs 29.3 us at B = 128), and (profiles/r3_s13, r3_s14, r3_s16) two
 // m-groups of waves, weights 3 / 4 k-tiles ahead, whole images as four 64-channel slices -- all within noise.
 __global__ __launch_bounds__(256) void conv3x3_slice2_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
