@@ -861,6 +861,16 @@ __global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restric
   sat_stamp_end(st, t0);
 }
 
+// VGG19's block-5 convs (14 x 14, 512 -> 512, four launches): half images (one-row halo each side) x four
+// 128-channel slices, eight waves of 16 channels (130 KB of LDS, one workgroup per CU)
+__global__ __launch_bounds__(512) void conv3x3_half512_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                              const float* __restrict__ bias, bf16* __restrict__ y,
+                                                              int nbands, SatStamps st) {
+  const SatStampT0 t0 = sat_stamp_begin(st);
+  conv3x3_band_body<14, 7, 512, 4, 1, 2>(x, wf, bias, y, nbands);
+  sat_stamp_end(st, t0);
+}
+
 // The same idea for images small enough to stage whole (ResNet152 layer4's stride-1 c2: 7 x 7, 512 -> 512): a
 // workgroup takes G consecutive images (G * 49 pixels, their rows contiguous in memory and in LDS, plus the zero
 // row) and one of NSL output-channel slices; taps outside an image read the zero row.  The tile kernel runs this
@@ -1205,7 +1215,7 @@ extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int 
 }
 
 extern "C" int sat_conv3x3_frag_supported(int H, int W, int C, int dtype) {
-  return dtype == SAT_BF16 && ((H == 14 && W == 14 && C == 256) || (H == 28 && W == 28 && C == 128) ||
+  return dtype == SAT_BF16 && ((H == 14 && W == 14 && (C == 256 || C == 512)) || (H == 28 && W == 28 && C == 128) ||
                                (H == 7 && W == 7 && C == 512));
 }
 
@@ -1227,6 +1237,10 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
       hipLaunchKernelGGL(conv3x3_img_kernel<2>, dim3(groups), dim3(512), 0, s, xp, wp, b, yp, N, st);
     else
       hipLaunchKernelGGL(conv3x3_img_kernel<1>, dim3(groups), dim3(512), 0, s, xp, wp, b, yp, N, st);
+    return (int)hipGetLastError();
+  }
+  if (H == 14 && C == 512) {   // VGG19 block 5: half images x four 128-channel slices
+    hipLaunchKernelGGL(conv3x3_half512_kernel, dim3(sat_cdiv(2 * N, 8) * 8 * 4), dim3(512), 0, s, xp, wp, b, yp, 2 * N, st);
     return (int)hipGetLastError();
   }
   if (H == 28) {   // layer2 c2: 7-row bands, four workgroups per image

@@ -232,13 +232,16 @@ class Encoder(nn.Module):
                                  fused[1] if fused is not None else self._c2_frag_weights(blk)))
         else:
             first = True
+            hw = 224   # spatial size at this conv for the 224 x 224 input the plan assumes (forward checks the real one)
             for i, m in enumerate(mods):
                 if isinstance(m, nn.Conv2d):
                     relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
-                    plan.append(("conv", self._fold(m, None, IN_PAD if first else None), relu, None))
+                    f = self._fold(m, None, IN_PAD if first else None)
+                    plan.append(("conv", f, relu, self._conv_frag_weights(m, f, relu, hw)))
                     first = False
                 elif isinstance(m, nn.MaxPool2d):
                     plan.append(("pool", m.kernel_size, m.stride, m.padding))
+                    hw //= 2
         self._plan = plan
 
     def _fused_weights(self, plan, blk, ds):
@@ -257,6 +260,16 @@ class Encoder(nn.Module):
             w, b, _, _ = self._fold(conv, bn)
             frags.append((ops.mfma_frag_layout(w.reshape(w.shape[0], -1)), b))
         return tuple(frags)
+
+    def _conv_frag_weights(self, conv, folded, relu, hw):
+        """Fragment-layout weights of a VGG19 3x3 / stride-1 C -> C conv + ReLU that the staged-input kernel runs
+        at its spatial size (sat_conv3x3_frag: the 14 x 14, 512 -> 512 block-5 convs), else None."""
+        if not relu or conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1) \
+                or conv.in_channels != conv.out_channels or self.compute_dtype != torch.bfloat16 \
+                or not conv.weight.is_cuda or not ops.conv3x3_frag_supported(hw, hw, conv.out_channels, self.compute_dtype):
+            return None
+        w, b = folded[0], folded[1]
+        return ops.mfma_frag_layout(w.reshape(w.shape[0], -1)), b
 
     def _c2_frag_weights(self, blk):
         """Fragment-layout c2 weights of a stride-1 block whose 3x3 the band kernel runs (layer2), else None."""
@@ -349,6 +362,10 @@ class Encoder(nn.Module):
 
     def _run_step(self, y, step):
         if step[0] == "conv":
+            f = step[3]
+            if f is not None and self.c2_frag and y.shape[1] in self.c2_frag_sizes \
+                    and ops.conv3x3_frag_supported(y.shape[1], y.shape[2], y.shape[3], y.dtype):
+                return self._frag_conv("c2frag", ops.conv3x3_frag, y, f)
             return self._conv(y, step[1], step[2])
         if step[0] == "pool":
             return ops.maxpool2d_nhwc(y, step[1], step[2], step[3])
