@@ -83,7 +83,7 @@ def parse():
     ap.add_argument("--policy", default="",
                     help="extra SatPolicy fields for every encoder / decoder call, e.g. attn_bwd_chunks=1,gemm_stages=3 "
                          "or decoder_splits=2.0.0.0 (A/B; include/sat_hip.h)")
-    ap.add_argument("--c2-frag-sizes", default="7,14,28",
+    ap.add_argument("--c2-frag-sizes", default="7,14,28,112",
                     help="spatial sizes whose stride-1 3x3 convs run on the staged-input kernels (sat_conv3x3_frag); "
                          "the others on the tile kernel (A/B)")
     ap.add_argument("--fuse-layer2", action="store_true",

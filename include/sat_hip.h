@@ -175,7 +175,7 @@ int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int dtype, cons
                          const float* b1, const void* w2f, const float* b2, const void* w3f, const float* b3,
                          void* y, const SatPolicy* policy, void* stream);
 /* 1 if sat_conv3x3_frag runs this geometry (bf16: 14x14 C 256, 28x28 C 128, 7x7 C 512 -- the c2 of ResNet152's
- * layer3 / layer2 / layer4 identity blocks -- and 14x14 C 512, VGG19's block-5 convs), else 0. */
+ * layer3 / layer2 / layer4 identity blocks -- and VGG19's 14x14 C 512 block-5 and 112x112 C 128 block-2 convs), else 0. */
 int sat_conv3x3_frag_supported(int H, int W, int C, int dtype);
 /* 3x3 / stride 1 / pad 1 conv C -> C + folded bias + ReLU (a bottleneck's c2, encoder.py:13-17 through
  * torchvision), one workgroup per half image (14x14), 7-row band (28x28) or one / two whole images x a

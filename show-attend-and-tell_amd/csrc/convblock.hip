@@ -861,6 +861,18 @@ __global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restric
   sat_stamp_end(st, t0);
 }
 
+// VGG19 block 2's 112 x 112, 128 -> 128 conv as 2-row bands (one-row halo each side: 115 KB of LDS), every
+// workgroup streaming the whole 295 KB weight once for 224 output pixels, where the tile kernel fetches a 256-row
+// im2col A tile per 128 x 128 tile: 647-657 -> 542-548 us per launch (profiles/r3_s44).  Measured and removed: block
+// 1's 224 x 224, 64 -> 64 convs in the same form (two m-groups of waves): 858-860 vs 523 us.
+__global__ __launch_bounds__(512) void conv3x3_band112_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                              const float* __restrict__ bias, bf16* __restrict__ y,
+                                                              int nbands, SatStamps st) {
+  const SatStampT0 t0 = sat_stamp_begin(st);
+  conv3x3_band_body<112, 2, 128, 1, 1, 2>(x, wf, bias, y, nbands);
+  sat_stamp_end(st, t0);
+}
+
 // VGG19's block-5 convs (14 x 14, 512 -> 512, four launches): half images (one-row halo each side) x four
 // 128-channel slices, eight waves of 16 channels (130 KB of LDS, one workgroup per CU)
 __global__ __launch_bounds__(512) void conv3x3_half512_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
@@ -1216,7 +1228,7 @@ extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int 
 
 extern "C" int sat_conv3x3_frag_supported(int H, int W, int C, int dtype) {
   return dtype == SAT_BF16 && ((H == 14 && W == 14 && (C == 256 || C == 512)) || (H == 28 && W == 28 && C == 128) ||
-                               (H == 7 && W == 7 && C == 512));
+                               (H == 7 && W == 7 && C == 512) || (H == 112 && W == 112 && C == 128));
 }
 
 extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const void* x, const void* wf, const float* b,
@@ -1237,6 +1249,10 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
       hipLaunchKernelGGL(conv3x3_img_kernel<2>, dim3(groups), dim3(512), 0, s, xp, wp, b, yp, N, st);
     else
       hipLaunchKernelGGL(conv3x3_img_kernel<1>, dim3(groups), dim3(512), 0, s, xp, wp, b, yp, N, st);
+    return (int)hipGetLastError();
+  }
+  if (H == 112) {   // VGG19 block 2: 2-row bands
+    hipLaunchKernelGGL(conv3x3_band112_kernel, dim3(56 * N), dim3(512), 0, s, xp, wp, b, yp, 56 * N, st);
     return (int)hipGetLastError();
   }
   if (H == 14 && C == 512) {   // VGG19 block 5: half images x four 128-channel slices

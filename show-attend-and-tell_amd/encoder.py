@@ -162,8 +162,9 @@ class Encoder(nn.Module):
         # (sat_conv3x3_frag: input rows staged once in LDS, fragment-layout weights); False = the
         # tile kernel (A/B, tests)
         self.c2_frag = True
-        # ... at these spatial sizes (layer4 7, layer3 14, layer2 28); A/B: bench.py --c2-frag-sizes
-        self.c2_frag_sizes = (7, 14, 28)
+        # ... at these spatial sizes (layer4 7, layer3 14, layer2 28; VGG19 block 5 14, block 2 112);
+        # A/B: bench.py --c2-frag-sizes
+        self.c2_frag_sizes = (7, 14, 28, 112)
         # ... its c1 on the half-image 1x1 kernel (sat_conv1x1_frag: input slabs by LDS-DMA, weights
         # register-direct)
         self.c1_frag = True
