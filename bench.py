@@ -630,8 +630,9 @@ def main():
     enc = sat_amd.Encoder(args.network, dtype=torch.bfloat16).to(dev).eval()
     if args.fuse_every is None:
         args.fuse_every = 0   # profiles/r2_s62: none fused 6.79 ms, every 3rd 7.15, every block 7.48
-    if args.split_target is None:
-        args.split_target = 128 if args.network == "vgg19" else 64
+    if args.split_target is None:   # ResNet152 at B = 128: 96 (6.50 vs 6.53 ms; 6.76 vs 6.82 on a slower box), but
+        # 64 at B <= 64 (96 there: 4.21-4.23 vs 4.01-4.04 ms), profiles/r3_s46, r3_s47
+        args.split_target = 128 if args.network == "vgg19" else (96 if args.batch > 64 else 64)
     enc.fuse_layer2 = args.fuse_layer2
     enc.c2_frag_sizes = tuple(int(v) for v in args.c2_frag_sizes.split(",") if v)
     enc.fuse_blocks = (False if args.no_fuse_blocks or args.fuse_every == 0 else

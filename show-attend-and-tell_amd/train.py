@@ -363,7 +363,7 @@ def main(argv=None):
     encoder, decoder, word_dict, dt = build(args, device)
     decoder.record_tokens = False   # no fed-token record per training step
     if not args.no_overlap:   # the decoder shares the chip with the next batch's encoder (bench.py defaults)
-        decoder.split_target = 128 if args.network == "vgg19" else 64
+        decoder.split_target = 128 if args.network == "vgg19" else (96 if args.batch_size > 64 else 64)   # as bench.py
         # no layer3 block fused: the unfused c2 / c3 half-image kernels leave CUs to the decoder
         # (profiles/r2_s62_sched.txt)
         encoder.fuse_blocks = False
