@@ -63,9 +63,10 @@ def parse():
                          "64 with ResNet152 features, 128 with VGG19's: profiles/r2_s54_sched.txt)")
     ap.add_argument("--no-fuse-blocks", action="store_true",
                     help="run the layer3 identity bottlenecks as three conv launches (A/B of csrc/convblock.hip)")
-    ap.add_argument("--bwd", choices=["serial", "split"], default="split",
+    ap.add_argument("--bwd", choices=["auto", "serial", "split"], default="auto",
                     help="N = 1 decoder backward structure: one graph in order (serial), or two graphs as at N > 1 "
-                         "(split)")
+                         "(split: the head bucket's all-reduce runs between them); auto = serial at N = 1 (6.43-6.46 "
+                         "vs 6.48-6.54 ms split, profiles/r3_s51), split at N > 1")
     ap.add_argument("--no-transposed", action="store_true",
                     help="BPTT input-gradient products on the k-major weights instead of the transposed copies (A/B)")
     ap.add_argument("--no-skinny", action="store_true",

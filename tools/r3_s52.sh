@@ -1,0 +1,14 @@
+set -u
+OUT=gpurun_out/r3_s52; mkdir -p $OUT; export TMPDIR=/tmp
+timeout -k 10 300 python bench.py --no-cpu-baseline --fp32-steps 0 > $OUT/bench.log 2>&1 || { tail -5 $OUT/bench.log; exit 1; }
+python tools/bench_brief.py $OUT/bench.log | grep -v "^    "
+ab() {  # label, args...
+  local label=$1; shift; i=$((i+1))
+  timeout -k 10 200 python bench.py --steps 150 --no-cpu-baseline --fp32-steps 0 --no-diagnostics "$@" > $OUT/ab_$i.log 2>&1 || { tail -5 $OUT/ab_$i.log; exit 1; }
+  echo "[$label] $(python -c "import json,sys; d=json.loads([l for l in open('$OUT/ab_$i.log') if l.startswith('{')][-1]); print(d['value'], d['ms_per_step'])")"
+}
+i=0
+for r in 1 2 3; do
+ab "B64 serial" --batch 64
+ab "B64 split" --batch 64 --bwd split
+done
