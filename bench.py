@@ -47,13 +47,6 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--no-overlap", action="store_true",
                     help="graph mode: run the next batch's encoder after, not beside, this batch's decoder")
-    ap.add_argument("--enc-split", choices=["none", "layer2", "layer3", "layer4"], default="none",
-                    help="graph + overlap (ResNet152): the encoder runs as two graphs split at this stage; the "
-                         "decoder of batch i runs beside batch i+1's first part only, the second part (the fused, "
-                         "chip-filling layer3 blocks) starts when that decoder is done")
-    ap.add_argument("--enc-start", choices=["decoder", "phase2"], default="decoder",
-                    help="graph + overlap: batch i+1's encoder starts beside batch i's whole decoder (decoder), or "
-                         "only once its forward + head backward graph is done, beside the BPTT graph and Adam (phase2)")
     ap.add_argument("--feature-buffers", type=int, default=3, choices=[2, 3, 4],
                     help="graph + overlap: encoder output buffers (and graph sets) in flight; the next batch's encoder waits "
                          "for the decoder that last read its buffer (3: B = 64 4.08-4.11 vs 4.15 ms with 2, B = 128 "
@@ -102,8 +95,8 @@ def parse():
     ap.add_argument("--no-diagnostics", action="store_true",
                     help="skip the per-kernel roofline measurements after the timed region")
     ap.add_argument("--no-step-stamps", action="store_true",
-                    help="graph mode: no in-kernel launch timestamps in the encoder graphs (the in-step conv figures, "
-                         "LaunchStamps)")
+                    help="graph mode: no stamped diagnostic copies of the graphs after the timed region (the in-step "
+                         "conv / decoder figures, LaunchStamps / DecoderStamps; the timed graphs never carry stamps)")
     args = ap.parse_args()
     if args.bert:   # generate_json_data_bert.py:47,69: [CLS] + 30 + [SEP]; BertConfig() vocabulary
         args.vocab = 30522
@@ -235,16 +228,26 @@ class DecoderStamps:
         return out
 
     def group_spans_us(self):
-        st, en = self.buf[:, 1:, 0], self.buf[:, 1:, 1]
-        valid = st > 0
-        big = torch.iinfo(torch.int64).max
-        lo = torch.where(valid, st, torch.full_like(st, big)).min(dim=1).values.tolist()
-        hi = torch.where(valid, en, torch.zeros_like(en)).max(dim=1).values.tolist()
+        lo, hi = self._lo_hi()
         out = {}
         for gi, g in enumerate(self.groups):
             v = [(hi[k] - lo[k]) / 100.0 for k in range(gi * self.T1, (gi + 1) * self.T1) if hi[k] > 0]
             if v:
                 out[g] = v
+        return out
+
+    def group_intervals_us(self):
+        """Per group: first start of each of its launches to the first start of the next per-step launch of the
+        chain (forward: steps 0 .. T-2, backward: T-2 .. 0, groups in launch order; groups a build no longer
+        launches have no stamps and drop out) -- span plus the boundary after it, the per-dispatch duration a
+        rocprofv3 kernel trace reports.  The last launch of each chain has no successor and no interval."""
+        lo, hi = self._lo_hi()
+        T1, ng = self.T1, len(self.groups)
+        out = {}
+        for order, gs in ((range(T1), range(0, ng // 2)), (range(T1 - 1, -1, -1), range(ng // 2, ng))):
+            seq = [(g, t) for t in order for g in gs if hi[g * T1 + t] > 0]
+            for (g, t), (g2, t2) in zip(seq, seq[1:]):
+                out.setdefault(self.groups[g], []).append((lo[g2 * T1 + t2] - lo[g * T1 + t]) / 100.0)
         return out
 
 
@@ -397,10 +400,16 @@ def trunk_roofline(enc, imgs, launches, instep=None, overlapped=None, intervals=
         if dom["bound"] == "hbm":
             return dom["bytes"] / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s"
         return dom["flops"] / (us * 1e-6) / 1e12, BF16_DENSE_PEAK_TFLOPS, "TFLOP/s"
-    avg_us = dom["us"] / dom["n"]
+    # the headline duration is the launch interval (start of the launch to start of the next one, graphs replayed
+    # alone): the figure a rocprofv3 kernel trace of this command reproduces (its per-dispatch durations include the
+    # same boundary); the kernel's own span is kept beside it as avg_launch_us_span / frac_span
+    span_us = dom["us"] / dom["n"]
+    itv_us = dom["us_interval"] / dom["n"]
+    avg_us = itv_us if itv_us == itv_us else span_us
     achieved, peak, unit = rate(avg_us)
-    extra = {}
-    for key, k in (("overlapped", "us_overlapped"), ("interval", "us_interval")):
+    extra = {"duration": "interval" if itv_us == itv_us else "span",
+             "avg_launch_us_span": round(span_us, 2), "frac_span": round(rate(span_us)[0] / peak, 4)}
+    for key, k in (("overlapped", "us_overlapped"),):
         a = dom[k] / dom["n"]
         if a == a:
             extra[f"avg_launch_us_{key}"] = round(a, 2)
@@ -411,15 +420,14 @@ def trunk_roofline(enc, imgs, launches, instep=None, overlapped=None, intervals=
         "conv3x3_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c2frag" for i in idx)
         else "conv1x1_frag_kernel (csrc/convblock.hip), conv class" if all(last[i][0] == "c1frag" for i in idx)
         else "conv kernels, conv class")
-    timing = ("avg_launch_us: the kernels' own first-start / last-end in-kernel timestamps (LaunchStamps) of every "
-              "launch of the class in the captured encoder graphs replayed on their own after the timed region; "
-              "avg_launch_us_overlapped: the same timestamps inside the timed region's overlapped schedule (sharing "
-              "CUs with the decoder graphs); avg_launch_us_b2b: the class re-issued back to back into warm caches; "
-              f"avg_launch_us_eager_event_pairs: an event pair around every launch of {reps} eager forwards; "
-              "avg_launch_us_interval: first start of the launch to first start of the next one in the graphs "
-              "replayed alone (span + the boundary after it: the launch's share of the stream, the figure closest to "
-              "a rocprofv3 kernel trace's per-dispatch duration, which adds its own signalling: "
-              "profiles/r3_s8/prof_summary.json)"
+    timing = ("avg_launch_us (frac, achieved): first start of each launch of the class to the first start of the next "
+              "launch, from in-kernel timestamps (LaunchStamps) in stamped copies of the encoder graphs replayed on "
+              "their own after the timed region -- the kernel's span plus the boundary after it, the figure a "
+              "rocprofv3 kernel trace of this command reproduces (profiles/<round>/prof_summary.json "
+              "bench_over_rocprof); avg_launch_us_span / frac_span: the kernels' own first-start / last-end span; "
+              "avg_launch_us_overlapped: the span inside the overlapped schedule (sharing CUs with the decoder "
+              "graphs); avg_launch_us_b2b: the class re-issued back to back into warm caches; "
+              f"avg_launch_us_eager_event_pairs: an event pair around every launch of {reps} eager forwards"
               if instep is not None else
               "avg_launch_us: an event pair around every launch of the eager forwards (no in-kernel timestamps)")
 
@@ -517,14 +525,15 @@ def cpu_baseline(args):
                                          "parameters not frozen, encoder.py:13-17)"}}
 
 
-def decoder_step_roofline(dec, enc, imgs, caps, instep=None, overlapped=None, reps=20):
+def decoder_step_roofline(dec, enc, imgs, caps, instep=None, overlapped=None, intervals=None, reps=20):
     """The per-time-step decoder kernels (the fused attention + LSTM step of SURVEY 8(d) and the per-step
-    GEMMs) against 8 TB/s: algorithmic bytes per launch / time.  Per group, up to three durations [us]:
-    ``us`` the kernels' own first-start / last-end timestamps in the timed decoder graphs replayed on their own
-    after the timed region (DecoderStamps, ``instep``); ``us_overlapped`` the same inside the timed region's
-    overlapped schedule; ``us_b2b`` each group of the middle step re-issued ``reps`` times back to back between
-    HIP events (sat_decoder_step_bench).  A rocprofv3 kernel trace reports ~2 us more per decoder dispatch (its
-    per-dispatch signalling; profiles/r3_s8/prof_summary.json)."""
+    GEMMs) against 8 TB/s: algorithmic bytes per launch / time.  Per group, up to four durations [us]:
+    ``us`` (the frac figures) the launch interval -- first start of the launch to the first start of the next
+    per-step launch -- from in-kernel timestamps in stamped copies of the decoder graphs replayed on their own
+    after the timed region (DecoderStamps, ``intervals``): what a rocprofv3 kernel trace reports per dispatch;
+    ``us_span`` the kernels' own first-start / last-end span there (``instep``); ``us_overlapped`` the span
+    inside the overlapped schedule; ``us_b2b`` each group of the middle step re-issued ``reps`` times back to
+    back between HIP events (sat_decoder_step_bench)."""
     from sat_amd.diagnostics import FUSED, decoder_step_kernels
     with torch.no_grad():
         feats = enc(imgs)
@@ -532,9 +541,9 @@ def decoder_step_roofline(dec, enc, imgs, caps, instep=None, overlapped=None, re
 
     def avg(d):
         return {g: sum(v) / len(v) for g, v in (d or {}).items() if v}
-    t_span, t_ov = avg(instep), avg(overlapped)
-    primary = t_span or times_b2b
-    times = {g: primary.get(g, times_b2b[g]) for g in times_b2b}
+    t_span, t_ov, t_itv = avg(instep), avg(overlapped), avg(intervals)
+    primary = t_itv or t_span or times_b2b
+    times = {g: primary[g] for g in times_b2b if g in primary and times_b2b[g] > 0}
 
     def frac(b, us):
         return b / (us * 1e-6) / 1e9 / HBM_PEAK_GBS
@@ -544,25 +553,28 @@ def decoder_step_roofline(dec, enc, imgs, caps, instep=None, overlapped=None, re
             continue
         groups[g] = {"us": round(us, 2), "mb": round(by[g] / 1e6, 2), "gbs": round(by[g] / (us * 1e-6) / 1e9, 1),
                      "frac": round(frac(by[g], us), 4), "us_b2b": round(times_b2b[g], 2)}
-        for key, t in (("us_overlapped", t_ov),):
+        for key, t in (("us_span", t_span), ("us_overlapped", t_ov)):
             if g in t:
                 groups[g][key] = round(t[g], 2)
 
     def summary(keys):
-        by_ = sum(by[g] for g in keys if g in groups)
-        out = {}
-        for key, t in (("", times), ("_overlapped", t_ov), ("_b2b", times_b2b)):
-            if all(g in t for g in keys if g in groups):
-                us = sum(t[g] for g in keys if g in groups)
+        keys = [g for g in keys if g in groups]
+        by_ = sum(by[g] for g in keys)
+        out = {"kernels": keys, "launches_per_step": len(keys)}
+        for key, t in (("", times), ("_span", t_span), ("_overlapped", t_ov), ("_b2b", times_b2b)):
+            if keys and all(g in t for g in keys):
+                us = sum(t[g] for g in keys)
                 out[f"us_per_step{key}"] = round(us, 2)
                 out[f"frac{key}"] = round(frac(by_, us), 4)
-        out["achieved"] = round(by_ / (out["us_per_step"] * 1e-6) / 1e9, 1)
+        out["achieved"] = round(by_ / (out["us_per_step"] * 1e-6) / 1e9, 1) if "us_per_step" in out else None
         return out
-    src = ("us: the kernels' own first-start / last-end in-kernel timestamps in the timed decoder graphs replayed on "
-           "their own; us_overlapped: the same inside the timed region's overlapped schedule; " if t_span else "us: ") + \
+    src = ("us (frac): launch interval -- first start to the next per-step launch's first start -- from in-kernel "
+           "timestamps in stamped copies of the decoder graphs replayed on their own (the per-dispatch duration of "
+           "a rocprofv3 kernel trace); us_span: the kernels' own first-start / last-end span there; us_overlapped: "
+           "the span inside the overlapped schedule; " if t_itv else "us: ") + \
         f"us_b2b: each group of step (T-1)/2 re-issued {reps}x back to back between HIP events"
     return {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "timing": src, "groups": groups,
-            "fused_attention_lstm": dict(kernels=list(FUSED), **summary(FUSED)),
+            "fused_attention_lstm": summary(FUSED),
             "all_step_kernels": summary(list(groups))}
 
 
@@ -679,69 +691,55 @@ def main():
 
     use_graph = not args.no_graph
     overlap = use_graph and not args.no_overlap
-    g_encA = None
-    stamps_enc, stamps_dec = [], []   # in-kernel timestamps: LaunchStamps per encoder graph, DecoderStamps per pair
-    if use_graph:
-        # hipGraphs: the encoder trunk (so its kernels can be bracketed with events) and decoder
-        # fwd + loss + BPTT.  Adam and the RCCL all-reduce run eagerly after replay (Adam's bias
-        # corrections are step-dependent host scalars).  With --overlap (default) there are two of
-        # each, over two feature buffers: the frozen encoder of batch i+1 runs on its own stream
-        # while the decoder of batch i, its all-reduce and Adam run on the main stream (the
-        # encoder does not read any decoder parameter), so the latency-bound decoder kernels and
-        # the gradient exchange share the chip with the conv trunk.
-        nbuf = args.feature_buffers if overlap else 1
-        # encoder part A (plan[:split], beside the previous batch's decoder) and part B (plan[split:])
-        split = 0
-        if overlap and args.network == "resnet152" and args.enc_split != "none":
-            split = enc.stage_starts()[{"layer2": 1, "layer3": 2, "layer4": 3}[args.enc_split]]
-        stamp_enc = not args.no_step_stamps and not split
-        g_encA = [torch.cuda.CUDAGraph() for _ in range(nbuf)] if split else None
-        # one private memory pool per graph: no intermediate of one graph aliases another's
-        g_enc = [torch.cuda.CUDAGraph() for _ in range(nbuf)]
-        g_dec = [torch.cuda.CUDAGraph() for _ in range(nbuf)]   # fwd + loss + backward phase 1 (output head)
-        g_rec = [torch.cuda.CUDAGraph() for _ in range(nbuf)]   # backward phase 2 (BPTT + remaining wgrads)
-        feats_static, loss_static = [], []
-        n_plan = len(enc.compiled_plan(imgs.device, torch.bfloat16))
+    nbuf = args.feature_buffers if overlap else 1
+    # backward phase 1 (output head) and phase 2 (BPTT) as two graphs, the head bucket's all-reduce (N > 1)
+    # issued between them; --bwd serial: one graph
+    split_bwd = world > 1 or args.bwd == "split"
+    launches = conv_launches(args.network, B, fused=enc.fuse_blocks, fused2=enc.fuse_layer2)
+
+    def capture(stamped):
+        """hipGraphs of the step over ``nbuf`` feature buffers: per buffer the encoder trunk, the decoder's forward +
+        loss + backward phase 1 (output head) and, with split_bwd, phase 2 (BPTT + the remaining weight gradients).
+        Adam and the RCCL all-reduce run eagerly between replays (Adam's bias corrections are step-dependent host
+        scalars).  With overlap (default) the frozen encoder of batch i+1 runs on its own stream while the decoder
+        of batch i, its all-reduce and Adam run on the main stream (the encoder reads no decoder parameter).
+        stamped: every conv launch and every per-step decoder launch writes in-kernel timestamps (the diagnostic
+        copies captured after the timed region; the timed graphs carry no stamp pointers at all)."""
+        G = dict(enc=[], dec=[], rec=[], feats=[], loss=[], stamps_enc=[], stamps_dec=[])
         for k in range(nbuf):
-            if split:
-                with torch.cuda.graph(g_encA[k]):
-                    with torch.no_grad():
-                        mid = enc(imgs, steps=(0, split))
-                with torch.cuda.graph(g_enc[k]):
-                    with torch.no_grad():
-                        feats_static.append(enc(mid, steps=(split, n_plan)))
-            else:
-                if stamp_enc:   # every conv launch of this graph writes its in-kernel timestamps
-                    stamps_enc.append(LaunchStamps(len(conv_launches(args.network, B, fused=enc.fuse_blocks, fused2=enc.fuse_layer2)), dev,
-                                                   base=policy))
-                    enc.launch_policy = stamps_enc[-1].next_policy
-                with torch.cuda.graph(g_enc[k]):
-                    with torch.no_grad():
-                        feats_static.append(enc(imgs))
-                enc.launch_policy = None
-        # backward phase 1 (output head) and phase 2 (BPTT) as two graphs, the head bucket's all-reduce
-        # (N > 1) issued between them; --bwd serial: one graph
-        split_bwd = world > 1 or args.bwd == "split"
+            if stamped:
+                G["stamps_enc"].append(LaunchStamps(len(launches), dev, base=policy))
+                enc.launch_policy = G["stamps_enc"][-1].next_policy
+            g = torch.cuda.CUDAGraph()   # one private memory pool per graph: no intermediate aliases another's
+            with torch.cuda.graph(g):
+                with torch.no_grad():
+                    G["feats"].append(enc(imgs))
+            enc.launch_policy = None
+            G["enc"].append(g)
         dec.defer_recurrent_backward(split_bwd)
         for k in range(nbuf):
-            if not args.no_step_stamps:   # the per-step kernels of this graph pair write in-kernel timestamps
-                stamps_dec.append(DecoderStamps(args.seq, dev, base=policy))
-                dec.policy = stamps_dec[-1].policy
+            if stamped:
+                G["stamps_dec"].append(DecoderStamps(args.seq, dev, base=policy))
+                dec.policy = G["stamps_dec"][-1].policy
             opt.zero_grad(set_to_none=True)   # each capture overwrites the gradients (beta = 0)
-            with torch.cuda.graph(g_dec[k]):
-                preds, alphas = dec(feats_static[k], caps)
+            gd, gr = torch.cuda.CUDAGraph(), None
+            with torch.cuda.graph(gd):
+                preds, alphas = dec(G["feats"][k], caps)
                 loss_k, _ = sat_amd.caption_loss(preds, alphas, caps, pad_id=pad_id, skip_ids=skip_ids)
                 loss_k.backward()
             if split_bwd:
-                with torch.cuda.graph(g_rec[k]):
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
                     dec.finish_backward()
-            else:
-                g_rec[k] = None
-            loss_static.append(loss_k)
+            G["dec"].append(gd)
+            G["rec"].append(gr)
+            G["loss"].append(loss_k)
             dec.policy = policy
         dec.defer_recurrent_backward(False)
         torch.cuda.synchronize()
+        return G
 
+    G = capture(False) if use_graph else None
     enc_events = []
     if overlap and args.stream_priority != "equal":
         lo, hi = torch.cuda.Stream.priority_range()
@@ -753,65 +751,49 @@ def main():
     else:
         s_main = torch.cuda.current_stream()
         s_enc = torch.cuda.Stream() if overlap else s_main
-    nb = len(g_enc) if use_graph else 1
-    ev_enc = [torch.cuda.Event() for _ in range(max(nb, 2))]
-    ev_dec = [torch.cuda.Event() for _ in range(max(nb, 2))]
+    ev_enc = [torch.cuda.Event() for _ in range(max(nbuf, 2))]
+    ev_dec = [torch.cuda.Event() for _ in range(max(nbuf, 2))]
     dec_events = []   # (start, end) of each batch's decoder graphs on s_main (after its wait for the features)
-    ev_ph1 = torch.cuda.Event()   # --enc-start phase2: the decoder's forward + head backward graph is done
 
-    def replay_encoder(k, wait_dec, dec_ev=None):
-        """Batch k's encoder on s_enc.  wait_dec: feature buffer k was last read by the decoder two
-        batches ago.  Split encoder: part A right away (beside the running decoder), part B after
-        dec_ev (that decoder's end), so the chip-filling fused blocks do not starve it."""
+    def replay_encoder(G, k, wait_dec):
+        """Batch k's encoder on s_enc.  wait_dec: feature buffer k was last read by the decoder nbuf batches ago."""
         with torch.cuda.stream(s_enc):
             if wait_dec:
                 s_enc.wait_event(ev_dec[k])
-            if args.enc_start == "phase2" and dec_ev is not None:
-                s_enc.wait_event(ev_ph1)
-            if g_encA is not None:   # encoder time = the two parts' own spans (not the wait between)
-                st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                st.record(s_enc)
-                g_encA[k].replay()
-                en.record(s_enc)
-                enc_events.append((st, en))
-                if dec_ev is not None:
-                    s_enc.wait_event(dec_ev)
             st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             st.record(s_enc)
-            g_enc[k].replay()
+            G["enc"][k].replay()
             en.record(s_enc)
             ev_enc[k].record(s_enc)
         enc_events.append((st, en))
 
-    def run(n):
+    def run(n, G):
         """n full train steps (encoder fwd, decoder fwd + loss + bwd, all-reduce, Adam)."""
         loss = None
-        if use_graph:
-            replay_encoder(0, False)
+        if G is not None:
+            replay_encoder(G, 0, False)
         for i in range(n):
-            if use_graph:
-                k = i % len(g_enc)
+            if G is not None:
+                k = i % nbuf
                 s_main.wait_event(ev_enc[k])
                 d_st, d_en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 d_st.record(s_main)
-                g_dec[k].replay()
-                if args.enc_start == "phase2":
-                    ev_ph1.record(s_main)
+                G["dec"][k].replay()
                 # DP: the output-head bucket is final after phase 1 -> its all-reduce runs on RCCL's
                 # stream beside the BPTT graph; the rest follows phase 2 (SURVEY 8e)
                 w1 = allreduce_bucket_async(dec, 1) if world > 1 else None
-                if g_rec[k] is not None:
-                    g_rec[k].replay()
+                if G["rec"][k] is not None:
+                    G["rec"][k].replay()
                 w2 = allreduce_bucket_async(dec, 2) if world > 1 else None
                 d_en.record(s_main)
                 dec_events.append((d_st, d_en))
                 ev_dec[k].record(s_main)
-                loss = loss_static[k]
+                loss = G["loss"][k]
                 if i + 1 < n:
-                    if overlap:   # buffer (i + 1) % nb was last read by batch i + 1 - nb's decoder
-                        replay_encoder((i + 1) % nb, i >= nb - 1, ev_dec[k])
+                    if overlap:   # buffer (i + 1) % nbuf was last read by batch i + 1 - nbuf's decoder
+                        replay_encoder(G, (i + 1) % nbuf, i >= nbuf - 1)
                     else:
-                        replay_encoder(0, False)
+                        replay_encoder(G, 0, False)
                 if world > 1:
                     w1.wait()
                     w2.wait()
@@ -823,9 +805,7 @@ def main():
             opt.step()
         return loss
 
-    for st in stamps_enc + stamps_dec:   # timestamps off for the timed region
-        st.enable(False)
-    run(2)   # replay warm-up
+    run(2, G)   # replay warm-up
     enc_events.clear()
     dec_events.clear()
     torch.cuda.synchronize()
@@ -833,7 +813,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    loss = run(args.steps)
+    loss = run(args.steps, G)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -842,33 +822,39 @@ def main():
         t = torch.tensor([elapsed], device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    launches = conv_launches(args.network, B, fused=enc.fuse_blocks, fused2=enc.fuse_layer2)
+    loss_v = loss.item()
     enc_ms = sum(s.elapsed_time(e) for s, e in enc_events) if use_graph else None
     dec_ms = sum(s.elapsed_time(e) for s, e in dec_events) if use_graph and dec_events else None
     diag_phase = None
-    if (stamps_enc or stamps_dec) and not args.no_diagnostics:
-        # diagnostic phase (every rank: the all-reduces are collective): the same overlapped schedule with
-        # the kernels' timestamps switched on
+    stamps_enc, stamps_dec = [], []
+    if use_graph and not args.no_diagnostics and not args.no_step_stamps:
+        # diagnostic phase (every rank: the all-reduces are collective): stamped copies of the graphs, captured
+        # now (the timed graphs are released first), run in the same overlapped schedule with the timestamps on
+        loss = None
+        G = None
+        torch.cuda.synchronize()
+        G = capture(True)
+        stamps_enc, stamps_dec = G["stamps_enc"], G["stamps_dec"]
+        run(2, G)
         for st in stamps_enc + stamps_dec:
             st.enable(True)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         n_diag = max(4, min(20, args.steps))
-        run(n_diag)
+        run(n_diag, G)
         torch.cuda.synchronize()
         diag_phase = {"steps": n_diag, "ms_per_step": round(1000 * (time.perf_counter() - t1) / n_diag, 3)}
         for st in stamps_enc + stamps_dec:
             st.enable(False)
-    loss_v = loss.item()
     diag = rank == 0 and not args.no_diagnostics
 
-    def collect():
-        conv = instep_conv_durations(stamps_enc, launches) if stamps_enc else None
+    def collect(intervals=False):
+        conv = instep_conv_durations(stamps_enc, launches, intervals=intervals) if stamps_enc else None
         decd = None
         if stamps_dec:
             decd = {}
             for sd in stamps_dec:
-                for g, v in sd.group_spans_us().items():
+                for g, v in (sd.group_intervals_us() if intervals else sd.group_spans_us()).items():
                     decd.setdefault(g, []).extend(v)
         return conv, decd
 
@@ -879,8 +865,8 @@ def main():
     overlap_conv, overlap_dec = collect() if diag_phase else (None, None)
     chain_overlapped = chains() if diag_phase and stamps_dec else None
     chain_alone = None
-    alone_conv = alone_dec = alone_intervals = None
-    if diag and diag_phase and use_graph:
+    alone_conv = alone_dec = alone_intervals = alone_dec_intervals = None
+    if diag and diag_phase:
         # graph-alone phase: each encoder graph, then each decoder graph pair, replayed on its own (nothing
         # beside it) with the timestamps on -- the kernels' durations as a rocprofv3 kernel trace of this
         # command sees them (the trace all but serialises the two streams); the overlapped figures above
@@ -888,24 +874,24 @@ def main():
         for st in stamps_enc + stamps_dec:
             st.enable(True)
         torch.cuda.synchronize()
-        for k in range(len(g_enc)):
+        for k in range(nbuf):
             for _ in range(3):
-                g_enc[k].replay()
+                G["enc"][k].replay()
                 torch.cuda.synchronize()
             for _ in range(3):
-                g_dec[k].replay()
-                if g_rec[k] is not None:
-                    g_rec[k].replay()
+                G["dec"][k].replay()
+                if G["rec"][k] is not None:
+                    G["rec"][k].replay()
                 torch.cuda.synchronize()
         alone_conv, alone_dec = collect()
+        alone_intervals, alone_dec_intervals = collect(intervals=True)
         chain_alone = chains() if stamps_dec else None
-        alone_intervals = instep_conv_durations(stamps_enc, launches, intervals=True) if stamps_enc else None
         for st in stamps_enc + stamps_dec:
             st.enable(False)
     roof, trunk = trunk_roofline(enc, imgs, launches, instep=alone_conv or overlap_conv,
                                  overlapped=overlap_conv, intervals=alone_intervals) if diag else (None, None)
     step_kernels = decoder_step_roofline(dec, enc, imgs, caps, instep=alone_dec or overlap_dec,
-                                         overlapped=overlap_dec) if diag else None
+                                         overlapped=overlap_dec, intervals=alone_dec_intervals) if diag else None
     if step_kernels is not None and (chain_alone or chain_overlapped):
         step_kernels["step_chain"] = dict(alone=chain_alone, overlapped=chain_overlapped,
                                           note="per time step: first-kernel start to the next step's first-kernel "
@@ -937,6 +923,10 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1000 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            # this line measures one point of the curve: per-GPU work is fixed (weak scaling), and the 1 -> 8 curve
+            # exists only where the driver's SCALE runs (N = 1, 2, 4, 8 on one node) measured it
+            "scaling_curve": ("unmeasured: N = 1 only (the 2 / 4 / 8-GPU points come from the driver's SCALE runs)"
+                              if world == 1 else f"one point, N = {world}"),
             "dtype": "bf16", "data": "synthetic (224x224 N(0,1) images, random-token captions, random-init weights)",
             "config": {"workload": f"{'Flickr8k' if args.bert else 'COCO'}-shaped {args.network} encoder (bf16 fwd) + attention/{'greedy' if args.no_tf else 'tf'}/{'bert' if args.bert else 'ado'} decoder train "
                                    f"step, V={args.vocab}, T={args.seq}",
@@ -947,8 +937,7 @@ def main():
             "diagnostic_phase": dict(diag_phase, note="after the timed region: the same overlapped graphs with the "
                                      "kernels' in-kernel timestamps on (roofline in-step figures)") if diag_phase else None,
             "decoder_graphs_ms_per_step": round(dec_ms / args.steps, 3) if dec_ms else None,
-            "encoder_trunk": dict(trunk or {}, graph_ms_per_step=(round(enc_ms / args.steps, 3) if enc_ms else None),
-                                  split_at=args.enc_split if g_encA is not None else None),
+            "encoder_trunk": dict(trunk or {}, graph_ms_per_step=(round(enc_ms / args.steps, 3) if enc_ms else None)),
             "loss": round(loss_v, 4),
         }
         if fp32_leg is not None:

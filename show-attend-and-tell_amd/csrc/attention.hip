@@ -716,7 +716,13 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   __syncthreads();
   if (tid == 0) {
     const unsigned prev = __hip_atomic_fetch_add(a.ticket + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = prev == (unsigned)(NL - 1);
+    const bool last = prev == (unsigned)(NL - 1);
+    if (last) {   // agent-scope acquire on the reading CU besides the sc1 loads below (cdna_hip_programming.md §6
+                  // Guideline 16): one fence per row's last arriver, only on the NL > 1 path (small batches)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
   }
   __syncthreads();
   if (!s_last) return;   // workgroup-uniform

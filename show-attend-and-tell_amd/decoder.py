@@ -301,7 +301,11 @@ class Decoder(nn.Module):
         d.start_token = self.tokenizer.cls_token_id if self.use_bert else 0
         d.has_dropout_mask = int(self.training and self.dropout_mask is not None)
         d.split_target = int(self.split_target)
-        d.policy = L.policy_ptr(self.policy)
+        # the forward's own copy of the policy: carve() sizes and places the workspace regions from it, so a later
+        # (deferred) backward must see exactly the forward's fields even if self.policy is edited in between
+        if self.policy is not None:
+            d._policy = L.SatPolicy.from_buffer_copy(self.policy)
+            d.policy = ctypes.pointer(d._policy)
         # dropout masks: host seed drawn once per module from torch's RNG (train.py:37-43 seeding)
         # XOR a device step counter the forward itself advances -> graph replays draw fresh masks
         if self.training:

@@ -40,7 +40,10 @@ class _CaptionLossFn(torch.autograd.Function):
         ctx.save_for_backward(preds_c, caps)
         ctx.ws, ctx.dims, ctx.alpha_c = ws, (B, T, V, Lf), float(alpha_c)
         ctx.relu = bool(getattr(preds, "_sat_relu_logits", False))   # set by sat_amd.Decoder (ado)
-        loss, metrics = out[0], out[1:7]   # views of the kernel's output (no copy launches in the step)
+        # metrics: a view of the kernel's output (never modified by callers); loss: its own 4-byte tensor, so a
+        # caller may scale it in place (gradient accumulation, loss.mul_) -- a view of a custom Function's output
+        # buffer would make autograd reject that
+        loss, metrics = out[0].clone(), out[1:7]
         ctx.mark_non_differentiable(metrics)
         return loss, metrics
 

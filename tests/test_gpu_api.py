@@ -1,0 +1,85 @@
+"""Public-API behaviour of the modules around the HIP path (train.py:133-164 call pattern).
+
+* caption_loss returns a loss the caller may scale out of place or in place before backward (gradient
+  accumulation divides the loss, AMP-style loops scale it in place) with the gradient scaled accordingly;
+* a decoder forward keeps its own copy of the SatPolicy it ran with: editing dec.policy between a forward and its
+  (deferred) backward changes nothing, because the workspace regions are placed from the forward's policy.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import sat_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def sat():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import sat_amd
+    return sat_amd
+
+
+def _setup(sat, seed=5):
+    V, D, Lf, E, B, T = 60, 64, 16, 512, 3, 7
+    p = O.make_decoder_params(V, D, E, True, seed)
+    rng = np.random.default_rng(seed)
+    feats = torch.from_numpy(rng.standard_normal((B, Lf, D)).astype(np.float32)).to(DEV)
+    caps = O.make_captions(B, T, V, seed + 1).to(DEV)
+    dec = sat.Decoder(V, D, tf=True, ado=True, attention=True)
+    dec.load_state_dict(p, strict=True)
+    return dec.to(DEV).eval(), feats, caps
+
+
+def _grads(dec):
+    return {n: p.grad.detach().clone() for n, p in dec.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.parametrize("scale_mode", ["div", "inplace"])
+def test_loss_can_be_scaled_before_backward(sat, scale_mode):
+    dec, feats, caps = _setup(sat)
+    preds, alphas = dec(feats, caps)
+    loss, _ = sat.caption_loss(preds, alphas, caps)
+    loss.backward()
+    torch.cuda.synchronize()
+    ref = _grads(dec)
+    dec.zero_grad(set_to_none=True)
+    preds, alphas = dec(feats, caps)
+    loss, _ = sat.caption_loss(preds, alphas, caps)
+    if scale_mode == "div":
+        loss = loss / 2
+    else:
+        loss.mul_(0.5)
+    loss.backward()
+    torch.cuda.synchronize()
+    got = _grads(dec)
+    assert sorted(got) == sorted(ref)
+    for n, g in got.items():
+        assert torch.allclose(g, ref[n] * 0.5, rtol=1e-6, atol=1e-12), n
+
+
+def test_policy_edit_between_forward_and_deferred_backward(sat):
+    dec, feats, caps = _setup(sat)
+    feats = feats.bfloat16()
+    dec.train()
+    dec.dropout_mask = torch.ones(feats.shape[0], caps.shape[1] - 1, 512, dtype=torch.uint8, device=DEV)
+
+    def step(edit):
+        dec.zero_grad(set_to_none=True)
+        dec.policy = sat.Policy(decoder_splits=[2, 2, 2, 2])
+        dec.defer_recurrent_backward(True)
+        preds, alphas = dec(feats, caps)
+        sat.caption_loss(preds, alphas, caps)[0].backward()
+        if edit:   # a different split layout after the forward: the deferred phase 2 must not see it
+            dec.policy.decoder_splits[:] = [4, 4, 4, 4]
+            dec.policy.attn_bwd_chunks = 3
+        dec.finish_backward()
+        dec.defer_recurrent_backward(False)
+        torch.cuda.synchronize()
+        return _grads(dec)
+    a, b = step(False), step(True)
+    for n in a:
+        assert torch.equal(a[n], b[n]), n

@@ -1,0 +1,73 @@
+#!/bin/bash
+# One GPU-box session: every GPU step runs under its own time limit, the script stops at the first
+# failing GPU step (no retries), and every log lands under gpurun_out/TAG/.
+#
+# usage: bash tools/session.sh TAG step [step...]
+#   tests              the whole GPU suite (-m gpu)
+#   tests:EXPR         GPU tests selected by -k EXPR
+#   smoke              __graft_entry__.smoke()
+#   bench              the default bench line (the driver's command)
+#   bench64            the B = 64 line (cfg2 / cfg3's per-rank shape), no CPU baseline / fp32 leg
+#   benchq             a quick B = 128 line (100 steps, no CPU baseline / fp32 leg)
+#   cfg4 | cfg5        the --no-tf / --bert --network vgg19 lines
+#   prof               rocprofv3 --kernel-trace --stats of the default bench command (+ tools/prof_summary.py)
+#   pmcdec             two PMC passes (FETCH_SIZE, WRITE_SIZE) over the decoder's per-step kernels
+#                      (tools/decoder_pmc.py; summary -> gpurun_out/TAG/pmc_decoder.json)
+#   ab:LABEL:ARGS      one A/B bench line (ARGS comma-separated bench.py flags, e.g. ab:st80:--split-target,80);
+#                      prints value and ms/step
+#   py:SCRIPT[:ARGS]   python SCRIPT ARGS (comma-separated) under a 300 s limit
+set -u
+TAG=${1:?tag}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "[$(date +%T)] $name: $*"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc"
+  tail -3 "$OUT/$name.log" | cut -c1-400
+  return $rc
+}
+line() {  # value and ms/step of a bench log
+  python - "$1" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+print(d["value"], d["ms_per_step"])
+PY
+}
+QUIET="--no-cpu-baseline --fp32-steps 0"
+n=0
+for s in "$@"; do
+  n=$((n + 1))
+  case $s in
+    tests) run tests 900 python -u -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider --timeout 300 \
+               --timeout-method thread
+           rc=$?; grep -E "^FAILED" "$OUT/tests.log" | head -30; [ $rc -le 1 ] || exit $rc ;;
+    tests:*) run tests_$n 600 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 300 \
+               --timeout-method thread -k "${s#tests:}"
+           rc=$?; grep -E "^FAILED" "$OUT/tests_$n.log" | head -30; [ $rc -le 1 ] || exit $rc ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench) run bench 400 python bench.py || exit $? ;;
+    bench64) run bench64 300 python bench.py --batch 64 $QUIET || exit $? ;;
+    benchq) run benchq 300 python bench.py --steps 100 $QUIET || exit $? ;;
+    cfg4) run cfg4 300 python bench.py --no-tf $QUIET || exit $? ;;
+    cfg5) run cfg5 300 python bench.py --bert --network vgg19 $QUIET || exit $? ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+              python bench.py || exit $?
+          python tools/prof_summary.py "$OUT/prof" "$OUT/prof.log" "$OUT/prof_summary.json" | head -60 ;;
+    pmcdec)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        run pmc_$c 300 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmc_$c" -o run --output-format csv -- \
+            python tools/decoder_pmc.py || exit $?
+      done
+      python tools/decoder_pmc.py --analyze "$OUT/pmc_FETCH_SIZE" "$OUT/pmc_WRITE_SIZE" "$OUT/pmc_decoder.json" ;;
+    ab:*) rest=${s#ab:}; label=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+          run ab_${n}_$label 300 python bench.py --steps 150 $QUIET --no-diagnostics ${args//,/ } || exit $?
+          echo "[$label] $(line "$OUT/ab_${n}_$label.log")" ;;
+    py:*) rest=${s#py:}; script=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+          run py_${n}_$(basename "$script" .py) 300 python "$script" ${args//,/ } || exit $? ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
