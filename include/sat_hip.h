@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SAT_ABI_VERSION 3
+#define SAT_ABI_VERSION 4
 
 enum { SAT_F32 = 0, SAT_BF16 = 1 };
 enum { SAT_ACT_NONE = 0, SAT_ACT_RELU = 1, SAT_ACT_TANH = 2, SAT_ACT_SIGMOID = 3 };
@@ -80,6 +80,9 @@ typedef struct {
                          * (channel slices when B <= 64), 1 one workgroup per half image, 2 two 128-channel slices
                          * per half image; sat_conv3x3_frag at 7x7: 0 auto (two images per workgroup when B > 64),
                          * 1 two images, 2 one image per workgroup */
+  int fused_lstm;       /* bf16 decoder: the LSTM pointwise forward runs in the context GEMM's split-K reduction and the
+                         * backward in the dh GEMM's (the row-block's last-arriving workgroup): 0 auto (on where the
+                         * skinny kernel runs those products), 1 off (separate lstm_fwd / lstm_bwd launches) */
 } SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),
@@ -216,6 +219,15 @@ int sat_decoder_step_bench(const SatDecoderDims* dims, const SatDecoderLayout* l
                            const void* params_lp, const void* img_features, void* workspace, size_t workspace_bytes,
                            float* alphas, const float* d_alphas, int reps, float* us_out, void* stream);
 size_t sat_decoder_workspace_bytes(const SatDecoderDims* d);
+/* The per-step kernel instance a sat_decoder_forward / _backward with these dims (and policy) runs, for tests
+ * and bench reports: out[i] for i < n, in this order (SAT_DECODER_INSTANCE_FIELDS values):
+ *   0 h-GEMM split-K slabs, 1 context-GEMM slabs, 2 d(gated context) slabs, 3 dh slabs,
+ *   4 attention-backward slot chunks per batch row (1 = one workgroup per row, no last-arriver combine;
+ *     0 = the two-launch form or no attention), 5 backward products on the transposed weight copies,
+ *   6 LSTM forward folded into the context GEMM, 7 LSTM backward folded into the dh GEMM,
+ *   8 launches per forward time step, 9 launches per BPTT time step (teacher forcing, attention on). */
+enum { SAT_DECODER_INSTANCE_FIELDS = 10 };
+int sat_decoder_instance(const SatDecoderDims* d, const SatDecoderLayout* lay, int* out, int n);
 /* bf16 mode: rewrite the transposed weight copies layout->wih_ctx_t / hcat_t inside params_lp from the shadow's
  * own W_ih / hcat rows (after the shadow changed: the fused Adam step, a cast); a no-op when either is -1. */
 int sat_decoder_refresh_transposed(const SatDecoderDims* d, const SatDecoderLayout* lay, void* params_lp,

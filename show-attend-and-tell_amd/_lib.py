@@ -25,7 +25,7 @@ class SatConvGeom(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("N", "H", "W", "C", "KH", "KW", "stride", "pad", "OH", "OW")]
 
 
-ABI_VERSION = 3   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
+ABI_VERSION = 4   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
 
 
 class SatPolicy(ctypes.Structure):
@@ -33,7 +33,8 @@ class SatPolicy(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("conv_pipe", "conv_stream", "conv3x3_ws", "skinny", "gemm_stages", "gemm_tile",
                                      "gemm_linear_order", "gemm_epilogue", "attn_bwd",
                                      "attn_bwd_chunks", "gemm_split_wgs", "lstm_blocks")] + \
-               [("decoder_splits", c_int * 4), ("stamps", c_void_p), ("stamp_capacity", c_int), ("conv_slices", c_int)]
+               [("decoder_splits", c_int * 4), ("stamps", c_void_p), ("stamp_capacity", c_int), ("conv_slices", c_int),
+                ("fused_lstm", c_int)]
 
     def __init__(self, **kw):
         splits = kw.pop("decoder_splits", None)
@@ -99,6 +100,8 @@ _SIGNATURES = [
                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p]),
     ("sat_decoder_workspace_bytes", c_size_t, [ctypes.POINTER(SatDecoderDims)]),
+    ("sat_decoder_instance", c_int, [ctypes.POINTER(SatDecoderDims), ctypes.POINTER(SatDecoderLayout),
+                                     ctypes.POINTER(c_int), c_int]),
     ("sat_decoder_refresh_transposed", c_int, [ctypes.POINTER(SatDecoderDims), ctypes.POINTER(SatDecoderLayout),
                                                c_void_p, c_void_p]),
     ("sat_decoder_forward", c_int, [ctypes.POINTER(SatDecoderDims), ctypes.POINTER(SatDecoderLayout), c_void_p,

@@ -35,6 +35,7 @@ struct WS {
   float *dcomb, *dhd, *dctx_head, *dhg, *dgated, *dh_rec, *dc, *dWs_acc, *dv_acc, *dbv_acc, *part, *demb, *dpre0,
       *colsum, *de_all;
   unsigned* ticket;
+  unsigned* lstm_ticket;   // arrival counters of the fused LSTM steps: E / 8 (forward), then E / 32 (backward)
 };
 
 // split counts of the per-step skinny GEMMs (M = B rows).  bf16: the LDS-DMA kernel (128 x 64
@@ -161,6 +162,7 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   c.take(w->de_all, R * L * f);
   c.take(w->part, sat_attention_part_floats(d.B, d.L, d.D, d.E, d.dtype, d.split_target) * f);
   c.take(w->ticket, B * 4);
+  c.take(w->lstm_ticket, (E / 8 + E / 32 + 4) * 4);
   c.take(w->demb, R * E * f);
   c.take(w->dpre0, B * 2 * E * f); c.take(w->dpre0_t, B * 2 * E * ts);
   // column-sum scratch: the largest single sum, or all the bias sums of one backward phase in one launch pair
@@ -207,7 +209,8 @@ int combine_rows(const float* fh, const float* fz, const void* emb, int rows, in
 // backward), h into step 0's GEMM-input slot (dtype), c into step 0's cell slot (fp32).
 template <typename T>
 __global__ void init_state_kernel(const float* pre, int splits, long stride, int B, int E, float* hc0, T* h_t,
-                                  long h_ld, float* c_in, long c_ld) {
+                                  long h_ld, float* c_in, long c_ld, unsigned* zero, int n_zero) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n_zero; i += (long)gridDim.x * blockDim.x) zero[i] = 0u;
   const long n = (long)B * 2 * E;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int b = (int)(i / (2 * E)), j = (int)(i - (long)b * 2 * E);
@@ -216,6 +219,32 @@ __global__ void init_state_kernel(const float* pre, int splits, long stride, int
     if (j < E) h_t[(long)b * h_ld + j] = (T)v;
     else c_in[(long)b * c_ld + j - E] = v;
   }
+}
+
+// The two per-step GEMMs whose split-K reduction can carry the LSTM cell (skinny.hip): descriptors without
+// operand pointers (shape / split / policy only)
+inline SatGemm ctx_gemm_shape(const SatDecoderDims& d, const Splits& sp) {
+  SatGemm g;
+  g.M = d.B; g.N = 4 * d.E; g.K = d.D; g.dtype = d.dtype;
+  g.lda = (long)(d.T - 1) * d.D; g.ldb = d.E + d.D; g.ldc = 4 * d.E; g.c_dtype = SAT_F32;
+  g.partial_splits = sp.c; g.split_stride = (long)d.B * 4 * d.E;
+  return g;
+}
+inline SatGemm dh_gemm_shape(const SatDecoderDims& d, const Splits& sp) {
+  SatGemm g;
+  const long HG = 5L * d.E + d.D;
+  g.M = d.B; g.N = d.E; g.K = (int)HG; g.dtype = d.dtype;
+  g.lda = (long)(d.T - 1) * HG; g.ldb = HG; g.ldc = d.E; g.c_dtype = SAT_F32;
+  g.partial_splits = sp.dh; g.split_stride = (long)d.B * d.E;
+  return g;
+}
+// whether the LSTM cell forward runs inside the context GEMM, and the backward inside the dh GEMM (bf16, attention,
+// the skinny kernel on those products; SatPolicy::fused_lstm = 1 turns both off)
+inline int fused_fwd(const SatDecoderDims& d, const Splits& sp) {
+  return d.dtype == SAT_BF16 && d.attention && sat_skinny_lstm_fwd_ok(ctx_gemm_shape(d, sp), d.E);
+}
+inline int fused_bwd(const SatDecoderDims& d, const Splits& sp, bool tr) {
+  return d.dtype == SAT_BF16 && d.attention && tr && sat_skinny_lstm_bwd_ok(dh_gemm_shape(d, sp), d.E);
 }
 
 struct Ctx {
@@ -329,7 +358,7 @@ int fwd_cgemm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s)
                 4 * E, SAT_F32, SAT_ACT_NONE, s, nullptr, 0, SAT_F32, nullptr, 0, SAT_F32, sp.c, (long)B * 4 * E);
 }
 
-int fwd_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) {
+LstmFwdArgs lstm_fwd_args(const Ctx& c, const WS& w, const Splits& sp, int t) {
   const SatDecoderDims& d = c.d;
   const int B = d.B, D = d.D, E = d.E;
   const long T1 = c.T1, HG = c.HG;
@@ -347,10 +376,25 @@ int fwd_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) 
   l.c_next_in = t + 1 < T1 ? w.c_in + (long)(t + 1) * E : nullptr; l.c_next_in_ld = T1 * E;
   l.h_out = w.h_out + (long)t * E; l.h_out_ld = T1 * E;
   l.h_next_in_t = t + 1 < T1 ? c.at(w.h_in_t, (long)(t + 1) * E) : nullptr; l.h_next_in_t_ld = T1 * E;
-  return sat_lstm_fwd_launch(l, s);
+  return l;
 }
 
-int bwd_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) {
+int fwd_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) {
+  return sat_lstm_fwd_launch(lstm_fwd_args(c, w, sp, t), s);
+}
+
+// the context GEMM with the LSTM cell in its split-K reduction (one launch); *launched = 0: not eligible, nothing
+// launched (the caller runs fwd_cgemm + fwd_lstm)
+int fwd_cgemm_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s, int* launched) {
+  const SatDecoderDims& d = c.d;
+  SatGemm g = ctx_gemm_shape(d, sp);
+  g.A = c.at(w.gated_t, (long)t * d.D); g.B = c.W(c.lay.wih + d.E); g.C = w.gctx;
+  int err = 0;
+  *launched = sat_skinny_lstm_fwd_try(g, d.E, w.lstm_ticket, lstm_fwd_args(c, w, sp, t), s, &err);
+  return err;
+}
+
+LstmBwdArgs lstm_bwd_args(const Ctx& c, const WS& w, const Splits& sp, int t) {
   const SatDecoderDims& d = c.d;
   const int B = d.B, D = d.D, E = d.E;
   const long T1 = c.T1, HG = c.HG;
@@ -366,7 +410,11 @@ int bwd_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) 
   l.dc = w.dc; l.dc_zero = t == T1 - 1;
   l.d_gates = w.dhg + (long)t * HG + E + D; l.d_gates_ld = T1 * HG;
   l.d_gates_t = c.at(w.dhg_t, (long)t * HG + E + D); l.d_gates_t_ld = T1 * HG;
-  return sat_lstm_bwd_launch(l, s);
+  return l;
+}
+
+int bwd_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) {
+  return sat_lstm_bwd_launch(lstm_bwd_args(c, w, sp, t), s);
 }
 
 // input gradient: Y[M,N] = X[M,K] W[K,N]   (W stored [K][N] row-major = torch weight [out,in])
@@ -435,6 +483,17 @@ int bwd_dhgemm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s
                         nullptr, 0, sp.dh, (long)B * E);
   return dgrad_launch(c, B, E, 4 * E, c.at(w.dhg_t, (long)t * HG + E + D), T1 * HG,
                       c.W(c.lay.hcat_w + (long)(E + D) * E), E, w.dh_rec, E, s, nullptr, 0, sp.dh, (long)B * E);
+}
+
+// the dh GEMM of step t > 0 with step t-1's LSTM cell backward in its split-K reduction (one launch); *launched = 0:
+// not eligible, nothing launched (the caller runs bwd_dhgemm(t) and bwd_lstm(t - 1) at the start of step t-1)
+int bwd_dhgemm_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s, int* launched) {
+  const SatDecoderDims& d = c.d;
+  SatGemm g = dh_gemm_shape(d, sp);
+  g.A = c.at(w.dhg_t, (long)t * c.HG); g.B = c.W(c.lay.hcat_t); g.C = w.dh_rec;
+  int err = 0;
+  *launched = sat_skinny_lstm_bwd_try(g, w.lstm_ticket + d.E / 8, lstm_bwd_args(c, w, sp, t - 1), s, &err);
+  return err;
 }
 
 // In-kernel timestamps of the per-step kernels (SatPolicy::stamps, bench.py's in-step figures): the
@@ -544,6 +603,24 @@ extern "C" size_t sat_decoder_workspace_bytes(const SatDecoderDims* d) {
   return carve(*d, nullptr, &w);
 }
 
+extern "C" int sat_decoder_instance(const SatDecoderDims* dp, const SatDecoderLayout* lay, int* out, int n) {
+  SAT_CHECK((hipError_t)check_dims(dp));
+  SAT_REQUIRE(out && n > 0);
+  SatPolicyScope scope(dp->policy);
+  const SatDecoderDims& d = *dp;
+  const bool tr = lay && use_transposed(d, *lay);
+  const Splits sp = splits_for(d, tr);
+  const int VD = d.dtype == SAT_BF16 ? 8 : 4;
+  const bool split_bwd = d.attention && sat_policy().attn_bwd != 1 && d.E % 4 == 0 && sat_cdiv(d.D, 64 * VD) <= 8 &&
+                         sat_cdiv(d.E, 64 * VD) <= (d.dtype == SAT_BF16 ? 2 : 4);
+  const int ff = fused_fwd(d, sp), fb = fused_bwd(d, sp, tr);
+  const int v[SAT_DECODER_INSTANCE_FIELDS] = {
+      sp.h, sp.c, sp.g, sp.dh, split_bwd ? sat_attention_bwd_chunks(d.B, d.L, d.split_target) : 0, tr ? 1 : 0, ff, fb,
+      (d.attention ? 3 : 1) + (ff ? 0 : 1), (d.attention ? 3 : 1) + (fb ? 0 : 1)};
+  for (int i = 0; i < n && i < SAT_DECODER_INSTANCE_FIELDS; ++i) out[i] = v[i];
+  return 0;
+}
+
 extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLayout* lay, const float* params,
                                    const void* params_lp, const void* img_features, const int64_t* captions,
                                    const uint8_t* dropout_mask, void* workspace, size_t workspace_bytes, void* preds,
@@ -565,6 +642,7 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
   const long HG = c.HG;
   const bool att = d.attention != 0;
   const Splits sp = splits_for(d, c.tr);
+  const int ff = fused_fwd(d, sp);
   const StepIO io{img_features, alphas, nullptr};
 
   // fed tokens + embeddings
@@ -587,10 +665,12 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
     const int g = (int)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
     if (d.dtype == SAT_BF16)
       hipLaunchKernelGGL(init_state_kernel<bf16>, dim3(g), dim3(256), 0, s, (const float*)w.hc0pre, sp.i,
-                         (long)B * 2 * E, B, E, w.hc0, (bf16*)w.h_in_t, (long)T1 * E, w.c_in, (long)T1 * E);
+                         (long)B * 2 * E, B, E, w.hc0, (bf16*)w.h_in_t, (long)T1 * E, w.c_in, (long)T1 * E,
+                         w.lstm_ticket, E / 8 + E / 32);
     else
       hipLaunchKernelGGL(init_state_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)w.hc0pre, sp.i,
-                         (long)B * 2 * E, B, E, w.hc0, (float*)w.h_in_t, (long)T1 * E, w.c_in, (long)T1 * E);
+                         (long)B * 2 * E, B, E, w.hc0, (float*)w.h_in_t, (long)T1 * E, w.c_in, (long)T1 * E,
+                         w.lstm_ticket, E / 8 + E / 32);
     SAT_LAUNCH_CHECK();
   }
   if (att) {  // hoisted Ws = a W^T + b
@@ -616,15 +696,17 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
       StepTimer st(d, 0, t);
       SAT_CHECK((hipError_t)fwd_hgemm(c, w, sp, t, s));
     }
+    int cell_done = 0;   // the LSTM cell ran inside the context GEMM
     if (att) {
       {
         StepTimer st(d, 1, t);
         SAT_CHECK((hipError_t)fwd_attn(c, w, sp, io, t, s));
       }
       StepTimer st(d, 2, t);
-      SAT_CHECK((hipError_t)fwd_cgemm(c, w, sp, t, s));
+      if (ff) SAT_CHECK((hipError_t)fwd_cgemm_lstm(c, w, sp, t, s, &cell_done));
+      if (!cell_done) SAT_CHECK((hipError_t)fwd_cgemm(c, w, sp, t, s));
     }
-    {
+    if (!cell_done) {
       StepTimer st(d, 3, t);
       SAT_CHECK((hipError_t)fwd_lstm(c, w, sp, t, s));
     }
@@ -763,7 +845,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   SatGemm g_wihc = wg(4 * E, D, R, dg_t, HG, w.gated_t, D, G(lay->wih + E), E + D);
   {   // one launch zeroes the BPTT accumulators, the split attention backward's tickets, (beta = 0) the dense
       // embedding gradient the scatter-add after the loop accumulates into, and the atomic split-K targets
-    SatZeroSeg seg[12];
+    SatZeroSeg seg[12];   // <= 3 + 1 + 1 + 5
     int nz = 0;
     if (att) {
       seg[nz++] = SatZeroSeg{w.dv_acc, 1, (long)B * E, (long)B * E};
@@ -771,13 +853,16 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
       seg[nz++] = SatZeroSeg{(float*)w.ticket, 1, B, B};
     }
     if (!d.bert && !accumulate) seg[nz++] = SatZeroSeg{G(lay->embedding), 1, (long)V * E, (long)V * E};
+    seg[nz++] = SatZeroSeg{(float*)(w.lstm_ticket + E / 8), 1, E / 32, E / 32};
     SatGemm* gs[5] = {&g_hcat, &g_wihx, &g_wihc, &g_init, &g_attw};
     prezero(gs, att ? 5 : 4, seg, nz);
     SAT_CHECK((hipError_t)sat_zero_segs(seg, nz, s));
   }
   const StepIO io{img_features, const_cast<float*>(alphas), d_alphas};
+  const int fb = fused_bwd(d, sp, c.tr);
+  int cell_done = 0;   // step t's LSTM cell backward already ran inside step t+1's dh GEMM
   for (int t = T1 - 1; t >= 0; --t) {
-    {
+    if (!cell_done) {
       StepTimer st(d, 4, t);
       SAT_CHECK((hipError_t)bwd_lstm(c, w, sp, t, s));
     }
@@ -790,7 +875,9 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
       SAT_CHECK((hipError_t)bwd_attn(c, w, sp, io, t, s));
     }
     StepTimer st(d, 7, t);
-    SAT_CHECK((hipError_t)bwd_dhgemm(c, w, sp, t, s));
+    cell_done = 0;
+    if (fb && t > 0) SAT_CHECK((hipError_t)bwd_dhgemm_lstm(c, w, sp, t, s, &cell_done));
+    if (!cell_done) SAT_CHECK((hipError_t)bwd_dhgemm(c, w, sp, t, s));
   }
 
   // ---------------- weight gradients, batched over all B*(T-1) rows ----------------
@@ -851,6 +938,7 @@ extern "C" int sat_decoder_step_bench(const SatDecoderDims* dp, const SatDecoder
   Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D,
         use_transposed(d, *lay)};
   const Splits sp = splits_for(d, c.tr);
+  const int ff = fused_fwd(d, sp), fb = fused_bwd(d, sp, c.tr);
   const StepIO io{img_features, alphas, d_alphas};
   const int t = (d.T - 1) / 2;
   hipEvent_t e0, e1;
@@ -860,17 +948,23 @@ extern "C" int sat_decoder_step_bench(const SatDecoderDims* dp, const SatDecoder
   for (int k = 0; k < 8 && rc == 0; ++k) {
     us_out[k] = 0.f;
     if (!d.attention && (k == 1 || k == 2 || k == 5 || k == 6)) continue;
+    if ((ff && k == 3) || (fb && k == 4)) continue;   // the cell runs inside the context / dh GEMM (groups 2 / 7)
     for (int r = -1; r < reps && rc == 0; ++r) {   // r = -1: warm-up launch
       if (r == 0) rc = (int)hipEventRecord(e0, s);
+      int done = 0;
       switch (k) {
         case 0: rc = fwd_hgemm(c, w, sp, t, s); break;
         case 1: rc = fwd_attn(c, w, sp, io, t, s); break;
-        case 2: rc = fwd_cgemm(c, w, sp, t, s); break;
+        case 2: rc = ff ? fwd_cgemm_lstm(c, w, sp, t, s, &done) : 0;
+                if (rc == 0 && !done) rc = fwd_cgemm(c, w, sp, t, s);
+                break;
         case 3: rc = fwd_lstm(c, w, sp, t, s); break;
         case 4: rc = bwd_lstm(c, w, sp, t, s); break;
         case 5: rc = bwd_ggemm(c, w, sp, t, s); break;
         case 6: rc = bwd_attn(c, w, sp, io, t, s); break;
-        default: rc = bwd_dhgemm(c, w, sp, t, s); break;
+        default: rc = fb ? bwd_dhgemm_lstm(c, w, sp, t, s, &done) : 0;
+                 if (rc == 0 && !done) rc = bwd_dhgemm(c, w, sp, t, s);
+                 break;
       }
     }
     if (rc == 0) rc = (int)hipEventRecord(e1, s);

@@ -35,12 +35,8 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
     }
     __syncthreads();
     if (q == 0 && ok) {
-      const float ig = 1.f / (1.f + expf(-sg[0][u]));
-      const float fg = 1.f / (1.f + expf(-sg[1][u]));
-      const float gg = tanhf(sg[2][u]);
-      const float og = 1.f / (1.f + expf(-sg[3][u]));
-      const float c = fg * a.c_prev[(long)b * a.c_prev_ld + j] + ig * gg;
-      const float h = og * tanhf(c);
+      float c, h;
+      lstm_cell_fwd(sg[0][u], sg[1][u], sg[2][u], sg[3][u], a.c_prev[(long)b * a.c_prev_ld + j], c, h);
       a.c_out[(long)b * a.c_out_ld + j] = c;
       if (a.c_next_in) a.c_next_in[(long)b * a.c_next_in_ld + j] = c;
       a.h_out[(long)b * a.h_out_ld + j] = h;
@@ -87,21 +83,13 @@ __device__ __forceinline__ void lstm_bwd_gp_kernel_body(LstmBwdArgs a) {
     }
     __syncthreads();
     if (ok) {
-      const float ig = 1.f / (1.f + expf(-sg[0][u]));
-      const float fg = 1.f / (1.f + expf(-sg[1][u]));
-      const float gg = tanhf(sg[2][u]);
-      const float og = 1.f / (1.f + expf(-sg[3][u]));
-      const float tc = tanhf(cn);
       const float dh = ((sdh[0][u] + sdh[1][u]) + (sdh[2][u] + sdh[3][u])) + hh;
-      const float dc = dcin + dh * og * (1.f - tc * tc);
-      float dq;
-      if (q == 0) dq = dc * gg * ig * (1.f - ig);
-      else if (q == 1) dq = dc * cp * fg * (1.f - fg);
-      else if (q == 2) dq = dc * ig * (1.f - gg * gg);
-      else dq = dh * tc * og * (1.f - og);
+      float d4[4], dco;
+      lstm_cell_bwd(sg[0][u], sg[1][u], sg[2][u], sg[3][u], cp, cn, dcin, dh, d4, dco);
+      const float dq = d4[q];
       a.d_gates[(long)b * a.d_gates_ld + q * E + j] = dq;
       if (a.d_gates_t) ((T*)a.d_gates_t)[(long)b * a.d_gates_t_ld + q * E + j] = (T)dq;
-      if (q == 0) a.dc[i] = dc * fg;
+      if (q == 0) a.dc[i] = dco;
     }
     __syncthreads();
   }

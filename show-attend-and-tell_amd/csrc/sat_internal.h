@@ -172,3 +172,41 @@ __device__ __forceinline__ float4 sum_parts4(const float* p, long idx, int n, lo
   for (; sp < n; ++sp) a1 = f4add(a1, *(const float4*)(p + idx + sp * stride));
   return f4add(f4add(a0, a1), f4add(a2, a3));
 }
+
+// ---- LSTM cell arithmetic (nn.LSTMCell, gate order i, f, g, o; decoder.py:115), shared by the separate pointwise
+// kernels (lstm.hip) and the GEMMs that fold them into their split-K reduction (skinny.hip): one expression each,
+// so both forms round identically ----
+__device__ __forceinline__ void lstm_cell_fwd(float gi, float gf, float gg, float go, float c_prev, float& c, float& h) {
+  const float ig = 1.f / (1.f + expf(-gi));
+  const float fg = 1.f / (1.f + expf(-gf));
+  const float g = tanhf(gg);
+  const float og = 1.f / (1.f + expf(-go));
+  c = fg * c_prev + ig * g;
+  h = og * tanhf(c);
+}
+// dh: dL/dh of this cell (recurrent + head), dc_in: dL/dc from the next step; dq[4]: dL/d(gate pre-activations),
+// dc_out: dL/dc_prev
+__device__ __forceinline__ void lstm_cell_bwd(float gi, float gf, float gg, float go, float c_prev, float c_new,
+                                              float dc_in, float dh, float* dq, float& dc_out) {
+  const float ig = 1.f / (1.f + expf(-gi));
+  const float fg = 1.f / (1.f + expf(-gf));
+  const float g = tanhf(gg);
+  const float og = 1.f / (1.f + expf(-go));
+  const float tc = tanhf(c_new);
+  const float dc = dc_in + dh * og * (1.f - tc * tc);
+  dq[0] = dc * g * ig * (1.f - ig);
+  dq[1] = dc * c_prev * fg * (1.f - fg);
+  dq[2] = dc * ig * (1.f - g * g);
+  dq[3] = dh * tc * og * (1.f - og);
+  dc_out = dc * fg;
+}
+
+// the LSTM cell folded into the skinny GEMM's split-K reduction (skinny.hip): the context GEMM of a forward step
+// with gate-interleaved column blocks, and the recurrent dL/dh GEMM of BPTT step t carrying step t-1's cell
+// backward.  *_ok: the problem fits (shape, splits, policy; no pointers checked); *_try: 1 when launched (error in
+// *err), 0 when not eligible (the caller launches the GEMM and the pointwise kernel separately).  ticket: zeroed
+// arrival counters, E / 8 (forward) or E / 32 (backward) of them, left zeroed.
+int sat_skinny_lstm_fwd_ok(const SatGemm& g, int E);
+int sat_skinny_lstm_bwd_ok(const SatGemm& g, int E);
+int sat_skinny_lstm_fwd_try(const SatGemm& g, int E, unsigned* ticket, const LstmFwdArgs& l, hipStream_t st, int* err);
+int sat_skinny_lstm_bwd_try(const SatGemm& g, unsigned* ticket, const LstmBwdArgs& l, hipStream_t st, int* err);

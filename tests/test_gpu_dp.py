@@ -27,13 +27,14 @@ def sat():
     return sat_amd
 
 
-def _full_batch(sat):
+def _full_batch(sat, case):
     sys.path.insert(0, HERE)
     import dp_rank_worker as W
-    p, feats, caps, mask = W.case_inputs()
-    dec = W.make_decoder(sat, p, torch.device("cuda"))
+    c = W.DP_CASES[case]
+    p, feats, caps, mask = W.case_inputs(c)
+    dec = W.make_decoder(sat, p, torch.device("cuda"), c)
     dec.dropout_mask = mask
-    opt = sat.Adam(dec.parameters(), lr=W.DP_CASE["lr"])
+    opt = sat.Adam(dec.parameters(), lr=c["lr"])
     opt.zero_grad()
     caps_d = caps.cuda()
     preds, alphas = dec(feats.cuda(), caps_d)
@@ -45,14 +46,22 @@ def _full_batch(sat):
     return grads, W.weights(dec)
 
 
-def test_dp_two_ranks_equal_full_batch(sat, tmp_path):
+# toy fp32 (the exact-parity path) and cfg3's per-rank shape in bf16 (ResNet152 / COCO decoder, 64 images per rank,
+# bench.py's split target for B <= 64): in bf16 every per-row product of the two half batches is the full batch's
+# bit for bit up to the exact factor 2 of the loss mean, so the averaged gradients differ from the full batch's only
+# by the fp32 summation order of the batched weight-gradient GEMMs and the embedding scatter-add
+TOL = {"toy_fp32": (5e-4, 2e-3), "cfg3_bf16": (1e-3, 1e-2)}
+
+
+@pytest.mark.parametrize("case", ["toy_fp32", "cfg3_bf16"])
+def test_dp_two_ranks_equal_full_batch(sat, tmp_path, case):
     world = 2
     init = tmp_path / "init"
     outs = [tmp_path / f"rank{r}.pt" for r in range(world)]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_rank_worker.py"), str(r), str(world),
-                               str(init), str(outs[r])], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
-                              text=True) for r in range(world)]
+                               str(init), str(outs[r]), case], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(world)]
     logs = []
     for pr in procs:
         try:
@@ -64,8 +73,9 @@ def test_dp_two_ranks_equal_full_batch(sat, tmp_path):
     for pr, log in zip(procs, logs):
         assert pr.returncode == 0, log[-3000:]
     res = [torch.load(o, weights_only=True) for o in outs]
-    g_full, w_full = _full_batch(sat)
+    g_full, w_full = _full_batch(sat, case)
     lr = 1e-4
+    tol_norm, tol_elem = TOL[case]
     for form in ("eager", "graph"):
         for r in range(world):
             g, w = res[r][f"{form}_grads"], res[r][f"{form}_weights"]
@@ -78,8 +88,8 @@ def test_dp_two_ranks_equal_full_batch(sat, tmp_path):
                     assert got.abs().max().item() < 1e-5, (form, n)
                     continue
                 # mean of the two half-batch gradients == full-batch gradient, up to fp32 summation order
-                assert ((got - ref).norm() / ref.norm()).item() < 5e-4, (form, r, n)
-                assert (got - ref).abs().max().item() <= 2e-3 * scale, (form, r, n)
+                assert ((got - ref).norm() / ref.norm()).item() < tol_norm, (form, r, n)
+                assert (got - ref).abs().max().item() <= tol_elem * scale, (form, r, n)
                 # Adam's first step moves every weight by ~lr * sign(g): compare where the sign is not
                 # at the fp32 noise level
                 sure = ref.abs() > 1e-4 * scale

@@ -100,3 +100,31 @@ def test_oracle_beam_search(path):
         assert math.isinf(score)
     else:
         assert abs(score - float(g["score"])) <= 1e-5 * max(1.0, abs(score))
+
+
+def test_greedy_equals_teacher_forcing_on_its_own_tokens():
+    """The premise of the GPU greedy tests' conditioned oracle (test_gpu_shapes._oracle_fed): the greedy decoder
+    (decoder.py:131-133, argmax fed back) is the teacher-forced decoder run on the tokens it fed itself -- same
+    preds, alphas, loss against the real captions and gradients (the argmax is a constant for autograd)."""
+    V, D, E, B, T = 40, 32, 512, 3, 7
+    p = O.make_decoder_params(V, D, E, True, 3)
+    feats = torch.randn(B, 9, D, generator=torch.Generator().manual_seed(4)).relu()
+    caps = O.make_captions(B, T, V, 5)
+    masks = O.make_dropout_masks(B, T - 1, E, 6)
+    names = O.trainable_names(V, D, E, True, True, False)
+
+    def run(tf, fed_caps):
+        q = {k: v.clone().requires_grad_(k in names) for k, v in p.items()}
+        preds, alphas, toks = O.decoder_forward(q, feats, fed_caps, tf=tf, ado=True, attention=True, training=True,
+                                                dropout_masks=masks)
+        loss = O.caption_loss(preds, alphas, caps)
+        loss.backward()
+        return preds.detach(), alphas.detach(), loss.item(), toks, {k: q[k].grad for k in names}
+    pg, ag, lg, toks, gg = run(False, caps)
+    fed = caps.clone()
+    fed[:, :T - 1] = toks
+    pt, at, lt, toks2, gt = run(True, fed)
+    assert torch.equal(toks, toks2)
+    assert torch.equal(pg, pt) and torch.equal(ag, at) and lg == lt
+    for k in names:
+        assert torch.equal(gg[k], gt[k]), k
