@@ -142,8 +142,44 @@ def analyze(fdir, wdir, out_path=None):
             json.dump(res, f, indent=1)
 
 
+def counters(d, out_path=None):
+    """Mean of every collected counter per kernel (short name) over the last train step's per-step dispatches
+    (the last T-1 forward and T-1 backward windows); for the SQ / TCC groups of tools/session.sh pmcdec2."""
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    rows = {}
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                did = int(r["Dispatch_Id"])
+                e = rows.setdefault(did, {"k": r["Kernel_Name"]})
+                e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    seq = [rows[k] for k in sorted(rows)]
+    last_fwd = max(i for i, e in enumerate(seq) if "attn_fwd" in e["k"])
+    first = last_fwd - 40 * (T - 1)   # the last step's forward + backward: ~4-8 launches per time step each
+    res = {}
+    for e in seq[max(0, first):]:
+        n = short(e["k"])
+        if not any(x in n for x in ("attn_", "skinny", "lstm", "fast_gemm")):
+            continue
+        g = res.setdefault(n, {"n": 0})
+        g["n"] += 1
+        for c, v in e.items():
+            if c != "k":
+                g[c] = g.get(c, 0.0) + v
+    for n, g in res.items():
+        for c in list(g):
+            if c != "n":
+                g[c] = round(g[c] / g["n"], 1)
+    print(json.dumps(res, indent=1))
+    if out_path:
+        with open(out_path, "w") as f:
+            json.dump(res, f, indent=1)
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "--analyze":
+    if len(sys.argv) > 1 and sys.argv[1] == "--counters":
+        counters(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
+    elif len(sys.argv) > 1 and sys.argv[1] == "--analyze":
         analyze(sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else None)
     else:
         run()

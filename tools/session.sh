@@ -10,9 +10,11 @@
 #   bench64            the B = 64 line (cfg2 / cfg3's per-rank shape), no CPU baseline / fp32 leg
 #   benchq             a quick B = 128 line (100 steps, no CPU baseline / fp32 leg)
 #   cfg4 | cfg5        the --no-tf / --bert --network vgg19 lines
+#   gloo2              bench.py as two ranks over gloo on the one GPU at --batch 64 (the N > 1 path, cfg3 per rank)
 #   prof               rocprofv3 --kernel-trace --stats of the default bench command (+ tools/prof_summary.py)
 #   pmcdec             two PMC passes (FETCH_SIZE, WRITE_SIZE) over the decoder's per-step kernels
 #                      (tools/decoder_pmc.py; summary -> gpurun_out/TAG/pmc_decoder.json)
+#   pmcdec2            SQ / TCC counter groups over the same decoder run (per-kernel means -> pmc2_*.json)
 #   ab:LABEL:ARGS      one A/B bench line (ARGS comma-separated bench.py flags, e.g. ab:st80:--split-target,80);
 #                      prints value and ms/step
 #   py:SCRIPT[:ARGS]   python SCRIPT ARGS (comma-separated) under a 300 s limit
@@ -53,6 +55,9 @@ for s in "$@"; do
     bench64) run bench64 300 python bench.py --batch 64 $QUIET || exit $? ;;
     benchq) run benchq 300 python bench.py --steps 100 $QUIET || exit $? ;;
     cfg4) run cfg4 300 python bench.py --no-tf $QUIET || exit $? ;;
+    gloo2) # the N > 1 path rehearsed on one GPU: two ranks over gloo at cfg3's per-rank batch (64)
+           run gloo2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+               --master-port 29531 bench.py --gpus 2 --batch 64 --dist-backend gloo --steps 30 $QUIET || exit $? ;;
     cfg5) run cfg5 300 python bench.py --bert --network vgg19 $QUIET || exit $? ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
               python bench.py || exit $?
@@ -63,6 +68,15 @@ for s in "$@"; do
             python tools/decoder_pmc.py || exit $?
       done
       python tools/decoder_pmc.py --analyze "$OUT/pmc_FETCH_SIZE" "$OUT/pmc_WRITE_SIZE" "$OUT/pmc_decoder.json" ;;
+    pmcdec2)   # SQ and TCC counter groups over the same decoder run (one rocprofv3 pass per group)
+      i=0
+      for G in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_INSTS_VALU" \
+               "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
+        i=$((i + 1))
+        run pmc2_$i 300 rocprofv3 --pmc $G --kernel-trace -d "$OUT/pmc2_$i" -o run --output-format csv -- \
+            python tools/decoder_pmc.py || exit $?
+        python tools/decoder_pmc.py --counters "$OUT/pmc2_$i" "$OUT/pmc2_$i.json" | head -80
+      done ;;
     ab:*) rest=${s#ab:}; label=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
           run ab_${n}_$label 300 python bench.py --steps 150 $QUIET --no-diagnostics ${args//,/ } || exit $?
           echo "[$label] $(line "$OUT/ab_${n}_$label.log")" ;;
