@@ -217,9 +217,12 @@ class DecoderStamps:
             order = list(order)
             iv, ks = [], []
             for a, b in zip(order, order[1:]):
-                sa, sb = start(groups[0], a), start(groups[0], b)
-                spans = [span(g, a) for g in groups]
-                if sa is not None and sb is not None and all(v is not None for v in spans):
+                # the step's first launch to the next step's first launch; the spans of the groups the build runs
+                # per step (groups folded into another kernel have no stamps)
+                sa = next((start(g, a) for g in groups if start(g, a) is not None), None)
+                sb = next((start(g, b) for g in groups if start(g, b) is not None), None)
+                spans = [v for v in (span(g, a) for g in groups) if v is not None]
+                if sa is not None and sb is not None and spans:
                     iv.append((sb - sa) / 100.0)
                     ks.append(sum(spans))
             if iv:
@@ -895,7 +898,7 @@ def main():
     if step_kernels is not None and (chain_alone or chain_overlapped):
         step_kernels["step_chain"] = dict(alone=chain_alone, overlapped=chain_overlapped,
                                           note="per time step: first-kernel start to the next step's first-kernel "
-                                               "start (interval) beside the sum of the step's four kernel spans")
+                                               "start (interval) beside the sum of the step's kernel spans")
     fp32_leg = fp32_step(args, enc, dec, imgs, caps, pad_id, skip_ids, world) if world == 1 and args.fp32_steps > 0 \
         else None
     if roof is not None:

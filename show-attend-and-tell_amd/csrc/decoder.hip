@@ -241,7 +241,7 @@ inline SatGemm dh_gemm_shape(const SatDecoderDims& d, const Splits& sp) {
 // whether the LSTM cell forward runs inside the context GEMM, and the backward inside the dh GEMM (bf16, attention,
 // the skinny kernel on those products; SatPolicy::fused_lstm = 1 turns both off)
 inline int fused_fwd(const SatDecoderDims& d, const Splits& sp) {
-  return d.dtype == SAT_BF16 && d.attention && sat_skinny_lstm_fwd_ok(ctx_gemm_shape(d, sp), d.E);
+  return d.dtype == SAT_BF16 && d.attention && sat_skinny_lstm_fwd_ok(ctx_gemm_shape(d, sp), d.E, sp.h);
 }
 inline int fused_bwd(const SatDecoderDims& d, const Splits& sp, bool tr) {
   return d.dtype == SAT_BF16 && d.attention && tr && sat_skinny_lstm_bwd_ok(dh_gemm_shape(d, sp), d.E);

@@ -206,7 +206,7 @@ __device__ __forceinline__ void lstm_cell_bwd(float gi, float gf, float gg, floa
 // backward.  *_ok: the problem fits (shape, splits, policy; no pointers checked); *_try: 1 when launched (error in
 // *err), 0 when not eligible (the caller launches the GEMM and the pointwise kernel separately).  ticket: zeroed
 // arrival counters, E / 8 (forward) or E / 32 (backward) of them, left zeroed.
-int sat_skinny_lstm_fwd_ok(const SatGemm& g, int E);
+int sat_skinny_lstm_fwd_ok(const SatGemm& g, int E, int h_splits);
 int sat_skinny_lstm_bwd_ok(const SatGemm& g, int E);
 int sat_skinny_lstm_fwd_try(const SatGemm& g, int E, unsigned* ticket, const LstmFwdArgs& l, hipStream_t st, int* err);
 int sat_skinny_lstm_bwd_try(const SatGemm& g, unsigned* ticket, const LstmBwdArgs& l, hipStream_t st, int* err);

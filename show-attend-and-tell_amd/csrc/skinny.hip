@@ -154,19 +154,22 @@ __device__ __forceinline__ float4 ld4_sc1(__amdgpu_buffer_rsrc_t r, long elem) {
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(elem * 4), 0, kSc1);
   return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
-// sum_parts4 (sat_internal.h) over sc1 loads: the same summation order per element
-__device__ __forceinline__ float4 sum_parts4_sc1(__amdgpu_buffer_rsrc_t r, long idx, int n, long stride) {
-  float4 a0 = ld4_sc1(r, idx);
-  if (n <= 1) return a0;
-  float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f), a2 = a1, a3 = a1;
-  int sp = 1;
-  for (; sp + 2 < n; sp += 3) {
-    const float4 x = ld4_sc1(r, idx + sp * stride), y = ld4_sc1(r, idx + (sp + 1) * stride),
-                 z = ld4_sc1(r, idx + (sp + 2) * stride);
-    a1 = f4add(a1, x); a2 = f4add(a2, y); a3 = f4add(a3, z);
+// sum_parts4's summation order (sat_internal.h) over N values already in registers: (a0 + a1) + (a2 + a3) with
+// a1..a3 taking the slabs 1, 2, 3, 4, 5, 6, ... round robin (compile-time N: every load of a reducer is issued
+// before the first add, one memory round trip per item instead of one per slab)
+template <int N>
+__device__ __forceinline__ float4 sum_slabs(const float4 (&p)[N]) {
+  if constexpr (N == 1) {
+    return p[0];
+  } else {
+    float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f), a2 = a1, a3 = a1;
+    int sp = 1;
+#pragma unroll
+    for (; sp + 2 < N; sp += 3) { a1 = f4add(a1, p[sp]); a2 = f4add(a2, p[sp + 1]); a3 = f4add(a3, p[sp + 2]); }
+#pragma unroll
+    for (; sp < N; ++sp) a1 = f4add(a1, p[sp]);
+    return f4add(f4add(p[0], a1), f4add(a2, a3));
   }
-  for (; sp < n; ++sp) a1 = f4add(a1, ld4_sc1(r, idx + sp * stride));
-  return f4add(f4add(a0, a1), f4add(a2, a3));
 }
 
 // Write this split's tile to its slab (write-through), drain, count the arrival; true in the last arriver.
@@ -199,30 +202,34 @@ struct SkLstmFwdArgs {
   LstmFwdArgs l;       // the cell step; its cpart / c_splits are g's slabs
 };
 
-template <typename T, int MB, int NW>
+template <typename T, int MB, int NW, int SC, int HS>
 __global__ __launch_bounds__(NW * 64) void skinny_lstm_fwd_kernel(SkLstmFwdArgs a) {
   const SatStampT0 t0 = sat_stamp_begin(a.g.st);
   __shared__ __attribute__((aligned(16))) float red[MB * 16 * SK_RLD];
   __shared__ int s_last;
   skinny_tile<MB, NW>(a.g, red);
-  const int S = gridDim.y;
   const __amdgpu_buffer_rsrc_t rc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.g.C, (short)0, (int)((long)S * a.g.split_stride * 4), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.g.C, (short)0, (int)((long)SC * a.g.split_stride * 4), 0x00020000);
   if (publish_and_count<MB, NW>(a.g, red, rc, a.ticket, &s_last)) {
-    // the cells of units u0 .. u0+7, every row: a thread per (row, 4 units); operands requested before use
+    // the cells of units u0 .. u0+7, every row: a thread per (row, 4 units), every operand requested up front
     const LstmFwdArgs& l = a.l;
     const int E = a.g.gate_E, u0 = blockIdx.x * 8;
     for (int it = threadIdx.x; it < a.g.M * 2; it += NW * 64) {
       const int b = it >> 1, j = u0 + (it & 1) * 4;
-      float4 v[4];
+      float4 xq[4], hq[4][HS], cq[4][SC];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {   // lstm_fwd_gp_kernel's order: (xpart + sum of h slabs) + sum of c slabs
-        const float4 x = *(const float4*)(l.xpart + (long)b * l.xpart_ld + q * E + j);
-        const float4 h = sum_parts4(l.hpart, (long)b * l.hpart_ld + q * E + j, l.h_splits, l.h_split_stride);
-        const float4 c = sum_parts4_sc1(rc, (long)b * a.g.ldc + q * E + j, S, a.g.split_stride);
-        v[q] = f4add(f4add(x, h), c);
+      for (int q = 0; q < 4; ++q) {
+        xq[q] = *(const float4*)(l.xpart + (long)b * l.xpart_ld + q * E + j);
+#pragma unroll
+        for (int k = 0; k < HS; ++k) hq[q][k] = *(const float4*)(l.hpart + k * l.h_split_stride + (long)b * l.hpart_ld + q * E + j);
+#pragma unroll
+        for (int k = 0; k < SC; ++k) cq[q][k] = ld4_sc1(rc, k * a.g.split_stride + (long)b * a.g.ldc + q * E + j);
       }
       const float4 cp = *(const float4*)(l.c_prev + (long)b * l.c_prev_ld + j);
+      float4 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)   // lstm_fwd_gp_kernel's order: (xpart + sum of h slabs) + sum of c slabs
+        v[q] = f4add(f4add(xq[q], sum_slabs<HS>(hq[q])), sum_slabs<SC>(cq[q]));
       const float gi[4] = {v[0].x, v[0].y, v[0].z, v[0].w}, gf[4] = {v[1].x, v[1].y, v[1].z, v[1].w},
                   gg[4] = {v[2].x, v[2].y, v[2].z, v[2].w}, go[4] = {v[3].x, v[3].y, v[3].z, v[3].w},
                   cpv[4] = {cp.x, cp.y, cp.z, cp.w};
@@ -258,27 +265,23 @@ struct SkLstmBwdArgs {
   LstmBwdArgs l;       // step t-1's cell backward; its dh_rec / dh_splits are g's slabs
 };
 
-template <typename T, int MB, int NW>
+template <typename T, int MB, int NW, int SC>
 __global__ __launch_bounds__(NW * 64) void skinny_lstm_bwd_kernel(SkLstmBwdArgs a) {
   const SatStampT0 t0 = sat_stamp_begin(a.g.st);
   __shared__ __attribute__((aligned(16))) float red[MB * 16 * SK_RLD];
   __shared__ int s_last;
   skinny_tile<MB, NW>(a.g, red);
-  const int S = gridDim.y;
   const __amdgpu_buffer_rsrc_t rc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.g.C, (short)0, (int)((long)S * a.g.split_stride * 4), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.g.C, (short)0, (int)((long)SC * a.g.split_stride * 4), 0x00020000);
   if (publish_and_count<MB, NW>(a.g, red, rc, a.ticket, &s_last)) {
     const LstmBwdArgs& l = a.l;
     const int E = l.E, u0 = blockIdx.x * SK_COLS;
     for (int it = threadIdx.x; it < a.g.M * 8; it += NW * 64) {
       const int b = it >> 3, j = u0 + (it & 7) * 4;
-      // lstm_bwd_gp_kernel's order: p_q = sum of slabs q, q+4, ... (q = 0..3), dh = ((p0 + p1) + (p2 + p3)) + head
-      float4 p[4];
+      // every operand of the item requested up front
+      float4 sl[SC];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        p[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int sp = q; sp < S; sp += 4) p[q] = f4add(p[q], ld4_sc1(rc, (long)sp * a.g.split_stride + (long)b * a.g.ldc + j));
-      }
+      for (int sp = 0; sp < SC; ++sp) sl[sp] = ld4_sc1(rc, (long)sp * a.g.split_stride + (long)b * a.g.ldc + j);
       float4 g4[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) g4[q] = *(const float4*)(l.gates + (long)b * l.gates_ld + q * E + j);
@@ -295,6 +298,14 @@ __global__ __launch_bounds__(NW * 64) void skinny_lstm_bwd_kernel(SkLstmBwdArgs 
           hh[0] = m.x ? hh[0] * 2.f : 0.f; hh[1] = m.y ? hh[1] * 2.f : 0.f;
           hh[2] = m.z ? hh[2] * 2.f : 0.f; hh[3] = m.w ? hh[3] * 2.f : 0.f;
         }
+      }
+      // lstm_bwd_gp_kernel's order: p_q = sum of slabs q, q+4, ... (q = 0..3), dh = ((p0 + p1) + (p2 + p3)) + head
+      float4 p[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        p[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int sp = q; sp < SC; sp += 4) p[q] = f4add(p[q], sl[sp]);
       }
       const float4 dh4 = f4add(f4add(p[0], p[1]), f4add(p[2], p[3]));
       const float dhs[4] = {dh4.x + hh[0], dh4.y + hh[1], dh4.z + hh[2], dh4.w + hh[3]};
@@ -370,24 +381,24 @@ void launch_mb(int nw, dim3 grid, hipStream_t st, const SkArgs& a) {
   else hipLaunchKernelGGL((skinny_gemm_kernel<MB, 4>), grid, dim3(256), 0, st, a);
 }
 
-template <int MB, int NW>
-void launch_one(dim3 grid, hipStream_t st, const SkLstmFwdArgs& a) {
-  hipLaunchKernelGGL((skinny_lstm_fwd_kernel<bf16, MB, NW>), grid, dim3(NW * 64), 0, st, a);
+// the fused kernels' compile-time slab counts: context slabs x h slabs (forward), dh slabs (backward); other
+// counts run the separate launches (the *_ok predicates say no)
+constexpr bool fwd_counts_ok(int sc, int hs) { return (sc == 2 || sc == 4) && (hs == 1 || hs == 2); }
+constexpr bool bwd_count_ok(int sc) { return sc == 6 || sc == 9; }
+
+template <int MB, int NW, int SC, int HS>
+void launch_fwd4(dim3 grid, hipStream_t st, const SkLstmFwdArgs& a) {
+  hipLaunchKernelGGL((skinny_lstm_fwd_kernel<bf16, MB, NW, SC, HS>), grid, dim3(NW * 64), 0, st, a);
 }
 template <int MB, int NW>
-void launch_one(dim3 grid, hipStream_t st, const SkLstmBwdArgs& a) {
-  hipLaunchKernelGGL((skinny_lstm_bwd_kernel<bf16, MB, NW>), grid, dim3(NW * 64), 0, st, a);
+void launch_fwd(int sc, int hs, dim3 grid, hipStream_t st, const SkLstmFwdArgs& a) {
+  if (sc == 2) hs == 1 ? launch_fwd4<MB, NW, 2, 1>(grid, st, a) : launch_fwd4<MB, NW, 2, 2>(grid, st, a);
+  else hs == 1 ? launch_fwd4<MB, NW, 4, 1>(grid, st, a) : launch_fwd4<MB, NW, 4, 2>(grid, st, a);
 }
-template <int MB, typename Args>
-void launch_nw(int nw, dim3 grid, hipStream_t st, const Args& a) {
-  if (nw == 8) launch_one<MB, 8>(grid, st, a);
-  else launch_one<MB, 4>(grid, st, a);
-}
-template <typename Args>
-void launch_fused(int M, int nw, dim3 grid, hipStream_t st, const Args& a) {
-  if (M <= 32) launch_nw<2>(nw, grid, st, a);
-  else if (M <= 64) launch_nw<4>(nw, grid, st, a);
-  else launch_nw<8>(nw, grid, st, a);
+template <int MB, int NW>
+void launch_bwd(int sc, dim3 grid, hipStream_t st, const SkLstmBwdArgs& a) {
+  if (sc == 6) hipLaunchKernelGGL((skinny_lstm_bwd_kernel<bf16, MB, NW, 6>), grid, dim3(NW * 64), 0, st, a);
+  else hipLaunchKernelGGL((skinny_lstm_bwd_kernel<bf16, MB, NW, 9>), grid, dim3(NW * 64), 0, st, a);
 }
 
 }  // namespace
@@ -413,17 +424,19 @@ int sat_skinny_splits(int M, int N, int K) {
   return K / 256;
 }
 
-int sat_skinny_lstm_fwd_ok(const SatGemm& g, int E) {
+int sat_skinny_lstm_fwd_ok(const SatGemm& g, int E, int h_splits) {
   SkArgs a;
   int nw;
-  return sat_policy().fused_lstm != 1 && E % 8 == 0 && g.N == 4 * E && !g.bias && g.partial_splits >= 1 &&
+  const int S = g.partial_splits > 1 ? g.partial_splits : 1;
+  return sat_policy().fused_lstm != 1 && E % 8 == 0 && g.N == 4 * E && !g.bias && fwd_counts_ok(S, h_splits) &&
          skinny_shape(g, sat_policy().skinny, &a, &nw);
 }
 
 int sat_skinny_lstm_bwd_ok(const SatGemm& g, int E) {
   SkArgs a;
   int nw;
-  return sat_policy().fused_lstm != 1 && E % SK_COLS == 0 && g.N == E && !g.bias && g.partial_splits >= 1 &&
+  const int S = g.partial_splits > 1 ? g.partial_splits : 1;
+  return sat_policy().fused_lstm != 1 && E % SK_COLS == 0 && g.N == E && !g.bias && bwd_count_ok(S) &&
          skinny_shape(g, sat_policy().skinny, &a, &nw);
 }
 
@@ -431,10 +444,12 @@ int sat_skinny_lstm_fwd_try(const SatGemm& g, int E, unsigned* ticket, const Lst
   *err = 0;
   SkLstmFwdArgs a{};
   int nw;
-  if (!sat_skinny_lstm_fwd_ok(g, E) || !skinny_shape(g, sat_policy().skinny, &a.g, &nw) || !skinny_ptrs(g) || !ticket)
+  const int hs = l.h_splits > 1 ? l.h_splits : 1;
+  if (!sat_skinny_lstm_fwd_ok(g, E, hs) || !skinny_shape(g, sat_policy().skinny, &a.g, &nw) || !skinny_ptrs(g) ||
+      !ticket)
     return 0;
   if (l.dtype != SAT_BF16 || (l.xpart_ld | l.hpart_ld | l.c_prev_ld | l.gates_ld | l.c_out_ld | l.h_out_ld) % 4 ||
-      (l.h_splits > 1 && l.h_split_stride % 4) || !al16(l.xpart) || !al16(l.hpart) || !al16(l.c_prev) ||
+      (hs > 1 && l.h_split_stride % 4) || !al16(l.xpart) || !al16(l.hpart) || !al16(l.c_prev) ||
       !al16(l.gates) || !al16(l.c_out) || !al16(l.h_out) || (l.c_next_in && (!al16(l.c_next_in) || l.c_next_in_ld % 4)))
     return 0;
   a.g.gate_E = E;
@@ -442,8 +457,11 @@ int sat_skinny_lstm_fwd_try(const SatGemm& g, int E, unsigned* ticket, const Lst
   a.g.st = sat_launch_stamps();
   a.ticket = ticket;
   a.l = l;
-  const dim3 grid(E / 8, g.partial_splits > 1 ? g.partial_splits : 1);
-  launch_fused(g.M, nw, grid, st, a);
+  const int S = g.partial_splits > 1 ? g.partial_splits : 1;
+  const dim3 grid(E / 8, S);
+  if (g.M <= 32) nw == 8 ? launch_fwd<2, 8>(S, hs, grid, st, a) : launch_fwd<2, 4>(S, hs, grid, st, a);
+  else if (g.M <= 64) nw == 8 ? launch_fwd<4, 8>(S, hs, grid, st, a) : launch_fwd<4, 4>(S, hs, grid, st, a);
+  else nw == 8 ? launch_fwd<8, 8>(S, hs, grid, st, a) : launch_fwd<8, 4>(S, hs, grid, st, a);
   *err = (int)hipGetLastError();
   return 1;
 }
@@ -459,12 +477,17 @@ int sat_skinny_lstm_bwd_try(const SatGemm& g, unsigned* ticket, const LstmBwdArg
       !al16(l.gates) || !al16(l.c_prev) || !al16(l.c_new) || !al16(l.dc) || !al16(l.d_gates) ||
       (l.dh_head && !al16(l.dh_head)) || (l.mask && (((uintptr_t)l.mask & 3) || l.mask_ld % 4)))
     return 0;
+  // eight waves: the cell backward of a 32-unit block is 8 M items, two per thread (the K split per wave halves)
+  a.g.kw = sat_cdiv(sat_cdiv(a.g.kc, 8), 32) * 32;
   a.g.split_stride = g.partial_splits > 1 ? g.split_stride : 0;
   a.g.st = sat_launch_stamps();
   a.ticket = ticket;
   a.l = l;
-  const dim3 grid(g.N / SK_COLS, g.partial_splits > 1 ? g.partial_splits : 1);
-  launch_fused(g.M, nw, grid, st, a);
+  const int S = g.partial_splits > 1 ? g.partial_splits : 1;
+  const dim3 grid(g.N / SK_COLS, S);
+  if (g.M <= 32) launch_bwd<2, 8>(S, grid, st, a);
+  else if (g.M <= 64) launch_bwd<4, 8>(S, grid, st, a);
+  else launch_bwd<8, 8>(S, grid, st, a);
   *err = (int)hipGetLastError();
   return 1;
 }

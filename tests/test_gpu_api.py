@@ -58,7 +58,9 @@ def test_loss_can_be_scaled_before_backward(sat, scale_mode):
     got = _grads(dec)
     assert sorted(got) == sorted(ref)
     for n, g in got.items():
-        assert torch.allclose(g, ref[n] * 0.5, rtol=1e-6, atol=1e-12), n
+        # the dense embedding gradient is a scatter-add with fp32 atomics (summation order varies run to run)
+        tol = 1e-6 * ref[n].abs().max().item() if n == "embedding.weight" else 1e-12
+        assert torch.allclose(g, ref[n] * 0.5, rtol=1e-6, atol=tol), n
 
 
 def test_policy_edit_between_forward_and_deferred_backward(sat):
@@ -82,4 +84,7 @@ def test_policy_edit_between_forward_and_deferred_backward(sat):
         return _grads(dec)
     a, b = step(False), step(True)
     for n in a:
-        assert torch.equal(a[n], b[n]), n
+        if n == "embedding.weight":   # fp32 atomic scatter-add: summation order varies run to run
+            assert torch.allclose(a[n], b[n], rtol=1e-5, atol=1e-6 * a[n].abs().max().item()), n
+        else:
+            assert torch.equal(a[n], b[n]), n

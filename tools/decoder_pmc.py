@@ -63,7 +63,14 @@ def read_counter(d, name):
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "").split("<")[0]
+    """Kernel name without namespace, template arguments and parameters (demangled or Itanium-mangled)."""
+    import re
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    m = re.match(r"_ZN12_GLOBAL__N_1(\d+)", n)
+    if m:
+        k = int(m.group(1))
+        return n[m.end():m.end() + k]
+    return n.split("<")[0].split("(")[0]
 
 
 def label(window, attn_key):

@@ -17,6 +17,7 @@
 #   pmcdec2            SQ / TCC counter groups over the same decoder run (per-kernel means -> pmc2_*.json)
 #   ab:LABEL:ARGS      one A/B bench line (ARGS comma-separated bench.py flags, e.g. ab:st80:--split-target,80);
 #                      prints value and ms/step
+#   abd:LABEL:ARGS     the same with the diagnostics (per-step decoder kernels, trunk classes; tools/bench_brief.py)
 #   py:SCRIPT[:ARGS]   python SCRIPT ARGS (comma-separated) under a 300 s limit
 set -u
 TAG=${1:?tag}; shift
@@ -80,6 +81,9 @@ for s in "$@"; do
     ab:*) rest=${s#ab:}; label=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
           run ab_${n}_$label 300 python bench.py --steps 150 $QUIET --no-diagnostics ${args//,/ } || exit $?
           echo "[$label] $(line "$OUT/ab_${n}_$label.log")" ;;
+    abd:*) rest=${s#abd:}; label=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+          run abd_${n}_$label 300 python bench.py --steps 100 $QUIET ${args//,/ } || exit $?
+          python tools/bench_brief.py "$OUT/abd_${n}_$label.log" ;;
     py:*) rest=${s#py:}; script=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
           run py_${n}_$(basename "$script" .py) 300 python "$script" ${args//,/ } || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
