@@ -80,9 +80,11 @@ typedef struct {
                          * (channel slices when B <= 64), 1 one workgroup per half image, 2 two 128-channel slices
                          * per half image; sat_conv3x3_frag at 7x7: 0 auto (two images per workgroup when B > 64),
                          * 1 two images, 2 one image per workgroup */
-  int fused_lstm;       /* bf16 decoder: the LSTM pointwise forward runs in the context GEMM's split-K reduction and the
-                         * backward in the dh GEMM's (the row-block's last-arriving workgroup): 0 auto (on where the
-                         * skinny kernel runs those products), 1 off (separate lstm_fwd / lstm_bwd launches) */
+  int fused_lstm;       /* bf16 decoder, LSTM cell per time step: 0 / 1 separate lstm_fwd / lstm_bwd launches (default);
+                         * 2 the cell forward inside the context GEMM's split-K reduction and the backward inside the dh
+                         * GEMM's (the column block's last-arriving workgroup; 3 launches per time step instead of 4 --
+                         * measured slower: the in-kernel hand-off costs more than the launch boundary it removes,
+                         * DESIGN.md 4.6) */
 } SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),

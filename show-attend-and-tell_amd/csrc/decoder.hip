@@ -239,7 +239,7 @@ inline SatGemm dh_gemm_shape(const SatDecoderDims& d, const Splits& sp) {
   return g;
 }
 // whether the LSTM cell forward runs inside the context GEMM, and the backward inside the dh GEMM (bf16, attention,
-// the skinny kernel on those products; SatPolicy::fused_lstm = 1 turns both off)
+// the skinny kernel on those products, SatPolicy::fused_lstm = 2; off by default: measured slower)
 inline int fused_fwd(const SatDecoderDims& d, const Splits& sp) {
   return d.dtype == SAT_BF16 && d.attention && sat_skinny_lstm_fwd_ok(ctx_gemm_shape(d, sp), d.E, sp.h);
 }

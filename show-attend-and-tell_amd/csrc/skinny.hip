@@ -428,7 +428,7 @@ int sat_skinny_lstm_fwd_ok(const SatGemm& g, int E, int h_splits) {
   SkArgs a;
   int nw;
   const int S = g.partial_splits > 1 ? g.partial_splits : 1;
-  return sat_policy().fused_lstm != 1 && E % 8 == 0 && g.N == 4 * E && !g.bias && fwd_counts_ok(S, h_splits) &&
+  return sat_policy().fused_lstm == 2 && E % 8 == 0 && g.N == 4 * E && !g.bias && fwd_counts_ok(S, h_splits) &&
          skinny_shape(g, sat_policy().skinny, &a, &nw);
 }
 
@@ -436,7 +436,7 @@ int sat_skinny_lstm_bwd_ok(const SatGemm& g, int E) {
   SkArgs a;
   int nw;
   const int S = g.partial_splits > 1 ? g.partial_splits : 1;
-  return sat_policy().fused_lstm != 1 && E % SK_COLS == 0 && g.N == E && !g.bias && bwd_count_ok(S) &&
+  return sat_policy().fused_lstm == 2 && E % SK_COLS == 0 && g.N == E && !g.bias && bwd_count_ok(S) &&
          skinny_shape(g, sat_policy().skinny, &a, &nw);
 }
 
