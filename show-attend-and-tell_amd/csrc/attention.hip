@@ -872,17 +872,10 @@ int sat_attention_fwd_launch(const AttnFwdArgs& args, hipStream_t s) {
 
 namespace {
 
-// FBU slots per wave per batch of loads: a chunk of at most 8 x 7 slots (L = 49 at one workgroup per row, the bench
-// instance) takes its annotation and Ws rows in ONE batch requested at entry when DCH <= 4 (bf16 D <= 2048: 7 x 4
-// uint4 of annotation rows per lane), instead of two round trips of 8 x 4 slots; SatPolicy::attn_bwd = 2 keeps the
-// two-batch form (A/B)
 template <typename T, int DCH, int ECH>
 void launch_bwd_split_e(int nl, hipStream_t s, const AttnBwdArgs& a) {
-  const int lc = sat_cdiv(a.L, nl);
-  if (DCH <= 4 && lc > 32 && lc <= 56 && sat_policy().attn_bwd != 2) {
-    hipLaunchKernelGGL((attn_bwd_split_kernel<T, DCH, ECH, 8, 7>), dim3(a.B, nl), dim3(8 * 64), 0, s, a);
-    return;
-  }
+  // FBU slots per wave per batch of loads.  Measured and not kept (profiles/r4_s4): one batch of 8 x 7 slots for the
+  // L = 49 row at one workgroup per row (231 VGPRs instead of 171): 17.8 -> 18.7 us per step, step 6.56 -> 6.61 ms
   constexpr int FBU = DCH >= 8 ? 2 : 4;
   hipLaunchKernelGGL((attn_bwd_split_kernel<T, DCH, ECH, 8, FBU>), dim3(a.B, nl), dim3(8 * 64), 0, s, a);
 }
