@@ -34,6 +34,10 @@
 
 #include <utility>
 
+#ifndef SAT_C2_ABL
+#define SAT_C2_ABL 0
+#endif
+
 namespace {
 
 typedef __attribute__((address_space(3))) void k_lds_void;
@@ -693,23 +697,34 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // SAT_C2_ABL (diagnostics builds only, tools/c2_ablation.py; product builds: 0): bit 0 no weight streaming (the
+  // prologue's fragments reused), bit 1 no MFMA, bit 2 no A fragment reads from LDS (the first read reused)
+  constexpr int ABL = SAT_C2_ABL;
+  bf16x8 af0[2][MB];
   static_for<NT>([&](auto Tc) {
     constexpr int T = decltype(Tc)::value, pl = T % NPL;
-    if constexpr (T + PF < NT) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
+    if constexpr (T + PF < NT && !(ABL & 1)) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
     if constexpr (pl == 0) tap_offsets(T / NPL);
-    const bf16x8 (&b)[2][2] = bq[T % (PF + 1)];
+    const bf16x8 (&b)[2][2] = bq[(ABL & 1) ? T % PF : T % (PF + 1)];
     bf16x8 af[2][MB];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < MB; ++i) af[ks][i] = *(const bf16x8*)(smem + pl * X1PL + offs[i][ks]);
+      for (int i = 0; i < MB; ++i) {
+        if constexpr ((ABL & 4) && T > 0) af[ks][i] = af0[ks][i];
+        else af[ks][i] = *(const bf16x8*)(smem + pl * X1PL + offs[i][ks]);
+        if constexpr ((ABL & 4) && T == 0) af0[ks][i] = af[ks][i];
+      }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < MB; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (ABL & 2) asm volatile("" ::"v"(b[ks][j]), "v"(af[ks][i]));
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+        }
     __builtin_amdgcn_s_setprio(0);
   });
 
