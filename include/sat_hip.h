@@ -80,11 +80,9 @@ typedef struct {
                          * (channel slices when B <= 64), 1 one workgroup per half image, 2 two 128-channel slices
                          * per half image; sat_conv3x3_frag at 7x7: 0 auto (two images per workgroup when B > 64),
                          * 1 two images, 2 one image per workgroup */
-  int fused_lstm;       /* bf16 decoder, LSTM cell per time step: 0 / 1 separate lstm_fwd / lstm_bwd launches (default);
-                         * 2 the cell forward inside the context GEMM's split-K reduction and the backward inside the dh
-                         * GEMM's (the column block's last-arriving workgroup; 3 launches per time step instead of 4 --
-                         * measured slower: the in-kernel hand-off costs more than the launch boundary it removes,
-                         * DESIGN.md 4.6) */
+  int fused_lstm;       /* bf16 decoder, LSTM cell per time step: 0 auto -- the cell forward in the epilogue of the context
+                         * GEMM and the backward in the epilogue of the dh GEMM, each a full-K row-block GEMM (3 launches
+                         * per time step; lstmgemm.hip); 1 the split-K products + separate lstm_fwd / lstm_bwd launches */
 } SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),

@@ -35,7 +35,6 @@ struct WS {
   float *dcomb, *dhd, *dctx_head, *dhg, *dgated, *dh_rec, *dc, *dWs_acc, *dv_acc, *dbv_acc, *part, *demb, *dpre0,
       *colsum, *de_all;
   unsigned* ticket;
-  unsigned* lstm_ticket;   // arrival counters of the fused LSTM steps: E / 8 (forward), then E / 32 (backward)
 };
 
 // split counts of the per-step skinny GEMMs (M = B rows).  bf16: the LDS-DMA kernel (128 x 64
@@ -162,7 +161,6 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   c.take(w->de_all, R * L * f);
   c.take(w->part, sat_attention_part_floats(d.B, d.L, d.D, d.E, d.dtype, d.split_target) * f);
   c.take(w->ticket, B * 4);
-  c.take(w->lstm_ticket, (E / 8 + E / 32 + 4) * 4);
   c.take(w->demb, R * E * f);
   c.take(w->dpre0, B * 2 * E * f); c.take(w->dpre0_t, B * 2 * E * ts);
   // column-sum scratch: the largest single sum, or all the bias sums of one backward phase in one launch pair
@@ -209,8 +207,7 @@ int combine_rows(const float* fh, const float* fz, const void* emb, int rows, in
 // backward), h into step 0's GEMM-input slot (dtype), c into step 0's cell slot (fp32).
 template <typename T>
 __global__ void init_state_kernel(const float* pre, int splits, long stride, int B, int E, float* hc0, T* h_t,
-                                  long h_ld, float* c_in, long c_ld, unsigned* zero, int n_zero) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n_zero; i += (long)gridDim.x * blockDim.x) zero[i] = 0u;
+                                  long h_ld, float* c_in, long c_ld) {
   const long n = (long)B * 2 * E;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int b = (int)(i / (2 * E)), j = (int)(i - (long)b * 2 * E);
@@ -221,30 +218,14 @@ __global__ void init_state_kernel(const float* pre, int splits, long stride, int
   }
 }
 
-// The two per-step GEMMs whose split-K reduction can carry the LSTM cell (skinny.hip): descriptors without
-// operand pointers (shape / split / policy only)
-inline SatGemm ctx_gemm_shape(const SatDecoderDims& d, const Splits& sp) {
-  SatGemm g;
-  g.M = d.B; g.N = 4 * d.E; g.K = d.D; g.dtype = d.dtype;
-  g.lda = (long)(d.T - 1) * d.D; g.ldb = d.E + d.D; g.ldc = 4 * d.E; g.c_dtype = SAT_F32;
-  g.partial_splits = sp.c; g.split_stride = (long)d.B * 4 * d.E;
-  return g;
+// whether the LSTM cell forward runs in the context GEMM's epilogue and the backward in the dh GEMM's (lstmgemm.hip:
+// full-K row blocks; bf16, attention, the transposed weight copies for the backward; SatPolicy::fused_lstm = 1: the
+// separate launches)
+inline int fused_fwd(const SatDecoderDims& d, const Splits& sp) {   // the epilogue sums <= 2 h-GEMM slabs
+  return d.dtype == SAT_BF16 && d.attention && sp.h <= 2 && sat_lstm_gemm_fwd_ok(d.B, d.E, d.D);
 }
-inline SatGemm dh_gemm_shape(const SatDecoderDims& d, const Splits& sp) {
-  SatGemm g;
-  const long HG = 5L * d.E + d.D;
-  g.M = d.B; g.N = d.E; g.K = (int)HG; g.dtype = d.dtype;
-  g.lda = (long)(d.T - 1) * HG; g.ldb = HG; g.ldc = d.E; g.c_dtype = SAT_F32;
-  g.partial_splits = sp.dh; g.split_stride = (long)d.B * d.E;
-  return g;
-}
-// whether the LSTM cell forward runs inside the context GEMM, and the backward inside the dh GEMM (bf16, attention,
-// the skinny kernel on those products, SatPolicy::fused_lstm = 2; off by default: measured slower)
-inline int fused_fwd(const SatDecoderDims& d, const Splits& sp) {
-  return d.dtype == SAT_BF16 && d.attention && sat_skinny_lstm_fwd_ok(ctx_gemm_shape(d, sp), d.E, sp.h);
-}
-inline int fused_bwd(const SatDecoderDims& d, const Splits& sp, bool tr) {
-  return d.dtype == SAT_BF16 && d.attention && tr && sat_skinny_lstm_bwd_ok(dh_gemm_shape(d, sp), d.E);
+inline int fused_bwd(const SatDecoderDims& d, const Splits&, bool tr) {
+  return d.dtype == SAT_BF16 && d.attention && tr && sat_lstm_gemm_bwd_ok(d.B, d.E, 5 * d.E + d.D);
 }
 
 struct Ctx {
@@ -383,14 +364,13 @@ int fwd_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) 
   return sat_lstm_fwd_launch(lstm_fwd_args(c, w, sp, t), s);
 }
 
-// the context GEMM with the LSTM cell in its split-K reduction (one launch); *launched = 0: not eligible, nothing
+// the context GEMM with the LSTM cell in its epilogue (one launch, lstmgemm.hip); *launched = 0: not eligible, nothing
 // launched (the caller runs fwd_cgemm + fwd_lstm)
 int fwd_cgemm_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s, int* launched) {
   const SatDecoderDims& d = c.d;
-  SatGemm g = ctx_gemm_shape(d, sp);
-  g.A = c.at(w.gated_t, (long)t * d.D); g.B = c.W(c.lay.wih + d.E); g.C = w.gctx;
   int err = 0;
-  *launched = sat_skinny_lstm_fwd_try(g, d.E, w.lstm_ticket, lstm_fwd_args(c, w, sp, t), s, &err);
+  *launched = sat_lstm_gemm_fwd_try(c.at(w.gated_t, (long)t * d.D), c.T1 * d.D, c.W(c.lay.wih + d.E), d.E + d.D, d.D,
+                                    lstm_fwd_args(c, w, sp, t), s, &err);
   return err;
 }
 
@@ -485,14 +465,13 @@ int bwd_dhgemm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s
                       c.W(c.lay.hcat_w + (long)(E + D) * E), E, w.dh_rec, E, s, nullptr, 0, sp.dh, (long)B * E);
 }
 
-// the dh GEMM of step t > 0 with step t-1's LSTM cell backward in its split-K reduction (one launch); *launched = 0:
-// not eligible, nothing launched (the caller runs bwd_dhgemm(t) and bwd_lstm(t - 1) at the start of step t-1)
+// the dh GEMM of step t > 0 with step t-1's LSTM cell backward in its epilogue (one launch, lstmgemm.hip);
+// *launched = 0: not eligible, nothing launched (the caller runs bwd_dhgemm(t) and bwd_lstm(t - 1) at step t-1)
 int bwd_dhgemm_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s, int* launched) {
   const SatDecoderDims& d = c.d;
-  SatGemm g = dh_gemm_shape(d, sp);
-  g.A = c.at(w.dhg_t, (long)t * c.HG); g.B = c.W(c.lay.hcat_t); g.C = w.dh_rec;
   int err = 0;
-  *launched = sat_skinny_lstm_bwd_try(g, w.lstm_ticket + d.E / 8, lstm_bwd_args(c, w, sp, t - 1), s, &err);
+  *launched = sat_lstm_gemm_bwd_try(c.at(w.dhg_t, (long)t * c.HG), c.T1 * c.HG, c.W(c.lay.hcat_t), c.HG, (int)c.HG,
+                                    lstm_bwd_args(c, w, sp, t - 1), s, &err);
   return err;
 }
 
@@ -665,12 +644,10 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
     const int g = (int)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
     if (d.dtype == SAT_BF16)
       hipLaunchKernelGGL(init_state_kernel<bf16>, dim3(g), dim3(256), 0, s, (const float*)w.hc0pre, sp.i,
-                         (long)B * 2 * E, B, E, w.hc0, (bf16*)w.h_in_t, (long)T1 * E, w.c_in, (long)T1 * E,
-                         w.lstm_ticket, E / 8 + E / 32);
+                         (long)B * 2 * E, B, E, w.hc0, (bf16*)w.h_in_t, (long)T1 * E, w.c_in, (long)T1 * E);
     else
       hipLaunchKernelGGL(init_state_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)w.hc0pre, sp.i,
-                         (long)B * 2 * E, B, E, w.hc0, (float*)w.h_in_t, (long)T1 * E, w.c_in, (long)T1 * E,
-                         w.lstm_ticket, E / 8 + E / 32);
+                         (long)B * 2 * E, B, E, w.hc0, (float*)w.h_in_t, (long)T1 * E, w.c_in, (long)T1 * E);
     SAT_LAUNCH_CHECK();
   }
   if (att) {  // hoisted Ws = a W^T + b
@@ -845,7 +822,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   SatGemm g_wihc = wg(4 * E, D, R, dg_t, HG, w.gated_t, D, G(lay->wih + E), E + D);
   {   // one launch zeroes the BPTT accumulators, the split attention backward's tickets, (beta = 0) the dense
       // embedding gradient the scatter-add after the loop accumulates into, and the atomic split-K targets
-    SatZeroSeg seg[12];   // <= 3 + 1 + 1 + 5
+    SatZeroSeg seg[12];
     int nz = 0;
     if (att) {
       seg[nz++] = SatZeroSeg{w.dv_acc, 1, (long)B * E, (long)B * E};
@@ -853,7 +830,6 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
       seg[nz++] = SatZeroSeg{(float*)w.ticket, 1, B, B};
     }
     if (!d.bert && !accumulate) seg[nz++] = SatZeroSeg{G(lay->embedding), 1, (long)V * E, (long)V * E};
-    seg[nz++] = SatZeroSeg{(float*)(w.lstm_ticket + E / 8), 1, E / 32, E / 32};
     SatGemm* gs[5] = {&g_hcat, &g_wihx, &g_wihc, &g_init, &g_attw};
     prezero(gs, att ? 5 : 4, seg, nz);
     SAT_CHECK((hipError_t)sat_zero_segs(seg, nz, s));

@@ -201,12 +201,13 @@ __device__ __forceinline__ void lstm_cell_bwd(float gi, float gf, float gg, floa
   dc_out = dc * fg;
 }
 
-// the LSTM cell folded into the skinny GEMM's split-K reduction (skinny.hip): the context GEMM of a forward step
-// with gate-interleaved column blocks, and the recurrent dL/dh GEMM of BPTT step t carrying step t-1's cell
-// backward.  *_ok: the problem fits (shape, splits, policy; no pointers checked); *_try: 1 when launched (error in
-// *err), 0 when not eligible (the caller launches the GEMM and the pointwise kernel separately).  ticket: zeroed
-// arrival counters, E / 8 (forward) or E / 32 (backward) of them, left zeroed.
-int sat_skinny_lstm_fwd_ok(const SatGemm& g, int E, int h_splits);
-int sat_skinny_lstm_bwd_ok(const SatGemm& g, int E);
-int sat_skinny_lstm_fwd_try(const SatGemm& g, int E, unsigned* ticket, const LstmFwdArgs& l, hipStream_t st, int* err);
-int sat_skinny_lstm_bwd_try(const SatGemm& g, unsigned* ticket, const LstmBwdArgs& l, hipStream_t st, int* err);
+// the LSTM cell in the epilogue of a full-K row-block GEMM (lstmgemm.hip): the forward step's context GEMM
+// (A = gated context [B][K], W = W_ih[:, E:] rows [4E][ldw]) and BPTT step t's recurrent dL/dh GEMM (A = [dU h |
+// d f_beta h | d gates] [B][K], W = hcat^T [E][ldw]) carrying step t-1's cell backward.  *_ok: the shape and the policy
+// allow it; *_try: 1 when launched (error in *err), 0 when not eligible (the caller runs the separate launches).
+int sat_lstm_gemm_fwd_ok(int B, int E, int K);
+int sat_lstm_gemm_bwd_ok(int B, int E, int K);
+int sat_lstm_gemm_fwd_try(const void* A, long lda, const void* W, long ldw, int K, const LstmFwdArgs& l, hipStream_t s,
+                          int* err);
+int sat_lstm_gemm_bwd_try(const void* A, long lda, const void* W, long ldw, int K, const LstmBwdArgs& l, hipStream_t s,
+                          int* err);

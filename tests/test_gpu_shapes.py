@@ -302,11 +302,12 @@ def _bench_oracle(name, c, dtype):
     return _ORACLE_CACHE[key]
 
 
-def _assert_bench_instance(inst, dtype):
+def _assert_bench_instance(inst, dtype, separate=False):
     assert inst["attn_bwd_chunks"] == 1, inst          # one workgroup per row, as bench.py runs it
     if dtype == torch.bfloat16:
-        assert inst["transposed"] == 1 and inst["fused_lstm_fwd"] == 0 and inst["fused_lstm_bwd"] == 0, inst
-        assert inst["fwd_launches_per_step"] == 4 and inst["bwd_launches_per_step"] == 4, inst
+        fused = 0 if separate else 1                   # lstmgemm.hip's row-block cells unless SatPolicy.fused_lstm = 1
+        assert inst["transposed"] == 1 and inst["fused_lstm_fwd"] == fused and inst["fused_lstm_bwd"] == fused, inst
+        assert inst["fwd_launches_per_step"] == 4 - fused and inst["bwd_launches_per_step"] == 4 - fused, inst
 
 
 @pytest.mark.parametrize("name", list(BENCH_CASES))
@@ -317,36 +318,35 @@ def test_bench_instance_fp32_matches_oracle(sat, name):
     _assert_fp32(c, h, _bench_oracle(name, c, torch.float32), _bench_oracle(name, c, torch.float64))
 
 
+@pytest.mark.parametrize("cells", ["fused", "separate"])
 @pytest.mark.parametrize("name", list(BENCH_CASES))
-def test_bench_instance_bf16_close_to_oracle(sat, name):
+def test_bench_instance_bf16_close_to_oracle(sat, name, cells):
+    """bf16 bench instance against the fp32 oracle, with the LSTM cells in the context / dh GEMM epilogues
+    (lstmgemm.hip, the default: three launches per time step each way) and as separate lstm_fwd / lstm_bwd
+    launches (SatPolicy.fused_lstm = 1)."""
     c = _bench_case(name)
-    h = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"])
-    _assert_bench_instance(h["instance"], torch.bfloat16)
+    pol = sat.Policy(fused_lstm=1) if cells == "separate" else None
+    h = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"], policy=pol)
+    _assert_bench_instance(h["instance"], torch.bfloat16, separate=cells == "separate")
     _assert_bf16(c, h, _bench_oracle(name, c, torch.float32))
 
 
-@pytest.mark.parametrize("name", ["b128_tf_st96", "b64_greedy_st64"])
-def test_fused_lstm_cells_bit_identical(sat, name):
-    """The LSTM cells inside the context / dh GEMMs' split-K reductions (skinny.hip, SatPolicy.fused_lstm = 2: three
-    launches per time step) against the separate lstm_fwd / lstm_bwd launches (the default) on the bench instance:
-    the forward (preds, alphas, fed tokens, loss) bit for bit (same summation order, shared cell arithmetic); the
-    gradients within fp32 rounding (the compiler may contract the cell backward's products differently in the two
-    kernels, and BPTT carries that through 26 steps)."""
-    c = _bench_case(name)
-    a = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"], policy=sat.Policy(fused_lstm=2))
-    b = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"])
-    assert a["instance"]["fused_lstm_fwd"] == 1 and a["instance"]["fused_lstm_bwd"] == 1
-    assert a["instance"]["fwd_launches_per_step"] == 3 and a["instance"]["bwd_launches_per_step"] == 3
-    assert b["instance"]["fwd_launches_per_step"] == 4 and b["instance"]["bwd_launches_per_step"] == 4
-    assert torch.equal(a["preds"], b["preds"]) and torch.equal(a["alphas"], b["alphas"])
-    assert torch.equal(a["tokens"], b["tokens"])
-    assert a["loss"] == b["loss"]
+def test_fused_lstm_cells_close_to_separate(sat):
+    """Row-block fused cells against the separate launches on the teacher-forced bench instance: the context GEMM
+    sums its K in another order (eight wave partials of a full-K tile against split-K slabs), so the two agree
+    to fp32 rounding of the gates carried through bf16 h casts -- not bit for bit."""
+    c = _bench_case("b128_tf_st96")
+    a = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"])
+    b = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"], policy=sat.Policy(fused_lstm=1))
+    assert a["instance"]["fwd_launches_per_step"] == 3 and b["instance"]["fwd_launches_per_step"] == 4
+    assert ((a["preds"] - b["preds"]).norm() / b["preds"].norm()).item() < 1e-2
+    assert ((a["alphas"] - b["alphas"]).norm() / b["alphas"].norm()).item() < 1e-2
+    assert abs(a["loss"] - b["loss"]) < 1e-3 * abs(b["loss"])
     for n in a["grads"]:
         ga, gb = a["grads"][n], b["grads"][n]
         if gb.norm().item() < 1e-7:
             continue
-        assert ((ga - gb).norm() / gb.norm()).item() < 1e-5, n
-        assert (ga - gb).abs().max().item() <= 1e-4 * gb.abs().max().item(), n
+        assert ((ga - gb).norm() / gb.norm()).item() < 5e-2, n
 
 
 def test_bleu_parity_at_eval_shape(sat):

@@ -83,13 +83,13 @@ def label(window, attn_key):
             out.append("attn_fwd")
         elif "attn_bwd" in n:
             out.append("attn_bwd")
-        elif "lstm_fwd" in n and "skinny" not in n:
+        elif "lstm_fwd" in n and "gemm" not in n:
             out.append("lstm_fwd")
-        elif "lstm_bwd" in n and "skinny" not in n:
+        elif "lstm_bwd" in n and "gemm" not in n:
             out.append("lstm_bwd")
-        elif "skinny_lstm_fwd" in n:
+        elif "lstm_gemm_fwd" in n:
             out.append("ctx_gemm+lstm_fwd")
-        elif "skinny_lstm_bwd" in n:
+        elif "lstm_gemm_bwd" in n:
             out.append("dh_gemm+lstm_bwd")
         else:
             nxt = short(window[i + 1][0]) if i + 1 < len(window) else ""
