@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SAT_ABI_VERSION 4
+#define SAT_ABI_VERSION 5
 
 enum { SAT_F32 = 0, SAT_BF16 = 1 };
 enum { SAT_ACT_NONE = 0, SAT_ACT_RELU = 1, SAT_ACT_TANH = 2, SAT_ACT_SIGMOID = 3 };
@@ -82,7 +82,10 @@ typedef struct {
                          * 1 two images, 2 one image per workgroup */
   int fused_lstm;       /* bf16 decoder, LSTM cell per time step: 0 auto -- the cell forward in the epilogue of the context
                          * GEMM and the backward in the epilogue of the dh GEMM, each a full-K row-block GEMM (3 launches
-                         * per time step; lstmgemm.hip); 1 the split-K products + separate lstm_fwd / lstm_bwd launches */
+                         * per time step; lstmgemm.hip) in the eight-wave form; 1 the split-K products + separate
+                         * lstm_fwd / lstm_bwd launches; 2 the eight-wave fused form; 3 the four-wave fused form */
+  int gemm_pipe;        /* 256x128 pipelined GEMM with fp32 output and k-major operands (the decoder's weight / input
+                         * gradients; gemmpipe.hip): 0 auto (k-major problems of >= 4 GFLOP), 1 off, 2 every eligible */
 } SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),

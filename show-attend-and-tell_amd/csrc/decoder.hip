@@ -747,7 +747,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   // and appended to one zeroing launch instead of a zeroing pass per product
   auto prezero = [&](SatGemm* const* gs, int n, SatZeroSeg* seg, int& nseg) {
     for (int i = 0; i < n; ++i)
-      if (!accumulate && sat_gemm_splits_atomically(*gs[i])) {
+      if (!accumulate && (sat_gemm_pipe_atomic(*gs[i]) || sat_gemm_splits_atomically(*gs[i]))) {
         seg[nseg++] = SatZeroSeg{(float*)gs[i]->C, gs[i]->M, gs[i]->N, gs[i]->ldc};
         gs[i]->c_zeroed = 1;
       }

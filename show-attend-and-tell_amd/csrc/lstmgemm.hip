@@ -23,7 +23,6 @@
 
 namespace {
 
-constexpr int LG_NW = 8;   // waves per workgroup (each a K / 8 slice)
 
 struct LstmGemmFwdArgs {
   int B, E, K;                 // K = D
@@ -39,11 +38,13 @@ struct LstmGemmBwdArgs {
   LstmBwdArgs l;               // step t-1's cell backward (dh_rec unused: the GEMM result)
 };
 
-// Per wave: K slice [w KS 32, (w + 1) KS 32); MB row blocks of 16 starting at row0, NJ column blocks of 16 whose W row
-// for lane fr of block j is wrow[j]; the wave's partial tile goes to red[w] ([MB 16][NJ 16 + 4] floats).
-template <int MB, int NJ, int KS>
+// Per wave (NW waves, wave w): K slice [w KS 32, (w + 1) KS 32) in batches of KB k-steps (every fragment of a batch
+// requested before its first MFMA); MB row blocks of 16 starting at row0, NJ column blocks of 16 whose W row for lane
+// fr of block j is wrow[j]; the wave's partial tile goes to red[w] ([MB 16][NJ 16 + 4] floats).
+template <int NW, int MB, int NJ, int KS, int KB>
 __device__ __forceinline__ void full_k_tile(const bf16* A, long lda, int row0, int M, const bf16* const (&wrow)[NJ],
                                             float* red) {
+  static_assert(KS % KB == 0, "whole batches");
   constexpr int LD = NJ * 16 + 4;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -52,28 +53,33 @@ __device__ __forceinline__ void full_k_tile(const bf16* A, long lda, int row0, i
   const bf16* ar[MB];
 #pragma unroll
   for (int i = 0; i < MB; ++i) ar[i] = A + (long)min(row0 + i * 16 + fr, M - 1) * lda;   // rows past M: never stored
-  bf16x8 af[KS][MB], bw[KS][NJ];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-    for (int i = 0; i < MB; ++i) af[ks][i] = *(const bf16x8*)(ar[i] + kbeg + ks * 32);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) bw[ks][j] = *(const bf16x8*)(wrow[j] + kbeg + ks * 32);
-  }
-  // every load of the wave is issued before the first MFMA: one memory round trip per wave (left to itself the
-  // scheduler interleaves them with the MFMAs to save registers, and the wave waits once per k-step)
-  __builtin_amdgcn_sched_barrier(0);
   f32x4 acc[MB][NJ];
 #pragma unroll
   for (int i = 0; i < MB; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
+  for (int b = 0; b < KS; b += KB) {
+    bf16x8 af[KB][MB], bw[KB][NJ];
 #pragma unroll
-    for (int i = 0; i < MB; ++i)
+    for (int ks = 0; ks < KB; ++ks) {
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < MB; ++i) af[ks][i] = *(const bf16x8*)(ar[i] + kbeg + (b + ks) * 32);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bw[ks][j] = *(const bf16x8*)(wrow[j] + kbeg + (b + ks) * 32);
+    }
+    // the batch's loads all go out before its first MFMA: one memory round trip per batch (left to itself the
+    // scheduler interleaves them with the MFMAs to save registers, and the wave waits once per k-step)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < KB; ++ks)
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   float* r = red + w * (MB * 16 * LD);
 #pragma unroll
   for (int i = 0; i < MB; ++i)
@@ -83,18 +89,20 @@ __device__ __forceinline__ void full_k_tile(const bf16* A, long lda, int row0, i
   __syncthreads();
 }
 
-// the eight waves' partials of one output element, in a fixed order
-template <int MB, int NJ>
-__device__ __forceinline__ float wave_sum8(const float* red, int row, int col) {
+// the NW waves' partials of one output element, in a fixed order
+template <int NW, int MB, int NJ>
+__device__ __forceinline__ float wave_partials_sum(const float* red, int row, int col) {
   constexpr int LD = NJ * 16 + 4, TS = MB * 16 * LD;
   const float* p = red + row * LD + col;
-  return ((p[0] + p[TS]) + (p[2 * TS] + p[3 * TS])) + ((p[4 * TS] + p[5 * TS]) + (p[6 * TS] + p[7 * TS]));
+  if constexpr (NW == 4) return (p[0] + p[TS]) + (p[2 * TS] + p[3 * TS]);
+  else return ((p[0] + p[TS]) + (p[2 * TS] + p[3 * TS])) + ((p[4 * TS] + p[5 * TS]) + (p[6 * TS] + p[7 * TS]));
 }
 
-template <int MB, int KS>
-__global__ __launch_bounds__(LG_NW * 64) void lstm_gemm_fwd_kernel(LstmGemmFwdArgs a) {
+template <int NW, int MB, int KS, int KB>
+__global__ __launch_bounds__(NW * 64) void lstm_gemm_fwd_kernel(LstmGemmFwdArgs a) {
+  static_assert(NW * 64 >= MB * 16 * 8, "one thread per cell");
   const SatStampT0 t0 = sat_stamp_begin(a.l.st);
-  __shared__ __attribute__((aligned(16))) float red[LG_NW * MB * 16 * (2 * 16 + 4)];
+  __shared__ __attribute__((aligned(16))) float red[NW * MB * 16 * (2 * 16 + 4)];
   const int E = a.E, u0 = blockIdx.x * 8, row0 = blockIdx.y * 16 * MB;
   const int fr = threadIdx.x & 15;
   const LstmFwdArgs& l = a.l;
@@ -118,11 +126,11 @@ __global__ __launch_bounds__(LG_NW * 64) void lstm_gemm_fwd_kernel(LstmGemmFwdAr
     const int c = jj * 16 + fr;
     wrow[jj] = a.W + (long)((c >> 3) * E + u0 + (c & 7)) * a.ldw;
   }
-  full_k_tile<MB, 2, KS>(a.A, a.lda, row0, a.B, wrow, red);
+  full_k_tile<NW, MB, 2, KS, KB>(a.A, a.lda, row0, a.B, wrow, red);
   if (cell) {
     float g[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) g[q] = (xq[q] + hq[q]) + wave_sum8<MB, 2>(red, r, q * 8 + k);   // lstm_fwd_gp's grouping
+    for (int q = 0; q < 4; ++q) g[q] = (xq[q] + hq[q]) + wave_partials_sum<NW, MB, 2>(red, r, q * 8 + k);   // lstm_fwd_gp's grouping
     float c, h;
     lstm_cell_fwd(g[0], g[1], g[2], g[3], cp, c, h);
 #pragma unroll
@@ -136,16 +144,16 @@ __global__ __launch_bounds__(LG_NW * 64) void lstm_gemm_fwd_kernel(LstmGemmFwdAr
   sat_stamp_end(a.l.st, t0);
 }
 
-template <int KS>
-__global__ __launch_bounds__(LG_NW * 64) void lstm_gemm_bwd_kernel(LstmGemmBwdArgs a) {
+template <int NW, int KS, int KB>
+__global__ __launch_bounds__(NW * 64) void lstm_gemm_bwd_kernel(LstmGemmBwdArgs a) {
   const SatStampT0 t0 = sat_stamp_begin(a.l.st);
-  __shared__ __attribute__((aligned(16))) float red[LG_NW * 16 * (16 + 4)];
+  __shared__ __attribute__((aligned(16))) float red[NW * 16 * (16 + 4)];
   const int E = a.E, u0 = blockIdx.x * 16, row0 = blockIdx.y * 16;
   const int fr = threadIdx.x & 15;
   const LstmBwdArgs& l = a.l;
   // the cell operands of this thread's (row, unit), requested before the GEMM's fragments
   const int r = threadIdx.x >> 4, k = threadIdx.x & 15, b = row0 + r, j = u0 + k;
-  const bool cell = threadIdx.x < 256 && b < a.B;
+  const bool cell = threadIdx.x < 256 && b < a.B;   // 16 x 16 cells
   const long i = (long)b * E + j;
   float gq[4] = {0.f, 0.f, 0.f, 0.f}, cp = 0.f, cn = 0.f, dcin = 0.f, hh = 0.f;
   if (cell) {
@@ -160,9 +168,9 @@ __global__ __launch_bounds__(LG_NW * 64) void lstm_gemm_bwd_kernel(LstmGemmBwdAr
     }
   }
   const bf16* wrow[1] = {a.W + (long)(u0 + fr) * a.ldw};
-  full_k_tile<1, 1, KS>(a.A, a.lda, row0, a.B, wrow, red);
+  full_k_tile<NW, 1, 1, KS, KB>(a.A, a.lda, row0, a.B, wrow, red);
   if (cell) {
-    const float dh = wave_sum8<1, 1>(red, r, k) + hh;
+    const float dh = wave_partials_sum<NW, 1, 1>(red, r, k) + hh;
     float d4[4], dco;
     lstm_cell_bwd(gq[0], gq[1], gq[2], gq[3], cp, cn, dcin, dh, d4, dco);
 #pragma unroll
@@ -177,34 +185,60 @@ __global__ __launch_bounds__(LG_NW * 64) void lstm_gemm_bwd_kernel(LstmGemmBwdAr
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-// compile-time k-steps per wave: K / (8 waves x 32)
+// Forms (SatPolicy::fused_lstm): 0 / 2 eight waves, every fragment of a wave requested at once (alone the
+// fastest); 3 four waves in two batches per wave (half the wave slots and ~90 VGPRs: room beside the encoder's
+// workgroups).  Compile-time k-steps per wave: K / (NW x 32).
+template <int NW>
+inline int ks_of(int K) { return K % (NW * 32) ? 0 : K / (NW * 32); }
+
 template <int MB>
-bool launch_fwd_ks(int ks, dim3 grid, hipStream_t s, const LstmGemmFwdArgs& a) {
-  switch (ks) {
-    case 2: hipLaunchKernelGGL((lstm_gemm_fwd_kernel<MB, 2>), grid, dim3(LG_NW * 64), 0, s, a); return true;
-    case 8: hipLaunchKernelGGL((lstm_gemm_fwd_kernel<MB, 8>), grid, dim3(LG_NW * 64), 0, s, a); return true;
+bool launch_fwd(int form, int K, dim3 grid, hipStream_t s, const LstmGemmFwdArgs& a) {
+  if (form == 3) {
+    switch (ks_of<4>(K)) {
+      case 4: hipLaunchKernelGGL((lstm_gemm_fwd_kernel<4, MB, 4, 2>), grid, dim3(256), 0, s, a); return true;
+      case 16: hipLaunchKernelGGL((lstm_gemm_fwd_kernel<4, MB, 16, 8>), grid, dim3(256), 0, s, a); return true;
+      default: return false;
+    }
+  }
+  switch (ks_of<8>(K)) {
+    case 2: hipLaunchKernelGGL((lstm_gemm_fwd_kernel<8, MB, 2, 2>), grid, dim3(512), 0, s, a); return true;
+    case 8: hipLaunchKernelGGL((lstm_gemm_fwd_kernel<8, MB, 8, 8>), grid, dim3(512), 0, s, a); return true;
     default: return false;
   }
 }
-bool launch_bwd_ks(int ks, dim3 grid, hipStream_t s, const LstmGemmBwdArgs& a) {
-  switch (ks) {
-    case 12: hipLaunchKernelGGL((lstm_gemm_bwd_kernel<12>), grid, dim3(LG_NW * 64), 0, s, a); return true;
-    case 17: hipLaunchKernelGGL((lstm_gemm_bwd_kernel<17>), grid, dim3(LG_NW * 64), 0, s, a); return true;
-    case 18: hipLaunchKernelGGL((lstm_gemm_bwd_kernel<18>), grid, dim3(LG_NW * 64), 0, s, a); return true;
+bool launch_bwd(int form, int K, dim3 grid, hipStream_t s, const LstmGemmBwdArgs& a) {
+  if (form == 3) {
+    switch (ks_of<4>(K)) {
+      case 24: hipLaunchKernelGGL((lstm_gemm_bwd_kernel<4, 24, 12>), grid, dim3(256), 0, s, a); return true;
+      case 34: hipLaunchKernelGGL((lstm_gemm_bwd_kernel<4, 34, 17>), grid, dim3(256), 0, s, a); return true;
+      case 36: hipLaunchKernelGGL((lstm_gemm_bwd_kernel<4, 36, 18>), grid, dim3(256), 0, s, a); return true;
+      default: return false;
+    }
+  }
+  switch (ks_of<8>(K)) {
+    case 12: hipLaunchKernelGGL((lstm_gemm_bwd_kernel<8, 12, 12>), grid, dim3(512), 0, s, a); return true;
+    case 17: hipLaunchKernelGGL((lstm_gemm_bwd_kernel<8, 17, 17>), grid, dim3(512), 0, s, a); return true;
+    case 18: hipLaunchKernelGGL((lstm_gemm_bwd_kernel<8, 18, 18>), grid, dim3(512), 0, s, a); return true;
     default: return false;
   }
 }
-inline int fwd_ks(int K) { return K % (LG_NW * 32) ? 0 : K / (LG_NW * 32); }
-inline bool fwd_ks_ok(int ks) { return ks == 2 || ks == 8; }
-inline bool bwd_ks_ok(int ks) { return ks == 12 || ks == 17 || ks == 18; }
+inline int form() { return sat_policy().fused_lstm == 3 ? 3 : 2; }
+inline bool fwd_ks_ok(int K) {
+  const int ks = form() == 3 ? ks_of<4>(K) : ks_of<8>(K);
+  return form() == 3 ? (ks == 4 || ks == 16) : (ks == 2 || ks == 8);
+}
+inline bool bwd_ks_ok(int K) {
+  const int ks = form() == 3 ? ks_of<4>(K) : ks_of<8>(K);
+  return form() == 3 ? (ks == 24 || ks == 34 || ks == 36) : (ks == 12 || ks == 17 || ks == 18);
+}
 
 }  // namespace
 
 int sat_lstm_gemm_fwd_ok(int B, int E, int K) {
-  return sat_policy().fused_lstm != 1 && B >= 1 && B <= 1024 && E % 8 == 0 && fwd_ks_ok(fwd_ks(K));
+  return sat_policy().fused_lstm != 1 && B >= 1 && B <= 1024 && E % 8 == 0 && fwd_ks_ok(K);
 }
 int sat_lstm_gemm_bwd_ok(int B, int E, int K) {
-  return sat_policy().fused_lstm != 1 && B >= 1 && B <= 1024 && E % 16 == 0 && bwd_ks_ok(fwd_ks(K));
+  return sat_policy().fused_lstm != 1 && B >= 1 && B <= 1024 && E % 16 == 0 && bwd_ks_ok(K);
 }
 
 int sat_lstm_gemm_fwd_try(const void* A, long lda, const void* W, long ldw, int K, const LstmFwdArgs& l, hipStream_t s,
@@ -218,10 +252,12 @@ int sat_lstm_gemm_fwd_try(const void* A, long lda, const void* W, long ldw, int 
   a.A = (const bf16*)A; a.lda = lda; a.W = (const bf16*)W; a.ldw = ldw;
   a.l = l;
   a.l.st = sat_launch_stamps();
-  // 32-row blocks (256 workgroups at B = 128); 16-row blocks below that keep the workgroup count up
-  const bool mb2 = l.B > 64;
+  // 32-row blocks (256 workgroups at B = 128); 16-row blocks below that keep the workgroup count up (and always for
+  // the four-wave form: one thread per cell)
+  const int f = form();
+  const bool mb2 = l.B > 64 && f != 3;
   const dim3 grid(l.E / 8, sat_cdiv(l.B, mb2 ? 32 : 16));
-  const bool ok = mb2 ? launch_fwd_ks<2>(fwd_ks(K), grid, s, a) : launch_fwd_ks<1>(fwd_ks(K), grid, s, a);
+  const bool ok = mb2 ? launch_fwd<2>(f, K, grid, s, a) : launch_fwd<1>(f, K, grid, s, a);
   if (!ok) return 0;
   *err = (int)hipGetLastError();
   return 1;
@@ -237,7 +273,7 @@ int sat_lstm_gemm_bwd_try(const void* A, long lda, const void* W, long ldw, int 
   a.l = l;
   a.l.st = sat_launch_stamps();
   const dim3 grid(l.E / 16, sat_cdiv(l.B, 16));
-  if (!launch_bwd_ks(fwd_ks(K), grid, s, a)) return 0;
+  if (!launch_bwd(form(), K, grid, s, a)) return 0;
   *err = (int)hipGetLastError();
   return 1;
 }

@@ -140,6 +140,10 @@ struct SatGemm {
 int sat_gemm_launch(const SatGemm& g, hipStream_t s);
 // bf16 NT fast path (convgemm.hip); returns 1 when it launched (error code in *err).
 int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err);
+// 256x128 pipelined bf16 GEMM with fp32 output and k-major operands (gemmpipe.hip: the decoder's weight / input
+// gradients); returns 1 when it launched.  sat_gemm_pipe_atomic: it would run g as fp32 atomics into a zeroed C.
+int sat_gemm_pipe_try(const SatGemm& g, hipStream_t s, int* err);
+int sat_gemm_pipe_atomic(const SatGemm& g);
 // 256x128 pipelined bf16 conv / NT GEMM (convpipe.hip); returns 1 when it launched.
 int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err);
 // weight-stationary streaming kernel for K <= 512 1x1 convs (convstream.hip); returns 1 when it launched.

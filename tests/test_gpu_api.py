@@ -85,6 +85,8 @@ def test_policy_edit_between_forward_and_deferred_backward(sat):
     a, b = step(False), step(True)
     # a backward that read the edited policy would place the workspace regions at other offsets (garbage
     # gradients); the forward's own copy keeps them within run-to-run rounding (fp32 atomics in the embedding
-    # scatter-add)
+    # scatter-add); attention.v.bias's gradient is zero up to rounding (softmax is shift-invariant), so the absolute
+    # floor is also tied to the largest gradient of the model
+    top = max(g.abs().max().item() for g in a.values())
     for n in a:
-        assert torch.allclose(a[n], b[n], rtol=1e-4, atol=1e-5 * a[n].abs().max().item()), n
+        assert torch.allclose(a[n], b[n], rtol=1e-4, atol=1e-5 * a[n].abs().max().item() + 1e-7 * top), n

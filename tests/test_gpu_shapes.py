@@ -331,12 +331,13 @@ def test_bench_instance_bf16_close_to_oracle(sat, name, cells):
     _assert_bf16(c, h, _bench_oracle(name, c, torch.float32))
 
 
-def test_fused_lstm_cells_close_to_separate(sat):
-    """Row-block fused cells against the separate launches on the teacher-forced bench instance: the context GEMM
-    sums its K in another order (eight wave partials of a full-K tile against split-K slabs), so the two agree
-    to fp32 rounding of the gates carried through bf16 h casts -- not bit for bit."""
+@pytest.mark.parametrize("form", [2, 3])
+def test_fused_lstm_cells_close_to_separate(sat, form):
+    """Row-block fused cells (eight- and four-wave forms) against the separate launches on the teacher-forced bench
+    instance: the context GEMM sums its K in another order (wave partials of a full-K tile against split-K slabs),
+    so the two agree to fp32 rounding of the gates carried through bf16 h casts -- not bit for bit."""
     c = _bench_case("b128_tf_st96")
-    a = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"])
+    a = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"], policy=sat.Policy(fused_lstm=form))
     b = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"], policy=sat.Policy(fused_lstm=1))
     assert a["instance"]["fwd_launches_per_step"] == 3 and b["instance"]["fwd_launches_per_step"] == 4
     assert ((a["preds"] - b["preds"]).norm() / b["preds"].norm()).item() < 1e-2

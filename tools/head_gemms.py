@@ -72,7 +72,7 @@ def main():
     ap.add_argument("--torch", action="store_true",
                     help="calibration: torch.matmul (hipBLASLt) of the same bf16 operands, bf16 output")
     a = ap.parse_args()
-    tot_us = tot_f = 0.0
+    tot_us = tot_f = tot_tile = 0.0
     for name, M, N, K, ta, tb, cdt, beta, *rest in SHAPES:
         act = rest[0] if rest else 0
         A, Bm, C = operands(M, N, K, ta, tb, cdt)
@@ -80,8 +80,10 @@ def main():
         us = time_one(A, Bm, C, ta, tb, beta, None, a.reps, act)
         tot_us += us
         tot_f += f
+        us_tile = time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_pipe=1), a.reps, act)
+        tot_tile += us_tile
         line = f"{name:30s} M {M:5d} N {N:5d} K {K:5d} {'T' if ta else 'N'}{'T' if tb else 'N'}  {us:8.1f} us " \
-               f"{f / us / 1e6:7.1f} TF/s"
+               f"{f / us / 1e6:7.1f} TF/s  [gemm_pipe off: {us_tile:.1f} us]"
         if a.tiles:
             alt = []
             for tile in (1, 2, 3, 4, 5):
@@ -111,7 +113,8 @@ def main():
                    for wgs in [int(v) for v in a.split_wgs.split(",")]]
             line += "  [" + " ".join(alt) + "]"
         print(line, flush=True)
-    print(f"total {tot_us:.1f} us for {tot_f / 1e9:.1f} GFLOP = {tot_f / tot_us / 1e6:.1f} TF/s", flush=True)
+    print(f"total {tot_us:.1f} us for {tot_f / 1e9:.1f} GFLOP = {tot_f / tot_us / 1e6:.1f} TF/s "
+          f"(gemm_pipe off: {tot_tile:.1f} us)", flush=True)
 
 
 if __name__ == "__main__":

@@ -12,6 +12,7 @@
 #   cfg4 | cfg5        the --no-tf / --bert --network vgg19 lines
 #   gloo2              bench.py as two ranks over gloo on the one GPU at --batch 64 (the N > 1 path, cfg3 per rank)
 #   prof               rocprofv3 --kernel-trace --stats of the default bench command (+ tools/prof_summary.py)
+#   prof:LABEL:ARGS    the same over a quick bench line with extra flags (A/B of per-kernel times)
 #   pmcdec             two PMC passes (FETCH_SIZE, WRITE_SIZE) over the decoder's per-step kernels
 #                      (tools/decoder_pmc.py; summary -> gpurun_out/TAG/pmc_decoder.json)
 #   pmcdec2            SQ / TCC counter groups over the same decoder run (per-kernel means -> pmc2_*.json)
@@ -60,6 +61,10 @@ for s in "$@"; do
            run gloo2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                --master-port 29531 bench.py --gpus 2 --batch 64 --dist-backend gloo --steps 30 $QUIET || exit $? ;;
     cfg5) run cfg5 300 python bench.py --bert --network vgg19 $QUIET || exit $? ;;
+    prof:*) rest=${s#prof:}; label=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+          run prof_$label 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$label" -o run --output-format csv -- \
+              python bench.py --steps 100 $QUIET --no-diagnostics ${args//,/ } || exit $?
+          python tools/prof_summary.py "$OUT/prof_$label" "$OUT/prof_$label.log" "$OUT/prof_$label.json" | head -40 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
               python bench.py || exit $?
           python tools/prof_summary.py "$OUT/prof" "$OUT/prof.log" "$OUT/prof_summary.json" | head -60 ;;
