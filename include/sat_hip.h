@@ -64,7 +64,8 @@ typedef struct {
   int attn_bwd;         /* attention backward per decoder step: 0 auto, 1 the two-launch form */
   int attn_bwd_chunks;  /* split attention backward: slot chunks per batch row (0 auto: ~256 workgroups) */
   int gemm_split_wgs;   /* bf16 tile GEMM, fp32 output: workgroups an atomic split-K aims for (0 = 320; problems with
-                         * fewer than half as many tiles and K >= 1024 are split) */
+                         * fewer than half as many tiles and K >= 1024 are split); the pipelined fp32-output GEMM
+                         * (gemm_pipe): > 0 aims its split-K at that many workgroups, 0 its rounds x k-tiles model */
   int lstm_blocks;      /* LSTM pointwise kernels: cap on the 256-thread blocks (0 = one per 64 units, <= 4096) */
   int decoder_splits[4];/* split-K counts of the per-step bf16 decoder GEMMs -- h: [U; f_beta; W_hh] h, c: context
                          * part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic */

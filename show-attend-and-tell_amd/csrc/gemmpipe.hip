@@ -284,13 +284,20 @@ __global__ __launch_bounds__(512) void gemm_pipe_kernel(GArgs a) {
 
 inline bool gal16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-// split count for `tiles` output tiles of nk k-tiles on 256 CUs (one workgroup each): the s in [1, 16] with at
-// least 4 k-tiles per split minimising rounds x k-tiles per split (ties: fewer splits, fewer atomics)
+// split count for `tiles` output tiles of nk k-tiles on 256 CUs (one workgroup each), at least 4 k-tiles per split:
+// SatPolicy::gemm_split_wgs > 0 aims at that many workgroups; else the s in [1, 16] minimising rounds x (k-tiles per
+// split + epilogue), the atomic epilogue priced at 3 k-tiles and the plain one at 1 (ties: fewer splits)
 int pick_splits(long tiles, int nk) {
+  const int smax = nk / 4 < 16 ? (nk / 4 > 1 ? nk / 4 : 1) : 16;
+  const int wgs = sat_policy().gemm_split_wgs;
+  if (wgs > 0) {
+    const int s = sat_cdiv(wgs, tiles);
+    return s < 1 ? 1 : (s > smax ? smax : s);
+  }
   int best = 1;
-  long best_cost = sat_cdiv(tiles, 256) * (long)nk;
-  for (int s = 2; s <= 16 && nk / s >= 4; ++s) {
-    const long cost = sat_cdiv(tiles * s, 256) * (long)sat_cdiv(nk, s);
+  long best_cost = sat_cdiv(tiles, 256) * (long)(nk + 1);
+  for (int s = 2; s <= smax; ++s) {
+    const long cost = sat_cdiv(tiles * s, 256) * (long)(sat_cdiv(nk, s) + 3);
     if (cost < best_cost) { best = s; best_cost = cost; }
   }
   return best;
