@@ -636,7 +636,7 @@ def main():
     policy = None
     extra = dict(skinny=1 if args.no_skinny else 0, conv3x3_ws=1 if args.no_ws3x3 else 0,
                  gemm_stages=args.gemm_stages, conv_slices=args.conv_slices)
-    for kv in (x for x in args.policy.split(",") if x):
+    for kv in (x for x in args.policy.replace("+", ",").split(",") if x):   # "+" also separates (tools/session.sh)
         k, v = kv.split("=")
         extra[k] = [int(t) for t in v.split(".")] if "." in v else int(v)   # decoder_splits=2.0.0.0
     if any(extra.values()):

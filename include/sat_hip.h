@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SAT_ABI_VERSION 5
+#define SAT_ABI_VERSION 6
 
 enum { SAT_F32 = 0, SAT_BF16 = 1 };
 enum { SAT_ACT_NONE = 0, SAT_ACT_RELU = 1, SAT_ACT_TANH = 2, SAT_ACT_SIGMOID = 3 };
@@ -86,7 +86,11 @@ typedef struct {
                          * per time step; lstmgemm.hip) in the eight-wave form; 1 the split-K products + separate
                          * lstm_fwd / lstm_bwd launches; 2 the eight-wave fused form; 3 the four-wave fused form */
   int gemm_pipe;        /* 256x128 pipelined GEMM with fp32 output and k-major operands (the decoder's weight / input
-                         * gradients; gemmpipe.hip): 0 auto (k-major problems of >= 4 GFLOP), 1 off, 2 every eligible */
+                         * gradients; gemmpipe.hip): 0 auto = off (measured slower than the tile kernel and hipBLASLt
+                         * on those shapes), 1 off, 2 every eligible */
+  int gemm_lib;         /* plain bf16 GEMMs with fp32 output and k-major operands (the decoder's batched weight / input
+                         * gradients) on hipBLASLt (gemmlib.hip): 0 auto (weight gradients, input gradients with
+                         * K <= 4096), 1 off (the hand-written tile kernels), 2 every eligible */
 } SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),

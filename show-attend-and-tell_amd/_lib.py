@@ -25,7 +25,7 @@ class SatConvGeom(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("N", "H", "W", "C", "KH", "KW", "stride", "pad", "OH", "OW")]
 
 
-ABI_VERSION = 5   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
+ABI_VERSION = 6   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
 
 
 class SatPolicy(ctypes.Structure):
@@ -34,7 +34,7 @@ class SatPolicy(ctypes.Structure):
                                      "gemm_linear_order", "gemm_epilogue", "attn_bwd",
                                      "attn_bwd_chunks", "gemm_split_wgs", "lstm_blocks")] + \
                [("decoder_splits", c_int * 4), ("stamps", c_void_p), ("stamp_capacity", c_int), ("conv_slices", c_int),
-                ("fused_lstm", c_int), ("gemm_pipe", c_int)]
+                ("fused_lstm", c_int), ("gemm_pipe", c_int), ("gemm_lib", c_int)]
 
     def __init__(self, **kw):
         splits = kw.pop("decoder_splits", None)

@@ -359,6 +359,7 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s) {
     if (sat_conv3x3_ws_try(g, s, &err)) return err;
     if (sat_conv_stream_try(g, s, &err)) return err;
     if (sat_conv_pipe_try(g, s, &err)) return err;
+    if (sat_gemm_lib_try(g, s, &err)) return err;
     if (sat_gemm_pipe_try(g, s, &err)) return err;
     if (sat_fast_gemm_try(g, s, &err)) return err;
   }

@@ -307,8 +307,9 @@ int pick_splits(long tiles, int nk) {
 
 int sat_gemm_pipe_try(const SatGemm& g, hipStream_t s, int* err) {
   *err = 0;
-  const int mode = sat_policy().gemm_pipe;   // 0 auto, 1 off, 2 every eligible problem
-  if (mode == 1) return 0;
+  // 0 auto = off: measured slower than the tile kernel on the decoder's shapes, 2 every eligible
+  const int mode = sat_policy().gemm_pipe;
+  if (mode != 2) return 0;
   if (g.dtype != SAT_BF16 || g.c_dtype != SAT_F32 || g.batch != 1 || g.aux || g.add1 || g.conv.C > 0) return 0;
   if (g.alpha != 1.f || (g.beta != 0.f && g.beta != 1.f) || g.partial_splits > 1) return 0;
   const bool at = g.transA != 0, bt = g.transB != 0;
@@ -351,7 +352,7 @@ int sat_gemm_pipe_try(const SatGemm& g, hipStream_t s, int* err) {
 // whether sat_gemm_pipe_try would run g as fp32 atomics that need C zeroed first (decoder.hip's prezero)
 int sat_gemm_pipe_atomic(const SatGemm& g) {
   const int mode = sat_policy().gemm_pipe;
-  if (mode == 1 || g.dtype != SAT_BF16 || g.c_dtype != SAT_F32 || g.beta != 0.f || g.bias || g.act != SAT_ACT_NONE ||
+  if (mode != 2 || g.dtype != SAT_BF16 || g.c_dtype != SAT_F32 || g.beta != 0.f || g.bias || g.act != SAT_ACT_NONE ||
       g.add1 || g.partial_splits > 1 || g.conv.C > 0)
     return 0;
   if (mode == 0 && (!(g.transA || g.transB) || 2.0 * g.M * g.N * g.K < 4e9)) return 0;

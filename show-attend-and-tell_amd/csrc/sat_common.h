@@ -144,6 +144,8 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err);
 // gradients); returns 1 when it launched.  sat_gemm_pipe_atomic: it would run g as fp32 atomics into a zeroed C.
 int sat_gemm_pipe_try(const SatGemm& g, hipStream_t s, int* err);
 int sat_gemm_pipe_atomic(const SatGemm& g);
+// the same products on hipBLASLt (gemmlib.hip, SatPolicy::gemm_lib); returns 1 when it launched.
+int sat_gemm_lib_try(const SatGemm& g, hipStream_t s, int* err);
 // 256x128 pipelined bf16 conv / NT GEMM (convpipe.hip); returns 1 when it launched.
 int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err);
 // weight-stationary streaming kernel for K <= 512 1x1 convs (convstream.hip); returns 1 when it launched.

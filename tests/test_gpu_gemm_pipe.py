@@ -5,6 +5,8 @@ Every operand layout (A and B each row-major or k-major), the split-K atomic epi
 the plain epilogue with bias + ReLU, beta = 1 accumulation, and edges: M not a multiple of 256, N not a multiple
 of 128, K not a multiple of 64 (the buffer-resource zero fill), each against an fp64 product of the same bf16
 operands (fp32 accumulation: 2e-5 relative) and against the 128x128 tile kernel (SatPolicy.gemm_pipe = 1).
+The same cases through hipBLASLt (csrc/gemmlib.hip, SatPolicy.gemm_lib = 2), which runs the decoder's weight
+gradients by default.
 """
 import pytest
 import torch
@@ -58,9 +60,9 @@ def test_gemm_pipe_matches_fp64_and_tile_kernel(sat, M, N, K, transA, transB, be
     if bias_relu:
         kw.update(bias=bias.to(DEV), act=sat._lib.ACT_RELU)
     out = {}
-    for mode in (2, 1):   # every eligible problem on the pipelined kernel / never
+    for mode in (2, 1):   # every eligible problem on the pipelined kernel / never (hipBLASLt off in both)
         C = C0.clone().to(DEV)
-        ops.gemm(Ad, Bd, C, policy=sat.Policy(gemm_pipe=mode), **kw)
+        ops.gemm(Ad, Bd, C, policy=sat.Policy(gemm_pipe=mode, gemm_lib=1), **kw)
         torch.cuda.synchronize()
         out[mode] = C.cpu()
     assert torch.isfinite(out[2]).all()
@@ -78,8 +80,28 @@ def test_gemm_pipe_leaves_rows_past_m_alone(sat):
     Bm = torch.randn(K, N, generator=g).bfloat16().to(DEV)
     big = torch.full((M + 5, N + 8), 7.0, device=DEV)
     C = big[:M, :N]
-    ops.gemm(A, Bm, C, transA=True, transB=True, policy=sat.Policy(gemm_pipe=2))
+    ops.gemm(A, Bm, C, transA=True, transB=True, policy=sat.Policy(gemm_pipe=2, gemm_lib=1))
     torch.cuda.synchronize()
     ref = A.double().T @ Bm.double()
     assert rel(C, ref) < 2e-5
+    assert (big[M:] == 7.0).all() and (big[:, N:] == 7.0).all()
+
+
+@pytest.mark.parametrize("M,N,K,transA,transB,beta,bias_relu", [c for c in CASES if not c[6]])
+def test_gemm_lib_matches_fp64(sat, M, N, K, transA, transB, beta, bias_relu):
+    """hipBLASLt (SatPolicy.gemm_lib = 2) on the same products: fp32 accumulation of the same bf16 operands."""
+    from sat_amd import ops
+    g = torch.Generator().manual_seed(M + 5 * N + 3 * K)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    Bm = torch.randn(N, K, generator=g).bfloat16()
+    C0 = torch.randn(M, N, generator=g)
+    ref = A.double() @ Bm.double().T + beta * C0.double()
+    Ad = (A.T.contiguous() if transA else A).to(DEV)
+    Bd = (Bm.T.contiguous() if transB else Bm).to(DEV)
+    big = torch.full((M + 3, N + 8), 7.0, device=DEV)
+    C = big[:M, :N]
+    C.copy_(C0.to(DEV))
+    ops.gemm(Ad, Bd, C, transA=transA, transB=transB, beta=beta, policy=sat.Policy(gemm_lib=2))
+    torch.cuda.synchronize()
+    assert rel(C, ref) < 2e-5, rel(C, ref)
     assert (big[M:] == 7.0).all() and (big[:, N:] == 7.0).all()

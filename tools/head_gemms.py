@@ -2,8 +2,9 @@
 
 B = 128, T = 27 (R = B * 26 = 3328 rows), V = 10000, E = 512, D = 2048, L = 49, bf16 operands: the hoisted
 Ws = a W^T, the input / output head products of the forward, and the weight / input gradients of the backward
-(decoder.hip).  Each product is re-issued back to back between HIP events; per tile configuration
-(SatPolicy.gemm_tile) when --tiles.
+(decoder.hip).  Each product is re-issued back to back between HIP events: the library default (hipBLASLt for the
+k-major fp32-output products, SatPolicy.gemm_lib), the hand-written tile kernel and the pipelined one (gemm_pipe);
+per tile configuration (SatPolicy.gemm_tile) when --tiles.
 
     python tools/head_gemms.py [--tiles] [--reps 10]
 """
@@ -67,7 +68,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tiles", action="store_true")
     ap.add_argument("--split", action="store_true", help="also the atomic split-K aimed at other workgroup counts")
-    ap.add_argument("--split-wgs", default="512,768,1024", help="--split: the SatPolicy.gemm_split_wgs values")
+    ap.add_argument("--split-wgs", default="256,512,1024", help="--split: the SatPolicy.gemm_split_wgs values")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--torch", action="store_true",
                     help="calibration: torch.matmul (hipBLASLt) of the same bf16 operands, bf16 output")
@@ -80,10 +81,11 @@ def main():
         us = time_one(A, Bm, C, ta, tb, beta, None, a.reps, act)
         tot_us += us
         tot_f += f
-        us_tile = time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_pipe=1), a.reps, act)
+        us_tile = time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_lib=1), a.reps, act)
+        us_pipe = time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_lib=1, gemm_pipe=2), a.reps, act)
         tot_tile += us_tile
         line = f"{name:30s} M {M:5d} N {N:5d} K {K:5d} {'T' if ta else 'N'}{'T' if tb else 'N'}  {us:8.1f} us " \
-               f"{f / us / 1e6:7.1f} TF/s  [gemm_pipe off: {us_tile:.1f} us]"
+               f"{f / us / 1e6:7.1f} TF/s  [hand-written: tile {us_tile:.1f} us, pipe {us_pipe:.1f} us]"
         if a.tiles:
             alt = []
             for tile in (1, 2, 3, 4, 5):
@@ -110,11 +112,11 @@ def main():
             line += f"  [hipBLASLt {st.elapsed_time(en) / a.reps * 1e3:.1f} us]"
         if a.split:
             alt = [f"w{wgs}:{time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_split_wgs=wgs), a.reps, act):.1f}"
-                   for wgs in [int(v) for v in a.split_wgs.split(",")]]
+                   for wgs in [int(v) for v in a.split_wgs.replace("/", ",").split(",")]]
             line += "  [" + " ".join(alt) + "]"
         print(line, flush=True)
     print(f"total {tot_us:.1f} us for {tot_f / 1e9:.1f} GFLOP = {tot_f / tot_us / 1e6:.1f} TF/s "
-          f"(gemm_pipe off: {tot_tile:.1f} us)", flush=True)
+          f"(hand-written tile kernels: {tot_tile:.1f} us)", flush=True)
 
 
 if __name__ == "__main__":
