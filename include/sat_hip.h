@@ -81,16 +81,17 @@ typedef struct {
                          * (channel slices when B <= 64), 1 one workgroup per half image, 2 two 128-channel slices
                          * per half image; sat_conv3x3_frag at 7x7: 0 auto (two images per workgroup when B > 64),
                          * 1 two images, 2 one image per workgroup */
-  int fused_lstm;       /* bf16 decoder, LSTM cell per time step: 0 auto -- the cell forward in the epilogue of the context
-                         * GEMM and the backward in the epilogue of the dh GEMM, each a full-K row-block GEMM (3 launches
-                         * per time step; lstmgemm.hip) in the eight-wave form; 1 the split-K products + separate
-                         * lstm_fwd / lstm_bwd launches; 2 the eight-wave fused form; 3 the four-wave fused form */
+  int fused_lstm;       /* bf16 decoder, LSTM cell per time step: 0 auto = 1; 1 the split-K context / dh products + separate
+                         * lstm_fwd / lstm_bwd launches (4 per time step each way); 2 the cell forward in the epilogue of
+                         * the context GEMM and the backward in the dh GEMM's, full-K row-block GEMMs (3 launches per
+                         * time step; lstmgemm.hip), eight waves per workgroup; 3 the same on four waves.  The fused
+                         * forms are faster alone and slower beside the encoder */
   int gemm_pipe;        /* 256x128 pipelined GEMM with fp32 output and k-major operands (the decoder's weight / input
                          * gradients; gemmpipe.hip): 0 auto = off (measured slower than the tile kernel and hipBLASLt
                          * on those shapes), 1 off, 2 every eligible */
   int gemm_lib;         /* plain bf16 GEMMs with fp32 output and k-major operands (the decoder's batched weight / input
                          * gradients) on hipBLASLt (gemmlib.hip): 0 auto (weight gradients, input gradients with
-                         * K <= 4096), 1 off (the hand-written tile kernels), 2 every eligible */
+                         * 1024 <= K <= 4096), 1 off (the hand-written tile kernels), 2 every eligible */
 } SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),

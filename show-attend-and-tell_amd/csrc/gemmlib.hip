@@ -62,10 +62,11 @@ bool make_plan(const SatGemm& g, Plan* p) {
 }
 
 // the shapes hipBLASLt takes in auto mode: k-major fp32-output products (the weight gradients; the input gradients
-// with K <= 4096 -- the vocabulary-deep dX of the output head measured faster on the tile kernel)
+// with 1024 <= K <= 4096 -- the vocabulary-deep dX of the output head and the 512-deep dX of f_z measured faster on
+// the tile kernel, profiles/r4_s10/head_gemms.log)
 bool auto_shape(const SatGemm& g) {
   if (g.transA && g.transB) return true;
-  return g.transB && !g.transA && g.K <= 4096;
+  return g.transB && !g.transA && g.K >= 1024 && g.K <= 4096;
 }
 
 }  // namespace

@@ -185,9 +185,9 @@ __global__ __launch_bounds__(NW * 64) void lstm_gemm_bwd_kernel(LstmGemmBwdArgs 
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-// Forms (SatPolicy::fused_lstm): 0 / 2 eight waves, every fragment of a wave requested at once (alone the
-// fastest); 3 four waves in two batches per wave (half the wave slots and ~90 VGPRs: room beside the encoder's
-// workgroups).  Compile-time k-steps per wave: K / (NW x 32).
+// Forms (SatPolicy::fused_lstm, opt-in: beside the encoder both lose to the separate launches): 2 eight
+// waves, every fragment of a wave requested at once (alone the fastest); 3 four waves in two batches per wave
+// (half the wave slots).  Compile-time k-steps per wave: K / (NW x 32).
 template <int NW>
 inline int ks_of(int K) { return K % (NW * 32) ? 0 : K / (NW * 32); }
 
@@ -235,10 +235,10 @@ inline bool bwd_ks_ok(int K) {
 }  // namespace
 
 int sat_lstm_gemm_fwd_ok(int B, int E, int K) {
-  return sat_policy().fused_lstm != 1 && B >= 1 && B <= 1024 && E % 8 == 0 && fwd_ks_ok(K);
+  return sat_policy().fused_lstm >= 2 && B >= 1 && B <= 1024 && E % 8 == 0 && fwd_ks_ok(K);
 }
 int sat_lstm_gemm_bwd_ok(int B, int E, int K) {
-  return sat_policy().fused_lstm != 1 && B >= 1 && B <= 1024 && E % 16 == 0 && bwd_ks_ok(K);
+  return sat_policy().fused_lstm >= 2 && B >= 1 && B <= 1024 && E % 16 == 0 && bwd_ks_ok(K);
 }
 
 int sat_lstm_gemm_fwd_try(const void* A, long lda, const void* W, long ldw, int K, const LstmFwdArgs& l, hipStream_t s,

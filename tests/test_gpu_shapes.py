@@ -302,10 +302,10 @@ def _bench_oracle(name, c, dtype):
     return _ORACLE_CACHE[key]
 
 
-def _assert_bench_instance(inst, dtype, separate=False):
+def _assert_bench_instance(inst, dtype, fused=False):
     assert inst["attn_bwd_chunks"] == 1, inst          # one workgroup per row, as bench.py runs it
     if dtype == torch.bfloat16:
-        fused = 0 if separate else 1                   # lstmgemm.hip's row-block cells unless SatPolicy.fused_lstm = 1
+        fused = 1 if fused else 0                      # lstmgemm.hip's row-block cells only with SatPolicy.fused_lstm >= 2
         assert inst["transposed"] == 1 and inst["fused_lstm_fwd"] == fused and inst["fused_lstm_bwd"] == fused, inst
         assert inst["fwd_launches_per_step"] == 4 - fused and inst["bwd_launches_per_step"] == 4 - fused, inst
 
@@ -321,13 +321,13 @@ def test_bench_instance_fp32_matches_oracle(sat, name):
 @pytest.mark.parametrize("cells", ["fused", "separate"])
 @pytest.mark.parametrize("name", list(BENCH_CASES))
 def test_bench_instance_bf16_close_to_oracle(sat, name, cells):
-    """bf16 bench instance against the fp32 oracle, with the LSTM cells in the context / dh GEMM epilogues
-    (lstmgemm.hip, the default: three launches per time step each way) and as separate lstm_fwd / lstm_bwd
-    launches (SatPolicy.fused_lstm = 1)."""
+    """bf16 bench instance against the fp32 oracle, with the LSTM cells as separate lstm_fwd / lstm_bwd launches
+    (the default) and in the context / dh GEMM epilogues (lstmgemm.hip, SatPolicy.fused_lstm = 2: three launches
+    per time step each way)."""
     c = _bench_case(name)
-    pol = sat.Policy(fused_lstm=1) if cells == "separate" else None
+    pol = sat.Policy(fused_lstm=2) if cells == "fused" else None
     h = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"], policy=pol)
-    _assert_bench_instance(h["instance"], torch.bfloat16, separate=cells == "separate")
+    _assert_bench_instance(h["instance"], torch.bfloat16, fused=cells == "fused")
     _assert_bf16(c, h, _bench_oracle(name, c, torch.float32))
 
 
@@ -338,7 +338,7 @@ def test_fused_lstm_cells_close_to_separate(sat, form):
     so the two agree to fp32 rounding of the gates carried through bf16 h casts -- not bit for bit."""
     c = _bench_case("b128_tf_st96")
     a = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"], policy=sat.Policy(fused_lstm=form))
-    b = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"], policy=sat.Policy(fused_lstm=1))
+    b = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"])
     assert a["instance"]["fwd_launches_per_step"] == 3 and b["instance"]["fwd_launches_per_step"] == 4
     assert ((a["preds"] - b["preds"]).norm() / b["preds"].norm()).item() < 1e-2
     assert ((a["alphas"] - b["alphas"]).norm() / b["alphas"].norm()).item() < 1e-2
