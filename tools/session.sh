@@ -18,6 +18,8 @@
 #   pmcdec2            SQ / TCC counter groups over the same decoder run (per-kernel means -> pmc2_*.json)
 #   ab:LABEL:ARGS      one A/B bench line (ARGS comma-separated bench.py flags, e.g. ab:st80:--split-target,80);
 #                      prints value and ms/step
+#   abl:LABEL:LIB:ARGS the same with the diagnostics build show-attend-and-tell_amd/libsat_hip_LIB.so
+#                      (tools/build_variant.sh) loaded instead of the product library
 #   abd:LABEL:ARGS     the same with the diagnostics (per-step decoder kernels, trunk classes; tools/bench_brief.py)
 #   py:SCRIPT[:ARGS]   python SCRIPT ARGS (comma-separated) under a 300 s limit
 set -u
@@ -85,6 +87,10 @@ for s in "$@"; do
       done ;;
     ab:*) rest=${s#ab:}; label=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
           run ab_${n}_$label 300 python bench.py --steps 150 $QUIET --no-diagnostics ${args//,/ } || exit $?
+          echo "[$label] $(line "$OUT/ab_${n}_$label.log")" ;;
+    abl:*) rest=${s#abl:}; label=${rest%%:*}; rest=${rest#*:}; lib=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+          SAT_HIP_LIB_TUNING=show-attend-and-tell_amd/libsat_hip_$lib.so \
+            run ab_${n}_$label 300 python bench.py --steps 150 $QUIET --no-diagnostics ${args//,/ } || exit $?
           echo "[$label] $(line "$OUT/ab_${n}_$label.log")" ;;
     abd:*) rest=${s#abd:}; label=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
           run abd_${n}_$label 300 python bench.py --steps 100 $QUIET ${args//,/ } || exit $?
