@@ -106,6 +106,7 @@ constexpr int younger_than_a(int T, int KT1, int NT, int PF, bool stream, int nb
 // <= 168 VGPRs: bottleneck_kernel_share)
 template <int IW, int RO, int CIN, int CMID, int PF, int ABL>
 __device__ __forceinline__ void bottleneck_body(const KArgs& a) {
+  const __amdgpu_buffer_rsrc_t rY = sat_out_rsrc(a.y, 0x7fffffffL);   // output stores (sat_common.h policy)
   static_assert(IW / RO == 2 && IW % RO == 0, "two workgroups per image");
   static_assert(CMID == 256 && CIN % 256 == 0 && CIN % 64 == 0, "256-wide phases");
   constexpr int IH = IW;
@@ -396,7 +397,7 @@ __device__ __forceinline__ void bottleneck_body(const KArgs& a) {
             if constexpr (ABL & 16) {
               if (p < PO) __builtin_nontemporal_store(o, yp);
             } else {
-              if (p < PO) *yp = o;
+              if (p < PO) sat_st8(rY, (unsigned)((char*)yp - (char*)a.y), o);
             }
           }
         }
@@ -431,6 +432,7 @@ __global__ __launch_bounds__(512) void bottleneck_kernel(KArgs a) {
 // Each conv sums K in the unfused kernels' order: bit-identical to the three launches.
 template <int IW, int RO, int CIN, int CMID, int PF>
 __device__ __forceinline__ void block_band_body(const KArgs& a) {
+  const __amdgpu_buffer_rsrc_t rY = sat_out_rsrc(a.y, 0x7fffffffL);   // output stores (sat_common.h policy)
   constexpr int IH = IW, NPART = IH / RO, PO = RO * IW;
   constexpr int SLOTS = RO + 2, P1 = SLOTS * IW;           // c1 pixels (slot rows) = 252
   constexpr int MB1 = (P1 + 15) / 16, MB2 = (PO + 15) / 16;   // 16, 13
@@ -610,7 +612,7 @@ __device__ __forceinline__ void block_band_body(const KArgs& a) {
           bf16* ob = (bf16*)&o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) ob[e] = (bf16)fmaxf(v[e] + (float)rh[e], 0.f);
-          if (p < PO) *(u32x2*)(a.y + (pix_img + (long)y0 * IW + p) * CIN + ch) = o;
+          if (p < PO) sat_st8(rY, (unsigned)(((pix_img + (long)y0 * IW + p) * CIN + ch) * 2), o);
         }
         zero_acc();
       }
@@ -635,6 +637,7 @@ __global__ __launch_bounds__(512) void block_band_kernel(KArgs a) {
 template <int IW, int RO, int C, int PF>
 __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                   const float* __restrict__ bias, bf16* __restrict__ y) {
+  const __amdgpu_buffer_rsrc_t rY = sat_out_rsrc(y, 0x7fffffffL);   // output stores (sat_common.h policy)
   static_assert(IW / RO == 2 && IW % RO == 0 && C == 256, "two workgroups per image, 256 channels");
   constexpr int IH = IW, PO = RO * IW, R1 = RO + 1, P1 = R1 * IW;
   constexpr int MB = (P1 + 15) / 16;
@@ -741,7 +744,7 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
       ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
       ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
       ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
-      if (p < PO) *(u32x2*)(y + (pix_img + (long)y0 * IW + p) * C + ch) = o;
+      if (p < PO) sat_st8(rY, (unsigned)(((pix_img + (long)y0 * IW + p) * C + ch) * 2), o);
     }
   }
 }
@@ -758,6 +761,7 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
 template <int IW, int RO, int C, int NSL, int WM, int PF, int NWV = 8>
 __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                   const float* __restrict__ bias, bf16* __restrict__ y, int nbands) {
+  const __amdgpu_buffer_rsrc_t rY = sat_out_rsrc(y, 0x7fffffffL);   // output stores (sat_common.h policy)
   constexpr int IH = IW, NPART = IH / RO, PO = RO * IW, MBT = (PO + 15) / 16;
   constexpr int MB = (MBT + WM - 1) / WM, WN = NWV / WM;   // m-blocks per wave; NWV waves = WM m-groups x WN
   constexpr int SLOTS = RO + 2, ZR = SLOTS * IW;        // LDS pixel rows + the zero row
@@ -862,7 +866,7 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
       ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
       ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
       ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
-      if (p < PO) *(u32x2*)(y_s + (size_t)(i * 16 * C + j * 16) * 2 + row_b) = o;
+      if (p < PO) sat_st8(rY, (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b), o);
     }
   }
 }
@@ -907,6 +911,7 @@ __global__ __launch_bounds__(512) void conv3x3_half512_kernel(const bf16* __rest
 template <int IW, int C, int G, int NSL, int PF>
 __device__ __forceinline__ void conv3x3_img_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                  const float* __restrict__ bias, bf16* __restrict__ y, int nimg) {
+  const __amdgpu_buffer_rsrc_t rY = sat_out_rsrc(y, 0x7fffffffL);   // output stores (sat_common.h policy)
   constexpr int IH = IW, PI = IH * IW, P = G * PI, MB = (P + 15) / 16, ZR = P;
   constexpr int ROWB = 128, XPL = (P + 1) * ROWB, NPL = C / 64, NJ = C / (16 * 8 * NSL), CS = C / NSL;
   constexpr int NT = 9 * C / 64, KS = 9 * C / 32, CPP = C / 8;
@@ -1004,7 +1009,7 @@ __device__ __forceinline__ void conv3x3_img_body(const bf16* __restrict__ x, con
       ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
       ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
       ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
-      if (p < nv) *(u32x2*)(y_s + (size_t)(i * 16 * C + j * 16) * 2 + row_b) = o;
+      if (p < nv) sat_st8(rY, (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b), o);
     }
   }
 }
@@ -1047,6 +1052,7 @@ template <int IW, int RO, int CI, int CM, int PF, int NSL = 1>
 __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                   const float* __restrict__ bias, bf16* __restrict__ y,
                                                   unsigned x_bytes, int nhalves) {
+  const __amdgpu_buffer_rsrc_t rY = sat_out_rsrc(y, 0x7fffffffL);   // output stores (sat_common.h policy)
   static_assert(IW / RO == 2 && IW % RO == 0 && CM == 256 && CI % 64 == 0, "two workgroups per image");
   constexpr int IH = IW, PO = RO * IW, MB = (PO + 15) / 16;
   constexpr int ROWB = 128, STG = 128 * ROWB;   // ring stage: 128 rows x 64 channels
@@ -1145,7 +1151,7 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
       ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
       ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
       ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
-      if (p < PO) *(u32x2*)(y + (pix0 + p) * CM + ch) = o;
+      if (p < PO) sat_st8(rY, (unsigned)(((pix0 + p) * CM + ch) * 2), o);
     }
   }
 }

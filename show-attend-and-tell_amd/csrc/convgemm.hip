@@ -360,12 +360,13 @@ __device__ __forceinline__ void fast_gemm_kernel_body(const FArgs& a) {
     __syncthreads();
     const int cc = tid % CPR;
     constexpr int RPP = NW * 64 / CPR;
+    const __amdgpu_buffer_rsrc_t rC = sat_out_rsrc(a.C, 2L * M * a.ldc);
 #pragma unroll
     for (int it = 0; it < BM / RPP; ++it) {
       const int rl = tid / CPR + it * RPP;
       const int row = m0 + rl;
       const uint4 u = *(const uint4*)(os + rl * ROWB2 + 16 * (cc ^ out_swz(rl)));
-      if (row < M) *(uint4*)((bf16*)a.C + (long)row * a.ldc + n0 + cc * 8) = u;
+      if (row < M) sat_st16(rC, (unsigned)(((long)row * a.ldc + n0 + cc * 8) * 2), u);
     }
   } else {
   __syncthreads();   // every wave done reading the ring before the epilogue reuses the LDS
@@ -410,6 +411,7 @@ __device__ __forceinline__ void fast_gemm_kernel_body(const FArgs& a) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) bias8[e] = (bias && col + e < N) ? bias[col + e] : 0.f;
   if (vec_ok) {
+    const __amdgpu_buffer_rsrc_t rCb = sat_out_rsrc(Cb, (a.c_bf16 ? 2L : 4L) * M * a.ldc);
     // all residual loads of this thread go out before the first store
     uint4 res[ITER];
     if (a.add1 && a.add1_bf16) {
@@ -448,7 +450,7 @@ __device__ __forceinline__ void fast_gemm_kernel_body(const FArgs& a) {
         bf16* h = (bf16*)&u;
 #pragma unroll
         for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
-        *(uint4*)((bf16*)Cb + (long)row * a.ldc + col) = u;
+        sat_st16(rCb, (unsigned)(((long)row * a.ldc + col) * 2), u);
       } else {
         float* p = (float*)Cb + (long)row * a.ldc + col;
         *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);

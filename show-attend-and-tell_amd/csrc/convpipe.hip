@@ -293,6 +293,7 @@ __device__ __forceinline__ void conv_pipe_kernel_body(const PArgs& a) {
   constexpr int RPP = NW * 64 / 16, PASSES = PBM / RPP;   // 16 chunks of 8 columns x RPP rows per pass
   const int cc = tid & 15, r0 = tid >> 4;
   const int col = n0 + cc * 8;
+  const __amdgpu_buffer_rsrc_t rC = sat_out_rsrc(a.C, 2L * M * a.ldc);
   if (col < N) {
     uint4 rv[PASSES];
     if constexpr (RES) {
@@ -318,7 +319,7 @@ __device__ __forceinline__ void conv_pipe_kernel_body(const PArgs& a) {
       bf16* o = (bf16*)&u;
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = (bf16)apply_act(v[e], ACT);
-      *(uint4*)(a.C + (long)row * a.ldc + col) = u;
+      sat_st16(rC, (unsigned)(((long)row * a.ldc + col) * 2), u);
     }
   }
 }

@@ -31,11 +31,6 @@
 //     ds_read_b128 fragment reads (verified for every lane group).
 #include "sat_common.h"
 
-// cache policy of the output stores (diagnostics builds, tools/build_variant.sh: 16 = sc1, write-through -- the line
-// leaves the XCD's L2 clean, so a concurrent kernel's end-of-kernel L2 writeback has less to flush)
-#ifndef SAT_STREAM_STORE_CPOL
-#define SAT_STREAM_STORE_CPOL 0
-#endif
 #include "sat_internal.h"
 
 namespace {
@@ -253,7 +248,7 @@ __device__ __forceinline__ void conv1x1_stream_kernel_body(const SArgs& a) {
       const int m = it * MT + r;
       const unsigned off = m < a.M ? (unsigned)(((long)m * a.N + ns + 8 * lc) * 2) : S_OOB;
       typedef unsigned __attribute__((ext_vector_type(4))) u32x4;
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rC, (int)off, 0, SAT_STREAM_STORE_CPOL);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rC, (int)off, 0, SAT_OUT_CPOL);   // sat_common.h: output cache policy
     }
     it += step;
     if (it >= a.items) break;

@@ -556,6 +556,9 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   const bool vec = ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0) &&
                    (((uintptr_t)p_lp & 7) == 0);
   const long n4 = vec ? n >> 2 : 0;
+  // the updated state leaves through write-through stores (sat_common.h): 12 B per parameter that the encoder's
+  // kernel boundaries beside this launch would otherwise write back from the L2s
+  const __amdgpu_buffer_rsrc_t rp = sat_out_rsrc(p, 4 * n), rm = sat_out_rsrc(m, 4 * n), rv = sat_out_rsrc(v, 4 * n);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 pp = ((float4*)p)[i], mm = ((float4*)m)[i], vv = ((float4*)v)[i];
     const float4 gg = ((const float4*)g)[i];
@@ -563,7 +566,9 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
     adam_elem(pp.y, gg.y, mm.y, vv.y, w1, b2, eps, step_size, bc2_sqrt);
     adam_elem(pp.z, gg.z, mm.z, vv.z, w1, b2, eps, step_size, bc2_sqrt);
     adam_elem(pp.w, gg.w, mm.w, vv.w, w1, b2, eps, step_size, bc2_sqrt);
-    ((float4*)p)[i] = pp; ((float4*)m)[i] = mm; ((float4*)v)[i] = vv;
+    sat_st16(rp, (unsigned)(i * 16), *(const uint4*)&pp);
+    sat_st16(rm, (unsigned)(i * 16), *(const uint4*)&mm);
+    sat_st16(rv, (unsigned)(i * 16), *(const uint4*)&vv);
     if (p_lp) {
       uint2 o;
       bf16* ob = (bf16*)&o;

@@ -98,6 +98,31 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   }
 }
 
+// ---- output stores with a cache policy ------------------------------------------------
+// The big activation writers store through a buffer resource over their output tensor so the cache policy can be
+// chosen: SAT_OUT_CPOL 16 = sc1, write-through -- the line leaves the XCD's L2 clean (MI355X_MICROARCH.md, "stores of
+// each flavour"), so the end-of-kernel L2 writeback of every kernel running beside it (the decoder's per-step
+// chain beside the encoder) has fewer dirty lines to flush (measured: 6.51-6.57 -> 6.46-6.47 ms per step,
+// profiles/r4_s13).  0 = plain write-back stores (diagnostics builds).
+#ifndef SAT_OUT_CPOL
+#define SAT_OUT_CPOL 16
+#endif
+#ifndef SAT_OUT8_CPOL   // the 8-B stores of the staged-input conv kernels (sc1 dwordx2: a fabric write per lane)
+#define SAT_OUT8_CPOL 0
+#endif
+typedef unsigned sat_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned sat_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sat_out_rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
+                                           0x00020000);
+}
+__device__ __forceinline__ void sat_st16(__amdgpu_buffer_rsrc_t r, unsigned byte_off, uint4 u) {
+  __builtin_amdgcn_raw_buffer_store_b128(sat_u32x4{u.x, u.y, u.z, u.w}, r, (int)byte_off, 0, SAT_OUT_CPOL);
+}
+__device__ __forceinline__ void sat_st8(__amdgpu_buffer_rsrc_t r, unsigned byte_off, sat_u32x2 u) {
+  __builtin_amdgcn_raw_buffer_store_b64(u, r, (int)byte_off, 0, SAT_OUT8_CPOL);
+}
+
 // wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
