@@ -104,6 +104,31 @@ constexpr int younger_than_a(int T, int KT1, int NT, int PF, bool stream, int nb
 // 65.6 -> 77.9 / 101.8 us, profiles/r2_s25_block_nt.txt); bit 5 per-workgroup rotation of the waves'
 // n-blocks, bit 6 k-major fragment layout; bit 7 the co-residency variant (one LDS activation image,
 // <= 168 VGPRs: bottleneck_kernel_share)
+// bias + ReLU of one C^T accumulator (4 consecutive channels of one pixel), rounded once to bf16
+__device__ __forceinline__ u32x2 relu_bf16x4(const f32x4& a, const float4& b) {
+  u32x2 o;
+  bf16* ob = (bf16*)&o;
+  ob[0] = (bf16)fmaxf(a[0] + b.x, 0.f);
+  ob[1] = (bf16)fmaxf(a[1] + b.y, 0.f);
+  ob[2] = (bf16)fmaxf(a[2] + b.z, 0.f);
+  ob[3] = (bf16)fmaxf(a[3] + b.w, 0.f);
+  return o;
+}
+#ifndef SAT_PAIR_STORES   // diagnostics builds: 0 = the 8-B stores of each lane's own accumulators
+#define SAT_PAIR_STORES 1
+#endif
+// 16-B stores from a pair of C^T n-blocks (j, j + 1): lanes fh and fh ^ 1 of a pixel swap halves, so the even lane
+// holds channels 4 fh .. 4 fh + 7 of block j (at off0) and the odd one 4 (fh - 1) .. 4 fh + 3 of block j + 1 (its own
+// 8 B at off1): whole 16-B write-through stores (sat_common.h) instead of 8-B ones.  Every lane runs the exchange.
+__device__ __forceinline__ void st_pair16(__amdgpu_buffer_rsrc_t r, unsigned off0, unsigned off1, u32x2 o0, u32x2 o1,
+                                          bool ok) {
+  const bool odd = (threadIdx.x >> 4) & 1;
+  const u32x2 send = odd ? o0 : o1;
+  const unsigned gx = (unsigned)__shfl_xor((int)send.x, 16, 64), gy = (unsigned)__shfl_xor((int)send.y, 16, 64);
+  const uint4 u = odd ? make_uint4(gx, gy, o1.x, o1.y) : make_uint4(o0.x, o0.y, gx, gy);
+  if (ok) sat_st16(r, odd ? off1 - 8 : off0, u);
+}
+
 template <int IW, int RO, int CIN, int CMID, int PF, int ABL>
 __device__ __forceinline__ void bottleneck_body(const KArgs& a) {
   const __amdgpu_buffer_rsrc_t rY = sat_out_rsrc(a.y, 0x7fffffffL);   // output stores (sat_common.h policy)
@@ -732,20 +757,20 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
   });
 
   // epilogue: the lane holds channels w*32 + j*16 + 4fh .. +3 of output pixel i*16 + fr
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int ch = w * 32 + j * 16 + 4 * fh;
+  if constexpr (SAT_PAIR_STORES) {
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
-      const int p = i * 16 + fr;
-      u32x2 o;
-      bf16* ob = (bf16*)&o;
-      ob[0] = (bf16)fmaxf(acc[i][j][0] + bv[j].x, 0.f);
-      ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
-      ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
-      ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
-      if (p < PO) sat_st8(rY, (unsigned)(((pix_img + (long)y0 * IW + p) * C + ch) * 2), o);
+      const unsigned o0 = (unsigned)(((pix_img + (long)y0 * IW + i * 16 + fr) * C + w * 32 + 4 * fh) * 2);
+      st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][0], bv[0]), relu_bf16x4(acc[i][1], bv[1]), i * 16 + fr < PO);
     }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+        if (i * 16 + fr < PO)
+          sat_st8(rY, (unsigned)(((pix_img + (long)y0 * IW + i * 16 + fr) * C + w * 32 + j * 16 + 4 * fh) * 2),
+                  relu_bf16x4(acc[i][j], bv[j]));
   }
 }
 
@@ -855,19 +880,22 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
 
   char* y_s = (char*)(y + (pix_img + (long)y0 * IW + wm * MB * 16) * C + cb + wn * NJ * 16);
   const unsigned row_b = (unsigned)(fr * C + 4 * fh) * 2;
+  if constexpr (NJ % 2 == 0 && SAT_PAIR_STORES) {
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
+    for (int j = 0; j < NJ; j += 2)
 #pragma unroll
-    for (int i = 0; i < MB; ++i) {
-      const int p = (wm * MB + i) * 16 + fr;
-      u32x2 o;
-      bf16* ob = (bf16*)&o;
-      ob[0] = (bf16)fmaxf(acc[i][j][0] + bv[j].x, 0.f);
-      ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
-      ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
-      ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
-      if (p < PO) sat_st8(rY, (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b), o);
-    }
+      for (int i = 0; i < MB; ++i) {
+        const unsigned o0 = (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b);
+        st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i][j + 1], bv[j + 1]),
+                  (wm * MB + i) * 16 + fr < PO);
+      }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+        if ((wm * MB + i) * 16 + fr < PO)
+          sat_st8(rY, (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b), relu_bf16x4(acc[i][j], bv[j]));
   }
 }
 
@@ -998,19 +1026,22 @@ __device__ __forceinline__ void conv3x3_img_body(const bf16* __restrict__ x, con
 
   char* y_s = (char*)(y + (long)img0 * PI * C + cb + w * NJ * 16);
   const unsigned row_b = (unsigned)(fr * C + 4 * fh) * 2;
+  if constexpr (NJ % 2 == 0 && SAT_PAIR_STORES) {
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
+    for (int j = 0; j < NJ; j += 2)
 #pragma unroll
-    for (int i = 0; i < MB; ++i) {
-      const int p = i * 16 + fr;
-      u32x2 o;
-      bf16* ob = (bf16*)&o;
-      ob[0] = (bf16)fmaxf(acc[i][j][0] + bv[j].x, 0.f);
-      ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
-      ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
-      ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
-      if (p < nv) sat_st8(rY, (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b), o);
-    }
+      for (int i = 0; i < MB; ++i) {
+        const unsigned o0 = (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b);
+        st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i][j + 1], bv[j + 1]),
+                  i * 16 + fr < nv);
+      }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+        if (i * 16 + fr < nv)
+          sat_st8(rY, (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b), relu_bf16x4(acc[i][j], bv[j]));
   }
 }
 
@@ -1139,20 +1170,22 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
     __builtin_amdgcn_s_setprio(0);
   });
 
+  if constexpr (NJ % 2 == 0 && SAT_PAIR_STORES) {
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int ch = (nb0 + j) * 16 + 4 * fh;
+    for (int j = 0; j < NJ; j += 2)
 #pragma unroll
-    for (int i = 0; i < MB; ++i) {
-      const int p = i * 16 + fr;
-      u32x2 o;
-      bf16* ob = (bf16*)&o;
-      ob[0] = (bf16)fmaxf(acc[i][j][0] + bv[j].x, 0.f);
-      ob[1] = (bf16)fmaxf(acc[i][j][1] + bv[j].y, 0.f);
-      ob[2] = (bf16)fmaxf(acc[i][j][2] + bv[j].z, 0.f);
-      ob[3] = (bf16)fmaxf(acc[i][j][3] + bv[j].w, 0.f);
-      if (p < PO) sat_st8(rY, (unsigned)(((pix0 + p) * CM + ch) * 2), o);
-    }
+      for (int i = 0; i < MB; ++i) {
+        const unsigned o0 = (unsigned)(((pix0 + i * 16 + fr) * CM + (nb0 + j) * 16 + 4 * fh) * 2);
+        st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i][j + 1], bv[j + 1]),
+                  i * 16 + fr < PO);
+      }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+        if (i * 16 + fr < PO)
+          sat_st8(rY, (unsigned)(((pix0 + i * 16 + fr) * CM + (nb0 + j) * 16 + 4 * fh) * 2), relu_bf16x4(acc[i][j], bv[j]));
   }
 }
 
