@@ -117,16 +117,17 @@ __device__ __forceinline__ u32x2 relu_bf16x4(const f32x4& a, const float4& b) {
 #ifndef SAT_PAIR_STORES   // diagnostics builds: 0 = the 8-B stores of each lane's own accumulators
 #define SAT_PAIR_STORES 1
 #endif
-// 16-B stores from a pair of C^T n-blocks (j, j + 1): lanes fh and fh ^ 1 of a pixel swap halves, so the even lane
-// holds channels 4 fh .. 4 fh + 7 of block j (at off0) and the odd one 4 (fh - 1) .. 4 fh + 3 of block j + 1 (its own
-// 8 B at off1): whole 16-B write-through stores (sat_common.h) instead of 8-B ones.  Every lane runs the exchange.
-__device__ __forceinline__ void st_pair16(__amdgpu_buffer_rsrc_t r, unsigned off0, unsigned off1, u32x2 o0, u32x2 o1,
-                                          bool ok) {
+// 16-B stores from two C^T accumulators A, B of each lane that cover the same 4 channels group (n-blocks j, j + 1 of
+// one pixel, or m-blocks i, i + 1 of one n-block): lanes fh and fh ^ 1 swap halves, so the even lane holds channels
+// 4 fh .. 4 fh + 7 of A (its own A at offA) and the odd one 4 (fh - 1) .. 4 fh + 3 of B (its own B at offB): whole
+// 16-B write-through stores (sat_common.h) instead of 8-B ones.  Every lane runs the exchange.
+__device__ __forceinline__ void st_pair16(__amdgpu_buffer_rsrc_t r, unsigned offA, unsigned offB, u32x2 a, u32x2 b,
+                                          bool okA, bool okB) {
   const bool odd = (threadIdx.x >> 4) & 1;
-  const u32x2 send = odd ? o0 : o1;
+  const u32x2 send = odd ? a : b;
   const unsigned gx = (unsigned)__shfl_xor((int)send.x, 16, 64), gy = (unsigned)__shfl_xor((int)send.y, 16, 64);
-  const uint4 u = odd ? make_uint4(gx, gy, o1.x, o1.y) : make_uint4(o0.x, o0.y, gx, gy);
-  if (ok) sat_st16(r, odd ? off1 - 8 : off0, u);
+  const uint4 u = odd ? make_uint4(gx, gy, b.x, b.y) : make_uint4(a.x, a.y, gx, gy);
+  if (odd ? okB : okA) sat_st16(r, odd ? offB - 8 : offA, u);
 }
 
 template <int IW, int RO, int CIN, int CMID, int PF, int ABL>
@@ -761,7 +762,8 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
       const unsigned o0 = (unsigned)(((pix_img + (long)y0 * IW + i * 16 + fr) * C + w * 32 + 4 * fh) * 2);
-      st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][0], bv[0]), relu_bf16x4(acc[i][1], bv[1]), i * 16 + fr < PO);
+      st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][0], bv[0]), relu_bf16x4(acc[i][1], bv[1]), i * 16 + fr < PO,
+                i * 16 + fr < PO);
     }
   } else {
 #pragma unroll
@@ -887,15 +889,23 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
       for (int i = 0; i < MB; ++i) {
         const unsigned o0 = (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b);
         st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i][j + 1], bv[j + 1]),
-                  (wm * MB + i) * 16 + fr < PO);
+                  (wm * MB + i) * 16 + fr < PO, (wm * MB + i) * 16 + fr < PO);
       }
-  } else {
+  } else {   // odd NJ: m-block pairs (pixels i 16 + fr and (i + 1) 16 + fr), the odd last m-block with 8-B stores
+    constexpr int MP = SAT_PAIR_STORES ? MB / 2 * 2 : 0;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j) {
 #pragma unroll
-      for (int i = 0; i < MB; ++i)
+      for (int i = 0; i < MP; i += 2) {
+        const unsigned oA = (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b);
+        st_pair16(rY, oA, oA + 32 * C, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i + 1][j], bv[j]),
+                  (wm * MB + i) * 16 + fr < PO, (wm * MB + i + 1) * 16 + fr < PO);
+      }
+#pragma unroll
+      for (int i = MP; i < MB; ++i)
         if ((wm * MB + i) * 16 + fr < PO)
           sat_st8(rY, (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b), relu_bf16x4(acc[i][j], bv[j]));
+    }
   }
 }
 
@@ -1033,15 +1043,23 @@ __device__ __forceinline__ void conv3x3_img_body(const bf16* __restrict__ x, con
       for (int i = 0; i < MB; ++i) {
         const unsigned o0 = (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b);
         st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i][j + 1], bv[j + 1]),
-                  i * 16 + fr < nv);
+                  i * 16 + fr < nv, i * 16 + fr < nv);
       }
-  } else {
+  } else {   // odd NJ: m-block pairs, the odd last m-block with 8-B stores
+    constexpr int MP = SAT_PAIR_STORES ? MB / 2 * 2 : 0;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j) {
 #pragma unroll
-      for (int i = 0; i < MB; ++i)
+      for (int i = 0; i < MP; i += 2) {
+        const unsigned oA = (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b);
+        st_pair16(rY, oA, oA + 32 * C, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i + 1][j], bv[j]),
+                  i * 16 + fr < nv, (i + 1) * 16 + fr < nv);
+      }
+#pragma unroll
+      for (int i = MP; i < MB; ++i)
         if (i * 16 + fr < nv)
           sat_st8(rY, (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b), relu_bf16x4(acc[i][j], bv[j]));
+    }
   }
 }
 
@@ -1177,15 +1195,23 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
       for (int i = 0; i < MB; ++i) {
         const unsigned o0 = (unsigned)(((pix0 + i * 16 + fr) * CM + (nb0 + j) * 16 + 4 * fh) * 2);
         st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i][j + 1], bv[j + 1]),
-                  i * 16 + fr < PO);
+                  i * 16 + fr < PO, i * 16 + fr < PO);
       }
-  } else {
+  } else {   // odd NJ: m-block pairs, the odd last m-block with 8-B stores
+    constexpr int MP = SAT_PAIR_STORES ? MB / 2 * 2 : 0;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j) {
 #pragma unroll
-      for (int i = 0; i < MB; ++i)
+      for (int i = 0; i < MP; i += 2) {
+        const unsigned oA = (unsigned)(((pix0 + i * 16 + fr) * CM + (nb0 + j) * 16 + 4 * fh) * 2);
+        st_pair16(rY, oA, oA + 32 * CM, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i + 1][j], bv[j]),
+                  i * 16 + fr < PO, (i + 1) * 16 + fr < PO);
+      }
+#pragma unroll
+      for (int i = MP; i < MB; ++i)
         if (i * 16 + fr < PO)
           sat_st8(rY, (unsigned)(((pix0 + i * 16 + fr) * CM + (nb0 + j) * 16 + 4 * fh) * 2), relu_bf16x4(acc[i][j], bv[j]));
+    }
   }
 }
 
