@@ -118,6 +118,9 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(SkArgs a) {
   float* const Cs = a.C + (long)s * a.split_stride;
   const float* const bias = s == 0 ? a.bias : nullptr;
   constexpr int PIECES = MB * 16 * (SK_COLS / 4);
+  // write-through (sat_common.h): the slabs go to memory while the kernel runs, so its end-of-kernel L2 writeback --
+  // on the decoder's per-step critical path -- has little left to flush
+  const __amdgpu_buffer_rsrc_t rC = sat_out_rsrc(Cs, 0x7fffffffL);
   for (int q = threadIdx.x; q < PIECES; q += NW * 64) {
     const int row = q >> 3, c4 = (q & 7) * 4;
     if (row >= a.M) continue;
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(SkArgs a) {
       const float4 b = *(const float4*)(bias + n);
       v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
     }
-    *(float4*)(Cs + (long)row * a.ldc + n) = v;
+    sat_st16(rC, (unsigned)(((long)row * a.ldc + n) * 4), *(const uint4*)&v);
   }
   sat_stamp_end(a.st, t0);
 }
