@@ -180,15 +180,26 @@ __device__ __forceinline__ void conv_ws_kernel_body(const WArgs& a) {
     // epilogue: lane holds channels 16 cg + 4fh .. +3 of output pixel (ph * 7 + i) * 16 + fr
     int n, y0, x0;
     item_origin(it, n, y0, x0);
-#pragma unroll
-    for (int i = 0; i < WS_MB; ++i) {
+    auto out_at = [&](int i, unsigned& off) {   // bias + act of m-block i, rounded once; its byte offset
       const int p = (ph * WS_MB + i) * 16 + fr, py = p / TW, px = p - py * TW;
       w_u32x2 o;
       bf16* ob = (bf16*)&o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) ob[j] = (bf16)apply_act(acc[i][j] + bias4[j], ACT);
-      const unsigned off = (unsigned)(((((long)n * a.H + y0 + py) * a.W + x0 + px) * WS_NOUT + 16 * cg + 4 * fh) * 2);
-      __builtin_amdgcn_raw_buffer_store_b64(o, rY, (int)off, 0, 0);
+      off = (unsigned)(((((long)n * a.H + y0 + py) * a.W + x0 + px) * WS_NOUT + 16 * cg + 4 * fh) * 2);
+      return o;
+    };
+    // m-block pairs through 16-B write-through stores (sat_common.h, sat_st_pair16), an odd last one with 8 B
+#pragma unroll
+    for (int i = 0; i + 1 < WS_MB; i += 2) {
+      unsigned offA, offB;
+      const w_u32x2 oa = out_at(i, offA), ob2 = out_at(i + 1, offB);
+      sat_st_pair16(rY, offA, offB, oa, ob2, true, true);
+    }
+    if constexpr (WS_MB % 2) {
+      unsigned off;
+      const w_u32x2 o = out_at(WS_MB - 1, off);
+      __builtin_amdgcn_raw_buffer_store_b64(o, rY, (int)off, 0, SAT_OUT8_CPOL);
     }
     it += step;
     if (it >= a.items) break;

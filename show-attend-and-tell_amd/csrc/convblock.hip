@@ -117,18 +117,6 @@ __device__ __forceinline__ u32x2 relu_bf16x4(const f32x4& a, const float4& b) {
 #ifndef SAT_PAIR_STORES   // diagnostics builds: 0 = the 8-B stores of each lane's own accumulators
 #define SAT_PAIR_STORES 1
 #endif
-// 16-B stores from two C^T accumulators A, B of each lane that cover the same 4 channels group (n-blocks j, j + 1 of
-// one pixel, or m-blocks i, i + 1 of one n-block): lanes fh and fh ^ 1 swap halves, so the even lane holds channels
-// 4 fh .. 4 fh + 7 of A (its own A at offA) and the odd one 4 (fh - 1) .. 4 fh + 3 of B (its own B at offB): whole
-// 16-B write-through stores (sat_common.h) instead of 8-B ones.  Every lane runs the exchange.
-__device__ __forceinline__ void st_pair16(__amdgpu_buffer_rsrc_t r, unsigned offA, unsigned offB, u32x2 a, u32x2 b,
-                                          bool okA, bool okB) {
-  const bool odd = (threadIdx.x >> 4) & 1;
-  const u32x2 send = odd ? a : b;
-  const unsigned gx = (unsigned)__shfl_xor((int)send.x, 16, 64), gy = (unsigned)__shfl_xor((int)send.y, 16, 64);
-  const uint4 u = odd ? make_uint4(gx, gy, b.x, b.y) : make_uint4(a.x, a.y, gx, gy);
-  if (odd ? okB : okA) sat_st16(r, odd ? offB - 8 : offA, u);
-}
 
 template <int IW, int RO, int CIN, int CMID, int PF, int ABL>
 __device__ __forceinline__ void bottleneck_body(const KArgs& a) {
@@ -762,7 +750,7 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
       const unsigned o0 = (unsigned)(((pix_img + (long)y0 * IW + i * 16 + fr) * C + w * 32 + 4 * fh) * 2);
-      st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][0], bv[0]), relu_bf16x4(acc[i][1], bv[1]), i * 16 + fr < PO,
+      sat_st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][0], bv[0]), relu_bf16x4(acc[i][1], bv[1]), i * 16 + fr < PO,
                 i * 16 + fr < PO);
     }
   } else {
@@ -888,7 +876,7 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
 #pragma unroll
       for (int i = 0; i < MB; ++i) {
         const unsigned o0 = (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b);
-        st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i][j + 1], bv[j + 1]),
+        sat_st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i][j + 1], bv[j + 1]),
                   (wm * MB + i) * 16 + fr < PO, (wm * MB + i) * 16 + fr < PO);
       }
   } else {   // odd NJ: m-block pairs (pixels i 16 + fr and (i + 1) 16 + fr), the odd last m-block with 8-B stores
@@ -898,7 +886,7 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
 #pragma unroll
       for (int i = 0; i < MP; i += 2) {
         const unsigned oA = (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b);
-        st_pair16(rY, oA, oA + 32 * C, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i + 1][j], bv[j]),
+        sat_st_pair16(rY, oA, oA + 32 * C, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i + 1][j], bv[j]),
                   (wm * MB + i) * 16 + fr < PO, (wm * MB + i + 1) * 16 + fr < PO);
       }
 #pragma unroll
@@ -1042,7 +1030,7 @@ __device__ __forceinline__ void conv3x3_img_body(const bf16* __restrict__ x, con
 #pragma unroll
       for (int i = 0; i < MB; ++i) {
         const unsigned o0 = (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b);
-        st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i][j + 1], bv[j + 1]),
+        sat_st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i][j + 1], bv[j + 1]),
                   i * 16 + fr < nv, i * 16 + fr < nv);
       }
   } else {   // odd NJ: m-block pairs, the odd last m-block with 8-B stores
@@ -1052,7 +1040,7 @@ __device__ __forceinline__ void conv3x3_img_body(const bf16* __restrict__ x, con
 #pragma unroll
       for (int i = 0; i < MP; i += 2) {
         const unsigned oA = (unsigned)(y_s - (char*)y + (size_t)(i * 16 * C + j * 16) * 2 + row_b);
-        st_pair16(rY, oA, oA + 32 * C, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i + 1][j], bv[j]),
+        sat_st_pair16(rY, oA, oA + 32 * C, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i + 1][j], bv[j]),
                   i * 16 + fr < nv, (i + 1) * 16 + fr < nv);
       }
 #pragma unroll
@@ -1194,7 +1182,7 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
 #pragma unroll
       for (int i = 0; i < MB; ++i) {
         const unsigned o0 = (unsigned)(((pix0 + i * 16 + fr) * CM + (nb0 + j) * 16 + 4 * fh) * 2);
-        st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i][j + 1], bv[j + 1]),
+        sat_st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i][j + 1], bv[j + 1]),
                   i * 16 + fr < PO, i * 16 + fr < PO);
       }
   } else {   // odd NJ: m-block pairs, the odd last m-block with 8-B stores
@@ -1204,7 +1192,7 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
 #pragma unroll
       for (int i = 0; i < MP; i += 2) {
         const unsigned oA = (unsigned)(((pix0 + i * 16 + fr) * CM + (nb0 + j) * 16 + 4 * fh) * 2);
-        st_pair16(rY, oA, oA + 32 * CM, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i + 1][j], bv[j]),
+        sat_st_pair16(rY, oA, oA + 32 * CM, relu_bf16x4(acc[i][j], bv[j]), relu_bf16x4(acc[i + 1][j], bv[j]),
                   i * 16 + fr < PO, (i + 1) * 16 + fr < PO);
       }
 #pragma unroll

@@ -88,9 +88,9 @@ __global__ __launch_bounds__(256) void nchw3_to_s2d16_bf16_kernel(const float* _
       o[(sy * 2 + 0) * 3 + c] = (bf16)v[sy][c].x;
       o[(sy * 2 + 1) * 3 + c] = (bf16)v[sy][c].y;
     }
-  uint4* dst = (uint4*)(y + p * 16);
-  dst[0] = u[0];
-  dst[1] = u[1];
+  const __amdgpu_buffer_rsrc_t rY = sat_out_rsrc(y, 32L * N * H2 * W2);   // write-through (sat_common.h)
+  sat_st16(rY, (unsigned)(p * 32), u[0]);
+  sat_st16(rY, (unsigned)(p * 32 + 16), u[1]);
 }
 
 // ---- max-pool NHWC (floor mode), 8 channels per thread (16-B bf16 / 2x16-B f32 accesses) ----
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) void maxpool_bf16_kernel(const bf16* __restric
   bf16* o = (bf16*)&u;
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = (bf16)m[e];
-  *(uint4*)(y + i * 8) = u;
+  sat_st16(sat_out_rsrc(y, 2L * N * OH * OW * C), (unsigned)(i * 16), u);   // write-through (sat_common.h)
 }
 
 template <typename TI, typename TO>

@@ -123,6 +123,19 @@ __device__ __forceinline__ void sat_st8(__amdgpu_buffer_rsrc_t r, unsigned byte_
   __builtin_amdgcn_raw_buffer_store_b64(u, r, (int)byte_off, 0, SAT_OUT8_CPOL);
 }
 
+// 16-B stores from two C^T accumulators A, B of each lane that cover the same 4 channels group (n-blocks j, j + 1 of
+// one pixel, or m-blocks i, i + 1 of one n-block): lanes fh and fh ^ 1 swap halves, so the even lane holds channels
+// 4 fh .. 4 fh + 7 of A (its own A at offA) and the odd one 4 (fh - 1) .. 4 fh + 3 of B (its own B at offB): whole
+// 16-B write-through stores (sat_common.h) instead of 8-B ones.  Every lane runs the exchange.
+__device__ __forceinline__ void sat_st_pair16(__amdgpu_buffer_rsrc_t r, unsigned offA, unsigned offB, sat_u32x2 a, sat_u32x2 b,
+                                          bool okA, bool okB) {
+  const bool odd = (threadIdx.x >> 4) & 1;
+  const sat_u32x2 send = odd ? a : b;
+  const unsigned gx = (unsigned)__shfl_xor((int)send.x, 16, 64), gy = (unsigned)__shfl_xor((int)send.y, 16, 64);
+  const uint4 u = odd ? make_uint4(gx, gy, b.x, b.y) : make_uint4(a.x, a.y, gx, gy);
+  if (odd ? okB : okA) sat_st16(r, odd ? offB - 8 : offA, u);
+}
+
 // wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
