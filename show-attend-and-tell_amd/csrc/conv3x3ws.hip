@@ -189,17 +189,19 @@ __device__ __forceinline__ void conv_ws_kernel_body(const WArgs& a) {
       off = (unsigned)(((((long)n * a.H + y0 + py) * a.W + x0 + px) * WS_NOUT + 16 * cg + 4 * fh) * 2);
       return o;
     };
-    // m-block pairs through 16-B write-through stores (sat_common.h, sat_st_pair16), an odd last one with 8 B
+    // m-block pairs through 16-B stores (sat_common.h, sat_st_pair16), an odd last one with 8 B; plain write-back
+    // here: write-through stores of the stem / layer1 outputs measured slower (6.28-6.31 vs 6.38-6.40 ms per step,
+    // profiles/r4_s19)
 #pragma unroll
     for (int i = 0; i + 1 < WS_MB; i += 2) {
       unsigned offA, offB;
       const w_u32x2 oa = out_at(i, offA), ob2 = out_at(i + 1, offB);
-      sat_st_pair16(rY, offA, offB, oa, ob2, true, true);
+      sat_st_pair16<0>(rY, offA, offB, oa, ob2, true, true);
     }
     if constexpr (WS_MB % 2) {
       unsigned off;
       const w_u32x2 o = out_at(WS_MB - 1, off);
-      __builtin_amdgcn_raw_buffer_store_b64(o, rY, (int)off, 0, SAT_OUT8_CPOL);
+      __builtin_amdgcn_raw_buffer_store_b64(o, rY, (int)off, 0, 0);
     }
     it += step;
     if (it >= a.items) break;

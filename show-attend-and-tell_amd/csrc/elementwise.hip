@@ -88,9 +88,9 @@ __global__ __launch_bounds__(256) void nchw3_to_s2d16_bf16_kernel(const float* _
       o[(sy * 2 + 0) * 3 + c] = (bf16)v[sy][c].x;
       o[(sy * 2 + 1) * 3 + c] = (bf16)v[sy][c].y;
     }
-  const __amdgpu_buffer_rsrc_t rY = sat_out_rsrc(y, 32L * N * H2 * W2);   // write-through (sat_common.h)
-  sat_st16(rY, (unsigned)(p * 32), u[0]);
-  sat_st16(rY, (unsigned)(p * 32 + 16), u[1]);
+  uint4* dst = (uint4*)(y + p * 16);   // plain stores: write-through measured slower for the stem (profiles/r4_s19)
+  dst[0] = u[0];
+  dst[1] = u[1];
 }
 
 // ---- max-pool NHWC (floor mode), 8 channels per thread (16-B bf16 / 2x16-B f32 accesses) ----
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) void maxpool_bf16_kernel(const bf16* __restric
   bf16* o = (bf16*)&u;
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = (bf16)m[e];
-  sat_st16(sat_out_rsrc(y, 2L * N * OH * OW * C), (unsigned)(i * 16), u);   // write-through (sat_common.h)
+  *(uint4*)(y + i * 8) = u;   // plain: write-through measured slower for the stem pool (profiles/r4_s19)
 }
 
 template <typename TI, typename TO>
@@ -556,8 +556,7 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   const bool vec = ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0) &&
                    (((uintptr_t)p_lp & 7) == 0);
   const long n4 = vec ? n >> 2 : 0;
-  // the updated state leaves through write-through stores (sat_common.h): 12 B per parameter that the encoder's
-  // kernel boundaries beside this launch would otherwise write back from the L2s
+  // plain write-back stores (write-through measured neutral here, profiles/r4_s14 / r4_s19)
   const __amdgpu_buffer_rsrc_t rp = sat_out_rsrc(p, 4 * n), rm = sat_out_rsrc(m, 4 * n), rv = sat_out_rsrc(v, 4 * n);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 pp = ((float4*)p)[i], mm = ((float4*)m)[i], vv = ((float4*)v)[i];
@@ -566,9 +565,9 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
     adam_elem(pp.y, gg.y, mm.y, vv.y, w1, b2, eps, step_size, bc2_sqrt);
     adam_elem(pp.z, gg.z, mm.z, vv.z, w1, b2, eps, step_size, bc2_sqrt);
     adam_elem(pp.w, gg.w, mm.w, vv.w, w1, b2, eps, step_size, bc2_sqrt);
-    sat_st16(rp, (unsigned)(i * 16), *(const uint4*)&pp);
-    sat_st16(rm, (unsigned)(i * 16), *(const uint4*)&mm);
-    sat_st16(rv, (unsigned)(i * 16), *(const uint4*)&vv);
+    sat_st16<0>(rp, (unsigned)(i * 16), *(const uint4*)&pp);
+    sat_st16<0>(rm, (unsigned)(i * 16), *(const uint4*)&mm);
+    sat_st16<0>(rv, (unsigned)(i * 16), *(const uint4*)&vv);
     if (p_lp) {
       uint2 o;
       bf16* ob = (bf16*)&o;

@@ -116,8 +116,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t sat_out_rsrc(const void* base,
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
                                            0x00020000);
 }
+template <int CPOL = SAT_OUT_CPOL>
 __device__ __forceinline__ void sat_st16(__amdgpu_buffer_rsrc_t r, unsigned byte_off, uint4 u) {
-  __builtin_amdgcn_raw_buffer_store_b128(sat_u32x4{u.x, u.y, u.z, u.w}, r, (int)byte_off, 0, SAT_OUT_CPOL);
+  __builtin_amdgcn_raw_buffer_store_b128(sat_u32x4{u.x, u.y, u.z, u.w}, r, (int)byte_off, 0, CPOL);
 }
 __device__ __forceinline__ void sat_st8(__amdgpu_buffer_rsrc_t r, unsigned byte_off, sat_u32x2 u) {
   __builtin_amdgcn_raw_buffer_store_b64(u, r, (int)byte_off, 0, SAT_OUT8_CPOL);
@@ -127,13 +128,14 @@ __device__ __forceinline__ void sat_st8(__amdgpu_buffer_rsrc_t r, unsigned byte_
 // one pixel, or m-blocks i, i + 1 of one n-block): lanes fh and fh ^ 1 swap halves, so the even lane holds channels
 // 4 fh .. 4 fh + 7 of A (its own A at offA) and the odd one 4 (fh - 1) .. 4 fh + 3 of B (its own B at offB): whole
 // 16-B write-through stores (sat_common.h) instead of 8-B ones.  Every lane runs the exchange.
+template <int CPOL = SAT_OUT_CPOL>
 __device__ __forceinline__ void sat_st_pair16(__amdgpu_buffer_rsrc_t r, unsigned offA, unsigned offB, sat_u32x2 a, sat_u32x2 b,
                                           bool okA, bool okB) {
   const bool odd = (threadIdx.x >> 4) & 1;
   const sat_u32x2 send = odd ? a : b;
   const unsigned gx = (unsigned)__shfl_xor((int)send.x, 16, 64), gy = (unsigned)__shfl_xor((int)send.y, 16, 64);
   const uint4 u = odd ? make_uint4(gx, gy, b.x, b.y) : make_uint4(a.x, a.y, gx, gy);
-  if (odd ? okB : okA) sat_st16(r, odd ? offB - 8 : offA, u);
+  if (odd ? okB : okA) sat_st16<CPOL>(r, odd ? offB - 8 : offA, u);
 }
 
 // wave64 reductions
