@@ -31,6 +31,10 @@
 //     ds_read_b128 fragment reads (verified for every lane group).
 #include "sat_common.h"
 
+#ifndef SAT_STREAM_WT_BYTES
+#define SAT_STREAM_WT_BYTES (64L << 20)
+#endif
+
 #include "sat_internal.h"
 
 namespace {
@@ -48,6 +52,7 @@ struct SArgs {
   int H, W, Cin, stride, OH, OW;     // input geometry (1x1 conv, pad 0)
   int slices, per_slice, items;      // N / 128, workgroups per slice, M-tiles
   int xcd_group;                     // 1: slice = (b / 8) % slices (one M-tile sequence per XCD)
+  int wt;                            // write-through output stores (sat_common.h), else write-back
   unsigned a_bytes;
   SatStamps st;                      // in-kernel launch timestamps (SatPolicy::stamps)
 };
@@ -248,7 +253,8 @@ __device__ __forceinline__ void conv1x1_stream_kernel_body(const SArgs& a) {
       const int m = it * MT + r;
       const unsigned off = m < a.M ? (unsigned)(((long)m * a.N + ns + 8 * lc) * 2) : S_OOB;
       typedef unsigned __attribute__((ext_vector_type(4))) u32x4;
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rC, (int)off, 0, SAT_OUT_CPOL);   // sat_common.h: output cache policy
+      if (a.wt) __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rC, (int)off, 0, SAT_OUT_CPOL);
+      else __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rC, (int)off, 0, 0);
     }
     it += step;
     if (it >= a.items) break;
@@ -331,6 +337,9 @@ int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err) {
   SArgs a{};
   a.M = g.M; a.N = g.N; a.K = K;
   a.A = (const bf16*)g.A; a.B = (const bf16*)g.B; a.C = (bf16*)g.C;
+  // write-through only for outputs up to SAT_STREAM_WT_BYTES (layer3 / layer4 sizes); the layer1 / layer2 outputs
+  // (100-200 MB, HBM-bound kernels) keep write-back stores
+  a.wt = 2L * g.M * g.N <= (long)SAT_STREAM_WT_BYTES;
   a.bias = g.bias; a.res = (const bf16*)g.add1;
   a.H = cv.H; a.W = cv.W; a.Cin = cv.C; a.stride = cv.stride; a.OH = cv.OH; a.OW = cv.OW;
   a.slices = slices; a.per_slice = per_slice; a.items = items;
