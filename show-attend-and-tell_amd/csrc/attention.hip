@@ -142,14 +142,12 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
 #pragma unroll
     for (int v = 0; v < FDV; ++v)
       xa[u][v] = ld16(ab + (long)(w + NW * u) * D + v * 64 * VN, w + NW * u < L && c0 + v * 64 * VN + lane * VN < D);
-  float gpre[CPT];
-#pragma unroll
-  for (int k = 0; k < CPT; ++k) {
-    const int col = k * NT + tid, dout = c0 + col;
-    gpre[k] = 0.f;
-    if (a.gate_pre && col < COLS && dout < D)
-      gpre[k] = sum_parts(a.gate_pre, (long)b * a.gate_ld + dout, a.hg_splits, a.hg_split_stride);
-  }
+  // the epilogue's threads own 4 consecutive columns each (col4 = 4 tid: 16-B write-through stores)
+  static_assert(COLS <= 4 * NT && COLS % 4 == 0, "four columns per epilogue thread");
+  const int col4 = 4 * tid;
+  const bool ep = col4 < COLS && c0 + col4 < D;   // D % 4 == 0 (host-checked): a quad is all in or all out
+  float4 gpre4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.gate_pre && ep) gpre4 = sum_parts4(a.gate_pre + (long)b * a.gate_ld, c0 + col4, a.hg_splits, a.hg_split_stride);
 
   const float bv = a.v_b[0];
   for (int l0 = w; l0 < L; l0 += NW * FU) {
@@ -239,9 +237,7 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   }
   // fixed summation order over the wave partials: c = sum over q = 0, 2, .., 6 of (p_q + p_(q+1)) per round of
   // 8 waves, waves 0-7 first, then waves 8-15 through the same 8 rows
-  float cacc[CPT];
-#pragma unroll
-  for (int k = 0; k < CPT; ++k) cacc[k] = 0.f;
+  float4 cacc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int half = 0; half < NW / 8; ++half) {
     if ((w >> 3) == half) {
@@ -251,27 +247,38 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
         for (int j = 0; j < VN; ++j) s_red[w & 7][v * 64 * VN + lane * VN + j] = part[v][j];
     }
     __syncthreads();
+    if (ep) {
 #pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const int col = k * NT + tid;
-      if (col < COLS && c0 + col < D) {
-#pragma unroll
-        for (int q = 0; q < 8; q += 2) cacc[k] += s_red[q][col] + s_red[q + 1][col];
+      for (int q = 0; q < 8; q += 2) {
+        const float4 x = *(const float4*)&s_red[q][col4], y = *(const float4*)&s_red[q + 1][col4];
+        cacc.x += x.x + y.x; cacc.y += x.y + y.y; cacc.z += x.z + y.z; cacc.w += x.w + y.w;
       }
     }
     if (half + 1 < NW / 8) __syncthreads();
   }
+  if (ep) {
+    const int dout = c0 + col4;
+    // fp32 outputs through 16-B write-through stores (sat_common.h): this step's end-of-kernel L2 writeback, on the
+    // per-step critical path, has less to flush; the bf16 copies (8 B per thread) stay write-back
+    sat_st16(sat_out_rsrc(a.ctx, 0x7fffffffL), (unsigned)(((long)b * a.ctx_ld + dout) * 4), *(const uint4*)&cacc);
+    const float c[4] = {cacc.x, cacc.y, cacc.z, cacc.w};
+    if (a.ctx_t) {
+      T* ct = (T*)a.ctx_t + (long)b * a.ctx_t_ld + dout;
 #pragma unroll
-  for (int k = 0; k < CPT; ++k) {
-    const int col = k * NT + tid, dout = c0 + col;
-    if (col < COLS && dout < D) {
-      const float c = cacc[k];
-      a.ctx[(long)b * a.ctx_ld + dout] = c;
-      if (a.ctx_t) ((T*)a.ctx_t)[(long)b * a.ctx_t_ld + dout] = (T)c;
-      if (a.gate_pre) {
-        const float g = 1.0f / (1.0f + expf(-gpre[k]));
-        if (a.gate) a.gate[(long)b * a.gate_out_ld + dout] = g;
-        if (a.gated) ((T*)a.gated)[(long)b * a.gated_ld + dout] = (T)(g * c);
+      for (int k = 0; k < 4; ++k) ct[k] = (T)c[k];
+    }
+    if (a.gate_pre) {
+      const float gp[4] = {gpre4.x, gpre4.y, gpre4.z, gpre4.w};
+      float g[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g[k] = 1.0f / (1.0f + expf(-gp[k]));
+      if (a.gate)
+        sat_st16(sat_out_rsrc(a.gate, 0x7fffffffL), (unsigned)(((long)b * a.gate_out_ld + dout) * 4),
+                 make_uint4(__float_as_uint(g[0]), __float_as_uint(g[1]), __float_as_uint(g[2]), __float_as_uint(g[3])));
+      if (a.gated) {
+        T* gd = (T*)a.gated + (long)b * a.gated_ld + dout;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gd[k] = (T)(g[k] * c[k]);
       }
     }
   }
