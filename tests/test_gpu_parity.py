@@ -591,7 +591,10 @@ def test_fast_conv_path(sat, N, C, H, Cout, k, stride, pad):
     (3, 64, 9, 64, 3, 1, 1, False, False),       # N = 64: half-empty column tile, no activation
     (2, 512, 7, 2048, 1, 1, 0, True, True),      # L4 c3 + residual
     (2, 64, 8, 200, 1, 1, 0, True, True),        # N tail (200 % 128), residual, single k-tile
-    (2, 128, 10, 128, 1, 1, 0, False, True)])    # two k-tiles (no steady-state iteration)
+    (2, 128, 10, 128, 1, 1, 0, False, True),     # two k-tiles (no steady-state iteration)
+    (2, 256, 28, 256, 3, 1, 1, True, False),     # VGG19 conv3 class on the 256 x 256 form, M tail (1568 rows)
+    (1, 512, 14, 512, 3, 1, 1, True, True),      # VGG19 conv5 class, two column tiles, residual
+    (1, 64, 9, 256, 1, 1, 0, False, True)])      # one k-tile, M = 81 (one partial row tile)
 def test_conv_pipe_kernel(sat, N, C, H, Cout, k, stride, pad, relu, resid):
     """convpipe.hip (256x128 tiles, 3-stage LDS-DMA ring, counted vmcnt) forced on every eligible
     shape: bit-identical to the 128-row kernel (same fp32 MFMA sums, same single rounding) and
@@ -610,12 +613,15 @@ def test_conv_pipe_kernel(sat, N, C, H, Cout, k, stride, pad, relu, resid):
     wd = w.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV)
     rd = res.permute(0, 2, 3, 1).contiguous().bfloat16().to(DEV) if resid else None
     outs = []
-    for mode in (2, 1):   # every eligible problem on the pipelined kernel, then never
+    # every eligible problem on the pipelined kernel, then never, then (Cout % 256 == 0) on the 256 x 256 form
+    modes = (2, 1, 3) if Cout % 256 == 0 else (2, 1)
+    for mode in modes:
         y = ops.conv2d_nhwc(xd, wd, b.to(DEV), stride, pad, relu, residual=rd, policy=sat.Policy(conv_pipe=mode))
         outs.append(y.float().permute(0, 3, 1, 2).cpu())
     assert rel(outs[0], ref) < 1e-2
     assert ((outs[0] - ref).abs() <= 1e-2 * ref.abs() + 2e-2).all()
-    assert torch.equal(outs[0], outs[1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
 
 
 @pytest.mark.parametrize("N,C,H,Cout,stride,relu,resid", [
@@ -651,7 +657,7 @@ def test_conv_stream_kernel(sat, N, C, H, Cout, stride, relu, resid):
     assert torch.equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("M,N,K", [(3328, 10000, 512), (6272, 512, 2048), (300, 136, 192)])
+@pytest.mark.parametrize("M,N,K", [(3328, 10000, 512), (6272, 512, 2048), (300, 136, 192), (300, 768, 320)])
 def test_conv_pipe_gemm(sat, M, N, K):
     """Plain NT GEMM through the pipelined kernel (bf16 out, bias, bf16 residual, ReLU) vs the
     128-row kernel (bit-identical) and torch fp32."""
@@ -664,13 +670,14 @@ def test_conv_pipe_gemm(sat, M, N, K):
     add1 = torch.randn(M, N, generator=g).bfloat16()
     ref = torch.relu(A.float() @ Bm.float().T + bias + add1.float())
     outs = []
-    for mode in (2, 1):
+    for mode in ((2, 1, 3) if N % 256 == 0 else (2, 1)):
         C = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
         ops.gemm(A.to(DEV), Bm.to(DEV), C, bias=bias.to(DEV), add1=add1.to(DEV), act=sat._lib.ACT_RELU,
                  policy=sat.Policy(conv_pipe=mode))
         outs.append(C.float().cpu())
     assert rel(outs[0], ref) < 8e-3
-    assert torch.equal(outs[0], outs[1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
 
 
 @pytest.mark.parametrize("M,N,K,out", [(3000, 1000, 520, torch.float32), (4096, 64, 512, torch.bfloat16),
