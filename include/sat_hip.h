@@ -50,9 +50,9 @@ typedef struct {
  * that dispatches among kernels: SatGemmArgs.policy, sat_conv2d_nhwc, SatDecoderDims.policy.  There
  * is no process-global tuning state: two callers in one process never see each other's policy. */
 typedef struct {
-  int conv_pipe;        /* pipelined conv / GEMM kernel: 0 auto (long-K, chip-filling; the 256x256 form when N % 256 == 0
-                         * and it fills a round of 256 tiles), 1 off, 2 every eligible on the 256x128 form, 3 every
-                         * eligible with N % 256 == 0 on the 256x256 form, 4 auto without the 256x256 form */
+  int conv_pipe;        /* pipelined conv / GEMM kernel: 0 auto (long-K, chip-filling, 256x128 tiles), 1 off, 2 every
+                         * eligible problem, 3 every eligible problem with N % 256 == 0 on the 256x256 form (opt-in:
+                         * measured slower), 4 = 0 */
   int conv_stream;      /* weight-stationary 1x1 kernel (K <= 512): 0 auto, 1 off, 2 every eligible */
   int conv3x3_ws;       /* 64 -> 64 3x3 weight-stationary halo kernel: 0 on, 1 off */
   int skinny;           /* register-direct skinny GEMM (M <= 128): 0 the decoder's K/256-split products, 1 off,

@@ -619,9 +619,11 @@ int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err) {
     a.a_bytes = (unsigned)a_bytes;
     a.b_bytes = (unsigned)b_bytes;
   }
-  // the 256 x 256 form: N a multiple of 256 and at least one round of 256 tiles (auto)
+  // the 256 x 256 form, opt-in (mode 3): measured slower than the 256 x 128 form on the VGG19 convs (0.31-0.34 vs
+  // 0.33-0.38 of peak, cfg5 11.77 vs 10.87 ms per step, profiles/r4_s24): one wave per SIMD leaves the fragment
+  // reads and the per-k-tile barrier exposed, and its 128 KiB of LDS keeps the decoder's kernels off the CU
   const long tiles_w = (long)sat_cdiv(g.M, WBM) * (g.N / WBN);
-  if (g.N % WBN == 0 && (mode == 3 || (mode == 0 && tiles_w >= 256))) {
+  if (g.N % WBN == 0 && mode == 3) {
     a.tiles_n = g.N / WBN;
     launch_wide(conv, g.add1 != nullptr, g.act, dim3((unsigned)tiles_w), s, a);
     *err = (int)hipGetLastError();
