@@ -452,9 +452,9 @@ __device__ __forceinline__ void fast_gemm_kernel_body(const FArgs& a) {
         for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
         sat_st16(rCb, (unsigned)(((long)row * a.ldc + col) * 2), u);
       } else {
-        float* p = (float*)Cb + (long)row * a.ldc + col;
-        *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
-        *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        const unsigned off = (unsigned)(((long)row * a.ldc + col) * 4);
+        sat_st16(rCb, off, make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])));
+        sat_st16(rCb, off + 16, make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])));
       }
     }
   } else if (col < N) {

@@ -395,9 +395,12 @@ __global__ void zero_multi_kernel(ZeroMultiArgs a) {
     const long R = a.rows[k], C = a.cols[k], ld = a.ld[k];
     if (((uintptr_t)p & 15) == 0 && C % 4 == 0 && ld % 4 == 0) {
       const long c4 = C >> 2, n4 = R * c4;
+      // write-through zeros (sat_common.h): megabytes of gradient accumulators that would otherwise sit dirty in
+      // the L2s while the encoder's kernel boundaries run beside this graph
+      const __amdgpu_buffer_rsrc_t rp = sat_out_rsrc(p, 4 * ((R - 1) * ld + C));
       for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
         const long r = i / c4;
-        *(float4*)(p + r * ld + 4 * (i - r * c4)) = make_float4(0.f, 0.f, 0.f, 0.f);
+        sat_st16(rp, (unsigned)((r * ld + 4 * (i - r * c4)) * 4), make_uint4(0u, 0u, 0u, 0u));
       }
     } else {
       for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < R * C; i += stride) {
