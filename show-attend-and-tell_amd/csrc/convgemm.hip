@@ -452,9 +452,11 @@ __device__ __forceinline__ void fast_gemm_kernel_body(const FArgs& a) {
         for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
         sat_st16(rCb, (unsigned)(((long)row * a.ldc + col) * 2), u);
       } else {
+        // write-back: fp32 outputs here (x gates, f_h / f_z) are re-read by the next kernels, and write-through
+        // measured slower (6.45 vs 6.40 ms per step, profiles/r4_s25)
         const unsigned off = (unsigned)(((long)row * a.ldc + col) * 4);
-        sat_st16(rCb, off, make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])));
-        sat_st16(rCb, off + 16, make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])));
+        sat_st16<0>(rCb, off, make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])));
+        sat_st16<0>(rCb, off + 16, make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])));
       }
     }
   } else if (col < N) {

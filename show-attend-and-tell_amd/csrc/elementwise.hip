@@ -388,6 +388,9 @@ struct ZeroMultiArgs {
   float* p[kZeroMaxSegs];
   long rows[kZeroMaxSegs], cols[kZeroMaxSegs], ld[kZeroMaxSegs];
 };
+#ifndef SAT_ZERO_CPOL   // diagnostics builds: the accumulator zeroing's store policy (sat_common.h)
+#define SAT_ZERO_CPOL SAT_OUT_CPOL
+#endif
 __global__ void zero_multi_kernel(ZeroMultiArgs a) {
   const long stride = (long)gridDim.x * blockDim.x;
   for (int k = 0; k < a.n; ++k) {
@@ -400,7 +403,7 @@ __global__ void zero_multi_kernel(ZeroMultiArgs a) {
       const __amdgpu_buffer_rsrc_t rp = sat_out_rsrc(p, 4 * ((R - 1) * ld + C));
       for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
         const long r = i / c4;
-        sat_st16(rp, (unsigned)((r * ld + 4 * (i - r * c4)) * 4), make_uint4(0u, 0u, 0u, 0u));
+        sat_st16<SAT_ZERO_CPOL>(rp, (unsigned)((r * ld + 4 * (i - r * c4)) * 4), make_uint4(0u, 0u, 0u, 0u));
       }
     } else {
       for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < R * C; i += stride) {
