@@ -32,6 +32,10 @@
 // (2 x CUs workgroups, last-arriver fixups from sc1-published fp32 partials: 30 -> 46 us and
 // 53 -> 68 us on the 392-tile L3 shapes).
 #include "sat_common.h"
+
+#ifndef SAT_SLAB_WT   // diagnostics builds: 0 = the per-step partial slabs with write-back stores
+#define SAT_SLAB_WT 1
+#endif
 #include "sat_internal.h"
 
 namespace {
@@ -452,11 +456,19 @@ __device__ __forceinline__ void fast_gemm_kernel_body(const FArgs& a) {
         for (int e = 0; e < 8; ++e) h[e] = (bf16)v[e];
         sat_st16(rCb, (unsigned)(((long)row * a.ldc + col) * 2), u);
       } else {
-        // write-back: fp32 outputs here (x gates, f_h / f_z) are re-read by the next kernels, and write-through
-        // measured slower (6.45 vs 6.40 ms per step, profiles/r4_s25)
+        // fp32 outputs: the per-step partial slabs (read once by the next launch, on the per-step chain) write
+        // through; the batched outputs (x gates, f_h / f_z: re-read by later kernels) stay write-back --
+        // write-through for those measured slower (6.45 vs 6.40 ms per step, profiles/r4_s25)
         const unsigned off = (unsigned)(((long)row * a.ldc + col) * 4);
-        sat_st16<0>(rCb, off, make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])));
-        sat_st16<0>(rCb, off + 16, make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])));
+        const uint4 u0 = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
+        const uint4 u1 = make_uint4(__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7]));
+        if (a.partial && SAT_SLAB_WT) {
+          sat_st16(rCb, off, u0);
+          sat_st16(rCb, off + 16, u1);
+        } else {
+          sat_st16<0>(rCb, off, u0);
+          sat_st16<0>(rCb, off + 16, u1);
+        }
       }
     }
   } else if (col < N) {
