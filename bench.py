@@ -925,6 +925,10 @@ def main():
             "unit": "images/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1000 * elapsed / args.steps, 3),
+            "timing": ("host wall clock (perf_counter) around exactly `steps` pipelined train steps, bracketed by a "
+                       "barrier + device synchronize on both sides, max over ranks; a step's encoder runs beside "
+                       "the previous batch's decoder, so per-step device times are not separable -- the mean over "
+                       "the window, not a per-step event median"),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             # this line measures one point of the curve: per-GPU work is fixed (weak scaling), and the 1 -> 8 curve
             # exists only where the driver's SCALE runs (N = 1, 2, 4, 8 on one node) measured it
