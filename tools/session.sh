@@ -15,6 +15,7 @@
 #   prof:LABEL:ARGS    the same over a quick bench line with extra flags (A/B of per-kernel times)
 #   pmcdec             two PMC passes (FETCH_SIZE, WRITE_SIZE) over the decoder's per-step kernels
 #                      (tools/decoder_pmc.py; summary -> gpurun_out/TAG/pmc_decoder.json)
+#   pmctrunk           FETCH_SIZE / WRITE_SIZE passes over an eager bench: per conv class HBM bytes (pmc_traffic.py)
 #   pmcdec2            SQ / TCC counter groups over the same decoder run (per-kernel means -> pmc2_*.json)
 #   ab:LABEL:ARGS      one A/B bench line (ARGS comma-separated bench.py flags, e.g. ab:st80:--split-target,80);
 #                      prints value and ms/step
@@ -76,6 +77,13 @@ for s in "$@"; do
             python tools/decoder_pmc.py || exit $?
       done
       python tools/decoder_pmc.py --analyze "$OUT/pmc_FETCH_SIZE" "$OUT/pmc_WRITE_SIZE" "$OUT/pmc_decoder.json" ;;
+    pmctrunk)   # the encoder conv classes' HBM traffic (tools/pmc_traffic.py): eager bench, two passes
+      for c in FETCH_SIZE WRITE_SIZE; do
+        run pmct_$c 400 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmct_$c" -o run --output-format csv -- \
+            python bench.py --no-graph --steps 3 --warmup 1 $QUIET --no-diagnostics || exit $?
+      done
+      python tools/pmc_traffic.py "$OUT/pmct_FETCH_SIZE" "$OUT/pmct_WRITE_SIZE" resnet152 128 \
+          "$OUT/pmc_traffic_resnet152.json" | tail -30 ;;
     pmcdec2)   # SQ and TCC counter groups over the same decoder run (one rocprofv3 pass per group)
       i=0
       for G in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_INSTS_VALU" \
