@@ -6,10 +6,6 @@
 #include "sat_common.h"
 #include "sat_internal.h"
 
-#ifndef SAT_LSTM_VEC_STORES   // diagnostics builds: 0 = one 4-B write-back store per thread
-#define SAT_LSTM_VEC_STORES 1
-#endif
-
 namespace {
 
 inline int grid_for(long n) {
@@ -22,16 +18,10 @@ inline int grid_for(long n) {
 // step at B=128, E=512, 4 + 8 slabs), the cell update reads the four gates back from LDS.
 template <typename T>
 __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
-  __shared__ float sg[4][64], sch[2][64];
+  __shared__ float sg[4][64];
   const int E = a.E;
   const int q = threadIdx.x >> 6, u = threadIdx.x & 63;
   const long units = (long)a.B * E;
-  // a.vec (launcher-checked: E % 64 == 0, 16-B aligned rows): the fp32 outputs leave as 16-B write-through stores
-  // (sat_common.h) from LDS -- thread t < 64 stores gate t >> 4, units 4 (t & 15) .. +3 -- so this launch's
-  // end-of-kernel L2 writeback on the per-step chain has little to flush; else one 4-B store per thread
-  const __amdgpu_buffer_rsrc_t rg = sat_out_rsrc(a.gates, 0x7fffffffL), rc = sat_out_rsrc(a.c_out, 0x7fffffffL),
-                               rn = sat_out_rsrc(a.c_next_in ? a.c_next_in : a.c_out, 0x7fffffffL),
-                               rh = sat_out_rsrc(a.h_out, 0x7fffffffL);
   for (long base = (long)blockIdx.x * 64; base < units; base += (long)gridDim.x * 64) {
     const long i = base + u;
     const bool ok = i < units;
@@ -41,38 +31,17 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
                 sum_parts(a.hpart, (long)b * a.hpart_ld + q * E + j, a.h_splits, a.h_split_stride);
       if (a.cpart) v += sum_parts(a.cpart, (long)b * a.cpart_ld + q * E + j, a.c_splits, a.c_split_stride);
       sg[q][u] = v;
-      if (!a.vec) a.gates[(long)b * a.gates_ld + q * E + j] = v;
+      a.gates[(long)b * a.gates_ld + q * E + j] = v;
     }
     __syncthreads();
     if (q == 0 && ok) {
       float c, h;
       lstm_cell_fwd(sg[0][u], sg[1][u], sg[2][u], sg[3][u], a.c_prev[(long)b * a.c_prev_ld + j], c, h);
-      if (a.vec) {
-        sch[0][u] = c;
-        sch[1][u] = h;
-      } else {
-        a.c_out[(long)b * a.c_out_ld + j] = c;
-        if (a.c_next_in) a.c_next_in[(long)b * a.c_next_in_ld + j] = c;
-        a.h_out[(long)b * a.h_out_ld + j] = h;
-      }
+      a.c_out[(long)b * a.c_out_ld + j] = c;
+      if (a.c_next_in) a.c_next_in[(long)b * a.c_next_in_ld + j] = c;
+      a.h_out[(long)b * a.h_out_ld + j] = h;
       if (a.h_out_t) ((T*)a.h_out_t)[(long)b * a.h_out_t_ld + j] = (T)h;
       if (a.h_next_in_t) ((T*)a.h_next_in_t)[(long)b * a.h_next_in_t_ld + j] = (T)h;
-    }
-    if (a.vec) {   // whole 64-unit blocks inside one row (E % 64 == 0)
-      __syncthreads();
-      const int t = threadIdx.x, b0 = (int)(base / E), j0 = (int)(base - (long)b0 * E);
-      if (base < units) {
-        if (t < 64) {
-          const int g = t >> 4, sg4 = 4 * (t & 15);
-          sat_st16(rg, (unsigned)(((long)b0 * a.gates_ld + g * E + j0 + sg4) * 4), *(const uint4*)&sg[g][sg4]);
-        } else if (t < 128) {
-          const int k = (t - 64) >> 4, s4 = 4 * (t & 15);   // k: 0 c_out, 1 c_next_in, 2 h_out, 3 unused
-          const uint4 v = *(const uint4*)&sch[k == 2 ? 1 : 0][s4];
-          if (k == 0) sat_st16(rc, (unsigned)(((long)b0 * a.c_out_ld + j0 + s4) * 4), v);
-          else if (k == 1 && a.c_next_in) sat_st16(rn, (unsigned)(((long)b0 * a.c_next_in_ld + j0 + s4) * 4), v);
-          else if (k == 2) sat_st16(rh, (unsigned)(((long)b0 * a.h_out_ld + j0 + s4) * 4), v);
-        }
-      }
     }
     __syncthreads();
   }
@@ -89,12 +58,10 @@ __global__ __launch_bounds__(256) void lstm_fwd_gp_kernel(LstmFwdArgs a) {
 // slabs s = q, q+4, ... of the recurrent dh; the four partial sums meet in LDS in a fixed order.
 template <typename T>
 __device__ __forceinline__ void lstm_bwd_gp_kernel_body(LstmBwdArgs a) {
-  __shared__ float sg[4][64], sdh[4][64], sdq[4][64], sdc[64];
+  __shared__ float sg[4][64], sdh[4][64];
   const int E = a.E;
   const int q = threadIdx.x >> 6, u = threadIdx.x & 63;
   const long units = (long)a.B * E;
-  // a.vec: the fp32 d gates and dc leave as 16-B write-through stores from LDS (lstm_fwd_gp_kernel_body)
-  const __amdgpu_buffer_rsrc_t rd = sat_out_rsrc(a.d_gates, 0x7fffffffL), rdc = sat_out_rsrc(a.dc, 0x7fffffffL);
   for (long base = (long)blockIdx.x * 64; base < units; base += (long)gridDim.x * 64) {
     const long i = base + u;
     const bool ok = i < units;
@@ -120,27 +87,9 @@ __device__ __forceinline__ void lstm_bwd_gp_kernel_body(LstmBwdArgs a) {
       float d4[4], dco;
       lstm_cell_bwd(sg[0][u], sg[1][u], sg[2][u], sg[3][u], cp, cn, dcin, dh, d4, dco);
       const float dq = d4[q];
-      if (a.vec) {
-        sdq[q][u] = dq;
-        if (q == 0) sdc[u] = dco;
-      } else {
-        a.d_gates[(long)b * a.d_gates_ld + q * E + j] = dq;
-        if (q == 0) a.dc[i] = dco;
-      }
+      a.d_gates[(long)b * a.d_gates_ld + q * E + j] = dq;
       if (a.d_gates_t) ((T*)a.d_gates_t)[(long)b * a.d_gates_t_ld + q * E + j] = (T)dq;
-    }
-    if (a.vec) {   // whole 64-unit blocks inside one row (E % 64 == 0)
-      __syncthreads();
-      const int t = threadIdx.x, b0 = (int)(base / E), j0 = (int)(base - (long)b0 * E);
-      if (base < units) {
-        if (t < 64) {
-          const int g = t >> 4, s4 = 4 * (t & 15);
-          sat_st16(rd, (unsigned)(((long)b0 * a.d_gates_ld + g * E + j0 + s4) * 4), *(const uint4*)&sdq[g][s4]);
-        } else if (t < 80) {
-          const int s4 = 4 * (t - 64);
-          sat_st16(rdc, (unsigned)((base + s4) * 4), *(const uint4*)&sdc[s4]);
-        }
-      }
+      if (q == 0) a.dc[i] = dco;
     }
     __syncthreads();
   }
@@ -318,14 +267,9 @@ inline long lstm_blocks(int B, int E) {
   const int cap = sat_policy().lstm_blocks > 0 ? sat_policy().lstm_blocks : 4096;
   return blocks > cap ? cap : blocks;
 }
-inline bool a16(const void* p) { return ((uintptr_t)p & 15) == 0; }
-
 int sat_lstm_fwd_launch(const LstmFwdArgs& args, hipStream_t s) {
   LstmFwdArgs a = args;
   a.st = sat_launch_stamps();
-  a.vec = SAT_LSTM_VEC_STORES && a.E % 64 == 0 && a.gates_ld % 4 == 0 && a.c_out_ld % 4 == 0 && a.h_out_ld % 4 == 0 &&
-          (!a.c_next_in || a.c_next_in_ld % 4 == 0) && a16(a.gates) && a16(a.c_out) && a16(a.h_out) &&
-          (!a.c_next_in || a16(a.c_next_in));
   const long blocks = lstm_blocks(a.B, a.E);
   DISPATCH_T(a.dtype, lstm_fwd_gp_kernel, dim3((int)blocks), a);
   return (int)hipGetLastError();
@@ -333,7 +277,6 @@ int sat_lstm_fwd_launch(const LstmFwdArgs& args, hipStream_t s) {
 int sat_lstm_bwd_launch(const LstmBwdArgs& args, hipStream_t s) {
   LstmBwdArgs a = args;
   a.st = sat_launch_stamps();
-  a.vec = SAT_LSTM_VEC_STORES && a.E % 64 == 0 && a.d_gates_ld % 4 == 0 && a16(a.d_gates) && a16(a.dc);
   const long blocks = lstm_blocks(a.B, a.E);
   DISPATCH_T(a.dtype, lstm_bwd_gp_kernel, dim3((int)blocks), a);
   return (int)hipGetLastError();

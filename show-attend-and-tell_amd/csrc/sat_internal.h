@@ -98,7 +98,6 @@ struct LstmFwdArgs {
   int h_splits; long h_split_stride;    // hpart = sum of h_splits slabs
   int c_splits; long c_split_stride;    // cpart = sum of c_splits slabs
   SatStamps st;                         // in-kernel launch timestamps (set by the launcher)
-  int vec;                              // set by the launcher: 16-B write-through output stores (lstm.hip)
 };
 int sat_lstm_fwd_launch(const LstmFwdArgs& a, hipStream_t s);
 
@@ -116,7 +115,6 @@ struct LstmBwdArgs {
   void* d_gates_t; long d_gates_t_ld;   // out dtype copy (nullable)
   int dh_splits; long dh_split_stride;  // dh_rec = sum of dh_splits slabs
   SatStamps st;                         // in-kernel launch timestamps (set by the launcher)
-  int vec;                              // set by the launcher: 16-B write-through output stores (lstm.hip)
 };
 int sat_lstm_bwd_launch(const LstmBwdArgs& a, hipStream_t s);
 
