@@ -86,8 +86,9 @@ typedef struct {
   int fused_lstm;       /* bf16 decoder, LSTM cell per time step: 0 auto = 1; 1 the split-K context / dh products + separate
                          * lstm_fwd / lstm_bwd launches (4 per time step each way); 2 the cell forward in the epilogue of
                          * the context GEMM and the backward in the dh GEMM's, full-K row-block GEMMs (3 launches per
-                         * time step; lstmgemm.hip), eight waves per workgroup; 3 the same on four waves.  The fused
-                         * forms are faster alone and slower beside the encoder */
+                         * time step; lstmgemm.hip), eight waves per workgroup; 3 the same on four waves; 4 / 5 the
+                         * eight-wave form for the backward / forward only.  The fused forms are faster alone and
+                         * slower beside the encoder */
   int gemm_pipe;        /* 256x128 pipelined GEMM with fp32 output and k-major operands (the decoder's weight / input
                          * gradients; gemmpipe.hip): 0 auto = off (measured slower than the tile kernel and hipBLASLt
                          * on those shapes), 1 off, 2 every eligible */

@@ -235,10 +235,12 @@ inline bool bwd_ks_ok(int K) {
 }  // namespace
 
 int sat_lstm_gemm_fwd_ok(int B, int E, int K) {
-  return sat_policy().fused_lstm >= 2 && B >= 1 && B <= 1024 && E % 8 == 0 && fwd_ks_ok(K);
+  const int f = sat_policy().fused_lstm;   // 2, 3: both directions; 4: backward only; 5: forward only
+  return (f == 2 || f == 3 || f == 5) && B >= 1 && B <= 1024 && E % 8 == 0 && fwd_ks_ok(K);
 }
 int sat_lstm_gemm_bwd_ok(int B, int E, int K) {
-  return sat_policy().fused_lstm >= 2 && B >= 1 && B <= 1024 && E % 16 == 0 && bwd_ks_ok(K);
+  const int f = sat_policy().fused_lstm;
+  return (f == 2 || f == 3 || f == 4) && B >= 1 && B <= 1024 && E % 16 == 0 && bwd_ks_ok(K);
 }
 
 int sat_lstm_gemm_fwd_try(const void* A, long lda, const void* W, long ldw, int K, const LstmFwdArgs& l, hipStream_t s,
