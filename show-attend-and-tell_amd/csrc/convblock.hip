@@ -1248,9 +1248,12 @@ __global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restric
 // Layer3 c1 / c2 launch form for a batch of N images: 1 = one workgroup per half image (2N workgroups), 2 = two
 // 128-channel slices per half image (4N).  SatPolicy::conv_slices forces
 // one; automatic: slices when the half images fill at most half the chip's 256 CUs (B <= 64 per GPU).
-int sat_frag_slices(int N) {
+// c2: the 3x3 (slices also at B = 128 with conv_slices = 3: two workgroups per CU, one's staging under the
+// other's MFMAs)
+int sat_frag_slices(int N, bool c2 = false) {
   const int f = sat_policy().conv_slices;
   if (f == 1 || f == 2) return f;
+  if (f == 3 && c2) return 2;
   return 2 * N <= 128 ? 2 : 1;
 }
 
@@ -1333,7 +1336,7 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   }
   // layer3 c2: half images (two workgroups per image), or two channel slices per half image when the half
   // images alone would leave CUs idle (SatPolicy::conv_slices)
-  const int mode = sat_frag_slices(N);
+  const int mode = sat_frag_slices(N, true);
   const int groups = sat_cdiv(2 * N, 8) * 8 * 2;   // whole groups of 8 half images x 2 slices
   if (mode == 1)
     hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp, st);
