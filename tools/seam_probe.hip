@@ -23,20 +23,25 @@
     }                                                                       \
   } while (0)
 
-constexpr int NWG = 256, NT = 256, WORDS = 16384 / 16;   // 16 KB per workgroup per round
+constexpr int NWG = 256, NT = 256, MAXW = 16384 / 16;   // up to 16 KB per workgroup per round
 
-__device__ __forceinline__ void round_work(const uint4* in, uint4* out, int r) {
-  for (int i = threadIdx.x; i < WORDS; i += NT) {
-    uint4 v = in[(long)blockIdx.x * WORDS + i];
+// `words` 16-B words read and written per workgroup; wt: the stores write through (sc1 buffer stores)
+__device__ __forceinline__ void round_work(const uint4* in, uint4* out, int r, int words, int wt) {
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)out, (short)0, 0x7fffffff, 0x00020000);
+  typedef unsigned __attribute__((ext_vector_type(4))) u4;
+  for (int i = threadIdx.x; i < words; i += NT) {
+    uint4 v = in[(long)blockIdx.x * MAXW + i];
     v.x += r;
-    out[(long)blockIdx.x * WORDS + i] = v;
+    const int off = (int)(((long)blockIdx.x * MAXW + i) * 16);
+    if (wt) __builtin_amdgcn_raw_buffer_store_b128(u4{v.x, v.y, v.z, v.w}, ro, off, 0, 16);
+    else __builtin_amdgcn_raw_buffer_store_b128(u4{v.x, v.y, v.z, v.w}, ro, off, 0, 0);
   }
 }
 
 __global__ __launch_bounds__(NT) void persistent_kernel(const uint4* in, uint4* out, unsigned* counter, int rounds,
-                                                        unsigned* err) {
+                                                        unsigned* err, int words, int wt) {
   for (int r = 0; r < rounds; ++r) {
-    round_work(in, out, r);
+    round_work(in, out, r, words, wt);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -57,7 +62,9 @@ __global__ __launch_bounds__(NT) void persistent_kernel(const uint4* in, uint4* 
   }
 }
 
-__global__ __launch_bounds__(NT) void round_kernel(const uint4* in, uint4* out, int r) { round_work(in, out, r); }
+__global__ __launch_bounds__(NT) void round_kernel(const uint4* in, uint4* out, int r, int words, int wt) {
+  round_work(in, out, r, words, wt);
+}
 
 int main() {
   const int R = 200;
@@ -76,36 +83,43 @@ int main() {
   CHECK(hipEventCreate(&e1));
   float ms = 0.f;
 
-  // persistent: one launch of R rounds (plus a 1-round launch to subtract the launch itself)
-  for (int rep = 0; rep < 3; ++rep) {
-    for (int rounds : {1, R}) {
-      CHECK(hipMemsetAsync(counter, 0, sizeof(unsigned), s));
-      CHECK(hipEventRecord(e0, s));
-      hipLaunchKernelGGL(persistent_kernel, dim3(NWG), dim3(NT), 0, s, in, out, counter, rounds, err);
-      CHECK(hipEventRecord(e1, s));
-      CHECK(hipEventSynchronize(e1));
-      CHECK(hipEventElapsedTime(&ms, e0, e1));
-      if (rep == 2) printf("persistent %3d rounds: %8.2f us  (%.2f us per round)\n", rounds, ms * 1e3, ms * 1e3 / rounds);
+  unsigned herr = 0;
+  for (int words : {0, 256, MAXW}) {
+    for (int wt = 0; wt < 2; ++wt) {
+      if (words == 0 && wt) continue;
+      float per_round = 0.f, per_launch = 0.f;
+      // persistent: one launch of R rounds
+      for (int rep = 0; rep < 3; ++rep) {
+        CHECK(hipMemsetAsync(counter, 0, sizeof(unsigned), s));
+        CHECK(hipEventRecord(e0, s));
+        hipLaunchKernelGGL(persistent_kernel, dim3(NWG), dim3(NT), 0, s, in, out, counter, R, err, words, wt);
+        CHECK(hipEventRecord(e1, s));
+        CHECK(hipEventSynchronize(e1));
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        per_round = ms * 1e3f / R;
+      }
+      // launches: R dependent one-round launches in a graph
+      hipGraph_t g;
+      hipGraphExec_t ge;
+      CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+      for (int r = 0; r < R; ++r) hipLaunchKernelGGL(round_kernel, dim3(NWG), dim3(NT), 0, s, in, out, r, words, wt);
+      CHECK(hipStreamEndCapture(s, &g));
+      CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+      for (int rep = 0; rep < 3; ++rep) {
+        CHECK(hipEventRecord(e0, s));
+        CHECK(hipGraphLaunch(ge, s));
+        CHECK(hipEventRecord(e1, s));
+        CHECK(hipEventSynchronize(e1));
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        per_launch = ms * 1e3f / R;
+      }
+      CHECK(hipGraphExecDestroy(ge));
+      CHECK(hipGraphDestroy(g));
+      printf("%5d B per workgroup (%s stores): persistent %.2f us per round, graph %.2f us per launch\n", words * 16,
+             wt ? "write-through" : "write-back", per_round, per_launch);
     }
   }
-  unsigned herr = 0;
   CHECK(hipMemcpy(&herr, err, sizeof(unsigned), hipMemcpyDeviceToHost));
-
-  // launches: R dependent one-round launches in a graph
-  hipGraph_t g;
-  hipGraphExec_t ge;
-  CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
-  for (int r = 0; r < R; ++r) hipLaunchKernelGGL(round_kernel, dim3(NWG), dim3(NT), 0, s, in, out, r);
-  CHECK(hipStreamEndCapture(s, &g));
-  CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-  for (int rep = 0; rep < 3; ++rep) {
-    CHECK(hipEventRecord(e0, s));
-    CHECK(hipGraphLaunch(ge, s));
-    CHECK(hipEventRecord(e1, s));
-    CHECK(hipEventSynchronize(e1));
-    CHECK(hipEventElapsedTime(&ms, e0, e1));
-    if (rep == 2) printf("graph of %d launches: %8.2f us  (%.2f us per launch)\n", R, ms * 1e3, ms * 1e3 / R);
-  }
   printf("barrier timeouts: %u\n", herr);
   CHECK(hipGraphExecDestroy(ge));
   CHECK(hipGraphDestroy(g));
