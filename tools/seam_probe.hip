@@ -5,7 +5,8 @@
 //
 //   hipcc -O3 --offload-arch=gfx950 tools/seam_probe.hip -o tools/seam_probe && tools/seam_probe
 //
-// Persistent form: every workgroup runs R rounds; a round = 16 KB read + 16 KB write (vector memory), then a grid
+// Persistent form: every workgroup runs R rounds; a round = 0, 4 or 16 KB read + written (write-back or write-through
+// 16-B stores), then a grid
 // barrier: every storing wave's vmcnt(0), workgroup barrier, one lane's agent release fence + agent atomic add on
 // the round counter, polling with agent-scope relaxed loads until all workgroups arrived, an agent acquire fence,
 // workgroup barrier (cdna_hip_programming.md sec. 6 Guideline 16).  Every poll loop is capped (a missing arrival
@@ -70,11 +71,11 @@ int main() {
   const int R = 200;
   uint4 *in, *out;
   unsigned *counter, *err;
-  CHECK(hipMalloc(&in, (size_t)NWG * WORDS * sizeof(uint4)));
-  CHECK(hipMalloc(&out, (size_t)NWG * WORDS * sizeof(uint4)));
+  CHECK(hipMalloc(&in, (size_t)NWG * MAXW * sizeof(uint4)));
+  CHECK(hipMalloc(&out, (size_t)NWG * MAXW * sizeof(uint4)));
   CHECK(hipMalloc(&counter, sizeof(unsigned)));
   CHECK(hipMalloc(&err, sizeof(unsigned)));
-  CHECK(hipMemset(in, 0, (size_t)NWG * WORDS * sizeof(uint4)));
+  CHECK(hipMemset(in, 0, (size_t)NWG * MAXW * sizeof(uint4)));
   CHECK(hipMemset(err, 0, sizeof(unsigned)));
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
@@ -121,7 +122,5 @@ int main() {
   }
   CHECK(hipMemcpy(&herr, err, sizeof(unsigned), hipMemcpyDeviceToHost));
   printf("barrier timeouts: %u\n", herr);
-  CHECK(hipGraphExecDestroy(ge));
-  CHECK(hipGraphDestroy(g));
   return herr ? 2 : 0;
 }
