@@ -94,7 +94,8 @@ typedef struct {
                          * on those shapes), 1 off, 2 every eligible */
   int gemm_lib;         /* plain bf16 GEMMs with fp32 output and k-major operands (the decoder's batched weight / input
                          * gradients) on hipBLASLt (gemmlib.hip): 0 auto (weight gradients, input gradients with
-                         * 1024 <= K <= 4096), 1 off (the hand-written tile kernels), 2 every eligible */
+                         * 1024 <= K <= 4096), 1 off (the hand-written tile kernels), 2 every eligible, 3 auto with a
+                         * 64 MB workspace (split-K algorithms allowed) */
 } SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),

@@ -73,7 +73,7 @@ def main():
     ap.add_argument("--torch", action="store_true",
                     help="calibration: torch.matmul (hipBLASLt) of the same bf16 operands, bf16 output")
     a = ap.parse_args()
-    tot_us = tot_f = tot_tile = 0.0
+    tot_us = tot_f = tot_tile = tot_ws = 0.0
     for name, M, N, K, ta, tb, cdt, beta, *rest in SHAPES:
         act = rest[0] if rest else 0
         A, Bm, C = operands(M, N, K, ta, tb, cdt)
@@ -83,9 +83,12 @@ def main():
         tot_f += f
         us_tile = time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_lib=1), a.reps, act)
         us_pipe = time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_lib=1, gemm_pipe=2), a.reps, act)
+        us_ws = time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_lib=3), a.reps, act)
+        tot_ws += us_ws
         tot_tile += us_tile
         line = f"{name:30s} M {M:5d} N {N:5d} K {K:5d} {'T' if ta else 'N'}{'T' if tb else 'N'}  {us:8.1f} us " \
-               f"{f / us / 1e6:7.1f} TF/s  [hand-written: tile {us_tile:.1f} us, pipe {us_pipe:.1f} us]"
+               f"{f / us / 1e6:7.1f} TF/s  [hand-written: tile {us_tile:.1f} us, pipe {us_pipe:.1f} us; library with a workspace " \
+               f"{us_ws:.1f} us]"
         if a.tiles:
             alt = []
             for tile in (1, 2, 3, 4, 5):
@@ -116,7 +119,7 @@ def main():
             line += "  [" + " ".join(alt) + "]"
         print(line, flush=True)
     print(f"total {tot_us:.1f} us for {tot_f / 1e9:.1f} GFLOP = {tot_f / tot_us / 1e6:.1f} TF/s "
-          f"(hand-written tile kernels: {tot_tile:.1f} us)", flush=True)
+          f"(hand-written tile kernels: {tot_tile:.1f} us; workspace {tot_ws:.1f} us)", flush=True)
 
 
 if __name__ == "__main__":
