@@ -80,7 +80,7 @@ typedef struct {
   uint64_t* stamps;
   int stamp_capacity;
   int conv_slices;      /* layer3 c1 / c2 half-image kernels (sat_conv1x1_frag, sat_conv3x3_frag at 14x14): 0 auto
-                         * (channel slices when B <= 64), 1 one workgroup per half image, 2 two 128-channel slices
+                         * (channel slices when B < 64), 1 one workgroup per half image, 2 two 128-channel slices
                          * per half image, 3 slices for the 3x3 only; sat_conv3x3_frag at 7x7: 0 auto (two images per workgroup when B > 64),
                          * 1 two images, 2 one image per workgroup */
   int fused_lstm;       /* bf16 decoder, LSTM cell per time step: 0 auto = 1; 1 the split-K context / dh products + separate

@@ -1247,14 +1247,16 @@ __global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restric
 
 // Layer3 c1 / c2 launch form for a batch of N images: 1 = one workgroup per half image (2N workgroups), 2 = two
 // 128-channel slices per half image (4N).  SatPolicy::conv_slices forces
-// one; automatic: slices when the half images fill at most half the chip's 256 CUs (B <= 64 per GPU).
+// one; automatic: slices when the half images fill less than half the chip's 256 CUs (B < 64 per GPU).
 // c2: the 3x3 (slices also at B = 128 with conv_slices = 3: two workgroups per CU, one's staging under the
 // other's MFMAs)
 int sat_frag_slices(int N, bool c2 = false) {
   const int f = sat_policy().conv_slices;
   if (f == 1 || f == 2) return f;
   if (f == 3 && c2) return 2;
-  return 2 * N <= 128 ? 2 : 1;
+  // auto: slices only below 64 images (128 half images); at B = 64 the whole-half-image kernels measured faster
+  // since the write-through stores (3.97-3.98 vs 4.01-4.04 ms per step, profiles/r4_s42 / r4_s43)
+  return 2 * N < 128 ? 2 : 1;
 }
 
 }  // namespace

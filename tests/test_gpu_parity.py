@@ -1085,7 +1085,7 @@ def test_bottleneck_fused_bit_identical(sat, N, H, C, M):
                                           (70, 7, 512, 0)])
 def test_conv3x3_frag_bit_identical(sat, N, H, C, slices):
     """csrc/convblock.hip's half-image 3x3 kernel (a layer3 c2 left unfused: 14x14, 256 -> 256), its two-slice
-    form (SatPolicy.conv_slices 2: each half image as two 128-channel workgroups, the default at B <= 64;
+    form (SatPolicy.conv_slices 2: each half image as two 128-channel workgroups, the default below B = 64;
     N = 70 leaves a partial group of 8 half images), its 7-row band form (layer2 c2: 28x28, 128 -> 128) and its
     whole-image form (layer4 c2: 7x7, 512 -> 512, one or two images x four 128-channel slices per workgroup; odd N
     leaves a one-image group) are bit-identical to the tile kernel on the same operands, and close to torch fp32."""
@@ -1107,7 +1107,7 @@ def test_conv3x3_frag_bit_identical(sat, N, H, C, slices):
 @pytest.mark.parametrize("N,slices", [(1, 1), (2, 1), (5, 1), (1, 2), (5, 2), (70, 2), (3, 0)])
 def test_conv1x1_frag_bit_identical(sat, N, slices):
     """csrc/convblock.hip's half-image 1x1 kernel (a layer3 c1 left unfused: 14x14, 1024 -> 256, input
-    slabs by LDS-DMA) and its two-slice form (SatPolicy.conv_slices 2, the default at B <= 64) are
+    slabs by LDS-DMA) and its two-slice form (SatPolicy.conv_slices 2, the default below B = 64) are
     bit-identical to sat_conv2d_nhwc on the same operands, and close to torch fp32."""
     from sat_amd import ops
     g = torch.Generator().manual_seed(60 + N)
