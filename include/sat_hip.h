@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SAT_ABI_VERSION 6
+#define SAT_ABI_VERSION 7
 
 enum { SAT_F32 = 0, SAT_BF16 = 1 };
 enum { SAT_ACT_NONE = 0, SAT_ACT_RELU = 1, SAT_ACT_TANH = 2, SAT_ACT_SIGMOID = 3 };
@@ -45,30 +45,33 @@ typedef struct {
 } SatConvGeom;
 
 /* Per-call kernel selection.  Every field 0 = the library's choice (what the product runs); the
- * other values force or exclude one kernel for a single call -- A/B measurements and the tests that
- * compare two kernels bit for bit.  Passed by pointer (nullable = all defaults) to every entry point
- * that dispatches among kernels: SatGemmArgs.policy, sat_conv2d_nhwc, SatDecoderDims.policy.  There
- * is no process-global tuning state: two callers in one process never see each other's policy. */
+ * other values force or exclude one kernel for a single call -- the tests that compare two kernels bit
+ * for bit, and A/B measurements.  Passed by pointer (nullable = all defaults) to every entry point that
+ * dispatches among kernels: SatGemmArgs.policy, sat_conv2d_nhwc, SatDecoderDims.policy.  There is no
+ * process-global tuning state: two callers in one process never see each other's policy. */
 typedef struct {
-  int conv_pipe;        /* pipelined conv / GEMM kernel: 0 auto (long-K, chip-filling, 256x128 tiles), 1 off, 2 every
-                         * eligible problem, 3 every eligible problem with N % 256 == 0 on the 256x256 form (opt-in:
-                         * measured slower), 4 = 0 */
+  int conv_pipe;        /* pipelined 256x128 conv / GEMM kernel: 0 auto (long-K, chip-filling problems), 1 off,
+                         * 2 every eligible problem */
   int conv_stream;      /* weight-stationary 1x1 kernel (K <= 512): 0 auto, 1 off, 2 every eligible */
   int conv3x3_ws;       /* 64 -> 64 3x3 weight-stationary halo kernel: 0 on, 1 off */
-  int skinny;           /* register-direct skinny GEMM (M <= 128): 0 the decoder's K/256-split products, 1 off,
+  int conv_slices;      /* layer3 c1 / c2 half-image kernels (sat_conv1x1_frag, sat_conv3x3_frag at 14x14): 0 auto
+                         * (two 128-channel slices per half image when B < 64), 1 one workgroup per half image, 2 the
+                         * slices; sat_conv3x3_frag at 7x7: 0 auto (two images per workgroup when B > 64), 1 two
+                         * images, 2 one image per workgroup */
+  int skinny;           /* register-direct skinny GEMM (M <= 128): 0 the decoder's split products, 1 off,
                          * 2 every eligible problem */
   int gemm_stages;      /* LDS ring depth of the bf16 tile kernel: 0 auto, 2, 3 */
-  int gemm_tile;        /* tile configuration: 0 auto, 1 = 128x128 / 8 waves, 2 = 128x64 / 8, 3 = 128x128 / 4,
+  int gemm_tile;        /* tile kernel configuration: 0 auto, 1 = 128x128 / 8 waves, 2 = 128x64 / 8, 3 = 128x128 / 4,
                          * 4 = 128x256 / 8, 5 = 256x128 / 8 (k-major operands use 1 or 3) */
-  int gemm_linear_order;/* 1 = plain tile order instead of the XCD-aware one */
+  int gemm_linear_order;/* 1 = plain tile order instead of the XCD-aware one (tile kernel) */
   int gemm_epilogue;    /* bf16-output epilogue of 128-row tiles: 0 bf16 LDS epilogue for every eligible launch,
                          * 1 for residual launches only, 2 fp32 tile staged in LDS */
+  int split_gemm;       /* bf16 products with fp32 output and a k-major operand (the decoder's batched weight / input
+                         * gradients; gemmsplit.hip: deterministic split-K, no atomics): 0 auto, 1 off (the tile
+                         * kernel), 2 128-row tiles only, 3 256-row tiles only */
+  int split_k;          /* split_gemm: 0 the planner's split count, n > 0 exactly n splits when the shape allows */
   int attn_bwd;         /* attention backward per decoder step: 0 auto, 1 the two-launch form */
   int attn_bwd_chunks;  /* split attention backward: slot chunks per batch row (0 auto: ~256 workgroups) */
-  int gemm_split_wgs;   /* bf16 tile GEMM, fp32 output: workgroups an atomic split-K aims for (0 = 320; problems with
-                         * fewer than half as many tiles and K >= 1024 are split); the pipelined fp32-output GEMM
-                         * (gemm_pipe): > 0 aims its split-K at that many workgroups, 0 its rounds x k-tiles model */
-  int lstm_blocks;      /* LSTM pointwise kernels: cap on the 256-thread blocks (0 = one per 64 units, <= 4096) */
   int decoder_splits[4];/* split-K counts of the per-step bf16 decoder GEMMs -- h: [U; f_beta; W_hh] h, c: context
                          * part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic */
   /* diagnostics (bench.py's in-step kernel timing): a device buffer; when non-null and stamps[0] != 0 (the
@@ -79,30 +82,17 @@ typedef struct {
    * 2 (stamp_capacity + 1) words, one per per-step kernel group and step (decoder.hip). */
   uint64_t* stamps;
   int stamp_capacity;
-  int conv_slices;      /* layer3 c1 / c2 half-image kernels (sat_conv1x1_frag, sat_conv3x3_frag at 14x14): 0 auto
-                         * (channel slices when B < 64), 1 one workgroup per half image, 2 two 128-channel slices
-                         * per half image, 3 slices for the 3x3 only; sat_conv3x3_frag at 7x7: 0 auto (two images per workgroup when B > 64),
-                         * 1 two images, 2 one image per workgroup */
-  int fused_lstm;       /* bf16 decoder, LSTM cell per time step: 0 auto = 1; 1 the split-K context / dh products + separate
-                         * lstm_fwd / lstm_bwd launches (4 per time step each way); 2 the cell forward in the epilogue of
-                         * the context GEMM and the backward in the dh GEMM's, full-K row-block GEMMs (3 launches per
-                         * time step; lstmgemm.hip), eight waves per workgroup; 3 the same on four waves; 4 / 5 the
-                         * eight-wave form for the backward / forward only.  The fused forms are faster alone and
-                         * slower beside the encoder */
-  int gemm_pipe;        /* 256x128 pipelined GEMM with fp32 output and k-major operands (the decoder's weight / input
-                         * gradients; gemmpipe.hip): 0 auto = off (measured slower than the tile kernel and hipBLASLt
-                         * on those shapes), 1 off, 2 every eligible */
-  int gemm_lib;         /* plain bf16 GEMMs with fp32 output and k-major operands (the decoder's batched weight / input
-                         * gradients) on hipBLASLt (gemmlib.hip): 0 auto (weight gradients, input gradients with
-                         * 1024 <= K <= 4096), 1 off (the hand-written tile kernels), 2 every eligible, 3 auto with a
-                         * 64 MB workspace (split-K algorithms allowed) */
 } SatPolicy;
 
 /* Generic GEMM:  C[m,n] = act(alpha*sum_k A(m,k)B(n,k) + bias[n] + add1[m,n] + beta*C[m,n]),
  * A(m,k) = transA ? A[k*lda+m] : A[m*lda+k];  B(n,k) = transB ? B[k*ldb+n] : B[n*ldb+k].
  * Optional aux output receives the same (post-activation) value in aux_dtype.
  * Replaces torch.nn.Linear forward/backward (e.g. attention.py:15-16,
- * decoder.py:99,125,143-146,151-158). */
+ * decoder.py:99,125,143-146,151-158).
+ * workspace (nullable, device, workspace_bytes >= sat_gemm_workspace_bytes()): lets a product with fp32 output and
+ * a k-major operand split K over workgroups with a deterministic in-launch reduction (partial tiles + arrival
+ * tickets, zeroed by the call itself); without it such a product runs unsplit.  One workspace serves calls that
+ * are ordered on one stream. */
 typedef struct {
   int M, N, K, dtype;
   const void* A; int64_t lda; int transA;
@@ -114,6 +104,7 @@ typedef struct {
   int act;
   void* aux; int64_t ld_aux; int aux_dtype;
   const SatPolicy* policy;    /* nullable: library defaults */
+  void* workspace; int64_t workspace_bytes;
 } SatGemmArgs;
 
 /* Decoder problem description (decoder.py:9-67 constructor flags + shapes). */
@@ -155,6 +146,7 @@ const char* sat_error_string(int code);
 
 /* --- generic building blocks -------------------------------------------- */
 int sat_gemm(const SatGemmArgs* args, void* stream);
+size_t sat_gemm_workspace_bytes(void);
 /* elementwise cast between SAT_F32 and SAT_BF16 storage (n elements). */
 int sat_cast(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, void* stream);
 
@@ -237,9 +229,8 @@ size_t sat_decoder_workspace_bytes(const SatDecoderDims* d);
  *   0 h-GEMM split-K slabs, 1 context-GEMM slabs, 2 d(gated context) slabs, 3 dh slabs,
  *   4 attention-backward slot chunks per batch row (1 = one workgroup per row, no last-arriver combine;
  *     0 = the two-launch form or no attention), 5 backward products on the transposed weight copies,
- *   6 LSTM forward folded into the context GEMM, 7 LSTM backward folded into the dh GEMM,
- *   8 launches per forward time step, 9 launches per BPTT time step (teacher forcing, attention on). */
-enum { SAT_DECODER_INSTANCE_FIELDS = 10 };
+ *   6 launches per forward time step, 7 launches per BPTT time step (teacher forcing). */
+enum { SAT_DECODER_INSTANCE_FIELDS = 8 };
 int sat_decoder_instance(const SatDecoderDims* d, const SatDecoderLayout* lay, int* out, int n);
 /* bf16 mode: rewrite the transposed weight copies layout->wih_ctx_t / hcat_t inside params_lp from the shadow's
  * own W_ih / hcat rows (after the shadow changed: the fused Adam step, a cast); a no-op when either is -1. */

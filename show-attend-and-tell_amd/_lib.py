@@ -25,16 +25,15 @@ class SatConvGeom(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("N", "H", "W", "C", "KH", "KW", "stride", "pad", "OH", "OW")]
 
 
-ABI_VERSION = 6   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
+ABI_VERSION = 7   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
 
 
 class SatPolicy(ctypes.Structure):
     """Per-call kernel selection (include/sat_hip.h SatPolicy); all zeros = the library's defaults."""
-    _fields_ = [(n, c_int) for n in ("conv_pipe", "conv_stream", "conv3x3_ws", "skinny", "gemm_stages", "gemm_tile",
-                                     "gemm_linear_order", "gemm_epilogue", "attn_bwd",
-                                     "attn_bwd_chunks", "gemm_split_wgs", "lstm_blocks")] + \
-               [("decoder_splits", c_int * 4), ("stamps", c_void_p), ("stamp_capacity", c_int), ("conv_slices", c_int),
-                ("fused_lstm", c_int), ("gemm_pipe", c_int), ("gemm_lib", c_int)]
+    _fields_ = [(n, c_int) for n in ("conv_pipe", "conv_stream", "conv3x3_ws", "conv_slices", "skinny", "gemm_stages",
+                                     "gemm_tile", "gemm_linear_order", "gemm_epilogue", "split_gemm", "split_k",
+                                     "attn_bwd", "attn_bwd_chunks")] + \
+               [("decoder_splits", c_int * 4), ("stamps", c_void_p), ("stamp_capacity", c_int)]
 
     def __init__(self, **kw):
         splits = kw.pop("decoder_splits", None)
@@ -53,7 +52,8 @@ class SatGemmArgs(ctypes.Structure):
                 ("add1", c_void_p), ("ld_add1", c_int64), ("add1_dtype", c_int),
                 ("act", c_int),
                 ("aux", c_void_p), ("ld_aux", c_int64), ("aux_dtype", c_int),
-                ("policy", ctypes.POINTER(SatPolicy))]
+                ("policy", ctypes.POINTER(SatPolicy)),
+                ("workspace", c_void_p), ("workspace_bytes", c_int64)]
 
 
 class SatDecoderDims(ctypes.Structure):
@@ -77,6 +77,7 @@ _SIGNATURES = [
     ("sat_abi_version", c_int, []),
     ("sat_error_string", ctypes.c_char_p, [c_int]),
     ("sat_gemm", c_int, [ctypes.POINTER(SatGemmArgs), c_void_p]),
+    ("sat_gemm_workspace_bytes", c_size_t, []),
     ("sat_cast", c_int, [c_void_p, c_int, c_void_p, c_int, c_int64, c_void_p]),
     ("sat_mean_rows_abi", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     ("sat_nchw_to_nhwc", c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),

@@ -260,7 +260,8 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
     const int dout = c0 + col4;
     // fp32 outputs through 16-B write-through stores (sat_common.h): this step's end-of-kernel L2 writeback, on the
     // per-step critical path, has less to flush; the bf16 copies (8 B per thread) stay write-back
-    sat_st16(sat_out_rsrc(a.ctx, 0x7fffffffL), (unsigned)(((long)b * a.ctx_ld + dout) * 4), *(const uint4*)&cacc);
+    // (a resource per batch row: its offsets stay far below the 2 GiB cap whatever B and the row stride)
+    sat_st16(sat_out_rsrc(a.ctx + (long)b * a.ctx_ld, 4L * a.D), (unsigned)(dout * 4), *(const uint4*)&cacc);
     const float c[4] = {cacc.x, cacc.y, cacc.z, cacc.w};
     if (a.ctx_t) {
       T* ct = (T*)a.ctx_t + (long)b * a.ctx_t_ld + dout;
@@ -273,7 +274,7 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) g[k] = 1.0f / (1.0f + expf(-gp[k]));
       if (a.gate)
-        sat_st16(sat_out_rsrc(a.gate, 0x7fffffffL), (unsigned)(((long)b * a.gate_out_ld + dout) * 4),
+        sat_st16(sat_out_rsrc(a.gate + (long)b * a.gate_out_ld, 4L * a.D), (unsigned)(dout * 4),
                  make_uint4(__float_as_uint(g[0]), __float_as_uint(g[1]), __float_as_uint(g[2]), __float_as_uint(g[3])));
       if (a.gated) {
         T* gd = (T*)a.gated + (long)b * a.gated_ld + dout;
@@ -722,6 +723,11 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its sc1 stores are done
   __syncthreads();
   if (tid == 0) {
+    // agent-scope release before the ticket (the payload is already write-through and drained -- MI355X_MICROARCH.md
+    // "Valid forms" -- the fence makes the hand-off a release / acquire pair under the memory model as well; the
+    // second wait keeps the compiler from dropping the fence's own, cdna_hip_programming.md Guideline 16 Pitfall 12)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = __hip_atomic_fetch_add(a.ticket + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool last = prev == (unsigned)(NL - 1);
     if (last) {   // agent-scope acquire on the reading CU besides the sc1 loads below (cdna_hip_programming.md §6

@@ -1248,12 +1248,9 @@ __global__ void frag_layout_kernel(const bf16* __restrict__ src, bf16* __restric
 // Layer3 c1 / c2 launch form for a batch of N images: 1 = one workgroup per half image (2N workgroups), 2 = two
 // 128-channel slices per half image (4N).  SatPolicy::conv_slices forces
 // one; automatic: slices when the half images fill less than half the chip's 256 CUs (B < 64 per GPU).
-// c2: the 3x3 (slices also at B = 128 with conv_slices = 3: two workgroups per CU, one's staging under the
-// other's MFMAs)
-int sat_frag_slices(int N, bool c2 = false) {
+int sat_frag_slices(int N) {
   const int f = sat_policy().conv_slices;
   if (f == 1 || f == 2) return f;
-  if (f == 3 && c2) return 2;
   // auto: slices only below 64 images (128 half images); at B = 64 the whole-half-image kernels measured faster
   // since the write-through stores (3.97-3.98 vs 4.01-4.04 ms per step, profiles/r4_s42 / r4_s43)
   return 2 * N < 128 ? 2 : 1;
@@ -1279,8 +1276,21 @@ extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int 
                                     const float* b1, const void* w2f, const float* b2, const void* w3f,
                                     const float* b3, void* y, const SatPolicy* policy, void* stream) {
   SAT_REQUIRE(N > 0 && x && w1f && w2f && w3f && b1 && b2 && b3 && y && x != y);
-  SatPolicyScope scope(policy);
   SAT_REQUIRE(sat_bottleneck_fused_supported(H, W, Cin, Cmid, dtype));
+  {   // 32-bit buffer offsets (the input resource, sat_out_rsrc's 2 GiB cap on the output): image chunks below 2 GiB
+    const long img = 2L * H * W * Cin;
+    const int cap = (int)(((1L << 31) - 1) / img);
+    if (N > cap) {
+      for (int n0 = 0; n0 < N; n0 += cap) {
+        const int rc = sat_bottleneck_fused(N - n0 < cap ? N - n0 : cap, H, W, Cin, Cmid, dtype,
+                                            (const char*)x + n0 * img, w1f, b1, w2f, b2, w3f, b3, (char*)y + n0 * img,
+                                            policy, stream);
+        if (rc) return rc;
+      }
+      return 0;
+    }
+  }
+  SatPolicyScope scope(policy);
   auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
   SAT_REQUIRE(al(x, 16) && al(y, 16) && al(w1f, 16) && al(w2f, 16) && al(w3f, 16) && al(b1, 16) && al(b2, 16) &&
               al(b3, 16));
@@ -1307,9 +1317,21 @@ extern "C" int sat_conv3x3_frag_supported(int H, int W, int C, int dtype) {
 extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const void* x, const void* wf, const float* b,
                                 void* y, const SatPolicy* policy, void* stream) {
   SAT_REQUIRE(N > 0 && x && wf && b && y && x != y);
+  SAT_REQUIRE(sat_conv3x3_frag_supported(H, W, C, dtype));
+  {   // image chunks whose input and output stay below 2 GiB (32-bit buffer offsets, sat_out_rsrc's cap)
+    const long img = 2L * H * W * C;
+    const int cap = (int)(((1L << 31) - 1) / img);
+    if (N > cap) {
+      for (int n0 = 0; n0 < N; n0 += cap) {
+        const int rc = sat_conv3x3_frag(N - n0 < cap ? N - n0 : cap, H, W, C, dtype, (const char*)x + n0 * img, wf, b,
+                                        (char*)y + n0 * img, policy, stream);
+        if (rc) return rc;
+      }
+      return 0;
+    }
+  }
   SatPolicyScope scope(policy);
   const SatStamps st = sat_launch_stamps();
-  SAT_REQUIRE(sat_conv3x3_frag_supported(H, W, C, dtype));
   auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
   SAT_REQUIRE(al(x, 16) && al(y, 16) && al(wf, 16) && al(b, 16));
   const hipStream_t s = (hipStream_t)stream;
@@ -1338,7 +1360,7 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   }
   // layer3 c2: half images (two workgroups per image), or two channel slices per half image when the half
   // images alone would leave CUs idle (SatPolicy::conv_slices)
-  const int mode = sat_frag_slices(N, true);
+  const int mode = sat_frag_slices(N);
   const int groups = sat_cdiv(2 * N, 8) * 8 * 2;   // whole groups of 8 half images x 2 slices
   if (mode == 1)
     hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp, st);
@@ -1355,6 +1377,19 @@ extern "C" int sat_conv1x1_frag(int N, int H, int W, int Cin, int Cout, int dtyp
                                 const float* b, void* y, const SatPolicy* policy, void* stream) {
   SAT_REQUIRE(N > 0 && x && wf && b && y && x != y);
   SAT_REQUIRE(sat_conv1x1_frag_supported(H, W, Cin, Cout, dtype));
+  {   // image chunks whose input and output stay below 2 GiB (32-bit buffer offsets, sat_out_rsrc's cap)
+    const long img = 2L * H * W * (Cin > Cout ? Cin : Cout);
+    const int cap = (int)(((1L << 31) - 1) / img);
+    if (N > cap) {
+      for (int n0 = 0; n0 < N; n0 += cap) {
+        const int rc = sat_conv1x1_frag(N - n0 < cap ? N - n0 : cap, H, W, Cin, Cout, dtype,
+                                        (const char*)x + 2L * n0 * H * W * Cin, wf, b, (char*)y + 2L * n0 * H * W * Cout,
+                                        policy, stream);
+        if (rc) return rc;
+      }
+      return 0;
+    }
+  }
   SatPolicyScope scope(policy);
   auto al = [](const void* p, int a) { return ((uintptr_t)p & (a - 1)) == 0; };
   SAT_REQUIRE(al(x, 16) && al(y, 16) && al(wf, 16) && al(b, 16));

@@ -531,6 +531,9 @@ void launch_tile(int t, int ns, dim3 grid, hipStream_t s, const FArgs& a) {
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// workgroups the atomic split-K of an fp32-output product aims for (the k-major products split on gemmsplit.hip)
+constexpr int kSplitWgs = 320;
+
 }  // namespace
 
 // Returns 1 if the problem was handled by the fast path, 0 if the caller should use the generic kernel.
@@ -540,12 +543,10 @@ int sat_gemm_splits_atomically(const SatGemm& g) {
   if (g.dtype != SAT_BF16 || g.c_dtype != SAT_F32 || g.act != SAT_ACT_NONE || g.add1 || g.beta != 0.f ||
       g.conv.C > 0 || g.partial_splits > 1 || g.K < 1024)
     return 0;
-  const SatPolicy& pol = sat_policy();
   const bool tr = g.transA || g.transB;
   const int tcfg = (!tr && g.N <= 64) ? T128x64W8 : T128x128W8;
   const long tiles = (long)sat_cdiv(g.M, tile_bm(tcfg)) * sat_cdiv(g.N, tile_bn(tcfg));
-  const int split_wgs = pol.gemm_split_wgs > 0 ? pol.gemm_split_wgs : 320;
-  return tiles < split_wgs / 2 ? 1 : 0;
+  return tiles < kSplitWgs / 2 ? 1 : 0;
 }
 
 int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
@@ -556,6 +557,9 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   const int force_stages = pol.gemm_stages == 2 || pol.gemm_stages == 3 ? pol.gemm_stages : 0;
   const int res_lds = pol.gemm_epilogue == 1 ? 1 : (pol.gemm_epilogue == 2 ? 0 : 2);
   if (!al16(g.B) || !al16(g.A)) return 0;
+  // the epilogues store through a buffer resource (32-bit offsets, sat_out_rsrc's 2 GiB cap): larger outputs take the
+  // generic kernel's plain stores
+  if ((long)(g.c_dtype == SAT_BF16 ? 2 : 4) * ((long)(g.M - 1) * g.ldc + g.N) >= (1L << 31)) return 0;
   const bool conv = g.conv.C > 0;
   const bool at = g.transA != 0, bt = g.transB != 0;
   if (conv && at) return 0;
@@ -581,8 +585,8 @@ int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   int splitk = 1;
   const bool can_split = g.c_dtype == SAT_F32 && g.act == SAT_ACT_NONE && !g.add1 && (g.beta == 0.f || g.beta == 1.f) && !conv;
   if (g.beta != 0.f && !(can_split && g.beta == 1.f)) return 0;
-  // workgroups the atomic split-K aims for (SatPolicy::gemm_split_wgs; 0 = 320, split when tiles < half of it)
-  const int split_wgs = pol.gemm_split_wgs > 0 ? pol.gemm_split_wgs : 320;
+  // workgroups the atomic split-K aims for (split when tiles < half of it)
+  const int split_wgs = kSplitWgs;
   if (partial) {
     splitk = 1;
   } else if (tiles < split_wgs / 2) {

@@ -324,196 +324,6 @@ __device__ __forceinline__ void conv_pipe_kernel_body(const PArgs& a) {
   }
 }
 
-// ---- 256 x 256 form (conv_wide_kernel): 4 waves (2 M x 2 N), a 128 x 128 output tile per wave (64 accumulators,
-// the MFMA accumulators live in AGPRs), two-stage ring of 2 x 64 KiB.  Per k-tile a wave reads (128 + 128) x 64
-// operands from LDS for 2 MFLOP: half the LDS bytes per MFLOP of the 64 x 64 wave tiles above, whose LDS reads
-// take as long as their MFMAs (cdna_hip_programming.md sec. 5: the operand-bandwidth rule).  Same k order, bias,
-// residual, activation and single rounding as conv_pipe_kernel / fast_gemm_kernel: bit-identical.
-constexpr int WBM = 256, WBN = 256, W_NW = 4;
-constexpr int W_STAGE_A = WBM * PROW, W_STAGE_B = WBN * PROW, W_STAGE = W_STAGE_A + W_STAGE_B;   // 64 KiB
-constexpr int W_LDS = 2 * W_STAGE;                                                             // 128 KiB
-constexpr int W_AI = WBM / (8 * W_NW), W_BI = WBN / (8 * W_NW);   // 8 + 8 DMAs of 1 KiB per wave per stage
-constexpr int W_EPI_ROWS = 64, W_EPI_LD = WBN + 4;                 // epilogue in four 64-row quarters
-static_assert(W_EPI_ROWS * W_EPI_LD * 4 <= W_LDS, "epilogue quarter must fit in the ring");
-
-template <int AM, int ACT, bool RES>
-__device__ __forceinline__ void conv_wide_body(const PArgs& a) {
-  constexpr int MI = 8, NJ = 8;
-  __shared__ __attribute__((aligned(16))) char smem[W_LDS];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
-  int tile = blockIdx.x;
-  {   // XCD-aware order (cdna_hip_programming.md T1, bijective form)
-    const int nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = tile % 8;
-    tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
-  }
-  const int m0 = (tile / a.tiles_n) * WBM, n0 = (tile % a.tiles_n) * WBN;
-  const int M = a.M, N = a.N;
-
-  // per-lane DMA bookkeeping as conv_pipe_kernel_body (lane -> row lane >> 3 of an 8-row piece, slot lane & 7)
-  const int lrow = lane >> 3, slot = lane & 7;
-  int a_off[W_AI];
-  unsigned a_ok[W_AI];
-#pragma unroll
-  for (int j = 0; j < W_AI; ++j) {
-    const int r = (w * W_AI + j) * 8 + lrow;
-    const int chunk = slot ^ ((r >> 1) & 7);
-    const int row = m0 + r;
-    a_off[j] = 0;
-    a_ok[j] = 0u;
-    if (row < M) {
-      if constexpr (AM == 0) {
-        a_off[j] = (int)((long)row * a.lda) + 8 * chunk;
-        a_ok[j] = 1u;
-      } else {
-        const int ohw = a.OH * a.OW;
-        const int n = row / ohw, rem = row - n * ohw;
-        const int oh = rem / a.OW, ow = rem - oh * a.OW;
-        const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
-        a_off[j] = ((n * a.H + ih0) * a.W + iw0) * a.Cin + 8 * chunk;
-        const int KH = a.K / (a.KW * a.Cin);
-        unsigned m = 0u;
-        for (int kh = 0; kh < KH; ++kh)
-          for (int kw = 0; kw < a.KW; ++kw)
-            if ((unsigned)(ih0 + kh) < (unsigned)a.H && (unsigned)(iw0 + kw) < (unsigned)a.W) m |= 1u << (kh * a.KW + kw);
-        a_ok[j] = m;
-      }
-    }
-  }
-  unsigned b_voff[W_BI];
-#pragma unroll
-  for (int j = 0; j < W_BI; ++j) {
-    const int r = (w * W_BI + j) * 8 + lrow;
-    const int chunk = slot ^ ((r >> 1) & 7);
-    b_voff[j] = n0 + r < N ? 2u * (unsigned)((int)((long)(n0 + r) * a.ldb) + 8 * chunk) : P_OOB;
-  }
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, (int)a.a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, (short)0, (int)a.b_bytes, 0x00020000);
-  int s_k0 = 0, s_tap = 0, s_ci0 = 0, s_kw = 0, s_delta = 0;
-  auto stage = [&](int buf) {
-    char* sa = smem + buf * W_STAGE;
-    char* sb = sa + W_STAGE_A;
-#pragma unroll
-    for (int j = 0; j < W_AI; ++j) {
-      const bool ok = (a_ok[j] >> s_tap) & 1u;
-      pbdma(rA, sa + (w * W_AI + j) * 1024, ok ? 2u * (unsigned)(a_off[j] + s_delta) : P_OOB, 0u);
-    }
-#pragma unroll
-    for (int j = 0; j < W_BI; ++j) pbdma(rB, sb + (w * W_BI + j) * 1024, b_voff[j], 2u * (unsigned)s_k0);
-    s_k0 += PBK;   // advance the block-uniform k state (as conv_pipe_kernel_body)
-    if constexpr (AM == 0) {
-      s_delta = s_k0;
-    } else {
-      s_ci0 += PBK;
-      if (s_ci0 == a.Cin) {
-        s_ci0 = 0;
-        ++s_tap;
-        if (++s_kw == a.KW) s_kw = 0;
-        const int kh = s_tap / a.KW;
-        s_delta = (kh * a.W + s_kw) * a.Cin;
-      } else {
-        s_delta += PBK;
-      }
-    }
-  };
-
-  const int fr = lane & 15, fh = lane >> 4, sw = (fr >> 1) & 7;
-  const int a_rd = (wm * 128 + fr) * PROW, b_rd = W_STAGE_A + (wn * 128 + fr) * PROW;
-  const int co0 = 16 * ((0 * 4 + fh) ^ sw), co1 = 16 * ((1 * 4 + fh) ^ sw);
-  f32x4 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 xa[MI], xb[NJ];
-  auto frags = [&](int buf, int co, bf16x8 (&fa)[MI], bf16x8 (&fb)[NJ]) {
-    const char* base = smem + buf * W_STAGE;
-#pragma unroll
-    for (int i = 0; i < MI; ++i) fa[i] = *(const bf16x8*)(base + a_rd + i * 16 * PROW + co);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) fb[j] = *(const bf16x8*)(base + b_rd + j * 16 * PROW + co);
-  };
-  auto mfma = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fb)[NJ]) {
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-  };
-
-  const int nk = a.K / PBK;
-  stage(0);
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    // tile t has landed (this wave's DMAs; the barrier: every wave's), and every wave's reads of the other stage
-    // (tile t-1) have retired: tile t+1 may overwrite it
-    p_wait_barrier<0>();
-    if (t + 1 < nk) stage(cur ^ 1);
-    frags(cur, co0, xa, xb);
-    mfma(xa, xb);
-    frags(cur, co1, xa, xb);
-    mfma(xa, xb);
-  }
-  p_wait_barrier<0>();   // every wave done with the ring
-
-  // ---- epilogue in four 64-row quarters: fp32 (acc + bias) through LDS, then 16-B row segments with the residual
-  // added in fp32, activation, one rounding (conv_pipe_kernel_body's arithmetic) ----
-  float* ep = (float*)smem;
-  const __amdgpu_buffer_rsrc_t rC = sat_out_rsrc(a.C, 2L * M * a.ldc);
-  float bcol[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int c = n0 + wn * 128 + j * 16 + fr;
-    bcol[j] = (a.bias && c < N) ? a.bias[c] : 0.f;
-  }
-  const int cc = tid & 31, r0 = tid >> 5;   // 32 chunks of 8 columns x 8 rows per pass
-  const int col = n0 + cc * 8;
-#pragma unroll
-  for (int qtr = 0; qtr < 4; ++qtr) {
-    if (wm == (qtr >> 1)) {
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int i = (qtr & 1) * 4 + ii;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            ep[(ii * 16 + fh * 4 + r) * W_EPI_LD + wn * 128 + j * 16 + fr] = acc[i][j][r] + bcol[j];
-      }
-    }
-    __syncthreads();
-    if (col < N) {
-#pragma unroll
-      for (int it = 0; it < W_EPI_ROWS / 8; ++it) {
-        const int rl = r0 + it * 8, row = m0 + qtr * W_EPI_ROWS + rl;
-        if (row >= M) break;
-        const float4 x0 = *(const float4*)(ep + rl * W_EPI_LD + cc * 8);
-        const float4 x1 = *(const float4*)(ep + rl * W_EPI_LD + cc * 8 + 4);
-        float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        if constexpr (RES) {
-          const uint4 rv = *(const uint4*)(a.res + (long)row * a.ldr + col);
-          const bf16* h = (const bf16*)&rv;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += (float)h[e];
-        }
-        uint4 u;
-        bf16* o = (bf16*)&u;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (bf16)apply_act(v[e], ACT);
-        sat_st16(rC, (unsigned)(((long)row * a.ldc + col) * 2), u);
-      }
-    }
-    __syncthreads();
-  }
-}
-
-template <int AM, int ACT, bool RES>
-__global__ __launch_bounds__(W_NW * 64) void conv_wide_kernel(PArgs a) {
-  const SatStampT0 t0 = sat_stamp_begin(a.st);
-  conv_wide_body<AM, ACT, RES>(a);
-  sat_stamp_end(a.st, t0);
-}
-
 template <int NW, int AM, int ACT, bool RES, int ABL, bool BUF>
 __global__ __launch_bounds__(NW * 64) void conv_pipe_kernel(PArgs a) {
   const SatStampT0 t0 = sat_stamp_begin(a.st);
@@ -542,21 +352,6 @@ void launch_nw(bool conv, bool res, int act, dim3 grid, hipStream_t s, const PAr
   }
 }
 
-template <int AM, bool RES>
-void launch_wide_act(int act, dim3 grid, hipStream_t s, const PArgs& a) {
-  if (act == SAT_ACT_RELU) hipLaunchKernelGGL((conv_wide_kernel<AM, SAT_ACT_RELU, RES>), grid, dim3(W_NW * 64), 0, s, a);
-  else hipLaunchKernelGGL((conv_wide_kernel<AM, SAT_ACT_NONE, RES>), grid, dim3(W_NW * 64), 0, s, a);
-}
-void launch_wide(bool conv, bool res, int act, dim3 grid, hipStream_t s, const PArgs& a) {
-  if (conv) {
-    if (res) launch_wide_act<1, true>(act, grid, s, a);
-    else launch_wide_act<1, false>(act, grid, s, a);
-  } else {
-    if (res) launch_wide_act<0, true>(act, grid, s, a);
-    else launch_wide_act<0, false>(act, grid, s, a);
-  }
-}
-
 inline bool pal16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
@@ -564,8 +359,7 @@ inline bool pal16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // Returns 1 if the problem was launched by the pipelined kernel (error code in *err), 0 otherwise.
 int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err) {
   *err = 0;
-  // 0 auto, 1 off, 2 every eligible problem (256 x 128), 3 every eligible problem with N % 256 == 0 on the 256 x 256
-  // form, 4 auto without the 256 x 256 form
+  // 0 auto, 1 off, 2 every eligible problem
   const int mode = sat_policy().conv_pipe;
   if (mode == 1) return 0;
   if (g.dtype != SAT_BF16 || g.c_dtype != SAT_BF16 || g.batch != 1 || g.aux || g.transA || g.transB) return 0;
@@ -583,7 +377,7 @@ int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err) {
   }
   if ((long)g.N * g.ldb >= (1L << 31)) return 0;
   const long tiles = (long)sat_cdiv(g.M, PBM) * sat_cdiv(g.N, PBN);
-  if (mode == 0 || mode == 4) {
+  if (mode != 2) {
     // long-K problems that fill most of the chip with 256 x 128 tiles (tools/pipe_ab.py: ResNet152
     // L3 c1/c2, L2 c2, L4, every VGG19 conv from 128 channels on: 1.05-1.26x); short-K problems,
     // N < 128 and the residual 1x1 convs stay on fast_gemm_kernel (two workgroups per CU)
@@ -615,19 +409,11 @@ int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err) {
   {
     const long a_bytes = conv ? 2L * g.conv.N * g.conv.H * g.conv.W * g.conv.C : 2L * ((long)(g.M - 1) * g.lda + g.K);
     const long b_bytes = 2L * ((long)(g.N - 1) * g.ldb + g.K);
-    if (a_bytes >= (1L << 31) || b_bytes >= (1L << 31)) return 0;
+    // every buffer offset is 32-bit (sat_out_rsrc caps the C resource at 2 GiB): C below that too
+    const long c_bytes = 2L * ((long)(g.M - 1) * g.ldc + g.N);
+    if (a_bytes >= (1L << 31) || b_bytes >= (1L << 31) || c_bytes >= (1L << 31)) return 0;
     a.a_bytes = (unsigned)a_bytes;
     a.b_bytes = (unsigned)b_bytes;
-  }
-  // the 256 x 256 form, opt-in (mode 3): measured slower than the 256 x 128 form on the VGG19 convs (0.31-0.34 vs
-  // 0.33-0.38 of peak, cfg5 11.77 vs 10.87 ms per step, profiles/r4_s24): one wave per SIMD leaves the fragment
-  // reads and the per-k-tile barrier exposed, and its 128 KiB of LDS keeps the decoder's kernels off the CU
-  const long tiles_w = (long)sat_cdiv(g.M, WBM) * (g.N / WBN);
-  if (g.N % WBN == 0 && mode == 3) {
-    a.tiles_n = g.N / WBN;
-    launch_wide(conv, g.add1 != nullptr, g.act, dim3((unsigned)tiles_w), s, a);
-    *err = (int)hipGetLastError();
-    return 1;
   }
   const dim3 grid((unsigned)tiles);
   launch_nw<8>(conv, g.add1 != nullptr, g.act, grid, s, a);

@@ -35,7 +35,13 @@ struct WS {
   float *dcomb, *dhd, *dctx_head, *dhg, *dgated, *dh_rec, *dc, *dWs_acc, *dv_acc, *dbv_acc, *part, *demb, *dpre0,
       *colsum, *de_all;
   unsigned* ticket;
+  // deterministic split-K of the batched weight / input gradients (gemmsplit.hip): partial tiles, and
+  // kTicketBlocks x kSatSplitTickets arrival tickets (each product of a backward phase has its own block, all zeroed
+  // by the phase's one zeroing launch)
+  float* gsplit;
+  unsigned* gtickets;
 };
+constexpr int kTicketBlocks = 16;   // phase 1: blocks 0-7, phase 2: 8-15
 
 // split counts of the per-step skinny GEMMs (M = B rows).  bf16: the LDS-DMA kernel (128 x 64
 // tiles, 128 x 128 for k-major weights) with partial-output split-K -- aim for ~0.75 waves of
@@ -161,6 +167,13 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   c.take(w->de_all, R * L * f);
   c.take(w->part, sat_attention_part_floats(d.B, d.L, d.D, d.E, d.dtype, d.split_target) * f);
   c.take(w->ticket, B * 4);
+  if (d.dtype == SAT_BF16) {
+    c.take(w->gsplit, sat_split_gemm_ws_bytes() - kSatSplitTickets * 4);
+    c.take(w->gtickets, (size_t)kTicketBlocks * kSatSplitTickets * 4);
+  } else {
+    w->gsplit = nullptr;
+    w->gtickets = nullptr;
+  }
   c.take(w->demb, R * E * f);
   c.take(w->dpre0, B * 2 * E * f); c.take(w->dpre0_t, B * 2 * E * ts);
   // column-sum scratch: the largest single sum, or all the bias sums of one backward phase in one launch pair
@@ -216,16 +229,6 @@ __global__ void init_state_kernel(const float* pre, int splits, long stride, int
     if (j < E) h_t[(long)b * h_ld + j] = (T)v;
     else c_in[(long)b * c_ld + j - E] = v;
   }
-}
-
-// whether the LSTM cell forward runs in the context GEMM's epilogue and the backward in the dh GEMM's (lstmgemm.hip:
-// full-K row blocks; bf16, attention, the transposed weight copies for the backward; SatPolicy::fused_lstm = 1: the
-// separate launches)
-inline int fused_fwd(const SatDecoderDims& d, const Splits& sp) {   // the epilogue sums <= 2 h-GEMM slabs
-  return d.dtype == SAT_BF16 && d.attention && sp.h <= 2 && sat_lstm_gemm_fwd_ok(d.B, d.E, d.D);
-}
-inline int fused_bwd(const SatDecoderDims& d, const Splits&, bool tr) {
-  return d.dtype == SAT_BF16 && d.attention && tr && sat_lstm_gemm_bwd_ok(d.B, d.E, 5 * d.E + d.D);
 }
 
 struct Ctx {
@@ -364,16 +367,6 @@ int fwd_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) 
   return sat_lstm_fwd_launch(lstm_fwd_args(c, w, sp, t), s);
 }
 
-// the context GEMM with the LSTM cell in its epilogue (one launch, lstmgemm.hip); *launched = 0: not eligible, nothing
-// launched (the caller runs fwd_cgemm + fwd_lstm)
-int fwd_cgemm_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s, int* launched) {
-  const SatDecoderDims& d = c.d;
-  int err = 0;
-  *launched = sat_lstm_gemm_fwd_try(c.at(w.gated_t, (long)t * d.D), c.T1 * d.D, c.W(c.lay.wih + d.E), d.E + d.D, d.D,
-                                    lstm_fwd_args(c, w, sp, t), s, &err);
-  return err;
-}
-
 LstmBwdArgs lstm_bwd_args(const Ctx& c, const WS& w, const Splits& sp, int t) {
   const SatDecoderDims& d = c.d;
   const int B = d.B, D = d.D, E = d.E;
@@ -397,11 +390,26 @@ int bwd_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s) 
   return sat_lstm_bwd_launch(lstm_bwd_args(c, w, sp, t), s);
 }
 
+// the workspace a batched backward product may split K over (gemmsplit.hip): ticket block `blk`
+struct SplitWS {
+  float* slab;
+  unsigned* tickets;
+  int blk;
+};
+inline void use_split(SatGemm& g, const SplitWS* sw) {
+  if (!sw || !sw->slab) return;
+  g.split_ws = sw->slab;
+  g.split_ws_bytes = (long)(sat_split_gemm_ws_bytes() - kSatSplitTickets * 4);
+  g.split_tickets = sw->tickets + (long)sw->blk * kSatSplitTickets;
+  g.tickets_zeroed = 1;
+}
+
 // input gradient: Y[M,N] = X[M,K] W[K,N]   (W stored [K][N] row-major = torch weight [out,in])
 int dgrad_launch(const Ctx& c, int M, int N, int K, const void* X, long ldx, const void* Wt, long ldw, float* out,
                  long ldo, hipStream_t s, const float* add1 = nullptr, long ld_add1 = 0, int splits = 0,
-                 long split_stride = 0, int a_tail = 0) {
+                 long split_stride = 0, int a_tail = 0, const SplitWS* sw = nullptr) {
   SatGemm g;
+  use_split(g, sw);
   g.a_tail = a_tail;
   g.partial_splits = splits; g.split_stride = split_stride;
   g.M = M; g.N = N; g.K = K; g.dtype = c.d.dtype;
@@ -463,16 +471,6 @@ int bwd_dhgemm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s
                         nullptr, 0, sp.dh, (long)B * E);
   return dgrad_launch(c, B, E, 4 * E, c.at(w.dhg_t, (long)t * HG + E + D), T1 * HG,
                       c.W(c.lay.hcat_w + (long)(E + D) * E), E, w.dh_rec, E, s, nullptr, 0, sp.dh, (long)B * E);
-}
-
-// the dh GEMM of step t > 0 with step t-1's LSTM cell backward in its epilogue (one launch, lstmgemm.hip);
-// *launched = 0: not eligible, nothing launched (the caller runs bwd_dhgemm(t) and bwd_lstm(t - 1) at step t-1)
-int bwd_dhgemm_lstm(const Ctx& c, const WS& w, const Splits& sp, int t, hipStream_t s, int* launched) {
-  const SatDecoderDims& d = c.d;
-  int err = 0;
-  *launched = sat_lstm_gemm_bwd_try(c.at(w.dhg_t, (long)t * c.HG), c.T1 * c.HG, c.W(c.lay.hcat_t), c.HG, (int)c.HG,
-                                    lstm_bwd_args(c, w, sp, t - 1), s, &err);
-  return err;
 }
 
 // In-kernel timestamps of the per-step kernels (SatPolicy::stamps, bench.py's in-step figures): the
@@ -592,10 +590,9 @@ extern "C" int sat_decoder_instance(const SatDecoderDims* dp, const SatDecoderLa
   const int VD = d.dtype == SAT_BF16 ? 8 : 4;
   const bool split_bwd = d.attention && sat_policy().attn_bwd != 1 && d.E % 4 == 0 && sat_cdiv(d.D, 64 * VD) <= 8 &&
                          sat_cdiv(d.E, 64 * VD) <= (d.dtype == SAT_BF16 ? 2 : 4);
-  const int ff = fused_fwd(d, sp), fb = fused_bwd(d, sp, tr);
   const int v[SAT_DECODER_INSTANCE_FIELDS] = {
-      sp.h, sp.c, sp.g, sp.dh, split_bwd ? sat_attention_bwd_chunks(d.B, d.L, d.split_target) : 0, tr ? 1 : 0, ff, fb,
-      (d.attention ? 3 : 1) + (ff ? 0 : 1), (d.attention ? 3 : 1) + (fb ? 0 : 1)};
+      sp.h, sp.c, sp.g, sp.dh, split_bwd ? sat_attention_bwd_chunks(d.B, d.L, d.split_target) : 0, tr ? 1 : 0,
+      d.attention ? 4 : 2, d.attention ? 4 : 2};
   for (int i = 0; i < n && i < SAT_DECODER_INSTANCE_FIELDS; ++i) out[i] = v[i];
   return 0;
 }
@@ -621,7 +618,6 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
   const long HG = c.HG;
   const bool att = d.attention != 0;
   const Splits sp = splits_for(d, c.tr);
-  const int ff = fused_fwd(d, sp);
   const StepIO io{img_features, alphas, nullptr};
 
   // fed tokens + embeddings
@@ -673,17 +669,15 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
       StepTimer st(d, 0, t);
       SAT_CHECK((hipError_t)fwd_hgemm(c, w, sp, t, s));
     }
-    int cell_done = 0;   // the LSTM cell ran inside the context GEMM
     if (att) {
       {
         StepTimer st(d, 1, t);
         SAT_CHECK((hipError_t)fwd_attn(c, w, sp, io, t, s));
       }
       StepTimer st(d, 2, t);
-      if (ff) SAT_CHECK((hipError_t)fwd_cgemm_lstm(c, w, sp, t, s, &cell_done));
-      if (!cell_done) SAT_CHECK((hipError_t)fwd_cgemm(c, w, sp, t, s));
+      SAT_CHECK((hipError_t)fwd_cgemm(c, w, sp, t, s));
     }
-    if (!cell_done) {
+    {
       StepTimer st(d, 3, t);
       SAT_CHECK((hipError_t)fwd_lstm(c, w, sp, t, s));
     }
@@ -739,22 +733,35 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
     g.C = out; g.ldc = ldo; g.c_dtype = SAT_F32; g.beta = beta;
     return g;
   };
-  auto wgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo,
-                   int a_tail = 0) {
-    return sat_gemm_launch(wg(M, N, K, X, ldx, Y, ldy, out, ldo, a_tail), s);
+  // the split-K workspace with ticket block blk (phase 1: 0-7, phase 2: 8-15; each zeroed by its phase's one
+  // zeroing launch below)
+  const SplitWS sws[kTicketBlocks] = {
+      {w.gsplit, w.gtickets, 0}, {w.gsplit, w.gtickets, 1}, {w.gsplit, w.gtickets, 2}, {w.gsplit, w.gtickets, 3},
+      {w.gsplit, w.gtickets, 4}, {w.gsplit, w.gtickets, 5}, {w.gsplit, w.gtickets, 6}, {w.gsplit, w.gtickets, 7},
+      {w.gsplit, w.gtickets, 8}, {w.gsplit, w.gtickets, 9}, {w.gsplit, w.gtickets, 10}, {w.gsplit, w.gtickets, 11},
+      {w.gsplit, w.gtickets, 12}, {w.gsplit, w.gtickets, 13}, {w.gsplit, w.gtickets, 14}, {w.gsplit, w.gtickets, 15}};
+  const SatZeroSeg tickets_ph1{(float*)w.gtickets, 1, 8L * kSatSplitTickets, 8L * kSatSplitTickets};
+  const SatZeroSeg tickets_ph2{(float*)w.gtickets + 8L * kSatSplitTickets, 1, 8L * kSatSplitTickets,
+                               8L * kSatSplitTickets};
+  auto wgs = [&](int blk, int M, int N, int K, const void* X, long ldx, const void* Y, long ldy, float* out, long ldo,
+                 int a_tail = 0) {
+    SatGemm g = wg(M, N, K, X, ldx, Y, ldy, out, ldo, a_tail);
+    use_split(g, &sws[blk]);
+    return g;
   };
-  // the targets of this phase's weight-gradient products that run as atomic split-K (beta = 0): marked zeroed
-  // and appended to one zeroing launch instead of a zeroing pass per product
+  // the targets of this phase's weight-gradient products that run as atomic split-K on the tile kernel (beta = 0):
+  // marked zeroed and appended to one zeroing launch instead of a zeroing pass per product (the split-K kernel
+  // writes C itself and needs none)
   auto prezero = [&](SatGemm* const* gs, int n, SatZeroSeg* seg, int& nseg) {
     for (int i = 0; i < n; ++i)
-      if (!accumulate && (sat_gemm_pipe_atomic(*gs[i]) || sat_gemm_splits_atomically(*gs[i]))) {
+      if (!accumulate && !sat_split_gemm_takes(*gs[i]) && sat_gemm_splits_atomically(*gs[i])) {
         seg[nseg++] = SatZeroSeg{(float*)gs[i]->C, gs[i]->M, gs[i]->N, gs[i]->ldc};
         gs[i]->c_zeroed = 1;
       }
   };
-  auto dgrad = [&](int M, int N, int K, const void* X, long ldx, const void* Wt, long ldw, float* out, long ldo,
-                   const float* add1 = nullptr, long ld_add1 = 0) {
-    return dgrad_launch(c, M, N, K, X, ldx, Wt, ldw, out, ldo, s, add1, ld_add1);
+  auto dgrad = [&](int blk, int M, int N, int K, const void* X, long ldx, const void* Wt, long ldw, float* out,
+                   long ldo, const float* add1 = nullptr, long ld_add1 = 0) {
+    return dgrad_launch(c, M, N, K, X, ldx, Wt, ldw, out, ldo, s, add1, ld_add1, 0, 0, 0, &sws[blk]);
   };
   auto colsum = [&](const void* X, int dt, long ld, int rows, int N, float* out, float* out2 = nullptr) {
     return sat_colsum(X, dt, ld, rows, N, out, accumulate, out2, w.colsum, s);
@@ -773,19 +780,20 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
         SAT_CHECK((hipError_t)sat_relu_mask_mul(d_preds, preds, (long)R * V, d.dtype, w.dpre_t, s));
         dpre = w.dpre_t;
       }
-      SatGemm gfo = wg(V, E, R, dpre, ldp, w.comb_t, E, G(lay->fout_w), E, VP != V);
-      SatGemm gfh = wg(E, E, R, w.dfh_t, E, w.hd_t, E, G(lay->fh_w), E);
-      SatGemm gfz = wg(E, D, R, w.dfz_t, E, w.ctx_t, D, G(lay->fz_w), D);
+      SatGemm gfo = wgs(0, V, E, R, dpre, ldp, w.comb_t, E, G(lay->fout_w), E, VP != V);
+      SatGemm gfh = wgs(2, E, E, R, w.dfh_t, E, w.hd_t, E, G(lay->fh_w), E);
+      SatGemm gfz = wgs(3, E, D, R, w.dfz_t, E, w.ctx_t, D, G(lay->fz_w), D);
       {
         SatGemm* gs[3] = {&gfo, &gfh, &gfz};
-        SatZeroSeg seg[3];
+        SatZeroSeg seg[4];
         int nseg = 0;
+        if (w.gtickets) seg[nseg++] = tickets_ph1;
         prezero(gs, 3, seg, nseg);
         SAT_CHECK((hipError_t)sat_zero_segs(seg, nseg, s));
       }
       SAT_CHECK((hipError_t)sat_gemm_launch(gfo, s));
       SAT_CHECK((hipError_t)dgrad_launch(c, R, E, V, dpre, ldp, c.W(lay->fout_w), E, w.dcomb, E, s, nullptr, 0, 0, 0,
-                                         VP != V));
+                                         VP != V, &sws[1]));
       SAT_CHECK((hipError_t)sat_ado_bwd_split(w.dcomb, w.fh, w.fz, (long)R * E, d.dtype, w.dfh_t, w.dfz_t, s));
       SAT_CHECK((hipError_t)sat_gemm_launch(gfh, s));
       SAT_CHECK((hipError_t)sat_gemm_launch(gfz, s));
@@ -794,8 +802,8 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
                                   {w.dfh_t, d.dtype, E, R, E, G(lay->fh_b), accumulate, nullptr},
                                   {w.dfz_t, d.dtype, E, R, E, G(lay->fz_b), accumulate, nullptr}};
       SAT_CHECK((hipError_t)sat_colsum_multi(cs, 3, w.colsum, s));
-      SAT_CHECK((hipError_t)dgrad(R, E, E, w.dfh_t, E, c.W(lay->fh_w), E, w.dhd, E));
-      if (att) SAT_CHECK((hipError_t)dgrad(R, D, E, w.dfz_t, E, c.W(lay->fz_w), D, w.dctx_head, D));
+      SAT_CHECK((hipError_t)dgrad(4, R, E, E, w.dfh_t, E, c.W(lay->fh_w), E, w.dhd, E));
+      if (att) SAT_CHECK((hipError_t)dgrad(5, R, D, E, w.dfz_t, E, c.W(lay->fz_w), D, w.dctx_head, D));
     } else {
       const void* dpre = d_preds;
       long ldp = V;
@@ -803,10 +811,19 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
         SAT_CHECK((hipError_t)sat_pad_rows(d_preds, nullptr, R, V, VP, d.dtype, w.dpre_t, s));
         dpre = w.dpre_t; ldp = VP;
       }
-      SAT_CHECK((hipError_t)wgrad(V, E, R, dpre, ldp, w.hd_t, E, G(lay->do_w), E, VP != V));
+      SatGemm gdo = wgs(0, V, E, R, dpre, ldp, w.hd_t, E, G(lay->do_w), E, VP != V);
+      {
+        SatGemm* gs[1] = {&gdo};
+        SatZeroSeg seg[2];
+        int nseg = 0;
+        if (w.gtickets) seg[nseg++] = tickets_ph1;
+        prezero(gs, 1, seg, nseg);
+        SAT_CHECK((hipError_t)sat_zero_segs(seg, nseg, s));
+      }
+      SAT_CHECK((hipError_t)sat_gemm_launch(gdo, s));
       SAT_CHECK((hipError_t)colsum(d_preds, d.dtype, V, R, V, G(lay->do_b)));
       SAT_CHECK((hipError_t)dgrad_launch(c, R, E, V, dpre, ldp, c.W(lay->do_w), E, w.dhd, E, s, nullptr, 0, 0, 0,
-                                         VP != V));
+                                         VP != V, &sws[1]));
     }
   }
   if (!(phase & 2)) return 0;
@@ -814,12 +831,12 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   // ---------------- recurrent BPTT (reverse time loop) ----------------
   // this phase's weight-gradient products (launched after the loop)
   const void* dg_t = c.at(w.dhg_t, E + D);   // d gates rows (ld HG)
-  SatGemm g_attw = wg(E, D, B * L, w.dWs_t, E, img_features, D, G(lay->attW_w), D);
-  SatGemm g_init = wg(2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D);
-  SatGemm g_hcat = att ? wg((int)HG, E, R, w.dhg_t, HG, w.h_in_t, E, G(lay->hcat_w), E)
-                       : wg(4 * E, E, R, dg_t, HG, w.h_in_t, E, G(lay->hcat_w + (long)(E + D) * E), E);
-  SatGemm g_wihx = wg(4 * E, E, R, dg_t, HG, w.emb_t, E, G(lay->wih), E + D);
-  SatGemm g_wihc = wg(4 * E, D, R, dg_t, HG, w.gated_t, D, G(lay->wih + E), E + D);
+  SatGemm g_attw = wgs(8, E, D, B * L, w.dWs_t, E, img_features, D, G(lay->attW_w), D);
+  SatGemm g_init = wgs(9, 2 * E, D, B, w.dpre0_t, 2 * E, w.mean_t, D, G(lay->init_w), D);
+  SatGemm g_hcat = att ? wgs(10, (int)HG, E, R, w.dhg_t, HG, w.h_in_t, E, G(lay->hcat_w), E)
+                       : wgs(10, 4 * E, E, R, dg_t, HG, w.h_in_t, E, G(lay->hcat_w + (long)(E + D) * E), E);
+  SatGemm g_wihx = wgs(11, 4 * E, E, R, dg_t, HG, w.emb_t, E, G(lay->wih), E + D);
+  SatGemm g_wihc = wgs(12, 4 * E, D, R, dg_t, HG, w.gated_t, D, G(lay->wih + E), E + D);
   {   // one launch zeroes the BPTT accumulators, the split attention backward's tickets, (beta = 0) the dense
       // embedding gradient the scatter-add after the loop accumulates into, and the atomic split-K targets
     SatZeroSeg seg[12];
@@ -830,15 +847,14 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
       seg[nz++] = SatZeroSeg{(float*)w.ticket, 1, B, B};
     }
     if (!d.bert && !accumulate) seg[nz++] = SatZeroSeg{G(lay->embedding), 1, (long)V * E, (long)V * E};
+    if (w.gtickets) seg[nz++] = tickets_ph2;
     SatGemm* gs[5] = {&g_hcat, &g_wihx, &g_wihc, &g_init, &g_attw};
     prezero(gs, att ? 5 : 4, seg, nz);
     SAT_CHECK((hipError_t)sat_zero_segs(seg, nz, s));
   }
   const StepIO io{img_features, const_cast<float*>(alphas), d_alphas};
-  const int fb = fused_bwd(d, sp, c.tr);
-  int cell_done = 0;   // step t's LSTM cell backward already ran inside step t+1's dh GEMM
   for (int t = T1 - 1; t >= 0; --t) {
-    if (!cell_done) {
+    {
       StepTimer st(d, 4, t);
       SAT_CHECK((hipError_t)bwd_lstm(c, w, sp, t, s));
     }
@@ -851,9 +867,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
       SAT_CHECK((hipError_t)bwd_attn(c, w, sp, io, t, s));
     }
     StepTimer st(d, 7, t);
-    cell_done = 0;
-    if (fb && t > 0) SAT_CHECK((hipError_t)bwd_dhgemm_lstm(c, w, sp, t, s, &cell_done));
-    if (!cell_done) SAT_CHECK((hipError_t)bwd_dhgemm(c, w, sp, t, s));
+    SAT_CHECK((hipError_t)bwd_dhgemm(c, w, sp, t, s));
   }
 
   // ---------------- weight gradients, batched over all B*(T-1) rows ----------------
@@ -885,7 +899,8 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   SAT_CHECK((hipError_t)sat_gemm_launch(g_wihx, s));
   SAT_CHECK((hipError_t)sat_gemm_launch(g_wihc, s));
   if (!d.bert) {  // dense embedding gradient (zeroed before the loop), scatter-added by fed token (decoder.py:87,133)
-    SAT_CHECK((hipError_t)dgrad(R, E, 4 * E, dg_t, HG, c.W(lay->wih), E + D, w.demb, E, d.ado ? w.dcomb : nullptr, E));
+    SAT_CHECK((hipError_t)dgrad(13, R, E, 4 * E, dg_t, HG, c.W(lay->wih), E + D, w.demb, E, d.ado ? w.dcomb : nullptr,
+                                E));
     SAT_CHECK((hipError_t)sat_embed_scatter_add(w.demb, w.tok, R, E, G(lay->embedding), s));
   }
   return 0;
@@ -914,7 +929,6 @@ extern "C" int sat_decoder_step_bench(const SatDecoderDims* dp, const SatDecoder
   Ctx c{d, *lay, params, params_lp, d.dtype == SAT_BF16 ? 2 : 4, d.T - 1, (long)d.B * (d.T - 1), 5L * d.E + d.D,
         use_transposed(d, *lay)};
   const Splits sp = splits_for(d, c.tr);
-  const int ff = fused_fwd(d, sp), fb = fused_bwd(d, sp, c.tr);
   const StepIO io{img_features, alphas, d_alphas};
   const int t = (d.T - 1) / 2;
   hipEvent_t e0, e1;
@@ -924,23 +938,17 @@ extern "C" int sat_decoder_step_bench(const SatDecoderDims* dp, const SatDecoder
   for (int k = 0; k < 8 && rc == 0; ++k) {
     us_out[k] = 0.f;
     if (!d.attention && (k == 1 || k == 2 || k == 5 || k == 6)) continue;
-    if ((ff && k == 3) || (fb && k == 4)) continue;   // the cell runs inside the context / dh GEMM (groups 2 / 7)
     for (int r = -1; r < reps && rc == 0; ++r) {   // r = -1: warm-up launch
       if (r == 0) rc = (int)hipEventRecord(e0, s);
-      int done = 0;
       switch (k) {
         case 0: rc = fwd_hgemm(c, w, sp, t, s); break;
         case 1: rc = fwd_attn(c, w, sp, io, t, s); break;
-        case 2: rc = ff ? fwd_cgemm_lstm(c, w, sp, t, s, &done) : 0;
-                if (rc == 0 && !done) rc = fwd_cgemm(c, w, sp, t, s);
-                break;
+        case 2: rc = fwd_cgemm(c, w, sp, t, s); break;
         case 3: rc = fwd_lstm(c, w, sp, t, s); break;
         case 4: rc = bwd_lstm(c, w, sp, t, s); break;
         case 5: rc = bwd_ggemm(c, w, sp, t, s); break;
         case 6: rc = bwd_attn(c, w, sp, io, t, s); break;
-        default: rc = fb ? bwd_dhgemm_lstm(c, w, sp, t, s, &done) : 0;
-                 if (rc == 0 && !done) rc = bwd_dhgemm(c, w, sp, t, s);
-                 break;
+        default: rc = bwd_dhgemm(c, w, sp, t, s); break;
       }
     }
     if (rc == 0) rc = (int)hipEventRecord(e1, s);

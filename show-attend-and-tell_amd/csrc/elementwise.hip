@@ -396,7 +396,8 @@ __global__ void zero_multi_kernel(ZeroMultiArgs a) {
   for (int k = 0; k < a.n; ++k) {
     float* p = a.p[k];
     const long R = a.rows[k], C = a.cols[k], ld = a.ld[k];
-    if (((uintptr_t)p & 15) == 0 && C % 4 == 0 && ld % 4 == 0) {
+    // 16-B write-through stores while the segment's byte extent fits the buffer resource (< 2 GiB)
+    if (((uintptr_t)p & 15) == 0 && C % 4 == 0 && ld % 4 == 0 && 4 * ((R - 1) * ld + C) < (1L << 31)) {
       const long c4 = C >> 2, n4 = R * c4;
       // write-through zeros (sat_common.h): megabytes of gradient accumulators that would otherwise sit dirty in
       // the L2s while the encoder's kernel boundaries run beside this graph
@@ -803,8 +804,14 @@ extern "C" int sat_adam_step(float* param, const float* grad, float* exp_avg, fl
                              int64_t n, float beta1, float beta2, float eps, float step_size,
                              float bias_correction2_sqrt, void* stream) {
   SAT_REQUIRE(param && grad && exp_avg && exp_avg_sq && n >= 0);
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
-                     exp_avg_sq, (bf16*)param_lp, (long)n, beta1, beta2, eps, step_size, bias_correction2_sqrt);
-  return (int)hipGetLastError();
+  // chunks of at most 2^28 elements: the kernel's buffer resources (sat_out_rsrc) take 32-bit byte offsets
+  constexpr int64_t kChunk = 1L << 28;
+  for (int64_t i = 0; i < n; i += kChunk) {
+    const int64_t m = n - i < kChunk ? n - i : kChunk;
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for((m + 3) / 4)), dim3(256), 0, (hipStream_t)stream, param + i, grad + i,
+                       exp_avg + i, exp_avg_sq + i, param_lp ? (bf16*)param_lp + i : nullptr, (long)m, beta1, beta2,
+                       eps, step_size, bias_correction2_sqrt);
+    SAT_LAUNCH_CHECK();
+  }
+  return 0;
 }

@@ -359,8 +359,7 @@ int sat_gemm_launch(const SatGemm& g, hipStream_t s) {
     if (sat_conv3x3_ws_try(g, s, &err)) return err;
     if (sat_conv_stream_try(g, s, &err)) return err;
     if (sat_conv_pipe_try(g, s, &err)) return err;
-    if (sat_gemm_lib_try(g, s, &err)) return err;
-    if (sat_gemm_pipe_try(g, s, &err)) return err;
+    if (sat_split_gemm_try(g, s, &err)) return err;
     if (sat_fast_gemm_try(g, s, &err)) return err;
   }
   const int vec = g.dtype == SAT_BF16 ? 8 : 4;
@@ -446,10 +445,18 @@ SatStampScope::~SatStampScope() {
 SatPolicyScope::SatPolicyScope(const SatPolicy* p) : prev(t_policy) { t_policy = p; }
 SatPolicyScope::~SatPolicyScope() { t_policy = prev; }
 
+extern "C" size_t sat_gemm_workspace_bytes(void) { return sat_split_gemm_ws_bytes(); }
+
 extern "C" int sat_gemm(const SatGemmArgs* a, void* stream) {
   SAT_REQUIRE(a != nullptr);
   SatPolicyScope scope(a->policy);
   SatGemm g;
+  if (a->workspace && a->workspace_bytes >= (int64_t)sat_split_gemm_ws_bytes()) {
+    // [partial tiles | tickets]: the tickets are zeroed by the split launch itself (tickets_zeroed = 0)
+    g.split_ws = (float*)a->workspace;
+    g.split_ws_bytes = (long)(sat_split_gemm_ws_bytes() - kSatSplitTickets * 4);
+    g.split_tickets = (unsigned*)((char*)a->workspace + g.split_ws_bytes);
+  }
   g.M = a->M; g.N = a->N; g.K = a->K; g.dtype = a->dtype;
   g.A = a->A; g.lda = a->lda; g.transA = a->transA;
   g.B = a->B; g.ldb = a->ldb; g.transB = a->transB;

@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const TT* __restrict__ pr
   };
   constexpr int VEC = 16 / sizeof(TT);
   if (V % VEC == 0) {
-    const __amdgpu_buffer_rsrc_t rdx = sat_out_rsrc(dpreds, (long)sizeof(TT) * gridDim.x * V);
+    const __amdgpu_buffer_rsrc_t rdx = sat_out_rsrc(dx, (long)sizeof(TT) * V);   // this row: offsets < 2 GiB
     constexpr int LU = 4;   // vectors per thread in flight
     const int NV = V / VEC;
     for (int c0 = threadIdx.x; c0 < NV; c0 += LU * 256) {
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const TT* __restrict__ pr
         TT* q = (TT*)&o;
 #pragma unroll
         for (int j = 0; j < VEC; ++j) q[j] = (TT)grad((float)h[j], c * VEC + j);
-        sat_st16(rdx, (unsigned)(((long)r * V + (long)c * VEC) * sizeof(TT)), o);   // write-through (sat_common.h)
+        sat_st16(rdx, (unsigned)((long)c * VEC * sizeof(TT)), o);   // write-through (sat_common.h)
       }
     }
   } else {

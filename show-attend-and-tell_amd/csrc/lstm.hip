@@ -260,12 +260,11 @@ __global__ void row_sum_acc_kernel(const float* X, int R, int N, float* out) {
     else hipLaunchKernelGGL(KERNEL<float>, grid, dim3(256), 0, s, __VA_ARGS__);               \
   } while (0)
 
-// blocks of 64 units (256 threads) for B x E units: one per 64 units, capped at 4096 or at SatPolicy::lstm_blocks
-// (A/B: fewer resident waves beside a concurrent encoder; the kernels stride over the rest)
+// blocks of 64 units (256 threads) for B x E units: one per 64 units, capped at 4096 (the kernels stride over the
+// rest)
 inline long lstm_blocks(int B, int E) {
-  long blocks = ((long)B * E + 63) / 64;
-  const int cap = sat_policy().lstm_blocks > 0 ? sat_policy().lstm_blocks : 4096;
-  return blocks > cap ? cap : blocks;
+  const long blocks = ((long)B * E + 63) / 64;
+  return blocks > 4096 ? 4096 : blocks;
 }
 int sat_lstm_fwd_launch(const LstmFwdArgs& args, hipStream_t s) {
   LstmFwdArgs a = args;

@@ -175,17 +175,23 @@ struct SatGemm {
   int a_tail = 0;
   // beta = 0 and the caller has already zeroed C: an atomic split-K launch skips its own zeroing pass
   int c_zeroed = 0;
+  // deterministic split-K of the fp32-output k-major products (gemmsplit.hip): partial tiles and one arrival
+  // ticket per output tile; tickets_zeroed: the caller zeroed the tickets (else the launch does)
+  float* split_ws = nullptr; long split_ws_bytes = 0;
+  unsigned* split_tickets = nullptr;
+  int tickets_zeroed = 0;
 };
 
 int sat_gemm_launch(const SatGemm& g, hipStream_t s);
 // bf16 NT fast path (convgemm.hip); returns 1 when it launched (error code in *err).
 int sat_fast_gemm_try(const SatGemm& g, hipStream_t s, int* err);
-// 256x128 pipelined bf16 GEMM with fp32 output and k-major operands (gemmpipe.hip: the decoder's weight / input
-// gradients); returns 1 when it launched.  sat_gemm_pipe_atomic: it would run g as fp32 atomics into a zeroed C.
-int sat_gemm_pipe_try(const SatGemm& g, hipStream_t s, int* err);
-int sat_gemm_pipe_atomic(const SatGemm& g);
-// the same products on hipBLASLt (gemmlib.hip, SatPolicy::gemm_lib); returns 1 when it launched.
-int sat_gemm_lib_try(const SatGemm& g, hipStream_t s, int* err);
+// pipelined bf16 GEMM with fp32 output, a k-major operand and deterministic split-K (gemmsplit.hip: the decoder's
+// batched weight / input gradients); returns 1 when it launched.  sat_split_gemm_takes: it would take g;
+// sat_split_gemm_ws_bytes: the workspace (partial tiles + tickets) its largest split needs.
+int sat_split_gemm_try(const SatGemm& g, hipStream_t s, int* err);
+int sat_split_gemm_takes(const SatGemm& g);
+size_t sat_split_gemm_ws_bytes();
+constexpr size_t kSatSplitTickets = 256;   // tickets one split launch may use
 // 256x128 pipelined bf16 conv / NT GEMM (convpipe.hip); returns 1 when it launched.
 int sat_conv_pipe_try(const SatGemm& g, hipStream_t s, int* err);
 // weight-stationary streaming kernel for K <= 512 1x1 convs (convstream.hip); returns 1 when it launched.

@@ -173,9 +173,8 @@ __device__ __forceinline__ float4 sum_parts4(const float* p, long idx, int n, lo
   return f4add(f4add(a0, a1), f4add(a2, a3));
 }
 
-// ---- LSTM cell arithmetic (nn.LSTMCell, gate order i, f, g, o; decoder.py:115), shared by the separate pointwise
-// kernels (lstm.hip) and the GEMMs that fold them into their split-K reduction (skinny.hip): one expression each,
-// so both forms round identically ----
+// ---- LSTM cell arithmetic (nn.LSTMCell, gate order i, f, g, o; decoder.py:115) of the pointwise kernels
+// (lstm.hip) ----
 __device__ __forceinline__ void lstm_cell_fwd(float gi, float gf, float gg, float go, float c_prev, float& c, float& h) {
   const float ig = 1.f / (1.f + expf(-gi));
   const float fg = 1.f / (1.f + expf(-gf));
@@ -200,14 +199,3 @@ __device__ __forceinline__ void lstm_cell_bwd(float gi, float gf, float gg, floa
   dq[3] = dh * tc * og * (1.f - og);
   dc_out = dc * fg;
 }
-
-// the LSTM cell in the epilogue of a full-K row-block GEMM (lstmgemm.hip): the forward step's context GEMM
-// (A = gated context [B][K], W = W_ih[:, E:] rows [4E][ldw]) and BPTT step t's recurrent dL/dh GEMM (A = [dU h |
-// d f_beta h | d gates] [B][K], W = hcat^T [E][ldw]) carrying step t-1's cell backward.  *_ok: the shape and the policy
-// allow it; *_try: 1 when launched (error in *err), 0 when not eligible (the caller runs the separate launches).
-int sat_lstm_gemm_fwd_ok(int B, int E, int K);
-int sat_lstm_gemm_bwd_ok(int B, int E, int K);
-int sat_lstm_gemm_fwd_try(const void* A, long lda, const void* W, long ldw, int K, const LstmFwdArgs& l, hipStream_t s,
-                          int* err);
-int sat_lstm_gemm_bwd_try(const void* A, long lda, const void* W, long ldw, int K, const LstmBwdArgs& l, hipStream_t s,
-                          int* err);

@@ -170,7 +170,9 @@ bool skinny_shape(const SatGemm& g, int mode, SkArgs* a, int* nw) {
 }
 
 bool skinny_ptrs(const SatGemm& g) {
-  return al16(g.A) && al16(g.B) && al16(g.C) && (!g.bias || al16(g.bias));
+  // + the slab stores' buffer resource takes 32-bit offsets (sat_out_rsrc's 2 GiB cap)
+  return al16(g.A) && al16(g.B) && al16(g.C) && (!g.bias || al16(g.bias)) &&
+         4L * ((long)(g.M - 1) * g.ldc + g.N) < (1L << 31);
 }
 
 template <int MB>

@@ -29,10 +29,26 @@ def linear(x, weight, bias=None, act=L.ACT_NONE, out_dtype=None, weight_lp=None)
     return y
 
 
+_GEMM_WS = {}
+
+
+def gemm_workspace(device, stream):
+    """The split-K workspace sat_gemm may use (include/sat_hip.h SatGemmArgs.workspace), one per device and stream:
+    calls ordered on one stream share it."""
+    key = (torch.device(device).index, int(stream))
+    ws = _GEMM_WS.get(key)
+    if ws is None:
+        ws = torch.empty(int(L.lib().sat_gemm_workspace_bytes()), dtype=torch.uint8, device=device)
+        _GEMM_WS[key] = ws
+    return ws
+
+
 def gemm(A, B, C, *, transA=False, transB=False, alpha=1.0, beta=0.0, bias=None, add1=None, act=L.ACT_NONE,
-         aux=None, policy=None):
+         aux=None, policy=None, workspace=True):
     """C = act(alpha * A' B'^T + bias + add1 + beta*C) with A' = A or A^T, B'(n,k) = B[n,k] or B[k,n].
-    ``policy``: an optional ``sat_amd.Policy`` (per-call kernel selection; None = library defaults)."""
+    ``policy``: an optional ``sat_amd.Policy`` (per-call kernel selection; None = library defaults).
+    ``workspace``: True = this stream's cached split-K workspace (``gemm_workspace``), a uint8 device tensor, or
+    None (products with fp32 output and a k-major operand then run unsplit)."""
     L.require_device(A, B, C)
     dt = L.dtype_code(A.dtype)
     if B.dtype != A.dtype:
@@ -59,7 +75,12 @@ def gemm(A, B, C, *, transA=False, transB=False, alpha=1.0, beta=0.0, bias=None,
     if aux is not None:
         a.aux, a.ld_aux, a.aux_dtype = aux.data_ptr(), aux.stride(0), L.dtype_code(aux.dtype)
     a.policy = L.policy_ptr(policy)
-    L.check(L.lib().sat_gemm(ctypes.byref(a), L.stream_of(C)), "sat_gemm")
+    stream = L.stream_of(C)
+    if workspace is True:
+        workspace = gemm_workspace(C.device, stream)
+    if workspace is not None:
+        a.workspace, a.workspace_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+    L.check(L.lib().sat_gemm(ctypes.byref(a), stream), "sat_gemm")
     return C
 
 

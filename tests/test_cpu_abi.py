@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol():
     lib = sat_amd._lib.lib()
     missing = [f for f in declared_functions() if not hasattr(lib, f)]
     assert not missing, missing
-    assert lib.sat_abi_version() == sat_amd._lib.ABI_VERSION == header_abi_version() == 6
+    assert lib.sat_abi_version() == sat_amd._lib.ABI_VERSION == header_abi_version() == 7
     assert set(declared_functions()) == set(sat_amd._lib.EXPORTED)
 
 
@@ -54,7 +54,7 @@ def test_library_refuses_other_abi_version(monkeypatch):
     with pytest.raises(RuntimeError, match="C-ABI version"):
         L.lib()
     monkeypatch.undo()
-    assert L.lib().sat_abi_version() == 6
+    assert L.lib().sat_abi_version() == 7
 
 
 def test_error_strings():
@@ -80,7 +80,8 @@ int main(void) {
   P(SatGemmArgs, B) P(SatGemmArgs, C) P(SatGemmArgs, alpha) P(SatGemmArgs, bias) P(SatGemmArgs, add1)
   P(SatGemmArgs, act) P(SatGemmArgs, aux) P(SatGemmArgs, aux_dtype) P(SatGemmArgs, policy)
   P(SatDecoderDims, dtype) P(SatDecoderDims, seed) P(SatDecoderDims, seed_ptr) P(SatDecoderDims, split_target)
-  P(SatDecoderDims, policy) P(SatPolicy, attn_bwd) P(SatPolicy, decoder_splits) P(SatPolicy, fused_lstm) P(SatPolicy, gemm_pipe) P(SatPolicy, gemm_lib)
+  P(SatDecoderDims, policy) P(SatPolicy, attn_bwd) P(SatPolicy, decoder_splits) P(SatPolicy, split_gemm) P(SatPolicy, split_k) P(SatPolicy, stamps)
+  P(SatPolicy, stamp_capacity) P(SatGemmArgs, workspace) P(SatGemmArgs, workspace_bytes)
   P(SatDecoderLayout, do_b) P(SatDecoderLayout, total)
   return 0;
 }

@@ -34,6 +34,8 @@ SHAPES = {
     # name: (D, L, E, V, T, tf, ado, bert)
     "resnet_ado_tf": (2048, 49, 512, 10000, 8, True, True, False),
     "vgg_bert_simple": (512, 196, 768, 30522, 8, True, False, True),
+    # cfg5 at the BERT caption length: T = 32, [CLS] w.. [PAD].. [SEP] (generate_json_data_bert.py:44-47)
+    "vgg_bert_t32": (512, 196, 768, 30522, 32, True, False, True),
     "vgg_ado_greedy": (512, 196, 512, 2600, 8, False, True, False),
 }
 B = 4
@@ -106,15 +108,15 @@ def _oracle_fed(c, fed, dtype):
 
 
 def _instance(sat, dec, feats, caps):
-    """sat_decoder_instance of this forward (include/sat_hip.h: splits, attention-backward chunks, fused cells,
-    launches per step)."""
+    """sat_decoder_instance of this forward (include/sat_hip.h: splits, attention-backward chunks, launches per
+    step)."""
     import ctypes
     L = sat._lib
-    out = (ctypes.c_int * 10)()
-    L.check(L.lib().sat_decoder_instance(ctypes.byref(dec._dims(feats, caps)), ctypes.byref(dec._layout()), out, 10),
+    out = (ctypes.c_int * 8)()
+    L.check(L.lib().sat_decoder_instance(ctypes.byref(dec._dims(feats, caps)), ctypes.byref(dec._layout()), out, 8),
             "sat_decoder_instance")
-    keys = ("h_splits", "ctx_splits", "dgated_splits", "dh_splits", "attn_bwd_chunks", "transposed", "fused_lstm_fwd",
-            "fused_lstm_bwd", "fwd_launches_per_step", "bwd_launches_per_step")
+    keys = ("h_splits", "ctx_splits", "dgated_splits", "dh_splits", "attn_bwd_chunks", "transposed",
+            "fwd_launches_per_step", "bwd_launches_per_step")
     return dict(zip(keys, list(out)))
 
 
@@ -161,9 +163,12 @@ def test_production_shape_fp32_matches_oracle(sat, name):
     _assert_fp32(c, _hip_step(sat, c, torch.float32), _oracle(c, torch.float32), _oracle(c, torch.float64))
 
 
-def _assert_fp32(c, h, o32, o64):
+def _assert_fp32(c, h, o32, o64, elem_tol=1e-3, sure_frac=1e-4):
     """fp32 HIP step vs the oracle: preds / alphas / loss 1e-4, greedy ids bit-exact up to the first rounding-
-    ambiguous step, gradients by the fp64 noise gauge, fused Adam exact, post-Adam weights at lr scale."""
+    ambiguous step, gradients by the fp64 noise gauge, fused Adam exact, post-Adam weights at lr scale.
+    elem_tol: elementwise gradient bound as a fraction of max|g|; sure_frac: post-Adam weights are compared where
+    |g| > sure_frac max|g| (the B = 4 shapes keep 1e-3 / 1e-4; the bench instances' K = B (T-1) = 3,328-term
+    weight-gradient sums take 2e-3 / 1e-3, see test_bench_instance_fp32_matches_oracle)."""
     loss32, g32, w32, preds32, alphas32 = o32
     _, g64, w64, _, _ = o64
     if c["tf"]:
@@ -209,10 +214,7 @@ def _assert_fp32(c, h, o32, o64):
         noise_elem = (r64 - ref).abs().max().item()
         assert abs(gr.norm().item() - ref_norm) <= max(2e-4, 2 * noise_norm) * ref_norm, n
         err = (gr - ref).abs().max().item()
-        # elementwise: 2e-3 of max|g| -- a weight-gradient element sums K = B (T-1) products (3,328 at the bench
-        # instance) whose magnitudes exceed the sum, so blocked fp32 accumulation in another order differs from the
-        # CPU's at that level (the norm check above stays at 2e-4)
-        assert err <= max(2e-3 * gr.abs().max().item(), 2 * noise_elem) + 1e-9, n
+        assert err <= max(elem_tol * gr.abs().max().item(), 2 * noise_elem) + 1e-9, n
     # Adam's first step moves a weight by lr * g / (|g| + eps): where |g| is within a few eps of zero
     # that ratio amplifies any rounding-level gradient difference.  So (a) the fused Adam arithmetic
     # is checked on the HIP gradients themselves, every element, and (b) the weights are compared with
@@ -225,8 +227,8 @@ def _assert_fp32(c, h, o32, o64):
             continue
         noise = (w64[n].double() - w32[n].double()).abs().max().item()
         # the first Adam step lr * g / (|g| + eps) resolves a gradient's rounding where |g| is within ~100 eps (1e-8):
-        # compare where |g| > 1e-3 max|g| and > 1e-6
-        sure = (g32[n].abs() > 1e-3 * g32[n].abs().max()) & (g32[n].abs() > 1e-6)
+        # compare where |g| > sure_frac max|g| and > 1e-6
+        sure = (g32[n].abs() > sure_frac * g32[n].abs().max()) & (g32[n].abs() > 1e-6)
         assert (w.double() - w32[n].double())[sure].abs().max().item() <= max(2e-3 * LR + 1e-6, 2 * noise), n
 
 
@@ -237,19 +239,26 @@ def test_production_shape_bf16_close_to_oracle(sat, name):
     _assert_bf16(c, _hip_step(sat, c, torch.bfloat16), _oracle(c, torch.float32))
 
 
-def _assert_bf16(c, h, o32):
+def _grad_errors(h, ref_grads):
+    """relative gradient error norm per parameter (the non-vanishing ones)"""
+    return {n: ((gr - ref_grads[n]).norm() / ref_grads[n].norm()).item() for n, gr in h["grads"].items()
+            if ref_grads[n].norm().item() >= 1e-7}
+
+
+def _assert_bf16(c, h, o32, grad_tol=5e-2):
+    """bf16 HIP step vs the fp32 oracle: preds / alphas 3e-2, loss 1e-2, gradients grad_tol of the norm (5e-2 at the
+    B = 4 shapes; the bench instances pass their own, measured bounds)."""
     loss32, g32, _, preds32, alphas32 = o32
     if c["tf"]:
         assert rel(h["preds"], preds32) < 3e-2
         assert rel(h["alphas"], alphas32) < 3e-2
         assert abs(h["loss"] - loss32.item()) <= 1e-2 * abs(loss32.item())
         for n, gr in h["grads"].items():
-            ref = g32[n]
-            if ref.norm().item() < 1e-7:
-                continue
             assert torch.isfinite(gr).all(), n
-            # the initial-state weights see the gradient after all T-1 bf16 BPTT steps: 8e-2
-            assert ((gr - ref).norm() / ref.norm()).item() < 8e-2, n
+        errs = _grad_errors(h, g32)
+        print("bf16 gradient errors vs fp32 oracle:", {n: round(e, 4) for n, e in errs.items()})
+        for n, e in errs.items():
+            assert e < (grad_tol[n] if isinstance(grad_tol, dict) else grad_tol), (n, e)
     else:
         tol = 1.5e-2 * preds32.abs().max().item()
         stops = _greedy_prefix(preds32, tol)
@@ -268,17 +277,17 @@ def _assert_bf16(c, h, o32):
         assert sorted(h["grads"]) == sorted(g_f)
         for n, gr in h["grads"].items():
             assert torch.isfinite(gr).all(), n
-            ref = g_f[n]
-            if ref.norm().item() < 1e-7:
-                continue
-            assert ((gr - ref).norm() / ref.norm()).item() < 8e-2, n
+        errs = _grad_errors(h, g_f)
+        print("bf16 gradient errors vs fed-token fp32 oracle:", {n: round(e, 4) for n, e in errs.items()})
+        for n, e in errs.items():
+            assert e < (grad_tol[n] if isinstance(grad_tol, dict) else grad_tol), (n, e)
 
 
 # bench.py's own decoder instances (bench.py main(): split target 96 at B = 128, 64 at B <= 64) at the ResNet152 /
 # COCO shape and the full caption length (D 2048, L 49, E 512, V 10000, T 27, --ado): the attention backward runs one
-# workgroup per batch row (no last-arriver combine), the skinny GEMMs on 8 / 4 row blocks and, in bf16, the LSTM
-# cells inside the context / dh GEMMs' split-K reductions -- instances the B = 4 cases above never reach.  cfg4's
-# per-rank greedy shape (B = 64, --tf off) runs the per-step head and argmax feedback beside them.
+# workgroup per batch row (no last-arriver combine), the skinny GEMMs on 8 / 4 row blocks and, in bf16, the batched
+# weight / input gradients on the split-K kernel (gemmsplit.hip) -- instances the B = 4 cases above never reach.
+# cfg4's per-rank greedy shape (B = 64, --tf off) runs the per-step head and argmax feedback beside them.
 BENCH_CASES = {
     # name: (B, tf, split_target)
     "b128_tf_st96": (128, True, 96),
@@ -302,12 +311,11 @@ def _bench_oracle(name, c, dtype):
     return _ORACLE_CACHE[key]
 
 
-def _assert_bench_instance(inst, dtype, fused=False):
+def _assert_bench_instance(inst, dtype):
     assert inst["attn_bwd_chunks"] == 1, inst          # one workgroup per row, as bench.py runs it
+    assert inst["fwd_launches_per_step"] == 4 and inst["bwd_launches_per_step"] == 4, inst
     if dtype == torch.bfloat16:
-        fused = 1 if fused else 0                      # lstmgemm.hip's row-block cells only with SatPolicy.fused_lstm >= 2
-        assert inst["transposed"] == 1 and inst["fused_lstm_fwd"] == fused and inst["fused_lstm_bwd"] == fused, inst
-        assert inst["fwd_launches_per_step"] == 4 - fused and inst["bwd_launches_per_step"] == 4 - fused, inst
+        assert inst["transposed"] == 1, inst
 
 
 @pytest.mark.parametrize("name", list(BENCH_CASES))
@@ -315,41 +323,43 @@ def test_bench_instance_fp32_matches_oracle(sat, name):
     c = _bench_case(name)
     h = _hip_step(sat, c, torch.float32, split_target=c["split_target"])
     _assert_bench_instance(h["instance"], torch.float32)
-    _assert_fp32(c, h, _bench_oracle(name, c, torch.float32), _bench_oracle(name, c, torch.float64))
+    # elementwise 2e-3 of max|g|: a weight-gradient element sums K = B (T-1) = 3,328 products whose magnitudes exceed
+    # the sum, so blocked fp32 accumulation in another order differs from the CPU's at that level (the norm check
+    # stays at 2e-4); post-Adam weights where |g| > 1e-3 max|g|
+    _assert_fp32(c, h, _bench_oracle(name, c, torch.float32), _bench_oracle(name, c, torch.float64),
+                 elem_tol=2e-3, sure_frac=1e-3)
 
 
-@pytest.mark.parametrize("cells", ["fused", "separate"])
+# bf16 gradient bounds of the bench instances, relative error norm against the fp32 oracle: 3e-2 for every weight
+# except init_h / init_c, which see the gradient after all 26 bf16 BPTT steps (and 5e-2 there)
+BENCH_BF16_GRAD_TOL = 3e-2
+BENCH_BF16_INIT_TOL = 5e-2
+
+
 @pytest.mark.parametrize("name", list(BENCH_CASES))
-def test_bench_instance_bf16_close_to_oracle(sat, name, cells):
-    """bf16 bench instance against the fp32 oracle, with the LSTM cells as separate lstm_fwd / lstm_bwd launches
-    (the default) and in the context / dh GEMM epilogues (lstmgemm.hip, SatPolicy.fused_lstm = 2: three launches
-    per time step each way)."""
+def test_bench_instance_bf16_close_to_oracle(sat, name):
+    """bf16 bench instance (the default kernels bench.py runs) against the fp32 oracle."""
     c = _bench_case(name)
-    pol = sat.Policy(fused_lstm=2) if cells == "fused" else None
-    h = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"], policy=pol)
-    _assert_bench_instance(h["instance"], torch.bfloat16, fused=cells == "fused")
-    _assert_bf16(c, h, _bench_oracle(name, c, torch.float32))
+    h = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"])
+    _assert_bench_instance(h["instance"], torch.bfloat16)
+    tol = {n: (BENCH_BF16_INIT_TOL if n.startswith("init_") else BENCH_BF16_GRAD_TOL) for n in h["grads"]}
+    _assert_bf16(c, h, _bench_oracle(name, c, torch.float32), grad_tol=tol)
 
 
-@pytest.mark.parametrize("form", [2, 3, 4, 5])   # both directions (8 / 4 waves), backward only, forward only
-def test_fused_lstm_cells_close_to_separate(sat, form):
-    """Row-block fused cells (eight- and four-wave forms) against the separate launches on the teacher-forced bench
-    instance: the context GEMM sums its K in another order (wave partials of a full-K tile against split-K slabs),
-    so the two agree to fp32 rounding of the gates carried through bf16 h casts -- not bit for bit."""
-    c = _bench_case("b128_tf_st96")
-    a = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"], policy=sat.Policy(fused_lstm=form))
+def test_bench_instance_bf16_gradients_deterministic(sat):
+    """Two bf16 steps from the same state produce bit-identical gradients: every split-K reduction of the step
+    (the per-step partial slabs, the batched products' last-arriver sums in split order) has a fixed order.  The
+    one exception is the dense embedding gradient, whose rows of repeated tokens meet in fp32 atomics
+    (embed_scatter_kernel, the order-dependent index_add of decoder.py:87's nn.Embedding backward)."""
+    c = _bench_case("b64_tf_st64")
+    a = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"])
     b = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"])
-    assert a["instance"]["fwd_launches_per_step"] == (4 if form == 4 else 3)
-    assert a["instance"]["bwd_launches_per_step"] == (4 if form == 5 else 3)
-    assert b["instance"]["fwd_launches_per_step"] == 4 and b["instance"]["bwd_launches_per_step"] == 4
-    assert ((a["preds"] - b["preds"]).norm() / b["preds"].norm()).item() < 1e-2
-    assert ((a["alphas"] - b["alphas"]).norm() / b["alphas"].norm()).item() < 1e-2
-    assert abs(a["loss"] - b["loss"]) < 1e-3 * abs(b["loss"])
+    assert torch.equal(a["preds"], b["preds"])
     for n in a["grads"]:
-        ga, gb = a["grads"][n], b["grads"][n]
-        if gb.norm().item() < 1e-7:
+        if n == "embedding.weight":
+            assert ((a["grads"][n] - b["grads"][n]).norm() / b["grads"][n].norm()).item() < 1e-6
             continue
-        assert ((ga - gb).norm() / gb.norm()).item() < 5e-2, n
+        assert torch.equal(a["grads"][n], b["grads"][n]), n
 
 
 def test_bleu_parity_at_eval_shape(sat):

@@ -19,6 +19,6 @@ for src in "$@"; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $flags -c "$src" -o "build/${b}_v_$name.o"
   objs="$objs build/${b}_v_$name.o"
 done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "../libsat_hip_$name.so" $objs -L/opt/rocm/lib -lhipblaslt \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "../libsat_hip_$name.so" $objs \
   -Wl,-rpath,/opt/rocm/lib
 echo "built show-attend-and-tell_amd/libsat_hip_$name.so"

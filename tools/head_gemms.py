@@ -2,11 +2,11 @@
 
 B = 128, T = 27 (R = B * 26 = 3328 rows), V = 10000, E = 512, D = 2048, L = 49, bf16 operands: the hoisted
 Ws = a W^T, the input / output head products of the forward, and the weight / input gradients of the backward
-(decoder.hip).  Each product is re-issued back to back between HIP events: the library default (hipBLASLt for the
-k-major fp32-output products, SatPolicy.gemm_lib), the hand-written tile kernel and the pipelined one (gemm_pipe);
-per tile configuration (SatPolicy.gemm_tile) when --tiles.
+(decoder.hip).  Each product is re-issued back to back between HIP events: the library default (the split-K kernel,
+gemmsplit.hip, for the fp32-output products with a k-major operand), the 128x128 tile kernel (SatPolicy.split_gemm
+= 1) and, with --forms, each split-K form (tile height x split count).
 
-    python tools/head_gemms.py [--tiles] [--reps 10]
+    python tools/head_gemms.py [--forms] [--reps 10] [--torch]
 """
 import argparse
 import os
@@ -40,6 +40,9 @@ SHAPES = [
     ("dW W_ih[:, E:]", 4 * E, D, R, True, True, torch.float32, 0.0),
     ("dX embedding", R, E, 4 * E, False, True, torch.float32, 0.0),
 ]
+# (label, split_gemm, split_k)
+FORMS = [("128x1", 2, 1), ("128x2", 2, 2), ("128x3", 2, 3), ("128x4", 2, 4), ("128x6", 2, 6), ("128x8", 2, 8),
+         ("256x1", 3, 1), ("256x2", 3, 2), ("256x3", 3, 3), ("256x4", 3, 4)]
 
 
 def operands(M, N, K, ta, tb, cdt):
@@ -66,14 +69,12 @@ def time_one(A, Bm, C, ta, tb, beta, policy, reps, act=0):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--tiles", action="store_true")
-    ap.add_argument("--split", action="store_true", help="also the atomic split-K aimed at other workgroup counts")
-    ap.add_argument("--split-wgs", default="256,512,1024", help="--split: the SatPolicy.gemm_split_wgs values")
+    ap.add_argument("--forms", action="store_true", help="every split-K form (tile height x splits) of the k-major products")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--torch", action="store_true",
                     help="calibration: torch.matmul (hipBLASLt) of the same bf16 operands, bf16 output")
     a = ap.parse_args()
-    tot_us = tot_f = tot_tile = tot_ws = 0.0
+    tot_us = tot_f = tot_tile = tot_lib = 0.0
     for name, M, N, K, ta, tb, cdt, beta, *rest in SHAPES:
         act = rest[0] if rest else 0
         A, Bm, C = operands(M, N, K, ta, tb, cdt)
@@ -81,21 +82,17 @@ def main():
         us = time_one(A, Bm, C, ta, tb, beta, None, a.reps, act)
         tot_us += us
         tot_f += f
-        us_tile = time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_lib=1), a.reps, act)
-        us_pipe = time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_lib=1, gemm_pipe=2), a.reps, act)
-        us_ws = time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_lib=3), a.reps, act)
-        tot_ws += us_ws
+        us_tile = time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(split_gemm=1), a.reps, act)
         tot_tile += us_tile
         line = f"{name:30s} M {M:5d} N {N:5d} K {K:5d} {'T' if ta else 'N'}{'T' if tb else 'N'}  {us:8.1f} us " \
-               f"{f / us / 1e6:7.1f} TF/s  [hand-written: tile {us_tile:.1f} us, pipe {us_pipe:.1f} us; library with a workspace " \
-               f"{us_ws:.1f} us]"
-        if a.tiles:
+               f"{f / us / 1e6:7.1f} TF/s  [tile kernel {us_tile:.1f} us]"
+        if a.forms and (ta or tb) and cdt == torch.float32:
             alt = []
-            for tile in (1, 2, 3, 4, 5):
+            for label, sg, sk in FORMS:
                 try:
-                    alt.append(f"t{tile}:{time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_tile=tile), a.reps, act):.1f}")
+                    alt.append(f"{label}:{time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(split_gemm=sg, split_k=sk), a.reps, act):.1f}")
                 except RuntimeError:
-                    alt.append(f"t{tile}:-")
+                    alt.append(f"{label}:-")
             line += "  [" + " ".join(alt) + "]"
         if a.torch:
             At = A.t() if ta else A          # [M, K] view
@@ -112,14 +109,13 @@ def main():
                 mm()
             en.record()
             en.synchronize()
-            line += f"  [hipBLASLt {st.elapsed_time(en) / a.reps * 1e3:.1f} us]"
-        if a.split:
-            alt = [f"w{wgs}:{time_one(A, Bm, C, ta, tb, beta, sat_amd.Policy(gemm_split_wgs=wgs), a.reps, act):.1f}"
-                   for wgs in [int(v) for v in a.split_wgs.replace("/", ",").split(",")]]
-            line += "  [" + " ".join(alt) + "]"
+            us_lib = st.elapsed_time(en) / a.reps * 1e3
+            tot_lib += us_lib
+            line += f"  [calibration, torch.matmul / hipBLASLt bf16 out: {us_lib:.1f} us]"
         print(line, flush=True)
     print(f"total {tot_us:.1f} us for {tot_f / 1e9:.1f} GFLOP = {tot_f / tot_us / 1e6:.1f} TF/s "
-          f"(hand-written tile kernels: {tot_tile:.1f} us; workspace {tot_ws:.1f} us)", flush=True)
+          f"(tile kernel for the k-major products: {tot_tile:.1f} us"
+          + (f"; torch.matmul calibration {tot_lib:.1f} us" if a.torch else "") + ")", flush=True)
 
 
 if __name__ == "__main__":

@@ -5,6 +5,7 @@
 # usage: bash tools/session.sh TAG step [step...]
 #   tests              the whole GPU suite (-m gpu)
 #   tests:EXPR         GPU tests selected by -k EXPR
+#   testsv:EXPR        the same with their output (-s), every selected test run
 #   smoke              __graft_entry__.smoke()
 #   bench              the default bench line (the driver's command)
 #   bench64            the B = 64 line (cfg2 / cfg3's per-rank shape), no CPU baseline / fp32 leg
@@ -55,6 +56,9 @@ for s in "$@"; do
     tests:*) run tests_$n 600 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 300 \
                --timeout-method thread -k "${s#tests:}"
            rc=$?; grep -E "^FAILED" "$OUT/tests_$n.log" | head -30; [ $rc -le 1 ] || exit $rc ;;
+    testsv:*) run testsv_$n 900 python -u -m pytest tests -m gpu -q -s -p no:cacheprovider --timeout 600 \
+               --timeout-method thread -k "${s#testsv:}"
+           rc=$?; grep -E "^FAILED|gradient errors" "$OUT/testsv_$n.log" | head -40; [ $rc -le 1 ] || exit $rc ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench) run bench 400 python bench.py || exit $? ;;
     bench64) run bench64 300 python bench.py --batch 64 $QUIET || exit $? ;;
