@@ -8,7 +8,9 @@ One step = encoder fwd + decoder fwd + fused loss + decoder bwd + RCCL grad
 all-reduce (N>1) + Adam, inputs resident in HBM before the timed region.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
-      (N>1 via: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+      N > 1: this process starts the N rank processes itself (torch.distributed.run, one rank per GPU, before
+      anything touches a GPU) and exits with their status; launched by torch.distributed.run directly it is one
+      of the ranks (WORLD_SIZE set) and checks that WORLD_SIZE == --gpus.
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -612,9 +614,48 @@ def fp32_step(args, enc, dec, imgs, caps, pad_id, skip_ids, world):
             "note": "exact-parity path (fp32 MFMA), eager, rank 0 only; not the headline value"}
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def rank_launch_command(argv, nproc, port):
+    """The command that runs this benchmark as `nproc` ranks on one node (one process per GPU over RCCL, or
+    several per GPU with --dist-backend gloo): torch.distributed.run with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 outside a torch.distributed.run rank: start the N ranks as a child process and return its exit
+    status.  This process never touches the GPU (no HIP call before or after), so the ranks own the devices."""
+    import subprocess
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(rank_launch_command(argv, args.gpus, free_port()), env=env).returncode
+
+
+def dist_info(args, world):
+    """the process group the step all-reduces over (N > 1) and the collective library's version"""
+    if world == 1:
+        return {"backend": None, "world_size": 1}
+    info = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
+    if info["backend"] == "nccl":   # "nccl" is RCCL on ROCm
+        try:
+            info["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
+        except Exception as e:   # noqa: BLE001 -- informational field
+            info["rccl_version"] = f"unavailable ({type(e).__name__})"
+    return info
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per GPU; --dist-backend gloo rehearses the N > 1 path with several ranks on one GPU
@@ -626,6 +667,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     import sat_amd
@@ -924,6 +966,7 @@ def main():
             "value": round(B * world * args.steps / elapsed, 2),
             "unit": "images/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "dist": dist_info(args, world),
             "ms_per_step": round(1000 * elapsed / args.steps, 3),
             "timing": ("host wall clock (perf_counter) around exactly `steps` pipelined train steps, bracketed by a "
                        "barrier + device synchronize on both sides, max over ranks; a step's encoder runs beside "

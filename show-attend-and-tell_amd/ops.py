@@ -35,7 +35,7 @@ _GEMM_WS = {}
 def gemm_workspace(device, stream):
     """The split-K workspace sat_gemm may use (include/sat_hip.h SatGemmArgs.workspace), one per device and stream:
     calls ordered on one stream share it."""
-    key = (torch.device(device).index, int(stream))
+    key = (torch.device(device).index, stream.value or 0)
     ws = _GEMM_WS.get(key)
     if ws is None:
         ws = torch.empty(int(L.lib().sat_gemm_workspace_bytes()), dtype=torch.uint8, device=device)

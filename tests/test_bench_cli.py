@@ -87,3 +87,49 @@ def test_step_group_bytes_bench_shape():
 def test_bench_defaults_time_enough_steps(monkeypatch):
     a = _parse(monkeypatch)
     assert a.steps >= 200 and a.fp32_steps > 0
+
+
+def test_gpus_flag_relaunches_as_ranks(monkeypatch):
+    """`python bench.py --gpus N` (N > 1, not already a rank) starts N ranks through torch.distributed.run with the
+    same arguments, on 127.0.0.1, and exits with their status; the parent touches no GPU."""
+    calls = []
+
+    class Done:
+        returncode = 3
+
+    def fake_run(cmd, env):
+        calls.append((cmd, env))
+        return Done()
+    import subprocess
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "7", "--dist-backend", "gloo"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 3
+    (cmd, env), = calls
+    i = cmd.index("-m")
+    assert cmd[i + 1] == "torch.distributed.run"
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-5:] == ["--gpus", "8", "--steps", "7", "--dist-backend", "gloo"][-5:]
+    assert cmd[cmd.index("--master-addr=127.0.0.1") + 2].endswith("bench.py")
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert not torch.cuda.is_initialized()
+
+
+def test_rank_checks_world_size(monkeypatch):
+    """A rank launched for --gpus 4 under a 2-rank torch.distributed.run refuses to measure."""
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4"])
+    with pytest.raises(SystemExit, match="WORLD_SIZE=2"):
+        bench.main()
+
+
+def test_single_gpu_runs_in_process(monkeypatch):
+    """--gpus 1 (the default) never relaunches."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "launch_ranks", lambda *a: pytest.fail("relaunched"))
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    monkeypatch.setattr(bench.torch.cuda, "set_device", lambda *a: (_ for _ in ()).throw(RuntimeError("stop")))
+    with pytest.raises(RuntimeError, match="stop"):
+        bench.main()

@@ -65,8 +65,8 @@ for s in "$@"; do
     benchq) run benchq 300 python bench.py --steps 100 $QUIET || exit $? ;;
     cfg4) run cfg4 300 python bench.py --no-tf $QUIET || exit $? ;;
     gloo2) # the N > 1 path rehearsed on one GPU: two ranks over gloo at cfg3's per-rank batch (64)
-           run gloo2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-               --master-port 29531 bench.py --gpus 2 --batch 64 --dist-backend gloo --steps 30 $QUIET || exit $? ;;
+           # (bench.py --gpus 2 starts the two ranks itself, as the driver's `bench.py --gpus N` does)
+           run gloo2 400 python bench.py --gpus 2 --batch 64 --dist-backend gloo --steps 30 $QUIET || exit $? ;;
     cfg5) run cfg5 300 python bench.py --bert --network vgg19 $QUIET || exit $? ;;
     prof:*) rest=${s#prof:}; label=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
           run prof_$label 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$label" -o run --output-format csv -- \
