@@ -339,17 +339,14 @@ BENCH_BF16_INIT_TOL = 7e-2
 
 @pytest.mark.parametrize("name", list(BENCH_CASES))
 def test_bench_instance_bf16_close_to_oracle(sat, name):
-    """bf16 bench instance (the default kernels bench.py runs) against the fp32 oracle; the distance to an all-bf16
-    oracle (torch CPU bf16: every op's output rounded) is printed beside it."""
+    """bf16 bench instance (the default kernels bench.py runs) against the fp32 oracle.  An all-bf16 oracle (torch
+    CPU bf16, every op's output rounded) is no tighter reference: it rounds independently of the HIP path, and
+    measured farther from it than the fp32 oracle for every weight (profiles/r5_s2b/testsv_1.log)."""
     c = _bench_case(name)
     h = _hip_step(sat, c, torch.bfloat16, split_target=c["split_target"])
     _assert_bench_instance(h["instance"], torch.bfloat16)
     tol = {n: (BENCH_BF16_INIT_TOL if n.startswith("init_") else BENCH_BF16_GRAD_TOL) for n in h["grads"]}
     _assert_bf16(c, h, _bench_oracle(name, c, torch.float32), grad_tol=tol)
-    if c["tf"]:
-        g16 = _bench_oracle(name, c, torch.bfloat16)[1]
-        print("bf16 gradient errors vs bf16 oracle:",
-              {n: round(e, 4) for n, e in _grad_errors(h, {k: v.float() for k, v in g16.items()}).items()})
 
 
 def test_bench_instance_bf16_gradients_deterministic(sat):
