@@ -346,25 +346,31 @@ def test_encoder_matches_oracle(sat, network):
     assert rel(yb.float(), ref) < 5e-2   # bf16 trunk: documented looser bound
 
 
-def test_resnet152_full_size_bf16_trunk(sat):
-    """cfg2's trunk at full size (224 x 224, B = 64, bf16, the kernels the bench runs: pipelined and
-    128-row conv GEMMs): two of the images against the fp32 oracle within the documented bf16 bound,
-    every output finite and non-negative (ReLU), and the result independent of the batch it ran in."""
+@pytest.mark.parametrize("batch,picks", [(64, (0, 1)), (128, (0, 37, 90, 127))])
+def test_resnet152_full_size_bf16_trunk(sat, batch, picks):
+    """cfg2's (B = 64) and the bench's (B = 128) trunk at full size (224 x 224, bf16, the kernels the bench runs at
+    that batch: the half-image / whole-image staged kernels, pipelined and 128-row conv GEMMs): images spread over
+    the batch against the fp32 oracle within the bf16 bound, every output finite and non-negative (ReLU), and the
+    result independent of the batch it ran in (the same kernels' per-pixel fp32 sums at B = 2, where the layer3 /
+    layer4 kernels run their small-batch forms)."""
     torch.manual_seed(0)
     p = O.make_resnet152_params(2)
     enc = sat.Encoder("resnet152", dtype=torch.bfloat16)
     enc.load_state_dict(p, strict=True)
     enc = enc.to(DEV).eval()
     g = torch.Generator().manual_seed(5)
-    x = torch.randn(64, 3, 224, 224, generator=g)
+    x = torch.randn(batch, 3, 224, 224, generator=g)
+    idx = list(picks)
     with torch.no_grad():
         y = enc(x.to(DEV))
-        y2 = enc(x[:2].contiguous().to(DEV))
-    assert y.shape == (64, 49, 2048) and y.dtype == torch.bfloat16
+        y2 = enc(x[idx].contiguous().to(DEV))
+    assert y.shape == (batch, 49, 2048) and y.dtype == torch.bfloat16
     assert torch.isfinite(y.float()).all() and (y.float() >= 0).all()
-    ref = O.resnet152_forward(p, x[:2])
-    assert rel(y[:2].float(), ref) < 5e-2
-    assert torch.equal(y[:2], y2)   # no cross-image coupling; same per-tile fp32 sums at M = 98 and 3136
+    ref = O.resnet152_forward(p, x[idx])
+    err = rel(y[idx].float(), ref)
+    print(f"bf16 ResNet152 trunk at B = {batch}, images {idx}: max-abs error / max|ref| = {err:.4f}")
+    assert err < 3e-2
+    assert torch.equal(y[idx], y2)   # no cross-image coupling
 
 
 def test_no_tf_full_shape_properties(sat):
