@@ -20,13 +20,26 @@
 //     instruction), with write-through (sc1) stores into slab s of the caller's workspace, drains them, and takes
 //     an agent-scope ticket; the workgroup that draws the last ticket adds the partials in split order 0, 1, ...,
 //     S-1 (its own from registers, the others by sc1 loads) and writes C.  The sum does not depend on which split
-//     finished last: bit-identical run to run.  Hand-off form: MI355X_MICROARCH.md "Valid forms", first row (sc1
-//     payload drained by every storing wave, barrier, one relaxed agent add; the last adder reads every handed-off
-//     byte with sc1 loads) -- no release fence, whose buffer_wbl2 would also write back the dirty L2 lines of the
-//     encoder kernels running beside the decoder;
+//     finished last: bit-identical run to run.  Hand-off: the payload write-through (sc1) and drained by every storing
+//     wave, a barrier, an agent-scope release + relaxed ticket add by one lane; the last adder takes an agent-scope
+//     acquire before its sc1 loads (cdna_hip_programming.md Guideline 16: a release / acquire pair under the memory
+//     model, besides the sc1 form MI355X_MICROARCH.md measures valid on its own);
 //   * XCD-aware order: the n-tiles of one (split, m-tile) panel share an XCD's L2.
 #include "sat_common.h"
 #include "sat_internal.h"
+
+#ifndef SAT_SPLIT_RELEASE   // diagnostics builds: 0 = no release fence on the writers (sc1 payload only)
+#define SAT_SPLIT_RELEASE 1
+#endif
+#ifndef SAT_SPLIT_DEBUG     // diagnostics builds: 1 = record every ticket draw (tools/debug_split_tickets.py)
+#define SAT_SPLIT_DEBUG 0
+#endif
+#if SAT_SPLIT_DEBUG
+__device__ unsigned g_sdbg[1 << 20];
+__device__ unsigned g_sdbg_n;
+__device__ unsigned g_sdbg_cs[64 * 256];   // per (launch % 64, tile): XOR of the final tile's bits
+static unsigned g_sdbg_launch = 0;
+#endif
 
 namespace {
 
@@ -68,6 +81,7 @@ struct SArgs {
   float* slab;            // splits > 1: [tile][split][BM x SBN] partials in the accumulator layout
   unsigned* tickets;      // splits > 1: one arrival counter per tile, zero at launch
   SatStamps st;
+  unsigned dbg_launch;    // SAT_SPLIT_DEBUG builds: launch number
 };
 
 // k-major tile of 256-B rows: chunk slot of k-row r (conflict-free for ds_read_b64_tr_b16)
@@ -271,7 +285,28 @@ __device__ __forceinline__ void split_gemm_body(const SArgs& a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its write-through stores are done
     __syncthreads();
     volatile unsigned* flag = (volatile unsigned*)(smem + G::EPI_BYTES);
-    if (tid == 0) *flag = __hip_atomic_fetch_add(a.tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+      if constexpr (SAT_SPLIT_RELEASE) {   // agent-scope release before the ticket (second wait: Guideline 16 Pitfall 12)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      const unsigned prev = __hip_atomic_fetch_add(a.tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if SAT_SPLIT_DEBUG
+      {
+        const unsigned i = atomicAdd(&g_sdbg_n, 1u);
+        if (i < (1u << 18)) {
+          g_sdbg[4 * i] = a.dbg_launch; g_sdbg[4 * i + 1] = (unsigned)tile; g_sdbg[4 * i + 2] = (unsigned)split;
+          g_sdbg[4 * i + 3] = prev;
+        }
+      }
+#endif
+      if (prev == (unsigned)(a.splits - 1)) {
+        // the last arriver: agent-scope acquire before it reads the other partial tiles
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = prev;
+    }
     __syncthreads();
     if (*flag != (unsigned)(a.splits - 1)) return;   // workgroup-uniform
     f32x4 tot[MI][NJ], part[MI][NJ];
@@ -301,6 +336,18 @@ __device__ __forceinline__ void split_gemm_body(const SArgs& a) {
       for (int j = 0; j < NJ; ++j) acc[i][j] = tot[i][j];
   }
 
+#if SAT_SPLIT_DEBUG
+  {
+    unsigned x = 0;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x ^= __float_as_uint(acc[i][j][r]) * (unsigned)(1 + ((i * NJ + j) * 4 + r));
+    atomicXor(&g_sdbg_cs[(a.dbg_launch % 64) * 256 + ((long)mt * a.tiles_n + nt) % 256], x);
+  }
+#endif
   // ---- C: the fp32 tile through LDS, 16-B row pieces (beta = 1 adds C) ----
   sg_wait_barrier<0>();   // every wave done with the ring
   float* ep = (float*)smem;
@@ -385,15 +432,18 @@ SPlan plan_split(const SatGemm& g, bool have_ws) {
   return best;
 }
 
-// the problems this kernel takes: bf16 operands, fp32 C, C = A B (+ C), at least one k-major operand, 16-B pieces
+// the problems this kernel takes: bf16 operands, fp32 C, C = A B (+ add1) (+ C), a k-major operand or an NN product
+// the tile kernel would split with atomics, 16-B pieces
 bool split_eligible(const SatGemm& g) {
   const int mode = sat_policy().split_gemm;
   if (mode == 1) return false;
   if (g.dtype != SAT_BF16 || g.c_dtype != SAT_F32 || g.batch != 1 || g.aux || g.bias || g.conv.C > 0 ||
       g.act != SAT_ACT_NONE || g.partial_splits > 1 || g.alpha != 1.f || (g.beta != 0.f && g.beta != 1.f))
     return false;
-  if (!(g.transA || g.transB)) return false;
   if (g.M <= 0 || g.N <= 0 || g.K <= 0) return false;
+  // both operands k-contiguous (NN): only the products the tile kernel would split with fp32 atomics (few 128 x 128
+  // tiles, K >= 1024) -- here they keep a fixed summation order (the decoder's gradients are bit-reproducible)
+  if (!(g.transA || g.transB) && !((long)sat_cdiv(g.M, 128) * sat_cdiv(g.N, 128) < 160 && g.K >= 1024)) return false;
   const bool at = g.transA != 0, bt = g.transB != 0;
   if (g.lda % 8 || g.ldb % 8 || g.ldc % 4 || g.N % 8) return false;
   // a K tail (K % 8 != 0) only where the straddling 8-element chunks read zeros: an m-major A zero-padded to the next
@@ -452,16 +502,41 @@ int sat_split_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
                                           (long)p.tiles_m * p.tiles_n, s));
   }
   a.st = sat_launch_stamps();
+#if SAT_SPLIT_DEBUG
+  a.dbg_launch = ++g_sdbg_launch;
+#endif
   const dim3 grid((unsigned)((long)p.tiles_m * p.tiles_n * p.splits));
   if (p.bm == 256) {
     if (at && bt) hipLaunchKernelGGL((split_gemm_kernel<256, true, true>), grid, dim3(512), 0, s, a);
     else if (at) hipLaunchKernelGGL((split_gemm_kernel<256, true, false>), grid, dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((split_gemm_kernel<256, false, true>), grid, dim3(512), 0, s, a);
+    else if (bt) hipLaunchKernelGGL((split_gemm_kernel<256, false, true>), grid, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((split_gemm_kernel<256, false, false>), grid, dim3(512), 0, s, a);
   } else {
     if (at && bt) hipLaunchKernelGGL((split_gemm_kernel<128, true, true>), grid, dim3(512), 0, s, a);
     else if (at) hipLaunchKernelGGL((split_gemm_kernel<128, true, false>), grid, dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((split_gemm_kernel<128, false, true>), grid, dim3(512), 0, s, a);
+    else if (bt) hipLaunchKernelGGL((split_gemm_kernel<128, false, true>), grid, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((split_gemm_kernel<128, false, false>), grid, dim3(512), 0, s, a);
   }
   *err = (int)hipGetLastError();
   return 1;
 }
+
+#if SAT_SPLIT_DEBUG
+// diagnostics builds: copy the ticket-draw records {launch, tile, split, prev} (n4 = 4 x records) and reset them
+extern "C" int sat_split_debug_read(unsigned* out, int n4, unsigned* count) {
+  SAT_CHECK(hipDeviceSynchronize());
+  SAT_CHECK(hipMemcpyFromSymbol(count, HIP_SYMBOL(g_sdbg_n), sizeof(unsigned)));
+  const unsigned m = *count * 4 < (unsigned)n4 ? *count * 4 : (unsigned)n4;
+  if (m) SAT_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sdbg), m * sizeof(unsigned)));
+  const unsigned z = 0;
+  SAT_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_sdbg_n), &z, sizeof(unsigned)));
+  return 0;
+}
+extern "C" int sat_split_debug_checksums(unsigned* out) {   // 64 x 256 words, then zeroed
+  SAT_CHECK(hipDeviceSynchronize());
+  SAT_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sdbg_cs), 64 * 256 * sizeof(unsigned)));
+  static unsigned zeros[64 * 256] = {};
+  SAT_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_sdbg_cs), zeros, sizeof(zeros)));
+  return 0;
+}
+#endif

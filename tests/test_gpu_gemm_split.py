@@ -2,7 +2,8 @@
 deterministic split-K that runs the decoder's batched weight / input gradients (decoder.py:115,117-125,149-158 and
 attention.py:15-16 backward, train.py:163).
 
-Every operand layout with a k-major operand (A k-major, B k-major or both), both tile heights (SatPolicy.split_gemm
+Every operand layout with a k-major operand (A k-major, B k-major or both) and the NN products the tile kernel would
+split with fp32 atomics, both tile heights (SatPolicy.split_gemm
 = 2: 128 rows, 3: 256 rows), forced split counts (SatPolicy.split_k) and the planner's choice, beta = 1
 accumulation, an fp32 addend, and edges (M not a multiple of the tile height, N not a multiple of 128, K not a
 multiple of 64: the buffer-resource zero fill), each against an fp64 product of the same bf16 operands (fp32
@@ -41,6 +42,8 @@ CASES = [
     (1000, 200, 1000, True, True, 0.0),     # edges everywhere: M, N, K tails
     (1024, 1024, 2048, True, False, 0.0),   # A k-major, B row-major
     (300, 136, 520, False, True, 1.0),      # B k-major, tails, accumulate
+    (300, 136, 1104, False, False, 0.0),    # NN with few tiles and K >= 1024 (the tile kernel's atomic split-K case)
+    (3, 512, 2624, False, False, 0.0),      # the per-step dh GEMM of a 3-row batch (K = 5E + D, 41 k-tiles)
 ]
 # (split_gemm, split_k): the planner, both tile heights unsplit and split
 FORMS = [(0, 0), (2, 1), (2, 2), (2, 4), (3, 1), (3, 2), (3, 3)]

@@ -7,8 +7,10 @@ name=$1; flags=$2; shift 2
 cd "$(dirname "$0")/../show-attend-and-tell_amd/csrc"
 make -s -j8
 objs=""
+srcs=$(sed -n 's/^SRCS := //p' Makefile)
 for f in build/*.o; do
   case $f in *_v_*) continue ;; esac
+  case " $srcs " in *" $(basename "$f" .o).hip "*) ;; *) continue ;; esac   # stale objects of removed sources
   b=$(basename "$f" .o)
   skip=0
   for src in "$@"; do [ "$b" = "$(basename "$src" .hip)" ] && skip=1; done
