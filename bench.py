@@ -79,7 +79,7 @@ def parse():
     ap.add_argument("--policy", default="",
                     help="extra SatPolicy fields for every encoder / decoder call, e.g. attn_bwd_chunks=1,gemm_stages=3 "
                          "or decoder_splits=2.0.0.0 (A/B; include/sat_hip.h)")
-    ap.add_argument("--c2-frag-sizes", default="7,14,28,112",
+    ap.add_argument("--c2-frag-sizes", default="7,14,28,56,112",
                     help="spatial sizes whose stride-1 3x3 convs run on the staged-input kernels (sat_conv3x3_frag); "
                          "the others on the tile kernel (A/B)")
     ap.add_argument("--fuse-layer2", action="store_true",
@@ -692,7 +692,7 @@ def main():
         # 64 at B <= 64 (96 there: 4.21-4.23 vs 4.01-4.04 ms), profiles/r3_s46, r3_s47
         args.split_target = 128 if args.network == "vgg19" else (96 if args.batch > 64 else 64)
     enc.fuse_layer2 = args.fuse_layer2
-    enc.c2_frag_sizes = tuple(int(v) for v in args.c2_frag_sizes.split(",") if v)
+    enc.c2_frag_sizes = tuple(int(v) for v in args.c2_frag_sizes.replace("/", ",").split(",") if v)
     enc.fuse_blocks = (False if args.no_fuse_blocks or args.fuse_every == 0 else
                        (True if args.fuse_every == 1 else args.fuse_every))
     enc.policy = policy

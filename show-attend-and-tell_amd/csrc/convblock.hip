@@ -918,6 +918,17 @@ __global__ __launch_bounds__(512) void conv3x3_band112_kernel(const bf16* __rest
   sat_stamp_end(st, t0);
 }
 
+// VGG19 block 3's 56 x 56, 256 -> 256 convs (three launches) as 2-row bands: the layer3 c2 half-image geometry
+// (112 output pixels x 256 channels per workgroup, 8 waves of 7 m-blocks x 2 n-blocks, 115 KB of LDS), 28
+// workgroups per image
+__global__ __launch_bounds__(512) void conv3x3_band56_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                             const float* __restrict__ bias, bf16* __restrict__ y,
+                                                             int nbands, SatStamps st) {
+  const SatStampT0 t0 = sat_stamp_begin(st);
+  conv3x3_band_body<56, 2, 256, 1, 1, 2>(x, wf, bias, y, nbands);
+  sat_stamp_end(st, t0);
+}
+
 // VGG19's block-5 convs (14 x 14, 512 -> 512, four launches): half images (one-row halo each side) x four
 // 128-channel slices, eight waves of 16 channels (130 KB of LDS, one workgroup per CU)
 __global__ __launch_bounds__(512) void conv3x3_half512_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
@@ -1311,7 +1322,8 @@ extern "C" int sat_bottleneck_fused(int N, int H, int W, int Cin, int Cmid, int 
 
 extern "C" int sat_conv3x3_frag_supported(int H, int W, int C, int dtype) {
   return dtype == SAT_BF16 && ((H == 14 && W == 14 && (C == 256 || C == 512)) || (H == 28 && W == 28 && C == 128) ||
-                               (H == 7 && W == 7 && C == 512) || (H == 112 && W == 112 && C == 128));
+                               (H == 7 && W == 7 && C == 512) || (H == 112 && W == 112 && C == 128) ||
+                               (H == 56 && W == 56 && C == 256));
 }
 
 extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const void* x, const void* wf, const float* b,
@@ -1348,6 +1360,10 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   }
   if (H == 112) {   // VGG19 block 2: 2-row bands
     hipLaunchKernelGGL(conv3x3_band112_kernel, dim3(56 * N), dim3(512), 0, s, xp, wp, b, yp, 56 * N, st);
+    return (int)hipGetLastError();
+  }
+  if (H == 56) {   // VGG19 block 3: 2-row bands
+    hipLaunchKernelGGL(conv3x3_band56_kernel, dim3(28 * N), dim3(512), 0, s, xp, wp, b, yp, 28 * N, st);
     return (int)hipGetLastError();
   }
   if (H == 14 && C == 512) {   // VGG19 block 5: half images x four 128-channel slices

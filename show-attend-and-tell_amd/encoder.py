@@ -164,7 +164,7 @@ class Encoder(nn.Module):
         self.c2_frag = True
         # ... at these spatial sizes (layer4 7, layer3 14, layer2 28; VGG19 block 5 14, block 2 112);
         # A/B: bench.py --c2-frag-sizes
-        self.c2_frag_sizes = (7, 14, 28, 112)
+        self.c2_frag_sizes = (7, 14, 28, 56, 112)
         # ... its c1 on the half-image 1x1 kernel (sat_conv1x1_frag: input slabs by LDS-DMA, weights
         # register-direct)
         self.c1_frag = True

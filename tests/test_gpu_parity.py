@@ -1088,11 +1088,12 @@ def test_bottleneck_fused_bit_identical(sat, N, H, C, M):
                                           (8, 14, 256, 0), (1, 28, 128, 0), (3, 28, 128, 0),
                                           (1, 14, 512, 0), (5, 14, 512, 0), (2, 112, 128, 0),
                                           (1, 7, 512, 0), (3, 7, 512, 1), (4, 7, 512, 1), (17, 7, 512, 2),
-                                          (70, 7, 512, 0)])
+                                          (70, 7, 512, 0), (1, 56, 256, 0), (3, 56, 256, 0)])
 def test_conv3x3_frag_bit_identical(sat, N, H, C, slices):
     """csrc/convblock.hip's half-image 3x3 kernel (a layer3 c2 left unfused: 14x14, 256 -> 256), its two-slice
     form (SatPolicy.conv_slices 2: each half image as two 128-channel workgroups, the default below B = 64;
-    N = 70 leaves a partial group of 8 half images), its 7-row band form (layer2 c2: 28x28, 128 -> 128) and its
+    N = 70 leaves a partial group of 8 half images), its 7-row band
+    form (layer2 c2: 28x28, 128 -> 128), its 2-row band form at 56x56 (VGG19 block 3, 256 -> 256) and its
     whole-image form (layer4 c2: 7x7, 512 -> 512, one or two images x four 128-channel slices per workgroup; odd N
     leaves a one-image group) are bit-identical to the tile kernel on the same operands, and close to torch fp32."""
     from sat_amd import ops
@@ -1362,13 +1363,14 @@ def test_adam_flat_runs_match_torch_adam(sat):
 
 
 def test_vgg19_block5_frag_equal_tile(sat):
-    """VGG19 trunk at 224 x 224 (bf16): its four block-5 convs (14 x 14, 512 -> 512) and block 2's 128 -> 128 conv on
-    the staged-input kernels (sat_conv3x3_frag) change no output bit against the tile kernel."""
+    """VGG19 trunk at 224 x 224 (bf16): its four block-5 convs (14 x 14, 512 -> 512), block 3's three 256 -> 256 convs
+    (56 x 56, 2-row bands) and block 2's 128 -> 128 conv on the staged-input kernels (sat_conv3x3_frag) change no
+    output bit against the tile kernel."""
     torch.manual_seed(0)
     enc = sat.Encoder("vgg19", dtype=torch.bfloat16).to(DEV).eval()
     x = torch.randn(3, 3, 224, 224, generator=torch.Generator().manual_seed(8)).to(DEV)
     plan = enc.compiled_plan(x.device, torch.bfloat16)
-    assert sum(1 for s in plan if s[0] == "conv" and s[3] is not None) == 4 + 1   # block 5, block 2's conv4
+    assert sum(1 for s in plan if s[0] == "conv" and s[3] is not None) == 4 + 3 + 1   # block 5, block 3, block 2
     with torch.no_grad():
         y_f = enc(x)
         enc.c2_frag = False
