@@ -897,12 +897,16 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
   }
 }
 
+// ResNet152 layer2's c2 (28 x 28, 128 -> 128) as 7-row bands on four waves of 32 channels (NJ = 2): every A
+// fragment read from LDS feeds two MFMAs (the eight-wave form of 16 channels per wave read one per MFMA: LDS-read
+// bound with MFMA and the weight stream), two workgroups per CU (65 KB of LDS, 256 threads, <= 256 VGPRs with the
+// weight prefetch one k-tile ahead): 36.0 -> 28.2 us back to back, 37.4 -> 27.3 us in-step (profiles/r5_s14)
 template <int PF>
-__global__ __launch_bounds__(512) void conv3x3_band_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
-                                                           const float* __restrict__ bias, bf16* __restrict__ y,
-                                                           int nbands, SatStamps st) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv3x3_band4w_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wf,
+                                                             const float* __restrict__ bias, bf16* __restrict__ y,
+                                                             int nbands, SatStamps st) {
   const SatStampT0 t0 = sat_stamp_begin(st);
-  conv3x3_band_body<28, 7, 128, 1, 1, PF>(x, wf, bias, y, nbands);
+  conv3x3_band_body<28, 7, 128, 1, 1, PF, 4>(x, wf, bias, y, nbands);
   sat_stamp_end(st, t0);
 }
 
@@ -1371,7 +1375,7 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
     return (int)hipGetLastError();
   }
   if (H == 28) {   // layer2 c2: 7-row bands, four workgroups per image
-    hipLaunchKernelGGL(conv3x3_band_kernel<2>, dim3(4 * N), dim3(512), 0, s, xp, wp, b, yp, 4 * N, st);
+    hipLaunchKernelGGL(conv3x3_band4w_kernel<1>, dim3(4 * N), dim3(256), 0, s, xp, wp, b, yp, 4 * N, st);
     return (int)hipGetLastError();
   }
   // layer3 c2: half images (two workgroups per image), or two channel slices per half image when the half

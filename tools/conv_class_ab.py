@@ -26,6 +26,8 @@ CLASSES = [
     ("L4dss2 1x1 1024->2048 /2", 14, 1024, 2048, 1, 2, 0, False),
     ("L3c2s2 3x3 256 /2", 28, 256, 256, 3, 2, 1, False),
     ("L3dss2 1x1 512->1024 /2", 28, 512, 1024, 1, 2, 0, False),
+    ("V4 3x3 128 (VGG19 block 2)", 112, 128, 128, 3, 1, 1, False),
+    ("V7 3x3 256 (VGG19 block 3)", 56, 256, 256, 3, 1, 1, False),
 ]
 POLICIES = [("default", {}), ("pipe off", dict(conv_pipe=1)), ("pipe all", dict(conv_pipe=2)),
             ("tile1", dict(conv_pipe=1, gemm_tile=1)), ("tile2", dict(conv_pipe=1, gemm_tile=2)),
@@ -36,7 +38,7 @@ POLICIES = [("default", {}), ("pipe off", dict(conv_pipe=1)), ("pipe all", dict(
 
 def main():
     g = torch.Generator(device=DEV).manual_seed(0)
-    only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
+    only = sys.argv[sys.argv.index("--only") + 1].replace("/", ",").split(",") if "--only" in sys.argv else None
     for name, H, Cin, Cout, k, s, p, res in CLASSES:
         if only and name.split()[0] not in only:
             continue
