@@ -1093,8 +1093,9 @@ def test_conv3x3_frag_bit_identical(sat, N, H, C, slices):
     """csrc/convblock.hip's half-image 3x3 kernel (a layer3 c2 left unfused: 14x14, 256 -> 256), its two-slice
     form (SatPolicy.conv_slices 2: each half image as two 128-channel workgroups, the default below B = 64;
     N = 70 leaves a partial group of 8 half images), its 7-row band form on four 32-channel waves (layer2 c2: 28x28,
-    128 -> 128), its 2-row band form at 56x56 (VGG19 block 3, 256 -> 256) and its whole-image form (layer4 c2: 7x7, 512 -> 512, one or two images x four 128-channel slices per workgroup; odd N
-    leaves a one-image group) are bit-identical to the tile kernel on the same operands, and close to torch fp32."""
+    128 -> 128), its 2-row band form at 56x56 (VGG19 block 3, 256 -> 256) and its whole-image form (layer4 c2: 7x7,
+    512 -> 512, one or two images x four 128-channel slices per workgroup; odd N leaves a one-image group) are
+    bit-identical to the tile kernel on the same operands, and close to torch fp32."""
     from sat_amd import ops
     g = torch.Generator().manual_seed(40 + N + H)
     x = torch.randn(N, H, H, C, generator=g).relu().bfloat16().to(DEV)
