@@ -18,7 +18,9 @@
 //     columns of one row;
 //   * the NW partial tiles meet in one 18 KB LDS tile in wave order (fixed summation order: results
 //     do not depend on scheduling), then the workgroup stores 16-B row pieces.
-// The context and dL/dh products with the LSTM cell in their epilogue run full-K row blocks instead (lstmgemm.hip).
+// Measured and not kept (profiles/r5_s10, r5_s16): an XCD-aware workgroup order (the column blocks of one split on
+// one XCD: fewer fabric reads of A, the h GEMM 7.5 -> 9.1 us), 64-column workgroups of eight waves (half the
+// workgroups and ~60 % of the bytes moved: 7.6 -> 11.9 us per product, step 6.40 -> 6.47-6.50 ms).
 #include "sat_common.h"
 #include "sat_internal.h"
 
