@@ -23,6 +23,7 @@
 #   abl:LABEL:LIB:ARGS the same with the diagnostics build show-attend-and-tell_amd/libsat_hip_LIB.so
 #                      (tools/build_variant.sh) loaded instead of the product library
 #   abd:LABEL:ARGS     the same with the diagnostics (per-step decoder kernels, trunk classes; tools/bench_brief.py)
+#   abdl:LABEL:LIB:ARGS  abd with the diagnostics build libsat_hip_LIB.so
 #   py:SCRIPT[:ARGS]   python SCRIPT ARGS (comma-separated) under a 300 s limit
 set -u
 TAG=${1:?tag}; shift
@@ -106,6 +107,10 @@ for s in "$@"; do
           echo "[$label] $(line "$OUT/ab_${n}_$label.log")" ;;
     abd:*) rest=${s#abd:}; label=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
           run abd_${n}_$label 300 python bench.py --steps 100 $QUIET ${args//,/ } || exit $?
+          python tools/bench_brief.py "$OUT/abd_${n}_$label.log" ;;
+    abdl:*) rest=${s#abdl:}; label=${rest%%:*}; rest=${rest#*:}; lib=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+          SAT_HIP_LIB_TUNING=show-attend-and-tell_amd/libsat_hip_$lib.so \
+            run abd_${n}_$label 300 python bench.py --steps 100 $QUIET ${args//,/ } || exit $?
           python tools/bench_brief.py "$OUT/abd_${n}_$label.log" ;;
     py:*) rest=${s#py:}; script=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
           run py_${n}_$(basename "$script" .py) 300 python "$script" ${args//,/ } || exit $? ;;
