@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SAT_ABI_VERSION 7
+#define SAT_ABI_VERSION 8
 
 enum { SAT_F32 = 0, SAT_BF16 = 1 };
 enum { SAT_ACT_NONE = 0, SAT_ACT_RELU = 1, SAT_ACT_TANH = 2, SAT_ACT_SIGMOID = 3 };
@@ -72,6 +72,8 @@ typedef struct {
   int split_k;          /* split_gemm: 0 the planner's split count, n > 0 exactly n splits when the shape allows */
   int attn_bwd;         /* attention backward per decoder step: 0 auto, 1 the two-launch form */
   int attn_bwd_chunks;  /* split attention backward: slot chunks per batch row (0 auto: ~256 workgroups) */
+  int attn_pipe;        /* attention forward / split backward over more slots than one batch of loads (L = 196):
+                         * 0 auto (slot batches double-buffered), 1 one batch at a time */
   int decoder_splits[4];/* split-K counts of the per-step bf16 decoder GEMMs -- h: [U; f_beta; W_hh] h, c: context
                          * part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic */
   /* diagnostics (bench.py's in-step kernel timing): a device buffer; when non-null and stamps[0] != 0 (the

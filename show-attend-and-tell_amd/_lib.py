@@ -25,14 +25,14 @@ class SatConvGeom(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("N", "H", "W", "C", "KH", "KW", "stride", "pad", "OH", "OW")]
 
 
-ABI_VERSION = 7   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
+ABI_VERSION = 8   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
 
 
 class SatPolicy(ctypes.Structure):
     """Per-call kernel selection (include/sat_hip.h SatPolicy); all zeros = the library's defaults."""
     _fields_ = [(n, c_int) for n in ("conv_pipe", "conv_stream", "conv3x3_ws", "conv_slices", "skinny", "gemm_stages",
                                      "gemm_tile", "gemm_linear_order", "gemm_epilogue", "split_gemm", "split_k",
-                                     "attn_bwd", "attn_bwd_chunks")] + \
+                                     "attn_bwd", "attn_bwd_chunks", "attn_pipe")] + \
                [("decoder_splits", c_int * 4), ("stamps", c_void_p), ("stamp_capacity", c_int)]
 
     def __init__(self, **kw):

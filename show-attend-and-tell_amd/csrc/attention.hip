@@ -88,7 +88,7 @@ constexpr int FNW = 16, FFU = 4;   // the default shape: 16 waves x 4 slots per 
 
 // FDV: 16-byte context vectors per lane (2: a workgroup owns 1024 bf16 / 512 fp32 columns)
 // NW waves, FU slots per wave per batch of loads (16 x 4: every slot of L = 49 in one batch).
-template <typename T, int CH, int FDV, int NW = FNW, int FU = FFU>   // CH = e-chunks of 64 x 16 bytes per lane covering E
+template <typename T, int CH, int FDV, int NW = FNW, int FU = FFU, bool PIPE = false>   // CH = e-chunks of 64 x 16 B per lane over E
 __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   constexpr int VN = V16<T>::N;            // elements per 16-byte vector
   constexpr int COLS = 64 * VN * FDV;      // context columns of one workgroup
@@ -141,7 +141,8 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   for (int u = 0; u < FU; ++u)
 #pragma unroll
     for (int v = 0; v < FDV; ++v)
-      xa[u][v] = ld16(ab + (long)(w + NW * u) * D + v * 64 * VN, w + NW * u < L && c0 + v * 64 * VN + lane * VN < D);
+      xa[u][v] = ld16(ab + (long)(w + NW * u) * D + v * 64 * VN,
+                      w + NW * u < L && c0 + v * 64 * VN + lane * VN < D);
   // the epilogue's threads own 4 consecutive columns each (col4 = 4 tid: 16-B write-through stores)
   static_assert(COLS <= 4 * NT && COLS % 4 == 0, "four columns per epilogue thread");
   const int col4 = 4 * tid;
@@ -150,16 +151,22 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   if (a.gate_pre && ep) gpre4 = sum_parts4(a.gate_pre + (long)b * a.gate_ld, c0 + col4, a.hg_splits, a.hg_split_stride);
 
   const float bv = a.v_b[0];
-  for (int l0 = w; l0 < L; l0 += NW * FU) {
-    if (l0 != w) {
+  // (the per-slot and per-column accumulations are explicit FMAs: the compiler's own contraction choice can differ
+  // between instantiations, and the PIPE / one-batch forms must agree bit for bit)
+  // slots in batches of NW x FU (one batch at L = 49).  PIPE (more slots than one batch of NW x 4, e.g. L = 196):
+  // batches of NW x 2 slots, the next batch's rows requested before the current batch's arithmetic (two register
+  // buffers: the same registers as one batch of NW x 4), so the batches' memory round trips overlap
+  constexpr int STEP = NW * FU;
+  auto load_ws = [&](int l0, uint4 (&dst)[FU][CH]) {
 #pragma unroll
-      for (int u = 0; u < FU; ++u)
+    for (int u = 0; u < FU; ++u)
 #pragma unroll
-        for (int c = 0; c < CH; ++c) {
-          const int l = l0 + NW * u, e = c * 64 * VN + lane * VN;
-          xv[u][c] = ld16(Ws + (long)l * E + e, l < L && e < E);
-        }
-    }
+      for (int c = 0; c < CH; ++c) {
+        const int l = l0 + NW * u, e = c * 64 * VN + lane * VN;
+        dst[u][c] = ld16(Ws + (long)l * E + e, l < L && e < E);
+      }
+  };
+  auto scores = [&](int l0, const uint4 (&src)[FU][CH]) {
 #pragma unroll
     for (int u = 0; u < FU; ++u) {
       const int l = l0 + NW * u;
@@ -167,12 +174,26 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
       float acc = 0.f;
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
-        const T* h = (const T*)&xv[u][c];
+        const T* h = (const T*)&src[u][c];
 #pragma unroll
-        for (int j = 0; j < VN; ++j) acc += v_r[c][j] * tanh_t<T>((float)h[j] + u_r[c][j]);   // v = 0 past E
+        for (int j = 0; j < VN; ++j) acc = fmaf(v_r[c][j], tanh_t<T>((float)h[j] + u_r[c][j]), acc);   // v = 0 past E
       }
       acc = wave_sum(acc);
       if (lane == 0) s_alpha[l] = acc + bv;
+    }
+  };
+  if constexpr (PIPE) {
+    for (int l0 = w; l0 < L; l0 += 2 * STEP) {
+      uint4 xn[FU][CH];
+      if (l0 + STEP < L) load_ws(l0 + STEP, xn);
+      scores(l0, xv);
+      if (l0 + 2 * STEP < L) load_ws(l0 + 2 * STEP, xv);
+      if (l0 + STEP < L) scores(l0 + STEP, xn);
+    }
+  } else {
+    for (int l0 = w; l0 < L; l0 += STEP) {
+      if (l0 != w) load_ws(l0, xv);
+      scores(l0, xv);
     }
   }
   if (s == 0 && w == 1 && a.uh_save) {   // U h + b of this row (the registers every wave holds)
@@ -212,15 +233,14 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   for (int v = 0; v < FDV; ++v)
 #pragma unroll
     for (int j = 0; j < VN; ++j) part[v][j] = 0.f;
-  for (int l0 = w; l0 < L; l0 += NW * FU) {
-    if (l0 != w) {
+  auto load_a = [&](int l0, uint4 (&dst)[FU][FDV]) {
 #pragma unroll
-      for (int u = 0; u < FU; ++u)
+    for (int u = 0; u < FU; ++u)
 #pragma unroll
-        for (int v = 0; v < FDV; ++v)
-          xa[u][v] = ld16(ab + (long)(l0 + NW * u) * D + v * 64 * VN,
-                          l0 + NW * u < L && c0 + v * 64 * VN + lane * VN < D);
-    }
+      for (int v = 0; v < FDV; ++v)
+        dst[u][v] = ld16(ab + (long)(l0 + NW * u) * D + v * 64 * VN, l0 + NW * u < L && c0 + v * 64 * VN + lane * VN < D);
+  };
+  auto context = [&](int l0, const uint4 (&src)[FU][FDV]) {
 #pragma unroll
     for (int u = 0; u < FU; ++u) {
       const int l = l0 + NW * u;
@@ -228,11 +248,25 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
         const float al = s_alpha[l];
 #pragma unroll
         for (int v = 0; v < FDV; ++v) {
-          const T* h = (const T*)&xa[u][v];
+          const T* h = (const T*)&src[u][v];
 #pragma unroll
-          for (int j = 0; j < VN; ++j) part[v][j] += al * (float)h[j];
+          for (int j = 0; j < VN; ++j) part[v][j] = fmaf(al, (float)h[j], part[v][j]);
         }
       }
+    }
+  };
+  if constexpr (PIPE) {   // the same two-buffer overlap as the scores
+    for (int l0 = w; l0 < L; l0 += 2 * STEP) {
+      uint4 an[FU][FDV];
+      if (l0 + STEP < L) load_a(l0 + STEP, an);
+      context(l0, xa);
+      if (l0 + 2 * STEP < L) load_a(l0 + 2 * STEP, xa);
+      if (l0 + STEP < L) context(l0 + STEP, an);
+    }
+  } else {
+    for (int l0 = w; l0 < L; l0 += STEP) {
+      if (l0 != w) load_a(l0, xa);
+      context(l0, xa);
     }
   }
   // fixed summation order over the wave partials: c = sum over q = 0, 2, .., 6 of (p_q + p_(q+1)) per round of
@@ -285,10 +319,10 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   }
 }
 
-template <typename T, int CH, int FDV, int NW = FNW, int FU = FFU>   // CH = e-chunks of 64 x 16 bytes per lane covering E
+template <typename T, int CH, int FDV, int NW = FNW, int FU = FFU, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnFwdArgs a) {
   const SatStampT0 t0 = sat_stamp_begin(a.st);
-  attn_fwd_kernel_body<T, CH, FDV, NW, FU>(a);
+  attn_fwd_kernel_body<T, CH, FDV, NW, FU, PIPE>(a);
   sat_stamp_end(a.st, t0);
 }
 
@@ -495,7 +529,7 @@ __global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int 
 // slots: partial dL/d(U h), dL/dv, dL/dv.bias.  With NL > 1 the partials meet in the last-arriving
 // workgroup of the row (agent-scope ticket; payload stored and loaded sc1, so no cache fence is needed:
 // MI355X_MICROARCH.md, visibility, first row of the sc1 table), summed in chunk order (deterministic).
-template <typename T, int DCH, int ECH, int FBW, int FBU>
+template <typename T, int DCH, int ECH, int FBW, int FBU, bool PIPE>
 __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   constexpr int VN = V16<T>::N;
   constexpr int EC = 64 * VN * ECH;
@@ -591,16 +625,19 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
 #pragma unroll
     for (int j = 0; j < VN; ++j) dctx[q][j] = s_dctx[q * 64 * VN + lane * VN + j];
   // ---- B + C: dL/dalpha and de per slot of the chunk ----
-  for (int l0 = l_beg + w; l0 < l_end; l0 += FBW * FBU) {
-    if (l0 != l_beg + w) {
+  // PIPE (a chunk deeper than one batch of loads, e.g. L = 196): the next batch's rows are requested before the
+  // current batch's arithmetic (two register buffers of half the batch: the same registers), as in the forward
+  constexpr int BST = FBW * FBU;
+  auto load_xa = [&](int l0, uint4 (&dst)[FBU][DCH]) {
 #pragma unroll
-      for (int u = 0; u < FBU; ++u)
+    for (int u = 0; u < FBU; ++u)
 #pragma unroll
-        for (int q = 0; q < DCH; ++q) {
-          const int l = l0 + FBW * u, d = q * 64 * VN + lane * VN;
-          xa[u][q] = ld16(ab + (long)l * D + q * 64 * VN, l < l_end && d < D);
-        }
-    }
+      for (int q = 0; q < DCH; ++q) {
+        const int l = l0 + FBW * u, d = q * 64 * VN + lane * VN;
+        dst[u][q] = ld16(ab + (long)l * D + q * 64 * VN, l < l_end && d < D);
+      }
+  };
+  auto dalpha = [&](int l0, const uint4 (&src)[FBU][DCH]) {
 #pragma unroll
     for (int u = 0; u < FBU; ++u) {
       const int l = l0 + FBW * u;
@@ -608,9 +645,9 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
       float p = 0.f;
 #pragma unroll
       for (int q = 0; q < DCH; ++q) {
-        const T* h = (const T*)&xa[u][q];
+        const T* h = (const T*)&src[u][q];
 #pragma unroll
-        for (int j = 0; j < VN; ++j) p += dctx[q][j] * (float)h[j];
+        for (int j = 0; j < VN; ++j) p = fmaf(dctx[q][j], (float)h[j], p);
       }
       p = wave_sum(p);
       if (lane == 0) {
@@ -619,6 +656,20 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
         s_de[l - l_beg] = de;
         a.de_out[(long)b * a.de_ld + l] = de;
       }
+    }
+  };
+  if constexpr (PIPE) {
+    for (int l0 = l_beg + w; l0 < l_end; l0 += 2 * BST) {
+      uint4 xn[FBU][DCH];
+      if (l0 + BST < l_end) load_xa(l0 + BST, xn);
+      dalpha(l0, xa);
+      if (l0 + 2 * BST < l_end) load_xa(l0 + 2 * BST, xa);
+      if (l0 + BST < l_end) dalpha(l0 + BST, xn);
+    }
+  } else {
+    for (int l0 = l_beg + w; l0 < l_end; l0 += BST) {
+      if (l0 != l_beg + w) load_xa(l0, xa);
+      dalpha(l0, xa);
     }
   }
   __syncthreads();
@@ -629,16 +680,16 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
 #pragma unroll
     for (int j = 0; j < VN; ++j) duh[q][j] = dv[q][j] = 0.f;
   float dbv = 0.f;
-  for (int l0 = l_beg + w; l0 < l_end; l0 += FBW * FBU) {
-    if (l0 != l_beg + w) {
+  auto load_xw = [&](int l0, uint4 (&dst)[FBU][ECH]) {
 #pragma unroll
-      for (int u = 0; u < FBU; ++u)
+    for (int u = 0; u < FBU; ++u)
 #pragma unroll
-        for (int q = 0; q < ECH; ++q) {
-          const int l = l0 + FBW * u, e = q * 64 * VN + lane * VN;
-          xw[u][q] = ld16(Ws + (long)l * E + q * 64 * VN, l < l_end && e < E);
-        }
-    }
+      for (int q = 0; q < ECH; ++q) {
+        const int l = l0 + FBW * u, e = q * 64 * VN + lane * VN;
+        dst[u][q] = ld16(Ws + (long)l * E + q * 64 * VN, l < l_end && e < E);
+      }
+  };
+  auto tanh_bwd = [&](int l0, const uint4 (&src)[FBU][ECH]) {
 #pragma unroll
     for (int u = 0; u < FBU; ++u) {
       const int l = l0 + FBW * u;
@@ -647,14 +698,28 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
       dbv += de;
 #pragma unroll
       for (int q = 0; q < ECH; ++q) {
-        const T* h = (const T*)&xw[u][q];
+        const T* h = (const T*)&src[u][q];
 #pragma unroll
         for (int j = 0; j < VN; ++j) {
           const float t = tanh_t<T>((float)h[j] + uu[q][j]);
-          duh[q][j] += de * vw[q][j] * (1.f - t * t);
-          dv[q][j] += de * t;
+          duh[q][j] = fmaf(de * vw[q][j], fmaf(-t, t, 1.f), duh[q][j]);
+          dv[q][j] = fmaf(de, t, dv[q][j]);
         }
       }
+    }
+  };
+  if constexpr (PIPE) {
+    for (int l0 = l_beg + w; l0 < l_end; l0 += 2 * BST) {
+      uint4 xn[FBU][ECH];
+      if (l0 + BST < l_end) load_xw(l0 + BST, xn);
+      tanh_bwd(l0, xw);
+      if (l0 + 2 * BST < l_end) load_xw(l0 + 2 * BST, xw);
+      if (l0 + BST < l_end) tanh_bwd(l0 + BST, xn);
+    }
+  } else {
+    for (int l0 = l_beg + w; l0 < l_end; l0 += BST) {
+      if (l0 != l_beg + w) load_xw(l0, xw);
+      tanh_bwd(l0, xw);
     }
   }
   // fold the waves in a fixed order: dL/d(U h) into registers of threads e < E, then dL/dv
@@ -762,10 +827,10 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
     __hip_atomic_store(a.ticket + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // ready for the next step
   }
 }
-template <typename T, int DCH, int ECH, int FBW, int FBU>
+template <typename T, int DCH, int ECH, int FBW, int FBU, bool PIPE = false>
 __global__ __launch_bounds__(FBW * 64) void attn_bwd_split_kernel(AttnBwdArgs a) {
   const SatStampT0 t0 = sat_stamp_begin(a.st);
-  attn_bwd_split_kernel_body<T, DCH, ECH, FBW, FBU>(a);
+  attn_bwd_split_kernel_body<T, DCH, ECH, FBW, FBU, PIPE>(a);
   sat_stamp_end(a.st, t0);
 }
 
@@ -852,11 +917,11 @@ inline int e_chunks(int E, int VN) {
   return c <= 1 ? 1 : (c <= 2 ? 2 : 4);
 }
 
-template <typename T, int FDV, int NW = FNW, int FU = FFU>
+template <typename T, int FDV, int NW = FNW, int FU = FFU, bool PIPE = false>
 void launch_fwd(int ch, dim3 grid, hipStream_t s, const AttnFwdArgs& a) {
-  if (ch == 1) hipLaunchKernelGGL((attn_fwd_kernel<T, 1, FDV, NW, FU>), grid, dim3(NW * 64), 0, s, a);
-  else if (ch == 2) hipLaunchKernelGGL((attn_fwd_kernel<T, 2, FDV, NW, FU>), grid, dim3(NW * 64), 0, s, a);
-  else hipLaunchKernelGGL((attn_fwd_kernel<T, 4, FDV, NW, FU>), grid, dim3(NW * 64), 0, s, a);
+  if (ch == 1) hipLaunchKernelGGL((attn_fwd_kernel<T, 1, FDV, NW, FU, PIPE>), grid, dim3(NW * 64), 0, s, a);
+  else if (ch == 2) hipLaunchKernelGGL((attn_fwd_kernel<T, 2, FDV, NW, FU, PIPE>), grid, dim3(NW * 64), 0, s, a);
+  else hipLaunchKernelGGL((attn_fwd_kernel<T, 4, FDV, NW, FU, PIPE>), grid, dim3(NW * 64), 0, s, a);
 }
 
 }  // namespace
@@ -875,10 +940,18 @@ int sat_attention_fwd_launch(const AttnFwdArgs& args, hipStream_t s) {
   // x 8 slots per workgroup (half the resident waves) -- 6.61-6.66 vs 6.57-6.58 ms per overlapped step
   const int NS = sat_cdiv(a.D, 64 * VD * 2);
   dim3 grid(a.B, NS);
+  // more slots than one batch of 16 x 4 (L = 196): batches of 16 x 2, double-buffered (bit-identical; cfg5 step
+  // 10.75 -> 10.55 ms with the backward's likewise, profiles/r5_s19).  Measured and removed (profiles/r5_s21): the
+  // row split over L into chunks whose last arriver combines the softmax (flash-decoding): 30.3 -> 26.9 us alone
+  // with two chunks per row but the cfg5 step 10.53 -> 10.83 ms (twice the workgroups beside the trunk), four
+  // chunks 37.8 us
+  const bool pipe = a.L > FNW * FFU && sat_policy().attn_pipe != 1;
   if (a.dtype == SAT_BF16) {
-    launch_fwd<bf16, 2>(e_chunks(a.E, 8), grid, s, a);
+    if (pipe) launch_fwd<bf16, 2, FNW, 2, true>(e_chunks(a.E, 8), grid, s, a);
+    else launch_fwd<bf16, 2>(e_chunks(a.E, 8), grid, s, a);
   } else {
-    launch_fwd<float, 2>(e_chunks(a.E, 4), grid, s, a);
+    if (pipe) launch_fwd<float, 2, FNW, 2, true>(e_chunks(a.E, 4), grid, s, a);
+    else launch_fwd<float, 2>(e_chunks(a.E, 4), grid, s, a);
   }
   return (int)hipGetLastError();
 }
@@ -890,7 +963,11 @@ void launch_bwd_split_e(int nl, hipStream_t s, const AttnBwdArgs& a) {
   // FBU slots per wave per batch of loads.  Measured and not kept (profiles/r4_s4): one batch of 8 x 7 slots for the
   // L = 49 row at one workgroup per row (231 VGPRs instead of 171): 17.8 -> 18.7 us per step, step 6.56 -> 6.61 ms
   constexpr int FBU = DCH >= 8 ? 2 : 4;
-  hipLaunchKernelGGL((attn_bwd_split_kernel<T, DCH, ECH, 8, FBU>), dim3(a.B, nl), dim3(8 * 64), 0, s, a);
+  // chunks deeper than one batch of 8 x FBU slots (L = 196): batches of half the size, double-buffered
+  if (sat_cdiv(a.L, nl) > 8 * FBU && sat_policy().attn_pipe != 1)
+    hipLaunchKernelGGL((attn_bwd_split_kernel<T, DCH, ECH, 8, FBU / 2, true>), dim3(a.B, nl), dim3(8 * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((attn_bwd_split_kernel<T, DCH, ECH, 8, FBU>), dim3(a.B, nl), dim3(8 * 64), 0, s, a);
 }
 template <typename T, int DCH>
 bool launch_bwd_split_d(int ech, int nl, hipStream_t s, const AttnBwdArgs& a) {

@@ -1211,6 +1211,40 @@ def test_attention_backward_one_launch_matches_two(sat, dtype, D, bert):
         assert err < tol, (n, err)
 
 
+@pytest.mark.parametrize("dtype,D,bert,Lf", [(torch.bfloat16, 512, True, 196), (torch.float32, 512, False, 196),
+                                             (torch.bfloat16, 2048, False, 100)])
+def test_attention_forward_pipelined_bit_identical(sat, dtype, D, bert, Lf):
+    """attn_fwd_kernel / attn_bwd_split_kernel over more slots than one batch of loads (L = 196: VGG19 features;
+    L = 100) with the slot batches double-buffered (SatPolicy.attn_pipe 0, the default there) against one batch at
+    a time (attn_pipe 1): each wave sums its slots in the same order, so predictions, alphas and every gradient are
+    bit-identical (E = 768 with BERT embeddings: the two-chunk forward that spilled registers before) -- except the
+    dense embedding gradient, order-dependent run to run (fp32 atomics over repeated tokens)."""
+    B, T = 16, 7
+    V = 30522 if bert else 500
+    pad_id, skip_ids = sat.special_ids(bert)
+    res = []
+    for mode in (0, 1):
+        torch.manual_seed(0)
+        dec = sat.Decoder(V, D, tf=True, ado=not bert, bert=bert, attention=True).to(DEV).eval()
+        dec.policy = sat.Policy(attn_pipe=mode)
+        g = torch.Generator().manual_seed(4)
+        feats = torch.randn(B, Lf, D, generator=g).to(DEV).to(dtype)
+        caps = O.make_captions(B, T, V, 1, bert=bert).to(DEV)
+        preds, alphas = dec(feats, caps)
+        loss, _ = sat.caption_loss(preds, alphas, caps, pad_id=pad_id, skip_ids=skip_ids)
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append((preds.float().cpu(), alphas.cpu(), {n: p.grad.detach().float().cpu().clone()
+                                                        for n, p in dec.named_parameters() if p.grad is not None}))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert set(res[0][2]) == set(res[1][2]) and res[0][2]
+    for n, g0 in res[0][2].items():
+        if n == "embedding.weight":   # repeated tokens' rows meet in fp32 atomics (embed_scatter_kernel): run-to-run
+            assert ((g0 - res[1][2][n]).norm() / g0.norm()).item() < 1e-6
+            continue
+        assert torch.equal(g0, res[1][2][n]), n
+
+
 @pytest.mark.parametrize("M,N,K,bias", [(128, 4608, 512, True), (128, 2048, 2048, False), (100, 1024, 1024, True),
                                         (32, 64, 96, False), (7, 96, 32, True)])
 def test_skinny_gemm_direct(sat, M, N, K, bias):
