@@ -28,6 +28,7 @@ CLASSES = [
     ("L3dss2 1x1 512->1024 /2", 28, 512, 1024, 1, 2, 0, False),
     ("V4 3x3 128 (VGG19 block 2)", 112, 128, 128, 3, 1, 1, False),
     ("V7 3x3 256 (VGG19 block 3)", 56, 256, 256, 3, 1, 1, False),
+    ("V12 3x3 512 (VGG19 block 4)", 28, 512, 512, 3, 1, 1, False),
 ]
 POLICIES = [("default", {}), ("pipe off", dict(conv_pipe=1)), ("pipe all", dict(conv_pipe=2)),
             ("tile1", dict(conv_pipe=1, gemm_tile=1)), ("tile2", dict(conv_pipe=1, gemm_tile=2)),
@@ -75,7 +76,7 @@ def main():
                 us = st.elapsed_time(en) / 10 * 1e3
                 if ref is None:
                     ref = y
-                same = "=" if torch.equal(y, ref) else "~"
+                same = "=" if torch.equal(y, ref) else f"~{(y.float() - ref.float()).abs().max().item():.1e}"
                 line += f"  {label} {us:.1f}{same} ({flops / us / 1e6:.0f} TF/s)"
             except RuntimeError as exc:
                 line += f"  {label} err({str(exc)[:30]})"
