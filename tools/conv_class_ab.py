@@ -29,6 +29,10 @@ CLASSES = [
     ("V4 3x3 128 (VGG19 block 2)", 112, 128, 128, 3, 1, 1, False),
     ("V7 3x3 256 (VGG19 block 3)", 56, 256, 256, 3, 1, 1, False),
     ("V12 3x3 512 (VGG19 block 4)", 28, 512, 512, 3, 1, 1, False),
+    ("V11 3x3 256->512 (VGG19 block 4)", 28, 256, 512, 3, 1, 1, False),
+    ("V6 3x3 128->256 (VGG19 block 3)", 56, 128, 256, 3, 1, 1, False),
+    ("V3 3x3 64->128 (VGG19 block 2)", 112, 64, 128, 3, 1, 1, False),
+    ("V1 3x3 64 (VGG19 block 1)", 224, 64, 64, 3, 1, 1, False),
 ]
 POLICIES = [("default", {}), ("pipe off", dict(conv_pipe=1)), ("pipe all", dict(conv_pipe=2)),
             ("tile1", dict(conv_pipe=1, gemm_tile=1)), ("tile2", dict(conv_pipe=1, gemm_tile=2)),
