@@ -312,10 +312,6 @@ def conv_launches(network, B, H=224, fused=True, fused2=False):
     return out
 
 
-CONV_KERNEL_NAMES = ("fast_gemm_kernel", "conv_pipe_kernel", "conv1x1_stream_kernel", "bottleneck_kernel",
-                     "conv_ws_kernel", "conv3x3_frag_kernel", "conv3x3_band_kernel", "conv1x1_frag_kernel")
-
-
 def instep_conv_durations(stamps, launches, intervals=False):
     """Per conv launch (conv_launches() order), its in-step durations [us] from the encoder graphs'
     in-kernel timestamps (LaunchStamps, the last replay of each graph); intervals: launch-start to next

@@ -17,7 +17,7 @@ from bench import conv_launches, BF16_DENSE_PEAK_TFLOPS, HBM_PEAK_GBS  # noqa: E
 
 
 CONV_KERNELS = ("fast_gemm_kernel", "conv_pipe_kernel", "conv1x1_stream_kernel", "bottleneck_kernel",
-                "conv_ws_kernel", "conv3x3_frag_kernel", "conv3x3_band_kernel", "conv1x1_frag_kernel")
+                "conv_ws_kernel", "conv3x3_frag_kernel", "conv3x3_half512_kernel", "conv3x3_band", "conv1x1_frag_kernel")
 
 
 def is_conv_kernel(name):

@@ -22,7 +22,7 @@ from bench import conv_launches  # noqa: E402
 
 
 CONV_KERNELS = ("fast_gemm_kernel", "conv_pipe_kernel", "conv1x1_stream_kernel",
-                "bottleneck_kernel", "conv_ws_kernel", "conv3x3_frag_kernel", "conv3x3_band_kernel",
+                "bottleneck_kernel", "conv_ws_kernel", "conv3x3_frag_kernel", "conv3x3_half512_kernel", "conv3x3_band",
                 "conv1x1_frag_kernel", "conv1x1_frag2_kernel", "conv3x3_slice2_kernel", "conv3x3_img_kernel",
                 "block_band_kernel")
 
