@@ -933,8 +933,6 @@ int sat_attention_fwd_launch(const AttnFwdArgs& args, hipStream_t s) {
   SAT_REQUIRE(a.L <= kMaxL && a.E % VD == 0 && a.E <= 1024);
   SAT_REQUIRE((a.uh_ld % 4) == 0 && (a.hg_splits <= 1 || a.hg_split_stride % 4 == 0));
   SAT_REQUIRE(a.D % VD == 0);
-  // bf16: 1024-column slices by default; 512-column ones (twice the workgroups, SatPolicy::attn_fwd = 2) measured
-  // no faster at B = 64 (7.82 vs 7.79 us per step) and slower at B = 128 (15.2 vs 10.3 us): profiles/r3_s14/
   // one workgroup of 16 waves per (row, 1024 bf16 columns).  Measured and removed (profiles/r3_s14, r3_s19): 512-column
   // slices (twice the workgroups; bit-identical) -- no faster at B = 64, 15.2 vs 10.3 us per step at B = 128; 8 waves
   // x 8 slots per workgroup (half the resident waves) -- 6.61-6.66 vs 6.57-6.58 ms per overlapped step
