@@ -1,3 +1,6 @@
+# Same-box A/B of a whole round: the previous round's tree and HEAD, alternating bench runs (GPU).
+#   git worktree add -f _r4end <previous round's last commit>; make -C _r4end/show-attend-and-tell_amd/csrc
+#   gpurun -- 'bash tools/ab_round.sh'            (logs under gpurun_out/r5_s30/)
 set -u
 O=gpurun_out/r5_s30; mkdir -p $O
 A="--steps 150 --no-cpu-baseline --fp32-steps 0 --no-diagnostics"
