@@ -658,8 +658,6 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
   static_assert(MB * 16 == P1, "whole m-blocks of input rows");
   constexpr int ROWB = 128, X1PL = (P1 + 1) * ROWB, NPL = C / 64;
   constexpr int NT = 9 * C / 64, KS = 9 * C / 32;
-  constexpr int NCHUNK = P1 * C / 8, PER_T = NCHUNK / 512;
-  static_assert(NCHUNK % 512 == 0, "whole input chunks per thread");
   __shared__ __attribute__((aligned(16))) char smem[NPL * X1PL];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -669,11 +667,31 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
   const int y0 = half * RO, ws = half ? IH - R1 : 0;
   const long pix_img = (long)img * IH * IW;
 
-  // input rows ws .. ws + R1 - 1 are one contiguous block: chunk q = 16 B of pixel q / 32
-  uint4 xin[PER_T];
-  const uint4* xs = (const uint4*)(x + (pix_img + (long)ws * IW) * C);
+  // The input rows ws .. ws + R1 - 1 (one contiguous block) go HBM -> LDS by buffer_load ... lds, plane by plane: the
+  // k-loop is tap-major with the 64-channel plane innermost, so k-tile p needs planes 0 .. p only.  Each wave DMAs
+  // 1-KB pieces (8 pixel rows of one plane; lane l fetches the chunk that lands in swizzled slot l % 8) in the order
+  // plane 0, [bias, the first PF weight tiles], planes 1 .. NPL-1, and waits for plane p right before k-tile p with a
+  // vmcnt that counts only the later planes' DMAs (the compiler's weight loads may sit anywhere: counting none of
+  // them can only wait longer), so planes 1 .. NPL-1 arrive under the MFMAs of the k-tiles before them.
+  constexpr int NPC = P1 / 8, PPW = (NPC + 7) / 8;   // 1-KB pieces per plane, per wave
+  static_assert(P1 % 8 == 0 && PPW == 2, "whole pieces, two per wave");
+  const __amdgpu_buffer_rsrc_t rX =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(x + (pix_img + (long)ws * IW) * C), (short)0, P1 * C * 2, 0x00020000);
+  unsigned dsrc[PPW];
+  int dpc[PPW];
 #pragma unroll
-  for (int u = 0; u < PER_T; ++u) xin[u] = xs[u * 512 + tid];
+  for (int u = 0; u < PPW; ++u) {
+    const int d = w + 8 * u < NPC ? w + 8 * u : w;   // waves without a second piece repeat their first (same bytes)
+    dpc[u] = d;
+    dsrc[u] = (unsigned)(((d * 8 + (lane >> 3)) * C + 8 * ((lane & 7) ^ (lane >> 3))) * 2);
+  }
+  auto dma_plane = [&](int pl) {
+#pragma unroll
+    for (int u = 0; u < PPW; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (k_lds_void*)(smem + pl * X1PL + dpc[u] * 1024), 16,
+                                               (int)(dsrc[u] + pl * 128), 0, 0, 0);
+  };
+  dma_plane(0);
   float4 bv[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + w * 32 + j * 16 + 4 * fh);
@@ -687,14 +705,9 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
         dst[ks][j] = *(const bf16x8*)(wf + ((long)((w * 2 + j) * KS + 2 * T + ks) * 64 + lane) * 8);
   };
   static_for<PF>([&](auto e) { load_b(decltype(e)::value, bq[decltype(e)::value]); });
-
 #pragma unroll
-  for (int u = 0; u < PER_T; ++u) {
-    const int q = u * 512 + tid, r = q / (C / 8), c = q % (C / 8);
-    *(uint4*)(smem + (c >> 3) * X1PL + r * ROWB + 16 * ((c & 7) ^ (r & 7))) = xin[u];
-  }
+  for (int pl = 1; pl < NPL; ++pl) dma_plane(pl);
   if (tid < NPL * 8) *(uint4*)(smem + (tid >> 3) * X1PL + P1 * ROWB + (tid & 7) * 16) = make_uint4(0, 0, 0, 0);
-  k_lds_barrier();
 
   int offs[MB][2];
   auto tap_offsets = [&](int tap) {
@@ -720,6 +733,7 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
   bf16x8 af0[2][MB];
   static_for<NT>([&](auto Tc) {
     constexpr int T = decltype(Tc)::value, pl = T % NPL;
+    if constexpr (T < NPL) k_wait_barrier<PPW * (NPL - 1 - T)>();   // plane T (and the zero rows) in LDS
     if constexpr (T + PF < NT && !(ABL & 1)) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
     if constexpr (pl == 0) tap_offsets(T / NPL);
     const bf16x8 (&b)[2][2] = bq[(ABL & 1) ? T % PF : T % (PF + 1)];
@@ -780,11 +794,12 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
   constexpr int IH = IW, NPART = IH / RO, PO = RO * IW, MBT = (PO + 15) / 16;
   constexpr int MB = (MBT + WM - 1) / WM, WN = NWV / WM;   // m-blocks per wave; NWV waves = WM m-groups x WN
   constexpr int SLOTS = RO + 2, ZR = SLOTS * IW;        // LDS pixel rows + the zero row
-  constexpr int ROWB = 128, XPL = (ZR + 1) * ROWB, NPL = C / 64, NJ = C / (16 * WN * NSL), CS = C / NSL;
-  constexpr int NT = 9 * C / 64, KS = 9 * C / 32, CPP = C / 8;   // CPP: 16-B chunks per pixel
-  constexpr int NTH = NWV * 64, PER_T = (ZR * CPP + NTH - 1) / NTH;
-  static_assert(IH % RO == 0 && C % (16 * WN * NSL) == 0 && NJ >= 1 && NWV % WM == 0 && NPL * 8 <= NTH,
-                "whole bands, 16-channel n-blocks per wave");
+  constexpr int ROWB = 128, NPL = C / 64, NJ = C / (16 * WN * NSL), CS = C / NSL;
+  constexpr int NT = 9 * C / 64, KS = 9 * C / 32;
+  // LDS-DMA pieces of 1 KB = 8 pixel rows of one plane, the zero row included (its lanes read out of bounds: zeros)
+  constexpr int NPC = ZR / 8 + 1, PPW = (NPC + NWV - 1) / NWV, XPL = NPC * 1024;
+  static_assert(C % (16 * WN * NSL) == 0 && NJ >= 1 && NWV % WM == 0 && IH % RO == 0, "whole bands, 16-channel n-blocks per wave");
+  static_assert(PPW * (NPL - 1) < 64, "plane waits fit vmcnt");
   __shared__ __attribute__((aligned(16))) char smem[NPL * XPL];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -799,16 +814,33 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
   const int img = band / NPART, part = band % NPART;
   const int y0 = part * RO;
   const int cb = slice * CS;                       // first output channel of this workgroup
-  const int s_lo = y0 == 0 ? 1 : 0, s_hi = y0 + RO == IH ? RO : RO + 1;   // slots inside the image
-  const int nchunk = (s_hi - s_lo + 1) * IW * CPP;
   const long pix_img = (long)img * IH * IW;
   const unsigned lane_b = (unsigned)lane * 16;
 
-  // the valid slots are one contiguous block of image rows
-  uint4 xin[PER_T];
-  const uint4* xs = (const uint4*)(x + (pix_img + (long)(y0 - 1 + s_lo) * IW) * C);
+  // Slot s holds image row y0 - 1 + s: the slots are consecutive image rows, so pixel row r of a plane is image pixel
+  // (y0 - 1) IW + r.  They go HBM -> LDS by buffer_load ... lds, plane by plane (lane l of a piece fetches the chunk
+  // that lands in swizzled slot l % 8); rows above or below the image and the zero row read out of bounds (zeros).
+  // Order: plane 0, [bias, the first PF weight tiles], planes 1 .. NPL-1; k-tile p (tap-major, plane innermost) waits
+  // for plane p with a vmcnt counting only the later planes' DMAs (the compiler's weight loads may sit anywhere:
+  // counting none of them can only wait longer), so the later planes arrive under the first k-tiles' MFMAs.
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)(x + pix_img * C), (short)0,
+                                                                       IH * IW * C * 2, 0x00020000);
+  unsigned dsrc[PPW];
+  int dpc[PPW];
 #pragma unroll
-  for (int u = 0; u < PER_T; ++u) xin[u] = xs[min(u * NTH + tid, nchunk - 1)];
+  for (int u = 0; u < PPW; ++u) {
+    const int d = w + NWV * u < NPC ? w + NWV * u : w;   // waves without another piece repeat their first (same bytes)
+    const int r = d * 8 + (lane >> 3), g = (y0 - 1) * IW + r;
+    dpc[u] = d;
+    dsrc[u] = r < ZR && g >= 0 ? (unsigned)((g * C + 8 * ((lane & 7) ^ (lane >> 3))) * 2) : K_OOB;
+  }
+  auto dma_plane = [&](int pl) {
+#pragma unroll
+    for (int u = 0; u < PPW; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (k_lds_void*)(smem + pl * XPL + dpc[u] * 1024), 16,
+                                               dsrc[u] == K_OOB ? (int)K_OOB : (int)(dsrc[u] + pl * 128), 0, 0, 0);
+  };
+  dma_plane(0);
   float4 bv[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) bv[j] = *(const float4*)(bias + cb + (wn * NJ + j) * 16 + 4 * fh);
@@ -823,12 +855,7 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
   };
   static_for<PF>([&](auto e) { load_b(decltype(e)::value, bq[decltype(e)::value]); });
 #pragma unroll
-  for (int u = 0; u < PER_T; ++u) {
-    const int q = u * NTH + tid, r = s_lo * IW + q / CPP, c = q % CPP;
-    if (q < nchunk) *(uint4*)(smem + (c >> 3) * XPL + r * ROWB + 16 * ((c & 7) ^ (r & 7))) = xin[u];
-  }
-  if (tid < NPL * 8) *(uint4*)(smem + (tid >> 3) * XPL + ZR * ROWB + (tid & 7) * 16) = make_uint4(0, 0, 0, 0);
-  k_lds_barrier();
+  for (int pl = 1; pl < NPL; ++pl) dma_plane(pl);
 
   int offs[MB][2];
   auto tap_offsets = [&](int tap) {
@@ -851,6 +878,7 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
   static_for<NT>([&](auto Tc) {
     constexpr int T = decltype(Tc)::value, pl = T % NPL;
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (T < NPL) k_wait_barrier<PPW * (NPL - 1 - T)>();   // plane T in LDS
     if constexpr (T + PF < NT) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
     if constexpr (pl == 0) tap_offsets(T / NPL);
     const bf16x8 (&b)[2][NJ] = bq[T % (PF + 1)];
