@@ -114,6 +114,9 @@ __device__ __forceinline__ u32x2 relu_bf16x4(const f32x4& a, const float4& b) {
   ob[3] = (bf16)fmaxf(a[3] + b.w, 0.f);
   return o;
 }
+#ifndef SAT_C2_PF   // the half-image 3x3 kernel's weight prefetch distance in k-tiles: 3 since its input staging
+#define SAT_C2_PF 3   // moved to LDS-DMA (227 VGPRs); step 6.294-6.317 -> 6.273 ms, 4: 6.287-6.293 (profiles/r5_s38, r5_s39)
+#endif
 #ifndef SAT_PAIR_STORES   // diagnostics builds: 0 = the 8-B stores of each lane's own accumulators
 #define SAT_PAIR_STORES 1
 #endif
@@ -1411,7 +1414,7 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   const int mode = sat_frag_slices(N);
   const int groups = sat_cdiv(2 * N, 8) * 8 * 2;   // whole groups of 8 half images x 2 slices
   if (mode == 1)
-    hipLaunchKernelGGL(conv3x3_frag_kernel<2>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp, st);
+    hipLaunchKernelGGL(conv3x3_frag_kernel<SAT_C2_PF>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp, st);
   else
     hipLaunchKernelGGL(conv3x3_slice2_kernel, dim3(groups), dim3(256), 0, s, xp, wp, b, yp, 2 * N, st);
   return (int)hipGetLastError();
