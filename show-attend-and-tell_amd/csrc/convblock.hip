@@ -117,6 +117,9 @@ __device__ __forceinline__ u32x2 relu_bf16x4(const f32x4& a, const float4& b) {
 #ifndef SAT_C2_PF   // the half-image 3x3 kernel's weight prefetch distance in k-tiles: 3 since its input staging
 #define SAT_C2_PF 3   // moved to LDS-DMA (227 VGPRs); step 6.294-6.317 -> 6.273 ms, 4: 6.287-6.293 (profiles/r5_s38, r5_s39)
 #endif
+#ifndef SAT_C1_PF   // diagnostics builds: the half-image 1x1 kernel's weight prefetch distance in k-tiles
+#define SAT_C1_PF 2
+#endif
 #ifndef SAT_PAIR_STORES   // diagnostics builds: 0 = the 8-B stores of each lane's own accumulators
 #define SAT_PAIR_STORES 1
 #endif
@@ -1253,7 +1256,7 @@ __global__ __launch_bounds__(512) void conv1x1_frag_kernel(const bf16* __restric
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
                                                            unsigned x_bytes, SatStamps st) {
   const SatStampT0 t0 = sat_stamp_begin(st);
-  conv1x1_frag_body<14, 7, 1024, 256, 2>(x, wf, bias, y, x_bytes, (int)gridDim.x);
+  conv1x1_frag_body<14, 7, 1024, 256, SAT_C1_PF>(x, wf, bias, y, x_bytes, (int)gridDim.x);
   sat_stamp_end(st, t0);
 }
 
