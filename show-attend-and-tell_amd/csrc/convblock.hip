@@ -117,6 +117,9 @@ __device__ __forceinline__ u32x2 relu_bf16x4(const f32x4& a, const float4& b) {
 #ifndef SAT_C2_PF   // the half-image 3x3 kernel's weight prefetch distance in k-tiles: 3 since its input staging
 #define SAT_C2_PF 3   // moved to LDS-DMA (227 VGPRs); step 6.294-6.317 -> 6.273 ms, 4: 6.287-6.293 (profiles/r5_s38, r5_s39)
 #endif
+#ifndef SAT_SL2_PF   // diagnostics builds: the two-slice 3x3 kernel's weight prefetch distance in k-tiles
+#define SAT_SL2_PF 2
+#endif
 #ifndef SAT_C1_PF   // diagnostics builds: the half-image 1x1 kernel's weight prefetch distance in k-tiles
 #define SAT_C1_PF 2
 #endif
@@ -1122,7 +1125,7 @@ __global__ __launch_bounds__(256) void conv3x3_slice2_kernel(const bf16* __restr
                                                              const float* __restrict__ bias, bf16* __restrict__ y,
                                                              int nbands, SatStamps st) {
   const SatStampT0 t0 = sat_stamp_begin(st);
-  conv3x3_band_body<14, 7, 256, 2, 1, 2, 4>(x, wf, bias, y, nbands);
+  conv3x3_band_body<14, 7, 256, 2, 1, SAT_SL2_PF, 4>(x, wf, bias, y, nbands);
   sat_stamp_end(st, t0);
 }
 
@@ -1414,7 +1417,11 @@ extern "C" int sat_conv3x3_frag(int N, int H, int W, int C, int dtype, const voi
   }
   // layer3 c2: half images (two workgroups per image), or two channel slices per half image when the half
   // images alone would leave CUs idle (SatPolicy::conv_slices)
+#ifdef SAT_C2_FORCE_SLICES   // diagnostics builds: layer3 c2 in the given form whatever the batch
+  const int mode = SAT_C2_FORCE_SLICES;
+#else
   const int mode = sat_frag_slices(N);
+#endif
   const int groups = sat_cdiv(2 * N, 8) * 8 * 2;   // whole groups of 8 half images x 2 slices
   if (mode == 1)
     hipLaunchKernelGGL(conv3x3_frag_kernel<SAT_C2_PF>, dim3(2 * N), dim3(512), 0, s, xp, wp, b, yp, st);
