@@ -320,7 +320,10 @@ int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err) {
   // NB = 2 (256-column slices; each A fragment read feeds two MFMAs) when N allows it, 32-row items;
   // NB = 1 (128-column slices) otherwise, 64-row items (32 at K = 512)
   const int NB = g.N % (2 * S_BN) == 0 ? 2 : 1;
-  const int MB = NB == 2 ? (K == 64 ? 4 : 2) : (K >= 512 ? 2 : 4);
+#ifndef SAT_STREAM_MB256   // diagnostics builds: 16-row blocks per item at K = 256 with 256-column slices
+#define SAT_STREAM_MB256 2
+#endif
+  const int MB = NB == 2 ? (K == 64 ? 4 : K == 256 ? SAT_STREAM_MB256 : 2) : (K >= 512 ? 2 : 4);
   const int MT = MB * 16;
   const int slices = g.N / (S_BN * NB);
   const int items = sat_cdiv(g.M, MT);
@@ -352,7 +355,7 @@ int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err) {
     switch (K) {
       case 64: launch_kt<2, 4, 2>(res, strided, g.act, grid, s, a); break;
       case 128: launch_kt<4, 2, 2>(res, strided, g.act, grid, s, a); break;
-      case 256: launch_kt<8, 2, 2>(res, strided, g.act, grid, s, a); break;
+      case 256: launch_kt<8, SAT_STREAM_MB256, 2>(res, strided, g.act, grid, s, a); break;
       default: launch_kt<16, 2, 2>(res, strided, g.act, grid, s, a); break;
     }
   } else {
