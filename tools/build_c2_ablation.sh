@@ -6,6 +6,6 @@ cd "$(dirname "$0")/../show-attend-and-tell_amd/csrc"
 make -s -j8
 for n in "$@"; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -DSAT_C2_ABL=$n -c convblock.hip -o build/convblock_abl$n.o
-  objs=$(ls build/*.o | grep -v convblock | grep -v _abl)
+  objs=$(ls build/*.o | grep -v convblock | grep -v _abl | grep -v _v_)
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../libsat_hip_abl$n.so $objs build/convblock_abl$n.o
 done
