@@ -96,6 +96,29 @@ constexpr int younger_than_a(int T, int KT1, int NT, int PF, bool stream, int nb
   return n;
 }
 
+// the same count for a ring whose input DMAs run `da` k-tiles ahead: prologue A0 B0 A1 B1 .. (A(e) for e < da, B(e)
+// for e < PF, interleaved), then per k-tile after its wait A(it + da) (< KT1), B(it + PF) (< NT, when weights stream)
+constexpr int younger_than_a_da(int T, int KT1, int NT, int PF, int da, int nb, int na) {
+  int n = 0;
+  bool after = false;
+  auto ev_a = [&](int idx) {
+    if (after) n += na;
+    if (idx == T) after = true;
+  };
+  auto ev_b = [&]() {
+    if (after) n += nb;
+  };
+  for (int e = 0; e < (da > PF ? da : PF); ++e) {
+    if (e < da) ev_a(e);
+    if (e < PF) ev_b();
+  }
+  for (int it = 0; it < T; ++it) {
+    if (it + da < KT1) ev_a(it + da);
+    if (it + PF < NT) ev_b();
+  }
+  return n;
+}
+
 // IW: image width = height, RO: output image rows per workgroup (IW % RO == 0, IW / RO == 2),
 // CIN: block input/output channels, CMID: bottleneck width (256: one 256-wide phase per conv);
 // PF: weight prefetch distance in k-tiles; ABL (diagnostics, tools/block_ab.py): bit 0 no MFMA,
@@ -119,6 +142,9 @@ __device__ __forceinline__ u32x2 relu_bf16x4(const f32x4& a, const float4& b) {
 #endif
 #ifndef SAT_SL2_PF   // diagnostics builds: the two-slice 3x3 kernel's weight prefetch distance in k-tiles
 #define SAT_SL2_PF 2
+#endif
+#ifndef SAT_C1_DA   // diagnostics builds: the half-image 1x1 kernel's input DMAs this many k-tiles ahead
+#define SAT_C1_DA 2
 #endif
 #ifndef SAT_C1_PF   // diagnostics builds: the half-image 1x1 kernel's weight prefetch distance in k-tiles
 #define SAT_C1_PF 2
@@ -1137,7 +1163,7 @@ __global__ __launch_bounds__(256) void conv3x3_slice2_kernel(const bf16* __restr
 // counted vmcnt + one barrier per k-tile), the weights register-direct two k-tiles ahead.  The tile
 // kernel (convpipe.hip) runs this shape as 196 tiles of 256 x 128 that each fetch 768 KB; here 256
 // workgroups each fetch 712 KB.  Same k order, bias, ReLU and rounding: bit-identical.
-template <int IW, int RO, int CI, int CM, int PF, int NSL = 1>
+template <int IW, int RO, int CI, int CM, int PF, int NSL = 1, int DA = 2>   // DA: input DMAs DA k-tiles ahead (ring of DA + 1)
 __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, const bf16* __restrict__ wf,
                                                   const float* __restrict__ bias, bf16* __restrict__ y,
                                                   unsigned x_bytes, int nhalves) {
@@ -1149,7 +1175,7 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
   constexpr int NT = CI / 64, KS = CI / 32;
   constexpr int NJ = 2 / NSL;                   // 16-channel n-blocks per wave (NSL channel slices per half image)
   static_assert(NSL == 1 || NSL == 2, "one or two channel slices");
-  __shared__ __attribute__((aligned(16))) char smem[3 * STG];
+  __shared__ __attribute__((aligned(16))) char smem[(DA + 1) * STG];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1170,7 +1196,7 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
     dsrc[u] = r < PO ? (unsigned)(((pix0 + r) * CI + 8 * c) * 2) : K_OOB;
   }
   auto dma_a = [&](int t) {
-    char* st = smem + (t % 3) * STG;
+    char* st = smem + (t % (DA + 1)) * STG;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (k_lds_void*)(st + (w * 2 + u) * 1024), 16,
@@ -1196,23 +1222,23 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // issue order A0 B0 A1 B1 B2 .. B(PF-1), then per k-tile after its wait A(T+2), B(T+PF): the order
-  // younger_than_a() counts (bias loads are older than A0 and retire first)
-  dma_a(0);
-  load_b(0, bq[0]);
-  dma_a(1);
-  load_b(1, bq[1]);
-  static_for<PF - 2>([&](auto e) { load_b(2 + decltype(e)::value, bq[2 + decltype(e)::value]); });
+  // issue order A0 B0 A1 B1 .. (A(e) for e < DA, B(e) for e < PF, interleaved), then per k-tile after its wait
+  // A(T+DA), B(T+PF): the order younger_than_a_da() counts (bias loads are older than A0 and retire first)
+  static_for<(DA > PF ? DA : PF)>([&](auto e) {
+    constexpr int E = decltype(e)::value;
+    if constexpr (E < DA) dma_a(E);
+    if constexpr (E < PF) load_b(E, bq[E]);
+  });
 
   static_for<NT>([&](auto Tc) {
     constexpr int T = decltype(Tc)::value;
     // this wave's DMAs of tile T have landed, every wave's too after the barrier; the barrier also
     // retires every wave's reads of stage (T + 2) % 3 (tile T - 1) before it is refilled
-    k_wait_barrier<younger_than_a(T, NT, NT, PF, true, 2 * NJ)>();
-    if constexpr (T + 2 < NT) dma_a(T + 2);
+    k_wait_barrier<younger_than_a_da(T, NT, NT, PF, DA, 2 * NJ, 2)>();
+    if constexpr (T + DA < NT) dma_a(T + DA);
     if constexpr (T + PF < NT) load_b(T + PF, bq[(T + PF) % (PF + 1)]);
     const bf16x8 (&b)[2][NJ] = bq[T % (PF + 1)];
-    const char* st = smem + (T % 3) * STG;
+    const char* st = smem + (T % (DA + 1)) * STG;
     bf16x8 af[2][MB];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -1259,7 +1285,7 @@ __global__ __launch_bounds__(512) void conv1x1_frag_kernel(const bf16* __restric
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
                                                            unsigned x_bytes, SatStamps st) {
   const SatStampT0 t0 = sat_stamp_begin(st);
-  conv1x1_frag_body<14, 7, 1024, 256, SAT_C1_PF>(x, wf, bias, y, x_bytes, (int)gridDim.x);
+  conv1x1_frag_body<14, 7, 1024, 256, SAT_C1_PF, 1, SAT_C1_DA>(x, wf, bias, y, x_bytes, (int)gridDim.x);
   sat_stamp_end(st, t0);
 }
 
