@@ -315,6 +315,9 @@ int sat_conv_stream_try(const SatGemm& g, hipStream_t s, int* err) {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
       return 0;
+#ifdef SAT_STREAM_CUS   // diagnostics builds: size the persistent grids for this many CUs (the rest left to a
+    n = SAT_STREAM_CUS;    // concurrent decoder)
+#endif
     g_stream_cus = n;
   }
   // NB = 2 (256-column slices; each A fragment read feeds two MFMAs) when N allows it, 32-row items;
