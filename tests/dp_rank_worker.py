@@ -1,5 +1,6 @@
 """One rank of the data-parallel GPU test (tests/test_gpu_dp.py launches two of these, gloo, both on
-cuda:0).  Not a test module: run as ``python tests/dp_rank_worker.py RANK WORLD INIT_FILE OUT [CASE]`` (CASE: a DP_CASES key).
+cuda:0, or one over RCCL: SAT_DP_BACKEND=nccl).  Not a test module: run as
+``python tests/dp_rank_worker.py RANK WORLD INIT_FILE OUT [CASE]`` (CASE: a DP_CASES key).
 
 Each rank takes its contiguous half of a global fp32 batch and runs the train step (train.py:128-164)
 through the HIP decoder twice:
@@ -62,16 +63,22 @@ def weights(dec):
 def main():
     rank, world, init_file, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
     c = DP_CASES[sys.argv[5] if len(sys.argv) > 5 else "toy_fp32"]
-    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    backend = os.environ.get("SAT_DP_BACKEND", "gloo")   # "nccl" is RCCL on ROCm (one rank per GPU)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", init_method=f"file://{init_file}", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
     import sat_amd
     from sat_amd.distributed import GradAllReduce, allreduce_bucket_async, shard_batch
     p, feats, caps, mask = case_inputs(c)
     f_loc = shard_batch(feats, rank, world).contiguous().to(dev)
     c_loc = shard_batch(caps, rank, world).contiguous().to(dev)
     m_loc = shard_batch(mask, rank, world).contiguous().to(dev)   # on the device: no copy inside a capture
-    res = {}
+    res = {"backend": dist.get_backend()}
+    if backend == "nccl":
+        res["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
 
     # -- eager: hook-driven bucket all-reduce
     dec = make_decoder(sat_amd, p, dev, c)

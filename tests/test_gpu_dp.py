@@ -105,3 +105,31 @@ def test_dp_two_ranks_equal_full_batch(sat, tmp_path, case):
     # library-drawn dropout: independent per rank in train mode, identical in eval mode
     assert torch.equal(res[0]["eval_preds"], res[1]["eval_preds"])
     assert not torch.equal(res[0]["train_preds"], res[1]["train_preds"])
+
+
+def test_dp_rccl_single_rank_equals_full_batch(sat, tmp_path):
+    """The RCCL leg of the same schedule (bench.py's default backend): one rank over the nccl backend (RCCL) on the
+    one GPU of the box, so torch.distributed's RCCL communicator, the ReduceOp.AVG bucket all-reduce of
+    sat_amd.distributed (eager hooks and the async form between the two graph replays) and their stream ordering run
+    on the device; with one rank the average is the identity, so both forms must reproduce the full-batch run."""
+    init, out = tmp_path / "init", tmp_path / "rank0.pt"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", SAT_DP_BACKEND="nccl")
+    pr = subprocess.run([sys.executable, os.path.join(HERE, "dp_rank_worker.py"), "0", "1", str(init), str(out),
+                         "toy_fp32"], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
+    assert pr.returncode == 0, pr.stdout[-3000:]
+    res = torch.load(out, weights_only=True)
+    assert res["backend"] == "nccl" and res["rccl_version"], res.get("backend")
+    g_full, w_full = _full_batch(sat, "toy_fp32")
+    tol_norm, tol_elem, _ = TOL["toy_fp32"]
+    for form in ("eager", "graph"):
+        g, w = res[f"{form}_grads"], res[f"{form}_weights"]
+        assert sorted(g) == sorted(g_full)
+        for n, ref in g_full.items():
+            got = g[n]
+            assert torch.isfinite(got).all(), (form, n)
+            if ref.norm().item() < 1e-7:   # attention.v.bias: analytically zero
+                assert got.abs().max().item() < 1e-5, (form, n)
+                continue
+            assert ((got - ref).norm() / ref.norm()).item() < tol_norm, (form, n)
+            assert (got - ref).abs().max().item() <= tol_elem * ref.abs().max().item(), (form, n)
+            assert torch.isfinite(w[n]).all(), (form, n)
