@@ -149,6 +149,16 @@ __device__ __forceinline__ u32x2 relu_bf16x4(const f32x4& a, const float4& b) {
 #ifndef SAT_C1_PF   // diagnostics builds: the half-image 1x1 kernel's weight prefetch distance in k-tiles
 #define SAT_C1_PF 2
 #endif
+// Weight-stream rotation (XCD-aware): the workgroups that share an XCD's L2 (blockIdx.x % 8 under round-robin
+// placement) start their waves on different channel groups, so at any moment they fetch different weight lines
+// instead of all hammering the same L2 channel: layer3 c2 29.2 -> 26.8 us per launch (profiles/r5_s60).
+// SAT_C2_ROT (layer3 c2): 1 rotate by blockIdx.x / 8, 2 by blockIdx.x, 0 off; SAT_WROT: the band and 1x1 forms.
+#ifndef SAT_C2_ROT
+#define SAT_C2_ROT 1
+#endif
+#ifndef SAT_WROT
+#define SAT_WROT 1
+#endif
 #ifndef SAT_PAIR_STORES   // diagnostics builds: 0 = the 8-B stores of each lane's own accumulators
 #define SAT_PAIR_STORES 1
 #endif
@@ -698,6 +708,9 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fh = lane >> 4;
+  // SAT_C2_ROT (diagnostics): the workgroups sharing an XCD (blockIdx.x % 8) rotate which 32-channel group each wave
+  // owns, so at any moment they stream different weight lines
+  const int wc = SAT_C2_ROT ? __builtin_amdgcn_readfirstlane((w + (int)(blockIdx.x >> (SAT_C2_ROT == 1 ? 3 : 0))) & 7) : w;
   const int img = blockIdx.x >> 1, half = blockIdx.x & 1;
   const int y0 = half * RO, ws = half ? IH - R1 : 0;
   const long pix_img = (long)img * IH * IW;
@@ -729,7 +742,7 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
   dma_plane(0);
   float4 bv[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + w * 32 + j * 16 + 4 * fh);
+  for (int j = 0; j < 2; ++j) bv[j] = *(const float4*)(bias + wc * 32 + j * 16 + 4 * fh);
 
   bf16x8 bq[PF + 1][2][2];
   auto load_b = [&](int T, bf16x8 (&dst)[2][2]) {
@@ -737,7 +750,7 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-        dst[ks][j] = *(const bf16x8*)(wf + ((long)((w * 2 + j) * KS + 2 * T + ks) * 64 + lane) * 8);
+        dst[ks][j] = *(const bf16x8*)(wf + ((long)((wc * 2 + j) * KS + 2 * T + ks) * 64 + lane) * 8);
   };
   static_for<PF>([&](auto e) { load_b(decltype(e)::value, bq[decltype(e)::value]); });
 #pragma unroll
@@ -798,7 +811,7 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
   if constexpr (SAT_PAIR_STORES) {
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
-      const unsigned o0 = (unsigned)(((pix_img + (long)y0 * IW + i * 16 + fr) * C + w * 32 + 4 * fh) * 2);
+      const unsigned o0 = (unsigned)(((pix_img + (long)y0 * IW + i * 16 + fr) * C + wc * 32 + 4 * fh) * 2);
       sat_st_pair16(rY, o0, o0 + 32, relu_bf16x4(acc[i][0], bv[0]), relu_bf16x4(acc[i][1], bv[1]), i * 16 + fr < PO,
                 i * 16 + fr < PO);
     }
@@ -808,7 +821,7 @@ __device__ __forceinline__ void conv3x3_frag_body(const bf16* __restrict__ x, co
 #pragma unroll
       for (int i = 0; i < MB; ++i)
         if (i * 16 + fr < PO)
-          sat_st8(rY, (unsigned)(((pix_img + (long)y0 * IW + i * 16 + fr) * C + w * 32 + j * 16 + 4 * fh) * 2),
+          sat_st8(rY, (unsigned)(((pix_img + (long)y0 * IW + i * 16 + fr) * C + wc * 32 + j * 16 + 4 * fh) * 2),
                   relu_bf16x4(acc[i][j], bv[j]));
   }
 }
@@ -840,7 +853,10 @@ __device__ __forceinline__ void conv3x3_band_body(const bf16* __restrict__ x, co
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fh = lane >> 4;
-  const int wm = w % WM, wn = w / WM;              // this wave's m-group and n-group
+  const int wm = w % WM;                           // this wave's m-group and (rotated, SAT_WROT) n-group
+  // (not the four-wave layer2 form: at 254 VGPRs the rotation tips it into scratch)
+  constexpr bool ROT = SAT_WROT && !(NWV == 4 && NSL == 1);
+  const int wn = ROT ? __builtin_amdgcn_readfirstlane((w / WM + (int)(blockIdx.x >> 3)) % WN) : w / WM;
   // slice-major over groups of 8 consecutive workgroups (one per XCD under round-robin placement), so the
   // NSL slices of one band land on one XCD and share its input rows in L2
   const int slice = NSL == 1 ? 0 : (int)((blockIdx.x >> 3) % NSL);
@@ -1185,7 +1201,8 @@ __device__ __forceinline__ void conv1x1_frag_body(const bf16* __restrict__ x, co
   const int slice = NSL == 1 ? 0 : (int)((blockIdx.x >> 3) % NSL);
   const int hb = NSL == 1 ? (int)blockIdx.x : (int)((blockIdx.x / (8 * NSL)) * 8 + (blockIdx.x & 7));
   if (hb >= nhalves) return;
-  const int nb0 = slice * (CM / 16 / NSL) + w * NJ;   // this wave's first 16-channel n-block
+  const int wr = SAT_WROT ? __builtin_amdgcn_readfirstlane((w + (int)(blockIdx.x >> 3)) & 7) : w;   // rotated group
+  const int nb0 = slice * (CM / 16 / NSL) + wr * NJ;   // this wave's first 16-channel n-block
   const long pix0 = (long)(hb >> 1) * IH * IW + (long)(hb & 1) * PO;
 
   const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)x_bytes, 0x00020000);
