@@ -1053,6 +1053,9 @@ __device__ __forceinline__ void conv3x3_img_body(const bf16* __restrict__ x, con
   const int img0 = grp * G, nv = min(G, nimg - img0) * PI;   // valid pixels of this group
   const int cb = slice * CS;
   const unsigned lane_b = (unsigned)lane * 16;
+  // XCD-aware weight rotation (SAT_WROT, as the band forms): the workgroups of one slice sharing an XCD start their
+  // waves on different channel groups
+  const int wr = SAT_WROT ? __builtin_amdgcn_readfirstlane((w + (int)((blockIdx.x >> 3) / NSL)) & 7) : w;
 
   uint4 xin[PER_T];
   const uint4* xs = (const uint4*)(x + (long)img0 * PI * C);
@@ -1060,14 +1063,14 @@ __device__ __forceinline__ void conv3x3_img_body(const bf16* __restrict__ x, con
   for (int u = 0; u < PER_T; ++u) xin[u] = xs[min(u * 512 + tid, nv * CPP - 1)];
   float4 bv[NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) bv[j] = *(const float4*)(bias + cb + (w * NJ + j) * 16 + 4 * fh);
+  for (int j = 0; j < NJ; ++j) bv[j] = *(const float4*)(bias + cb + (wr * NJ + j) * 16 + 4 * fh);
   bf16x8 bq[PF + 1][2][NJ];
   auto load_b = [&](int T, bf16x8 (&dst)[2][NJ]) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-        dst[ks][j] = *(const bf16x8*)((const char*)wf + (size_t)((cb / 16 + w * NJ + j) * KS + 2 * T + ks) * 1024 + lane_b);
+        dst[ks][j] = *(const bf16x8*)((const char*)wf + (size_t)((cb / 16 + wr * NJ + j) * KS + 2 * T + ks) * 1024 + lane_b);
   };
   static_for<PF>([&](auto e) { load_b(decltype(e)::value, bq[decltype(e)::value]); });
 #pragma unroll
@@ -1116,7 +1119,7 @@ __device__ __forceinline__ void conv3x3_img_body(const bf16* __restrict__ x, con
     }
   });
 
-  char* y_s = (char*)(y + (long)img0 * PI * C + cb + w * NJ * 16);
+  char* y_s = (char*)(y + (long)img0 * PI * C + cb + wr * NJ * 16);
   const unsigned row_b = (unsigned)(fr * C + 4 * fh) * 2;
   if constexpr (NJ % 2 == 0 && SAT_PAIR_STORES) {
 #pragma unroll
