@@ -645,6 +645,12 @@ def dist_info(args, world):
     return info
 
 
+# Graph captures run in thread-local capture mode: at N > 1 the RCCL process group's watchdog thread keeps querying
+# the events of the warm-up's all-reduces, and under the default (global) mode such a query from another thread
+# while this thread captures aborts the process (hipErrorStreamCaptureUnsupported; tests/test_gpu_dp.py's RCCL case)
+CAPTURE_MODE = "thread_local"
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -752,7 +758,7 @@ def main():
                 G["stamps_enc"].append(LaunchStamps(len(launches), dev, base=policy))
                 enc.launch_policy = G["stamps_enc"][-1].next_policy
             g = torch.cuda.CUDAGraph()   # one private memory pool per graph: no intermediate aliases another's
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                 with torch.no_grad():
                     G["feats"].append(enc(imgs))
             enc.launch_policy = None
@@ -764,13 +770,13 @@ def main():
                 dec.policy = G["stamps_dec"][-1].policy
             opt.zero_grad(set_to_none=True)   # each capture overwrites the gradients (beta = 0)
             gd, gr = torch.cuda.CUDAGraph(), None
-            with torch.cuda.graph(gd):
+            with torch.cuda.graph(gd, capture_error_mode=CAPTURE_MODE):
                 preds, alphas = dec(G["feats"][k], caps)
                 loss_k, _ = sat_amd.caption_loss(preds, alphas, caps, pad_id=pad_id, skip_ids=skip_ids)
                 loss_k.backward()
             if split_bwd:
                 gr = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gr):
+                with torch.cuda.graph(gr, capture_error_mode=CAPTURE_MODE):
                     dec.finish_backward()
             G["dec"].append(gd)
             G["rec"].append(gr)

@@ -107,10 +107,11 @@ def main():
     dec.defer_recurrent_backward(True)
     opt.zero_grad(set_to_none=True)
     g_dec, g_rec = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g_dec):
+    # thread-local capture: the RCCL watchdog thread may still query the eager all-reduces' events (bench.py)
+    with torch.cuda.graph(g_dec, capture_error_mode="thread_local"):
         preds, alphas = dec(f_loc, c_loc)
         sat_amd.caption_loss(preds, alphas, c_loc)[0].backward()
-    with torch.cuda.graph(g_rec):
+    with torch.cuda.graph(g_rec, capture_error_mode="thread_local"):
         dec.finish_backward()
     dec.defer_recurrent_backward(False)
     dec._grad_flat.fill_(float("nan"))   # every replay must overwrite the whole gradient
