@@ -66,6 +66,10 @@ def parse():
                     help="BPTT input-gradient products on the k-major weights instead of the transposed copies (A/B)")
     ap.add_argument("--no-skinny", action="store_true",
                     help="per-step decoder GEMMs on the LDS-DMA tile kernel instead of csrc/skinny.hip (A/B)")
+    ap.add_argument("--dp-rehearse", action="store_true",
+                    help="N = 1 only: run the data-parallel path anyway (a one-rank process group over --dist-backend: "
+                         "the eager warm-up's bucket all-reduces, the graphs captured beside the live watchdog, the "
+                         "async bucket all-reduces between replays) -- the RCCL code of the N > 1 runs on a one-GPU box")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="N > 1: RCCL (one rank per GPU) or gloo (rehearsal: several ranks may share a GPU)")
     ap.add_argument("--gemm-stages", type=int, default=0, choices=[0, 2, 3],
@@ -634,7 +638,7 @@ def launch_ranks(args, argv):
 
 def dist_info(args, world):
     """the process group the step all-reduces over (N > 1) and the collective library's version"""
-    if world == 1:
+    if not dist.is_initialized():
         return {"backend": None, "world_size": 1}
     info = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
     if info["backend"] == "nccl":   # "nccl" is RCCL on ROCm
@@ -658,12 +662,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
+    dp = world > 1 or args.dp_rehearse   # the data-parallel path (process group, bucket all-reduces)
+    if args.dp_rehearse and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per GPU; --dist-backend gloo rehearses the N > 1 path with several ranks on one GPU
     # (device = LOCAL_RANK modulo the visible GPUs; device_count() does not initialise the GPU)
     local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    if dp:
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -724,12 +734,12 @@ def main():
         return loss
 
     # eager DP: bucket all-reduces launched from inside the decoder's backward (phase hooks)
-    grad_ar = GradAllReduce(dec) if world > 1 else None
+    grad_ar = GradAllReduce(dec) if dp else None
     # eager warm-up (builds the encoder plan, caches, allocator pools)
     for _ in range(args.warmup):
         opt.zero_grad()
         loss = fwd_bwd()
-        if world > 1:
+        if dp:
             grad_ar.wait()
         opt.step()
     torch.cuda.synchronize()
@@ -741,7 +751,7 @@ def main():
     nbuf = args.feature_buffers if overlap else 1
     # backward phase 1 (output head) and phase 2 (BPTT) as two graphs, the head bucket's all-reduce (N > 1)
     # issued between them; --bwd serial: one graph
-    split_bwd = world > 1 or args.bwd == "split"
+    split_bwd = dp or args.bwd == "split"
     launches = conv_launches(args.network, B, fused=enc.fuse_blocks, fused2=enc.fuse_layer2)
 
     def capture(stamped):
@@ -828,10 +838,10 @@ def main():
                 G["dec"][k].replay()
                 # DP: the output-head bucket is final after phase 1 -> its all-reduce runs on RCCL's
                 # stream beside the BPTT graph; the rest follows phase 2
-                w1 = allreduce_bucket_async(dec, 1) if world > 1 else None
+                w1 = allreduce_bucket_async(dec, 1) if dp else None
                 if G["rec"][k] is not None:
                     G["rec"][k].replay()
-                w2 = allreduce_bucket_async(dec, 2) if world > 1 else None
+                w2 = allreduce_bucket_async(dec, 2) if dp else None
                 d_en.record(s_main)
                 dec_events.append((d_st, d_en))
                 ev_dec[k].record(s_main)
@@ -841,13 +851,13 @@ def main():
                         replay_encoder(G, (i + 1) % nbuf, i >= nbuf - 1)
                     else:
                         replay_encoder(G, 0, False)
-                if world > 1:
+                if dp:
                     w1.wait()
                     w2.wait()
             else:
                 opt.zero_grad()
                 loss = fwd_bwd()
-                if world > 1:
+                if dp:
                     grad_ar.wait()
             opt.step()
         return loss
@@ -856,16 +866,16 @@ def main():
     enc_events.clear()
     dec_events.clear()
     torch.cuda.synchronize()
-    if world > 1:
+    if dp:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     loss = run(args.steps, G)
     torch.cuda.synchronize()
-    if world > 1:
+    if dp:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dp:
         t = torch.tensor([elapsed], device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
@@ -997,7 +1007,7 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dp:
         dist.destroy_process_group()
 
 

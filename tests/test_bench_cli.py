@@ -133,3 +133,10 @@ def test_single_gpu_runs_in_process(monkeypatch):
     monkeypatch.setattr(bench.torch.cuda, "set_device", lambda *a: (_ for _ in ()).throw(RuntimeError("stop")))
     with pytest.raises(RuntimeError, match="stop"):
         bench.main()
+
+
+def test_dp_rehearse_flag(monkeypatch):
+    """--dp-rehearse (N = 1): the data-parallel path over a one-rank process group, off by default."""
+    assert _parse(monkeypatch).dp_rehearse is False
+    a = _parse(monkeypatch, "--dp-rehearse")
+    assert a.dp_rehearse is True and a.gpus == 1 and a.dist_backend == "nccl"

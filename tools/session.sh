@@ -11,6 +11,7 @@
 #   bench64            the B = 64 line (cfg2 / cfg3's per-rank shape), no CPU baseline / fp32 leg
 #   benchq             a quick B = 128 line (100 steps, no CPU baseline / fp32 leg)
 #   cfg4 | cfg5        the --no-tf / --bert --network vgg19 lines
+#   dpr                bench.py --dp-rehearse: the N > 1 path over a one-rank RCCL process group
 #   gloo2              bench.py as two ranks over gloo on the one GPU at --batch 64 (the N > 1 path, cfg3 per rank)
 #   prof               rocprofv3 --kernel-trace --stats of the default bench command (+ tools/prof_summary.py)
 #   prof:LABEL:ARGS    the same over a quick bench line with extra flags (A/B of per-kernel times)
@@ -65,6 +66,8 @@ for s in "$@"; do
     bench64) run bench64 300 python bench.py --batch 64 $QUIET || exit $? ;;
     benchq) run benchq 300 python bench.py --steps 100 $QUIET || exit $? ;;
     cfg4) run cfg4 300 python bench.py --no-tf $QUIET || exit $? ;;
+    dpr)   # the data-parallel path of bench.py over a one-rank RCCL process group (--dp-rehearse)
+      run dpr 300 python bench.py --dp-rehearse --steps 30 --no-cpu-baseline --fp32-steps 0 || exit $? ;;
     gloo2) # the N > 1 path rehearsed on one GPU: two ranks over gloo at cfg3's per-rank batch (64)
            # (bench.py --gpus 2 starts the two ranks itself, as the driver's `bench.py --gpus N` does)
            run gloo2 400 python bench.py --gpus 2 --batch 64 --dist-backend gloo --steps 30 $QUIET || exit $? ;;
