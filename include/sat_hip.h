@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SAT_ABI_VERSION 8
+#define SAT_ABI_VERSION 9
 
 enum { SAT_F32 = 0, SAT_BF16 = 1 };
 enum { SAT_ACT_NONE = 0, SAT_ACT_RELU = 1, SAT_ACT_TANH = 2, SAT_ACT_SIGMOID = 3 };
@@ -76,6 +76,12 @@ typedef struct {
                          * 0 auto (slot batches double-buffered), 1 one batch at a time */
   int decoder_splits[4];/* split-K counts of the per-step bf16 decoder GEMMs -- h: [U; f_beta; W_hh] h, c: context
                          * part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic */
+  int greedy_step;      /* bf16 forward without teacher forcing (decoder.py:118-133 per step): 0 the fused greedy step
+                         * (token table for the embedding half of the gate GEMM, dropout in the LSTM kernel, f_z beside
+                         * the context GEMM, f_h + combine in one launch, the vocabulary head with in-launch argmax
+                         * partials), 1 the per-op form (a GEMM / elementwise launch per reference op) */
+  int embed_grad;       /* dense embedding gradient (decoder.py:87,133 nn.Embedding backward): 0 per-token sums in row
+                         * order (sorted segments: bit-reproducible), 1 fp32 atomics */
   /* diagnostics (bench.py's in-step kernel timing): a device buffer; when non-null and stamps[0] != 0 (the
    * enable word, read by the kernels at every launch -- so a captured hipGraph can be replayed with stamps
    * on or off), every workgroup w < stamp_capacity of the call's launch writes {first-wave start, last-wave

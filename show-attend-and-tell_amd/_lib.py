@@ -25,7 +25,7 @@ class SatConvGeom(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("N", "H", "W", "C", "KH", "KW", "stride", "pad", "OH", "OW")]
 
 
-ABI_VERSION = 8   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
+ABI_VERSION = 9   # include/sat_hip.h SAT_ABI_VERSION: the library must match these structs
 
 
 class SatPolicy(ctypes.Structure):
@@ -33,7 +33,8 @@ class SatPolicy(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("conv_pipe", "conv_stream", "conv3x3_ws", "conv_slices", "skinny", "gemm_stages",
                                      "gemm_tile", "gemm_linear_order", "gemm_epilogue", "split_gemm", "split_k",
                                      "attn_bwd", "attn_bwd_chunks", "attn_pipe")] + \
-               [("decoder_splits", c_int * 4), ("stamps", c_void_p), ("stamp_capacity", c_int)]
+               [("decoder_splits", c_int * 4), ("greedy_step", c_int), ("embed_grad", c_int), ("stamps", c_void_p),
+                ("stamp_capacity", c_int)]
 
     def __init__(self, **kw):
         splits = kw.pop("decoder_splits", None)

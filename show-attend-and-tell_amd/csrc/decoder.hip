@@ -40,6 +40,14 @@ struct WS {
   // by the phase's one zeroing launch)
   float* gsplit;
   unsigned* gtickets;
+  // the fused greedy step (greedy_fused): token table xt [V][4E] = emb W_ih[:, :E]^T + b_ih, the ado head's f_z
+  // pre-activation slabs, the vocabulary head's per-block argmax partials
+  float* xt;
+  float* fzp;
+  float* am_val;
+  int32_t* am_idx;
+  // the sorted (deterministic) dense embedding gradient
+  void* emb_ws;
 };
 constexpr int kTicketBlocks = 16;   // phase 1: blocks 0-7, phase 2: 8-15
 
@@ -105,6 +113,15 @@ inline Splits splits_for(const SatDecoderDims& d, bool tr) {
 // whether a call may use the transposed weight copies (bf16, both offsets given, the skinny kernel not excluded)
 inline bool use_transposed(const SatDecoderDims& d, const SatDecoderLayout& lay) {
   return d.dtype == SAT_BF16 && lay.wih_ctx_t >= 0 && lay.hcat_t >= 0 && sat_policy().skinny != 1;
+}
+// the fused greedy step (SatPolicy::greedy_step): bf16, no teacher forcing, the head kernels' shapes
+inline bool greedy_fused(const SatDecoderDims& d) {
+  return d.dtype == SAT_BF16 && !d.tf && sat_policy().greedy_step != 1 && sat_greedy_supported(d.B, d.E);
+}
+// the dense embedding gradient as sorted per-token sums (SatPolicy::embed_grad)
+inline bool embed_sorted(const SatDecoderDims& d) {
+  return !d.bert && sat_policy().embed_grad != 1 && (long)d.B * (d.T - 1) <= sat_embed_sorted_max_rows() &&
+         d.V < (1 << 18) && d.E % 4 == 0;
 }
 
 struct Carver {
@@ -176,6 +193,17 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   }
   c.take(w->demb, R * E * f);
   c.take(w->dpre0, B * 2 * E * f); c.take(w->dpre0_t, B * 2 * E * ts);
+  if (greedy_fused(d)) {
+    c.take(w->xt, V * 4 * E * f);
+    c.take(w->fzp, sp.c * B * E * f);
+    c.take(w->am_val, (size_t)sat_cdiv(V, 32) * B * f);
+    c.take(w->am_idx, (size_t)sat_cdiv(V, 32) * B * 4);
+  } else {
+    w->xt = w->fzp = w->am_val = nullptr;
+    w->am_idx = nullptr;
+  }
+  if (embed_sorted(d)) c.take(w->emb_ws, sat_embed_sorted_ws_bytes((int)R, (int)E));
+  else w->emb_ws = nullptr;
   // column-sum scratch: the largest single sum, or all the bias sums of one backward phase in one launch pair
   // (phase 1: f_out / f_h / f_z biases; phase 2: attention W / v, init, [U; f_beta; W_hh] and gate biases)
   size_t maxN = V > HG ? V : HG;
@@ -492,6 +520,96 @@ struct StepTimer {
   StepTimer(const SatDecoderDims& d, int g, int t) : stamps(step_slot(d, g, t), stamp_cap(d)) {}
 };
 
+// The fused greedy step (bf16, no teacher forcing; decoder.py:96-133 with tf off).  Per time step:
+//   h GEMM -> attention -> context GEMM (+ the ado head's f_z slabs in the same launch) -> LSTM cell (+ dropout of h)
+//   -> [ado: f_h + ReLUs + combine, one launch] -> vocabulary head (+ per-block argmax partials) -> argmax (the next
+//   token, its embedding row and its token-table row)
+// against the per-op form's per-step embedding-half GEMM, dropout, f_z / f_h GEMMs, combine, vocabulary GEMM and
+// full-row argmax.  The embedding half of the gate GEMM depends only on the fed token, so it is one GEMM over the
+// vocabulary per forward (xt = emb W_ih[:, :E]^T + b_ih, once per weight version) and a row gather per step.
+int greedy_loop(const Ctx& c, const WS& w, const Splits& sp, const StepIO& io, void* preds, const uint8_t* mask_in,
+                int32_t* tokens, hipStream_t s) {
+  const SatDecoderDims& d = c.d;
+  const SatDecoderLayout& lay = c.lay;
+  const int B = d.B, D = d.D, E = d.E, V = d.V, T1 = d.T - 1;
+  const bool att = d.attention != 0;
+  SAT_CHECK((hipError_t)linear(c, V, 4 * E, E, c.W(lay.embedding), E, c.W(lay.wih), E + D, c.F(lay.bih), w.xt, 4 * E,
+                               SAT_F32, SAT_ACT_NONE, s));
+  // step 0's gate input: the start token's table row (the start rows' embeddings are already gathered)
+  SAT_CHECK((hipError_t)sat_embed_gather(w.xt, w.tok, B, 1, T1, 4 * E, SAT_F32, w.xg, (long)T1 * 4 * E, s));
+  for (int t = 0; t < T1; ++t) {
+    const long oE = (long)t * E, oD = (long)t * D;
+    {
+      StepTimer st(d, 0, t);
+      SAT_CHECK((hipError_t)fwd_hgemm(c, w, sp, t, s));
+    }
+    if (att) {
+      {
+        StepTimer st(d, 1, t);
+        SAT_CHECK((hipError_t)fwd_attn(c, w, sp, io, t, s));
+      }
+      StepTimer st(d, 2, t);
+      SatGemm g1;
+      g1.partial_splits = sp.c; g1.split_stride = (long)B * 4 * E;
+      g1.M = B; g1.N = 4 * E; g1.K = D; g1.dtype = d.dtype;
+      g1.A = c.at(w.gated_t, oD); g1.lda = c.T1 * D; g1.B = c.W(lay.wih + E); g1.ldb = E + D;
+      g1.C = w.gctx; g1.ldc = 4 * E; g1.c_dtype = SAT_F32;
+      SatGemm g2 = g1;   // f_z(context) pre-activation (ungated context, decoder.py:155), same K split
+      g2.N = E; g2.A = c.at(w.ctx_t, oD); g2.B = c.W(lay.fz_w); g2.ldb = D;
+      g2.C = w.fzp; g2.ldc = E; g2.split_stride = (long)B * E;
+      int err = 0;
+      if (!(d.ado && sat_skinny_dual_try(g1, g2, s, &err))) {
+        SAT_CHECK((hipError_t)sat_gemm_launch(g1, s));
+        if (d.ado) SAT_CHECK((hipError_t)sat_gemm_launch(g2, s));
+      }
+      SAT_CHECK((hipError_t)err);
+    } else if (d.ado) {   // uniform attention: f_z of the (constant) mean context, one slab
+      SAT_CHECK((hipError_t)linear(c, B, E, D, c.at(w.ctx_t, oD), c.T1 * D, c.W(lay.fz_w), D, nullptr, w.fzp, E,
+                                   SAT_F32, SAT_ACT_NONE, s));
+    }
+    {
+      StepTimer st(d, 3, t);
+      LstmFwdArgs l = lstm_fwd_args(c, w, sp, t);
+      l.hd_t = c.at(w.hd_t, oE); l.hd_ld = c.T1 * E;
+      l.drop_training = d.training; l.drop_has_mask = d.has_dropout_mask; l.drop_t = t;
+      l.mask_in = mask_in ? mask_in + oE : nullptr; l.mask_out = w.dmask + oE; l.mask_ld = c.T1 * E;
+      l.seed = d.seed; l.seed_ptr = d.seed_ptr;
+      SAT_CHECK((hipError_t)sat_lstm_fwd_launch(l, s));
+    }
+    HeadOutArgs ho{};
+    ho.B = B; ho.V = V; ho.E = E;
+    if (d.ado) {
+      HeadMidArgs hm{};
+      hm.B = B; hm.E = E;
+      hm.hd = (const bf16*)c.at(w.hd_t, oE); hm.hd_ld = c.T1 * E;
+      hm.fh_w = (const bf16*)c.W(lay.fh_w); hm.fh_b = c.F(lay.fh_b);
+      hm.fzp = w.fzp; hm.fzp_ld = E; hm.fz_splits = att ? sp.c : 1; hm.fz_split_stride = (long)B * E;
+      hm.fz_b = c.F(lay.fz_b);
+      hm.emb = (const bf16*)c.at(w.emb_t, oE); hm.emb_ld = c.T1 * E;
+      hm.fh = w.fh + oE; hm.fz = w.fz + oE; hm.f_ld = c.T1 * E;
+      hm.comb = (bf16*)c.at(w.comb_t, oE); hm.comb_ld = c.T1 * E;
+      SAT_CHECK((hipError_t)sat_greedy_head_mid(hm, s));
+      ho.relu = 1;
+      ho.x = hm.comb; ho.x_ld = hm.comb_ld;
+      ho.w = (const bf16*)c.W(lay.fout_w); ho.bias = c.F(lay.fout_b);
+    } else {
+      ho.relu = 0;
+      ho.x = (const bf16*)c.at(w.hd_t, oE); ho.x_ld = c.T1 * E;
+      ho.w = (const bf16*)c.W(lay.do_w); ho.bias = c.F(lay.do_b);
+    }
+    ho.preds = (bf16*)c.at(preds, (long)t * V); ho.preds_ld = c.T1 * V;
+    ho.pval = w.am_val; ho.pidx = w.am_idx;
+    SAT_CHECK((hipError_t)sat_greedy_head_out(ho, s));
+    if (t + 1 < T1)
+      SAT_CHECK((hipError_t)sat_greedy_argmax(w.am_val, w.am_idx, B, V, w.tok + t + 1, T1, c.F(lay.embedding), E,
+                                              (bf16*)c.at(w.emb_t, (long)(t + 1) * E), c.T1 * E, w.xt,
+                                              w.xg + (long)(t + 1) * 4 * E, c.T1 * 4 * E, s));
+  }
+  if (d.training && d.seed_ptr) SAT_CHECK((hipError_t)sat_bump_seed(d.seed_ptr, s));
+  if (tokens) SAT_CHECK(hipMemcpyAsync(tokens, w.tok, c.R * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
 int check_dims(const SatDecoderDims* d) {
   if (!d) return SAT_ERR_INVALID;
   if (d->B <= 0 || d->L <= 0 || d->D <= 0 || d->E <= 0 || d->V <= 0 || d->T < 3) return SAT_ERR_INVALID;
@@ -660,6 +778,8 @@ extern "C" int sat_decoder_forward(const SatDecoderDims* dp, const SatDecoderLay
   if (d.tf)  // embedding half of the LSTM input GEMM for all steps at once (+ b_ih)
     SAT_CHECK((hipError_t)linear(c, (int)c.R, 4 * E, E, w.emb_t, E, c.W(lay->wih), E + D, c.F(lay->bih), w.xg, 4 * E,
                                  SAT_F32, SAT_ACT_NONE, s));
+
+  if (greedy_fused(d)) return greedy_loop(c, w, sp, io, preds, dropout_mask, tokens, s);
 
   for (int t = 0; t < T1; ++t) {
     if (!d.tf)
@@ -901,7 +1021,10 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
   if (!d.bert) {  // dense embedding gradient (zeroed before the loop), scatter-added by fed token (decoder.py:87,133)
     SAT_CHECK((hipError_t)dgrad(13, R, E, 4 * E, dg_t, HG, c.W(lay->wih), E + D, w.demb, E, d.ado ? w.dcomb : nullptr,
                                 E));
-    SAT_CHECK((hipError_t)sat_embed_scatter_add(w.demb, w.tok, R, E, G(lay->embedding), s));
+    if (w.emb_ws)
+      SAT_CHECK((hipError_t)sat_embed_scatter_add_sorted(w.demb, w.tok, R, E, G(lay->embedding), w.emb_ws, s));
+    else
+      SAT_CHECK((hipError_t)sat_embed_scatter_add(w.demb, w.tok, R, E, G(lay->embedding), s));
   }
   return 0;
 }

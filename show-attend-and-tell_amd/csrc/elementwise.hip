@@ -463,14 +463,88 @@ __global__ void embed_scatter_kernel(const float* __restrict__ dX, const int32_t
   for (int e = threadIdx.x; e < E; e += blockDim.x) atomicAdd(dst + e, src[e]);
 }
 
-// ---- greedy argmax over V (first index wins ties, decoder.py:132) ----------
-// torch.argmax order: NaN is the largest value (first NaN wins), otherwise larger value, then
-// smaller index.  (x, xi) replaces (y, yi) when it comes first in that order.
-__device__ __forceinline__ bool am_better(float x, int xi, float y, int yi) {
-  const bool xn = x != x, yn = y != y;
-  if (xn || yn) return xn && (!yn || xi < yi);
-  return x > y || (x == y && xi < yi);
+// ---- deterministic embedding backward: per-token sums in row order (sat_embed_scatter_add_sorted) ----
+// 1. one workgroup sorts the keys (tok << 14 | r) in LDS (bitonic): equal tokens end up adjacent, in row order;
+// 2. the sorted positions are cut into pieces of kEmbPiece: a piece sums each run of one token over its rows in order;
+//    a run that is a whole token segment is added to G[tok] directly, a run cut by a piece boundary goes to the
+//    piece's head (slot 0) or tail (slot 1) partial;
+// 3. the piece where a cut segment starts adds that segment's partials in piece order and adds the sum to G[tok].
+// Every G row is written by one thread per column, once: the same bits on every run.
+constexpr int kEmbSortMax = 16384, kEmbPiece = 32;
+__global__ __launch_bounds__(1024) void embed_sort_kernel(const int32_t* __restrict__ tok, int R,
+                                                          int32_t* __restrict__ perm, int32_t* __restrict__ stok) {
+  __shared__ uint32_t key[kEmbSortMax];
+  int NP = 1;
+  while (NP < R) NP <<= 1;
+  for (int i = threadIdx.x; i < NP; i += blockDim.x)
+    key[i] = i < R ? ((uint32_t)tok[i] << 14) | (uint32_t)i : 0xffffffffu;
+  __syncthreads();
+  for (int k = 2; k <= NP; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < NP; i += blockDim.x) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint32_t x = key[i], y = key[ixj];
+          if ((x > y) == ((i & k) == 0)) { key[i] = y; key[ixj] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = threadIdx.x; i < R; i += blockDim.x) {
+    perm[i] = (int32_t)(key[i] & 0x3fffu);
+    stok[i] = (int32_t)(key[i] >> 14);
+  }
 }
+
+// grid (pieces, ceil(E / 256)), 64 threads: thread owns 4 columns
+__global__ __launch_bounds__(64) void embed_segsum_kernel(const float* __restrict__ dX, int E,
+                                                          const int32_t* __restrict__ perm,
+                                                          const int32_t* __restrict__ stok, int R, float* G,
+                                                          float* __restrict__ part) {
+  const int p = blockIdx.x, e = blockIdx.y * 256 + 4 * threadIdx.x;
+  const int s0 = p * kEmbPiece, s1 = min(R, s0 + kEmbPiece);
+  if (e >= E) return;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int rs = s0;
+  for (int s = s0; s < s1; ++s) {
+    acc = f4add(acc, *(const float4*)(dX + (long)perm[s] * E + e));
+    const int tk = stok[s];
+    if (s + 1 == s1 || stok[s + 1] != tk) {   // the run [rs, s] of token tk ends in this piece
+      const bool starts = rs == 0 || stok[rs - 1] != tk, ends = s + 1 == R || stok[s + 1] != tk;
+      if (starts && ends) {
+        float4* g = (float4*)(G + (long)tk * E + e);
+        *g = f4add(*g, acc);
+      } else {
+        *(float4*)(part + ((long)p * 2 + (rs == s0 ? 0 : 1)) * E + e) = acc;
+      }
+      acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      rs = s + 1;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void embed_segfix_kernel(const int32_t* __restrict__ stok, int R, int E,
+                                                          const float* __restrict__ part, float* G) {
+  const int p = blockIdx.x, e = blockIdx.y * 256 + 4 * threadIdx.x;
+  const int s0 = p * kEmbPiece, s1 = min(R, s0 + kEmbPiece);
+  if (e >= E) return;
+  const int tk = stok[s1 - 1];
+  if (s1 == R || stok[s1] != tk) return;   // the piece's last run ends here: complete, or another piece's segment
+  int rs = s1 - 1;
+  while (rs > s0 && stok[rs - 1] == tk) --rs;
+  if (rs == s0 && s0 > 0 && stok[s0 - 1] == tk) return;   // the segment started in an earlier piece
+  float4 acc = *(const float4*)(part + ((long)p * 2 + (rs == s0 ? 0 : 1)) * E + e);
+  for (int q = p + 1;; ++q) {   // the next pieces' head runs, in piece order
+    acc = f4add(acc, *(const float4*)(part + (long)q * 2 * E + e));
+    const int q1 = min(R, (q + 1) * kEmbPiece);
+    if (!(q1 < R && stok[q1 - 1] == tk && stok[q1] == tk)) break;   // the segment ends inside piece q
+  }
+  float4* g = (float4*)(G + (long)tk * E + e);
+  *g = f4add(*g, acc);
+}
+
+// ---- greedy argmax over V (first index wins ties, decoder.py:132) ----------
+__device__ __forceinline__ bool am_better(float x, int xi, float y, int yi) { return sat_argmax_better(x, xi, y, yi); }
 __device__ __forceinline__ void am_wave_reduce(float& v, int& i) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -708,6 +782,26 @@ int sat_embed_gather_captions(const float* W, const int64_t* caps, int B, int T,
 int sat_embed_scatter_add(const float* dX, const int32_t* tok, int R, int E, float* G, hipStream_t s) {
   if (R <= 0) return 0;
   hipLaunchKernelGGL(embed_scatter_kernel, dim3(R), dim3(256), 0, s, dX, tok, R, E, G);
+  return (int)hipGetLastError();
+}
+
+int sat_embed_sorted_max_rows() { return kEmbSortMax; }
+size_t sat_embed_sorted_ws_bytes(int R, int E) {
+  const long pieces = sat_cdiv(R, kEmbPiece);
+  return (size_t)(2L * R * 4 + 64) / 64 * 64 + (size_t)pieces * 2 * E * 4;
+}
+int sat_embed_scatter_add_sorted(const float* dX, const int32_t* tok, int R, int E, float* G, void* ws,
+                                 hipStream_t s) {
+  if (R <= 0) return 0;
+  if (R > kEmbSortMax || E % 4 || ((uintptr_t)dX & 15) || ((uintptr_t)G & 15) || !ws) return (int)hipErrorInvalidValue;
+  int32_t* perm = (int32_t*)ws;
+  int32_t* stok = perm + R;
+  float* part = (float*)((char*)ws + (2L * R * 4 + 64) / 64 * 64);
+  const int pieces = sat_cdiv(R, kEmbPiece);
+  hipLaunchKernelGGL(embed_sort_kernel, dim3(1), dim3(1024), 0, s, tok, R, perm, stok);
+  const dim3 g(pieces, sat_cdiv(E, 256));
+  hipLaunchKernelGGL(embed_segsum_kernel, g, dim3(64), 0, s, dX, E, perm, stok, R, G, part);
+  hipLaunchKernelGGL(embed_segfix_kernel, g, dim3(64), 0, s, stok, R, E, part, G);
   return (int)hipGetLastError();
 }
 

@@ -470,11 +470,21 @@ size_t sat_split_gemm_ws_bytes() {
   return (size_t)kSplitCUs * 256 * SBN * 4 + kSatSplitTickets * 4;   // partial tiles + tickets
 }
 
-int sat_split_gemm_takes(const SatGemm& g) { return split_eligible(g) ? 1 : 0; }
+// Without a workspace the kernel can only run unsplit: it takes such a call only where the planner would not split
+// it anyway.  A long-K product with few tiles (the NN shapes the tile kernel splits with atomics over ~300
+// workgroups, or a k-major weight gradient) falls through to sat_fast_gemm_try instead of running on a handful of
+// workgroups.
+static bool split_takes(const SatGemm& g) {
+  if (!split_eligible(g)) return false;
+  if (g.split_ws && g.split_tickets) return true;
+  return plan_split(g, true).splits <= 1;
+}
+
+int sat_split_gemm_takes(const SatGemm& g) { return split_takes(g) ? 1 : 0; }
 
 int sat_split_gemm_try(const SatGemm& g, hipStream_t s, int* err) {
   *err = 0;
-  if (!split_eligible(g)) return 0;
+  if (!split_takes(g)) return 0;
   const bool have_ws = g.split_ws && g.split_tickets;
   const SPlan p = plan_split(g, have_ws);
   if (p.bm == 0) return 0;

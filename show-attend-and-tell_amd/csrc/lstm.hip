@@ -13,6 +13,18 @@ inline int grid_for(long n) {
   return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
 }
 
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+// the dropout keep bit of element (b, t, e) drawn from the seed (dropout_kernel and the fused forms share it)
+__device__ __forceinline__ uint8_t dropout_keep(uint64_t seed, int b, int t, int e) {
+  return (uint8_t)(mix32(seed * 0x9E3779B97F4A7C15ULL + (((uint64_t)b << 40) ^ ((uint64_t)t << 20) ^ (uint64_t)e)) & 1u);
+}
+
 // Gate-parallel forward: a 256-thread block covers 64 units; thread (q, u) sums gate q of unit u
 // over its split-K slabs (4x the loads in flight of a unit-per-thread kernel: 9.5 -> 5.7 us per
 // step at B=128, E=512, 4 + 8 slabs), the cell update reads the four gates back from LDS.
@@ -42,6 +54,21 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
       a.h_out[(long)b * a.h_out_ld + j] = h;
       if (a.h_out_t) ((T*)a.h_out_t)[(long)b * a.h_out_t_ld + j] = (T)h;
       if (a.h_next_in_t) ((T*)a.h_next_in_t)[(long)b * a.h_next_in_t_ld + j] = (T)h;
+      if (a.hd_t) {   // dropout(h) for the greedy step's head: dropout_kernel's arithmetic
+        float y = h;
+        if (a.drop_training) {
+          uint8_t keep;
+          if (a.drop_has_mask) {
+            keep = a.mask_in[(long)b * a.mask_ld + j];
+          } else {
+            const uint64_t seed = a.seed_ptr ? a.seed ^ (*a.seed_ptr * 0xD1B54A32D192ED03ULL) : a.seed;
+            keep = dropout_keep(seed, b, a.drop_t, j);
+          }
+          if (a.mask_out) a.mask_out[(long)b * a.mask_ld + j] = keep;
+          y = keep ? h * 2.f : 0.f;
+        }
+        ((T*)a.hd_t)[(long)b * a.hd_ld + j] = (T)y;
+      }
     }
     __syncthreads();
   }
@@ -117,12 +144,6 @@ __global__ void tanh_pair_bwd_kernel(const float* dh, int dh_splits, long dh_spl
   }
 }
 
-__device__ __forceinline__ uint32_t mix32(uint64_t x) {
-  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL;
-  x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL;
-  x ^= x >> 33;
-  return (uint32_t)x;
-}
 
 // hd[b,t,e] = h[b,t,e] * keep * 2 (train) | h (eval); keep drawn from (seed, b, t, e) or given.
 // Rows r = b*T1 + t of this call live at r*ld in h / mask / out (per-step calls pass T1 = 1 and
@@ -142,7 +163,7 @@ __global__ void dropout_kernel(const float* h, long h_ld, int B, int T1, int E, 
     if (training) {
       uint8_t keep;
       if (has_mask) keep = mask_in[r * mask_ld + e];
-      else keep = (uint8_t)(mix32(seed * 0x9E3779B97F4A7C15ULL + (((uint64_t)b << 40) ^ ((uint64_t)t << 20) ^ (uint64_t)e)) & 1u);
+      else keep = dropout_keep(seed, b, t, e);
       if (mask_out) mask_out[r * mask_ld + e] = keep;
       y = keep ? x * 2.f : 0.f;
     }

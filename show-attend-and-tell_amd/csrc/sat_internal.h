@@ -31,6 +31,54 @@ int sat_embed_gather_captions(const float* W, const int64_t* caps, int B, int T,
                               long out_ld, int32_t* tok, hipStream_t s);
 int sat_argmax_rows(const void* X, int dtype, long ld, int B, int V, int32_t* out, long out_stride,
                     const float* emb, int E, void* emb_out, long emb_ld, hipStream_t s);
+// torch.argmax order (decoder.py:132): NaN is the largest value (first NaN wins), otherwise the larger value, then
+// the smaller index; (x, xi) replaces (y, yi) when it comes first in that order -- a total order, so any reduction
+// tree gives the same winner
+__device__ __forceinline__ bool sat_argmax_better(float x, int xi, float y, int yi) {
+  const bool xn = x != x, yn = y != y;
+  if (xn || yn) return xn && (!yn || xi < yi);
+  return x > y || (x == y && xi < yi);
+}
+
+// ---- deterministic dense embedding gradient (nn.Embedding backward = index_add over the fed tokens, decoder.py:87,
+// 133): G[tok[r], :] += dX[r, :] as per-token sums in row order (one sort launch + a segment-sum launch + a fix-up
+// launch for tokens whose rows span several pieces), no fp32 atomics.  R <= sat_embed_sorted_max_rows(), V < 2^18.
+int sat_embed_sorted_max_rows();
+size_t sat_embed_sorted_ws_bytes(int R, int E);
+int sat_embed_scatter_add_sorted(const float* dX, const int32_t* tok, int R, int E, float* G, void* ws, hipStream_t s);
+
+// ---- the greedy decoder step's output head (no teacher forcing, bf16; skinny.hip) ----
+// sat_skinny_dual_try: two skinny products of one shape in one launch (returns 1 when launched)
+int sat_skinny_dual_try(const SatGemm& g1, const SatGemm& g2, hipStream_t s, int* err);
+// advanced deep output, middle part (decoder.py:149-156): fh = relu(hd f_h^T + b_h), fz = relu(sum of fz_splits
+// f_z pre-activation slabs + b_z), comb = fh + fz + emb; fh / fz saved fp32 (the backward's ReLU masks)
+struct HeadMidArgs {
+  int B, E;
+  const bf16* hd; long hd_ld;                  // dropout(h) rows of the step
+  const bf16* fh_w; const float* fh_b;        // [E][E], [E]
+  const float* fzp; long fzp_ld; int fz_splits; long fz_split_stride; const float* fz_b;
+  const bf16* emb; long emb_ld;               // embedding rows fed at the step
+  float* fh; float* fz; long f_ld;            // out fp32
+  bf16* comb; long comb_ld;                   // out: f_out's input
+};
+int sat_greedy_head_mid(const HeadMidArgs& a, hipStream_t s);
+// vocabulary head of one step (decoder.py:125 / 157): preds = act(x W^T + b) in bf16, plus per 32-column block the
+// argmax of every row over the rounded logits (pval / pidx [ceil(V / 32)][B])
+struct HeadOutArgs {
+  int B, V, E, relu;
+  const bf16* x; long x_ld;
+  const bf16* w; const float* bias;           // [V][E], [V]
+  bf16* preds; long preds_ld;
+  float* pval; int32_t* pidx;
+};
+int sat_greedy_head_out(const HeadOutArgs& a, hipStream_t s);
+// the step's argmax from the block partials (first index on ties, NaN largest) -> the next fed token
+// (decoder.py:131-133), its embedding row (dtype emb_out) and its token-table row xt[id] (the embedding half of the
+// next step's LSTM input GEMM, + b_ih) into xg
+int sat_greedy_argmax(const float* pval, const int32_t* pidx, int B, int V, int32_t* tok, long tok_ld,
+                      const float* emb, int E, bf16* emb_out, long emb_ld, const float* xt, float* xg, long xg_ld,
+                      hipStream_t s);
+int sat_greedy_supported(int B, int E);
 int sat_cast_launch(const void* x, int xd, void* y, int yd, long n, hipStream_t s);
 
 // ---- attention (attention.py:14-21 + decoder.py:97-100 gate) ----
@@ -97,6 +145,12 @@ struct LstmFwdArgs {
   void* h_next_in_t; long h_next_in_t_ld;  // dtype copy as next step's input (nullable)
   int h_splits; long h_split_stride;    // hpart = sum of h_splits slabs
   int c_splits; long c_split_stride;    // cpart = sum of c_splits slabs
+  // nullable: dropout(h) (decoder.py:121-125) in dtype -- the greedy step's head input -- with the arithmetic of
+  // sat_dropout_apply (keep from mask_in, or drawn from (seed ^ *seed_ptr, b, drop_t, e); keep-mask to mask_out)
+  void* hd_t; long hd_ld;
+  int drop_training, drop_has_mask, drop_t;
+  const uint8_t* mask_in; uint8_t* mask_out; long mask_ld;
+  uint64_t seed; const uint64_t* seed_ptr;
   SatStamps st;                         // in-kernel launch timestamps (set by the launcher)
 };
 int sat_lstm_fwd_launch(const LstmFwdArgs& a, hipStream_t s);

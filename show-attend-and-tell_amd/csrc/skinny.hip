@@ -36,41 +36,43 @@ struct SkArgs {
   const bf16* W; long ldw;
   float* C; long ldc; long split_stride;
   const float* bias;
-  int gate_E;                          // > 0: gate-interleaved columns (local column c of block x = W row / output
-                                       // column (c >> 3) * gate_E + 8 x + (c & 7)); 0: block x owns 32 x .. 32 x + 31
+  // dual launch (sat_skinny_dual_try): column blocks x >= nb1 run a second product with the same M, K and split
+  // geometry (A2 . W2^T -> C2 slabs), so two per-step products that read different operands share one launch
+  int nb1;
+  const bf16* A2; long lda2;
+  const bf16* W2; long ldw2;
+  float* C2; long ldc2; long split_stride2;
   SatStamps st;
 };
 
-__device__ __forceinline__ int col_of(const SkArgs& a, int c) {
-  return a.gate_E > 0 ? (c >> 3) * a.gate_E + (int)blockIdx.x * 8 + (c & 7) : (int)blockIdx.x * SK_COLS + c;
-}
-
-// The GEMM of one (column block, split): every fragment load at entry, the MFMAs, and the waves' partial tiles
-// folded into red[MB * 16][SK_RLD] in wave order (ends behind a barrier).
+// The GEMM of one tile: rows row0 .. row0 + MB*16 - 1 of A (rows past M re-read row M-1 and are never stored) x
+// output columns col0 .. col0 + 31 (W rows past n_lim - 1 re-read row n_lim - 1), over the k range [kbeg, kend) of
+// this workgroup, which its NW waves split in kw-deep pieces (<= 4 k-steps of 32 each).  Every fragment load of a
+// wave is requested at entry; the waves' partial tiles are folded into red[MB * 16][SK_RLD] in wave order (ends
+// behind a barrier).
 template <int MB, int NW>
-__device__ __forceinline__ void skinny_tile(const SkArgs& a, float* red) {
+__device__ __forceinline__ void skinny_tile(const bf16* __restrict__ A, long lda, int M, int row0,
+                                            const bf16* __restrict__ W, long ldw, int n_lim, int col0, int kbeg,
+                                            int kend, int kw, float* red) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int fr = lane & 15, fh = lane >> 4;
-  const int s = blockIdx.y;
-  const int kbeg = s * a.kc + w * a.kw;
-  int kend = kbeg + a.kw;
-  kend = min(kend, min((s + 1) * a.kc, a.K));
-  const int nks = kend > kbeg ? (kend - kbeg) >> 5 : 0;   // wave-uniform, <= 4
+  const int k0 = kbeg + w * kw;
+  const int k1 = min(k0 + kw, kend);
+  const int nks = k1 > k0 ? (k1 - k0) >> 5 : 0;   // wave-uniform, <= 4
 
-  // every fragment load of the wave up front (rows past M re-read row M-1 and are never stored)
   const bf16* wr[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) wr[j] = a.W + (long)col_of(a, j * 16 + fr) * a.ldw;
+  for (int j = 0; j < 2; ++j) wr[j] = W + (long)min(col0 + j * 16 + fr, n_lim - 1) * ldw;
   bf16x8 af[4][MB], bw[4][2];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     if (ks < nks) {
-      const int k = kbeg + ks * 32 + 8 * fh;
+      const int k = k0 + ks * 32 + 8 * fh;
 #pragma unroll
       for (int i = 0; i < MB; ++i) {
-        const int row = min(i * 16 + fr, a.M - 1);
-        af[ks][i] = *(const bf16x8*)(a.A + (long)row * a.lda + k);
+        const int row = min(row0 + i * 16 + fr, M - 1);
+        af[ks][i] = *(const bf16x8*)(A + (long)row * lda + k);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) bw[ks][j] = *(const bf16x8*)(wr[j] + k);
@@ -114,11 +116,18 @@ template <int MB, int NW>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(SkArgs a) {
   const SatStampT0 t0 = sat_stamp_begin(a.st);
   __shared__ __attribute__((aligned(16))) float red[MB * 16 * SK_RLD];
-  skinny_tile<MB, NW>(a, red);
-  // store: 8 float4 pieces per row, bias in split 0
   const int s = blockIdx.y;
-  float* const Cs = a.C + (long)s * a.split_stride;
-  const float* const bias = s == 0 ? a.bias : nullptr;
+  const bool second = (int)blockIdx.x >= a.nb1;   // workgroup-uniform
+  const int bx = second ? (int)blockIdx.x - a.nb1 : (int)blockIdx.x;
+  const bf16* A = second ? a.A2 : a.A;
+  const bf16* W = second ? a.W2 : a.W;
+  const long lda = second ? a.lda2 : a.lda, ldw = second ? a.ldw2 : a.ldw;
+  skinny_tile<MB, NW>(A, lda, a.M, 0, W, ldw, 0x7fffffff, bx * SK_COLS, s * a.kc, min((s + 1) * a.kc, a.K), a.kw,
+                      red);
+  // store: 8 float4 pieces per row, bias in split 0 (first product only)
+  float* const Cs = second ? a.C2 + (long)s * a.split_stride2 : a.C + (long)s * a.split_stride;
+  const long ldc = second ? a.ldc2 : a.ldc;
+  const float* const bias = s == 0 && !second ? a.bias : nullptr;
   constexpr int PIECES = MB * 16 * (SK_COLS / 4);
   // write-through (sat_common.h): the slabs go to memory while the kernel runs, so its end-of-kernel L2 writeback --
   // on the decoder's per-step critical path -- has little left to flush
@@ -127,12 +136,12 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(SkArgs a) {
     const int row = q >> 3, c4 = (q & 7) * 4;
     if (row >= a.M) continue;
     float4 v = *(const float4*)(red + row * SK_RLD + c4);
-    const int n = col_of(a, c4);
+    const int n = bx * SK_COLS + c4;
     if (bias) {
       const float4 b = *(const float4*)(bias + n);
       v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
     }
-    sat_st16(rC, (unsigned)(((long)row * a.ldc + n) * 4), *(const uint4*)&v);
+    sat_st16(rC, (unsigned)(((long)row * ldc + n) * 4), *(const uint4*)&v);
   }
   sat_stamp_end(a.st, t0);
 }
@@ -167,6 +176,7 @@ bool skinny_shape(const SatGemm& g, int mode, SkArgs* a, int* nw) {
   x.W = (const bf16*)g.B; x.ldw = g.ldb;
   x.C = (float*)g.C; x.ldc = g.ldc; x.split_stride = S > 1 ? g.split_stride : 0;
   x.bias = g.bias;
+  x.nb1 = g.N / SK_COLS;
   *a = x;
   return true;
 }
@@ -181,6 +191,135 @@ template <int MB>
 void launch_mb(int nw, dim3 grid, hipStream_t st, const SkArgs& a) {
   if (nw == 8) hipLaunchKernelGGL((skinny_gemm_kernel<MB, 8>), grid, dim3(512), 0, st, a);
   else hipLaunchKernelGGL((skinny_gemm_kernel<MB, 4>), grid, dim3(256), 0, st, a);
+}
+
+// ---- the greedy decoder step's output head (no teacher forcing: decoder.py:117-133 per step) ----
+// Waves for a K = E product at <= 4 k-steps of 32 per wave.
+inline int head_waves(int E) { return E <= 512 ? 4 : 8; }
+inline int head_kw(int E) { return sat_cdiv(sat_cdiv(E, head_waves(E)), 32) * 32; }
+
+// advanced deep output's middle (decoder.py:149-156) for 32 rows x 32 columns: the f_h tile over all of K = E, then
+// fh = relu(. + b_h), fz = relu(sum of the f_z slabs + b_z), comb = fh + fz + emb (ado_combine_rows_kernel's order)
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void head_mid_kernel(HeadMidArgs a, int kw) {
+  __shared__ __attribute__((aligned(16))) float red[2 * 16 * SK_RLD];
+  const int bx = blockIdx.x, row0 = blockIdx.y * 32;
+  skinny_tile<2, NW>(a.hd, a.hd_ld, a.B, row0, a.fh_w, a.E, a.E, bx * SK_COLS, 0, a.E, kw, red);
+  for (int q = threadIdx.x; q < 32 * 8; q += NW * 64) {
+    const int rl = q >> 3, c4 = (q & 7) * 4, row = row0 + rl, n = bx * SK_COLS + c4;
+    if (row >= a.B) continue;
+    const float4 acc = *(const float4*)(red + rl * SK_RLD + c4);
+    const float4 bh = *(const float4*)(a.fh_b + n), bz = *(const float4*)(a.fz_b + n);
+    const float4 zp = sum_parts4(a.fzp, (long)row * a.fzp_ld + n, a.fz_splits, a.fz_split_stride);
+    const uint2 eu = *(const uint2*)(a.emb + (long)row * a.emb_ld + n);
+    const bf16* ev = (const bf16*)&eu;
+    const float h4[4] = {acc.x + bh.x, acc.y + bh.y, acc.z + bh.z, acc.w + bh.w};
+    const float z4[4] = {zp.x + bz.x, zp.y + bz.y, zp.z + bz.z, zp.w + bz.w};
+    float fh[4], fz[4];
+    uint2 cu;
+    bf16* cv = (bf16*)&cu;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      fh[k] = h4[k] > 0.f ? h4[k] : 0.f;
+      fz[k] = z4[k] > 0.f ? z4[k] : 0.f;
+      cv[k] = (bf16)(fh[k] + fz[k] + (float)ev[k]);
+    }
+    *(float4*)(a.fh + (long)row * a.f_ld + n) = make_float4(fh[0], fh[1], fh[2], fh[3]);
+    *(float4*)(a.fz + (long)row * a.f_ld + n) = make_float4(fz[0], fz[1], fz[2], fz[3]);
+    *(uint2*)(a.comb + (long)row * a.comb_ld + n) = cu;
+  }
+}
+
+// vocabulary head of the step for all rows x 32 columns (K = E unsplit): act(x W^T + b) rounded to bf16 into preds,
+// and every row's argmax over the block's rounded logits into the partials
+template <int MB, int NW>
+__global__ __launch_bounds__(NW * 64) void head_out_kernel(HeadOutArgs a, int kw, SatStamps st) {
+  const SatStampT0 t0 = sat_stamp_begin(st);
+  __shared__ __attribute__((aligned(16))) float red[MB * 16 * SK_RLD];
+  const int bx = blockIdx.x;
+  skinny_tile<MB, NW>(a.x, a.x_ld, a.B, 0, a.w, a.E, a.V, bx * SK_COLS, 0, a.E, kw, red);
+  constexpr int PIECES = MB * 16 * (SK_COLS / 4);   // a multiple of 64: whole waves take part in the shuffles
+  const bool vec = (a.V & 3) == 0 && (((uintptr_t)a.preds | (uintptr_t)(a.preds_ld * 2)) & 7) == 0;
+  for (int q = threadIdx.x; q < PIECES; q += NW * 64) {
+    const int row = q >> 3, c4 = (q & 7) * 4, n = bx * SK_COLS + c4;
+    const float4 v4 = *(const float4*)(red + row * SK_RLD + c4);
+    const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    uint2 pu;
+    bf16* pv = (bf16*)&pu;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int col = n + k;
+      float x = v[k] + (col < a.V ? a.bias[col] : 0.f);
+      if (a.relu) x = x > 0.f ? x : 0.f;
+      pv[k] = (bf16)x;
+      if (row < a.B && col < a.V) {
+        const float xr = (float)pv[k];
+        if (sat_argmax_better(xr, col, best, bi)) { best = xr; bi = col; }
+      }
+    }
+    if (row < a.B) {
+      bf16* dst = a.preds + (long)row * a.preds_ld + n;
+      if (vec && n + 3 < a.V) {
+        *(uint2*)dst = pu;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (n + k < a.V) dst[k] = pv[k];
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {   // the 8 lanes of a row (consecutive q)
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (sat_argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+    }
+    if ((q & 7) == 0 && row < a.B) {
+      a.pval[(long)bx * a.B + row] = best;
+      a.pidx[(long)bx * a.B + row] = bi;
+    }
+  }
+  sat_stamp_end(st, t0);
+}
+
+// one workgroup per row: the argmax over the block partials, then the next step's inputs of that row
+__global__ __launch_bounds__(256) void greedy_argmax_kernel(const float* __restrict__ pval,
+                                                            const int32_t* __restrict__ pidx, int ncb, int B, int V,
+                                                            int32_t* __restrict__ tok, long tok_ld,
+                                                            const float* __restrict__ emb, int E,
+                                                            bf16* __restrict__ emb_out, long emb_ld,
+                                                            const float* __restrict__ xt, float* __restrict__ xg,
+                                                            long xg_ld) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int c = tid; c < ncb; c += 256) {
+    const float x = pval[(long)c * B + b];
+    const int xi = pidx[(long)c * B + b];
+    if (sat_argmax_better(x, xi, best, bi)) { best = x; bi = xi; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (sat_argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+  }
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  if ((tid & 63) == 0) { sv[tid >> 6] = best; si[tid >> 6] = bi; }
+  __syncthreads();
+  best = sv[0]; bi = si[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w)
+    if (sat_argmax_better(sv[w], si[w], best, bi)) { best = sv[w]; bi = si[w]; }
+  const int id = (bi < 0 || bi >= V) ? 0 : bi;
+  if (tid == 0) tok[(long)b * tok_ld] = id;
+  const float* er = emb + (long)id * E;
+  for (int e = tid; e < E; e += 256) emb_out[(long)b * emb_ld + e] = (bf16)er[e];
+  const float4* xr = (const float4*)(xt + (long)id * 4 * E);
+  float4* xo = (float4*)(xg + (long)b * xg_ld);
+  for (int i = tid; i < E; i += 256) xo[i] = xr[i];   // 4E floats = E float4
 }
 
 }  // namespace
@@ -199,6 +338,30 @@ int sat_skinny_try(const SatGemm& g, hipStream_t st, int* err) {
   return 1;
 }
 
+// Two products with the same M, K and partial-split geometry, no bias on the second, in one launch (the greedy step's
+// context GEMM and the ado head's f_z pre-activation, decoder.py:109-115,151-155: both read the attention output of
+// the step).  Returns 1 when it launched, 0 when either is not a skinny problem of that shape (the caller then
+// launches them one by one).
+int sat_skinny_dual_try(const SatGemm& g1, const SatGemm& g2, hipStream_t st, int* err) {
+  *err = 0;
+  SkArgs a, b;
+  int nw1, nw2;
+  const int mode = sat_policy().skinny;
+  if (!skinny_shape(g1, mode, &a, &nw1) || !skinny_ptrs(g1) || !skinny_shape(g2, mode, &b, &nw2) || !skinny_ptrs(g2))
+    return 0;
+  if (g1.M != g2.M || g1.K != g2.K || a.kc != b.kc || a.kw != b.kw || nw1 != nw2 || g2.bias) return 0;
+  const int S1 = g1.partial_splits > 1 ? g1.partial_splits : 1, S2 = g2.partial_splits > 1 ? g2.partial_splits : 1;
+  if (S1 != S2) return 0;
+  a.A2 = b.A; a.lda2 = b.lda; a.W2 = b.W; a.ldw2 = b.ldw; a.C2 = b.C; a.ldc2 = b.ldc; a.split_stride2 = b.split_stride;
+  a.st = sat_launch_stamps();
+  const dim3 grid(g1.N / SK_COLS + g2.N / SK_COLS, S1);
+  if (g1.M <= 32) launch_mb<2>(nw1, grid, st, a);
+  else if (g1.M <= 64) launch_mb<4>(nw1, grid, st, a);
+  else launch_mb<8>(nw1, grid, st, a);
+  *err = (int)hipGetLastError();
+  return 1;
+}
+
 // splits the decoder asks for when the skinny kernel runs its per-step GEMMs: 256-deep K per split
 // (less A per workgroup: every workgroup reads all M rows of its K range), 0 = not eligible
 int sat_skinny_splits(int M, int N, int K) {
@@ -206,3 +369,39 @@ int sat_skinny_splits(int M, int N, int K) {
   return K / 256;
 }
 
+
+int sat_greedy_supported(int B, int E) { return B >= 1 && B <= 128 && E % 32 == 0 && E >= 32 && E <= 1024; }
+
+int sat_greedy_head_mid(const HeadMidArgs& a, hipStream_t s) {
+  if (!sat_greedy_supported(a.B, a.E)) return (int)hipErrorInvalidValue;
+  const dim3 grid(a.E / SK_COLS, sat_cdiv(a.B, 32));
+  if (head_waves(a.E) == 4) hipLaunchKernelGGL(head_mid_kernel<4>, grid, dim3(256), 0, s, a, head_kw(a.E));
+  else hipLaunchKernelGGL(head_mid_kernel<8>, grid, dim3(512), 0, s, a, head_kw(a.E));
+  return (int)hipGetLastError();
+}
+
+int sat_greedy_head_out(const HeadOutArgs& a, hipStream_t s) {
+  if (!sat_greedy_supported(a.B, a.E) || a.V < 1) return (int)hipErrorInvalidValue;
+  const dim3 grid(sat_cdiv(a.V, SK_COLS));
+  const int nw = head_waves(a.E), kw = head_kw(a.E);
+  const SatStamps st = sat_launch_stamps();
+#define SAT_HEAD_OUT(MB)                                                                                            \
+  do {                                                                                                            \
+    if (nw == 4) hipLaunchKernelGGL((head_out_kernel<MB, 4>), grid, dim3(256), 0, s, a, kw, st);                   \
+    else hipLaunchKernelGGL((head_out_kernel<MB, 8>), grid, dim3(512), 0, s, a, kw, st);                           \
+  } while (0)
+  if (a.B <= 32) SAT_HEAD_OUT(2);
+  else if (a.B <= 64) SAT_HEAD_OUT(4);
+  else SAT_HEAD_OUT(8);
+#undef SAT_HEAD_OUT
+  return (int)hipGetLastError();
+}
+
+int sat_greedy_argmax(const float* pval, const int32_t* pidx, int B, int V, int32_t* tok, long tok_ld,
+                      const float* emb, int E, bf16* emb_out, long emb_ld, const float* xt, float* xg, long xg_ld,
+                      hipStream_t s) {
+  if (((uintptr_t)xt & 15) || ((uintptr_t)xg & 15) || (xg_ld & 3)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(greedy_argmax_kernel, dim3(B), dim3(256), 0, s, pval, pidx, sat_cdiv(V, SK_COLS), B, V, tok,
+                     tok_ld, emb, E, emb_out, emb_ld, xt, xg, xg_ld);
+  return (int)hipGetLastError();
+}

@@ -34,13 +34,28 @@ _GEMM_WS = {}
 
 def gemm_workspace(device, stream):
     """The split-K workspace sat_gemm may use (include/sat_hip.h SatGemmArgs.workspace), one per device and stream:
-    calls ordered on one stream share it."""
+    calls ordered on one stream share it.
+
+    The split kernel's arrival tickets and partial tiles live in the workspace, so two launches that may run at the
+    same time must not share one.  Under stream capture the current stream is torch's shared capture stream, and
+    graphs captured on it could be replayed concurrently on different streams: during a capture every call gets a
+    workspace of its own (allocated in the graph's private pool, alive as long as the graph's pool).  Graphs that use
+    ``gemm`` on the cached workspace (eager calls) are therefore never tied to each other."""
+    if torch.cuda.is_current_stream_capturing():
+        return torch.empty(int(L.lib().sat_gemm_workspace_bytes()), dtype=torch.uint8, device=device)
     key = (torch.device(device).index, stream.value or 0)
     ws = _GEMM_WS.get(key)
     if ws is None:
         ws = torch.empty(int(L.lib().sat_gemm_workspace_bytes()), dtype=torch.uint8, device=device)
         _GEMM_WS[key] = ws
     return ws
+
+
+def _may_split(A, C, bias, aux, act, K):
+    """Whether sat_gemm could take the split-K path for this call (csrc/gemmsplit.hip split_eligible): bf16 operands,
+    an fp32 C, no bias / aux / activation epilogue and a long K.  Other calls never touch a workspace."""
+    return (A.dtype == torch.bfloat16 and C.dtype == torch.float32 and bias is None and aux is None
+            and act == L.ACT_NONE and K >= 512)
 
 
 def gemm(A, B, C, *, transA=False, transB=False, alpha=1.0, beta=0.0, bias=None, add1=None, act=L.ACT_NONE,
@@ -77,7 +92,8 @@ def gemm(A, B, C, *, transA=False, transB=False, alpha=1.0, beta=0.0, bias=None,
     a.policy = L.policy_ptr(policy)
     stream = L.stream_of(C)
     if workspace is True:
-        workspace = gemm_workspace(C.device, stream)
+        workspace = (gemm_workspace(C.device, stream)
+                     if policy is not None or _may_split(A, C, bias, aux, act, K) else None)
     if workspace is not None:
         a.workspace, a.workspace_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
     L.check(L.lib().sat_gemm(ctypes.byref(a), stream), "sat_gemm")

@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol():
     lib = sat_amd._lib.lib()
     missing = [f for f in declared_functions() if not hasattr(lib, f)]
     assert not missing, missing
-    assert lib.sat_abi_version() == sat_amd._lib.ABI_VERSION == header_abi_version() == 8
+    assert lib.sat_abi_version() == sat_amd._lib.ABI_VERSION == header_abi_version() == 9
     assert set(declared_functions()) == set(sat_amd._lib.EXPORTED)
 
 
@@ -54,7 +54,7 @@ def test_library_refuses_other_abi_version(monkeypatch):
     with pytest.raises(RuntimeError, match="C-ABI version"):
         L.lib()
     monkeypatch.undo()
-    assert L.lib().sat_abi_version() == L.ABI_VERSION == 8
+    assert L.lib().sat_abi_version() == L.ABI_VERSION == 9
 
 
 def test_error_strings():

@@ -114,6 +114,9 @@ def test_split_gemm_addend_and_poisoned_workspace(sat):
 
 
 def test_split_gemm_without_workspace_runs_unsplit(sat):
+    """No workspace: the split kernel declines a product it would split (it falls through to the tile kernel), and
+    the few-tile NN long-K shape the tile kernel splits with atomics does not run unsplit on a handful of
+    workgroups either: both stay correct."""
     from sat_amd import ops
     M, N, K = 512, 512, 3328
     A, Bm, _, Ad, Bd = _operands(M, N, K, True, True, 4)
@@ -121,6 +124,56 @@ def test_split_gemm_without_workspace_runs_unsplit(sat):
     ops.gemm(Ad, Bd, C, transA=True, transB=True, workspace=None, policy=sat.Policy(split_k=4))
     torch.cuda.synchronize()
     assert rel(C, A.double() @ Bm.double().T) < 2e-5
+    A, Bm, _, Ad, Bd = _operands(300, 136, 1104, False, False, 6)
+    C = torch.empty(300, 136, device=DEV)
+    ops.gemm(Ad, Bd, C, workspace=None)
+    torch.cuda.synchronize()
+    assert rel(C, A.double() @ Bm.double().T) < 2e-5
+
+
+def test_gemm_workspace_private_per_capture(sat):
+    """Two graphs captured on torch's shared capture stream get split-K workspaces of their own (their tickets
+    would race if the graphs were replayed concurrently on two streams), and replaying both concurrently gives the
+    eager results."""
+    from sat_amd import ops
+    M, N, K = 512, 2048, 3328
+    _, _, _, Ad, Bd = _operands(M, N, K, True, True, 11)
+    eager = torch.empty(M, N, device=DEV)
+    ops.gemm(Ad, Bd, eager, transA=True, transB=True)
+    seen = []
+    orig = ops.gemm_workspace
+
+    def spy(device, stream):
+        ws = orig(device, stream)
+        seen.append(ws.data_ptr())
+        return ws
+    outs, graphs = [], []
+    ops.gemm_workspace = spy
+    try:
+        for _ in range(2):
+            C = torch.empty(M, N, device=DEV)
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g):
+                ops.gemm(Ad, Bd, C, transA=True, transB=True)
+            outs.append(C)
+            graphs.append(g)
+    finally:
+        ops.gemm_workspace = orig
+    assert len(seen) == 2 and seen[0] != seen[1]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for C in outs:
+            C.fill_(float("nan"))
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s1):
+            graphs[0].replay()
+        with torch.cuda.stream(s2):
+            graphs[1].replay()
+        torch.cuda.synchronize()
+        for C in outs:
+            assert torch.equal(C, eager)
 
 
 def test_gemm_output_past_2gib_uses_plain_stores(sat):
