@@ -120,8 +120,85 @@ def make_dropout_masks(B, steps, E, seed):
 # Attention / decoder (attention.py, decoder.py)
 # ----------------------------------------------------------------------------
 
-def linear(x, p, name):
-    return F.linear(x, p[name + ".weight"], p[name + ".bias"])
+# ----------------------------------------------------------------------------
+# bf16 rounding mirror (test infrastructure): the HIP performance mode keeps bf16 copies of the weights and of the
+# GEMM operands and accumulates in fp32.  Inside ``bf16_mirror()`` the decoder below rounds exactly there -- every
+# Linear's input and weight (x, W -> bf16 values; the product and the bias add exact in the caller's dtype), the
+# outputs the HIP path stores in bf16 (Ws = a W^T + b, attention.py:16, and the vocabulary logits, decoder.py:125 /
+# 157), the embedding rows the ado combine adds (decoder.py:156), and in backward the gradient entering every such
+# product (the HIP path stores it in bf16 before its input- and weight-gradient GEMMs; the bias gradients of the
+# output-head Linears are column sums of those bf16 values, the others of the fp32 ones).  Everything else (the
+# attention softmax / context, the gates, the LSTM cell, h, c, the loss) stays in the caller's dtype.  Run in fp64,
+# it is the reference the bf16 kernels are measured against with fp32 accumulation noise as the only difference.
+# ----------------------------------------------------------------------------
+
+class _MirrorState:
+    on = False
+
+
+_MIRROR = _MirrorState()
+
+
+class bf16_mirror:
+    """Context manager: the decoder functions of this module round where the HIP bf16 path rounds."""
+
+    def __enter__(self):
+        self.prev = _MIRROR.on
+        _MIRROR.on = True
+        return self
+
+    def __exit__(self, *exc):
+        _MIRROR.on = self.prev
+        return False
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).to(x.dtype)
+
+
+def _rb(x):
+    """x rounded to bf16 values (same dtype) with a straight-through gradient."""
+    return x + (_bf(x) - x).detach()
+
+
+class _BF16Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, round_out, round_bias_grad):
+        xr, wr = _bf(x), _bf(w)
+        ctx.save_for_backward(xr, wr)
+        ctx.rbg = round_bias_grad
+        ctx.has_b = b is not None
+        y = F.linear(xr, wr, b)
+        return _bf(y) if round_out else y
+
+    @staticmethod
+    def backward(ctx, g):
+        xr, wr = ctx.saved_tensors
+        gr = _bf(g)
+        dx = gr @ wr
+        g2 = gr.reshape(-1, gr.shape[-1])
+        dw = g2.T @ xr.reshape(-1, xr.shape[-1])
+        db = None
+        if ctx.has_b:
+            db = (gr if ctx.rbg else g).reshape(-1, g.shape[-1]).sum(0)
+        return dx, dw, db, None, None
+
+
+def _lin(x, w, b, round_out=False, round_bias_grad=False, mirror=True):
+    if mirror and _MIRROR.on:
+        return _BF16Linear.apply(x, w, b, round_out, round_bias_grad)
+    return F.linear(x, w, b)
+
+
+# Linears whose output the HIP bf16 path stores in bf16, and those whose bias gradient is a column sum of a bf16
+# gradient (the output head's)
+_ROUND_OUT = ("attention.W", "f_out", "deep_output")
+_ROUND_BIAS_GRAD = ("f_h", "f_z", "f_out", "deep_output")
+
+
+def linear(x, p, name, mirror=True):
+    return _lin(x, p[name + ".weight"], p[name + ".bias"], round_out=any(name.endswith(k) for k in _ROUND_OUT),
+                round_bias_grad=name in _ROUND_BIAS_GRAD, mirror=mirror)
 
 
 def attention_forward(p, img_features, hidden_state, prefix="attention."):
@@ -130,7 +207,7 @@ def attention_forward(p, img_features, hidden_state, prefix="attention."):
     U_h = linear(hidden_state, p, prefix + "U").unsqueeze(1)
     W_s = linear(img_features, p, prefix + "W")
     att = torch.tanh(W_s + U_h)
-    e = linear(att, p, prefix + "v").squeeze(2)
+    e = linear(att, p, prefix + "v", mirror=False).squeeze(2)   # fp32 weights in the HIP attention kernel
     alpha = torch.softmax(e, dim=1)
     context = (img_features * alpha.unsqueeze(2)).sum(1)
     return context, alpha
@@ -146,7 +223,7 @@ def init_lstm_state(p, img_features):
 
 def lstm_cell(p, x, h, c):
     """torch.nn.LSTMCell (decoder.py:53,115): gate order (i, f, g, o)."""
-    g = F.linear(x, p["lstm.weight_ih"], p["lstm.bias_ih"]) + F.linear(h, p["lstm.weight_hh"], p["lstm.bias_hh"])
+    g = _lin(x, p["lstm.weight_ih"], p["lstm.bias_ih"]) + _lin(h, p["lstm.weight_hh"], p["lstm.bias_hh"])
     i, f, gg, o = g.chunk(4, dim=1)
     c2 = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
     h2 = torch.sigmoid(o) * torch.tanh(c2)
@@ -157,6 +234,8 @@ def advanced_deep_output(p, h, context, emb):
     """decoder.py:149-158 (ungated context, ReLU on the logits)."""
     ht = torch.relu(linear(h, p, "f_h"))
     zt = torch.relu(linear(context, p, "f_z"))
+    if _MIRROR.on:
+        emb = _rb(emb)   # the bf16 embedding rows of the HIP combine
     return torch.relu(linear(ht + zt + emb, p, "f_out"))
 
 
@@ -175,8 +254,8 @@ def decoder_forward(p, img_features, captions, *, tf, ado, attention, bert=False
     T1 = captions.shape[1] - 1                                    # decoder.py:77
     start = SPECIAL_BERT["start"] if bert else SPECIAL_PLAIN["start"]
     prev_tok = torch.full((B,), start, dtype=torch.long)           # decoder.py:79-82
-    preds = torch.zeros(B, T1, V)
-    alphas = torch.zeros(B, T1, L)
+    preds = torch.zeros(B, T1, V, dtype=img_features.dtype)
+    alphas = torch.zeros(B, T1, L, dtype=img_features.dtype)
     in_tokens = torch.zeros(B, T1, dtype=torch.long)
 
     def dropout(x, t):
