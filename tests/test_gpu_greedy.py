@@ -69,25 +69,40 @@ def _greedy_seeded(sat, c, form):
                      grads=grads, tokens=dec.last_tokens.long().cpu())
 
 
+# bounds against the bf16 rounding mirror of the oracle (oracle/sat_oracle.py bf16_mirror, fp64) at these B <= 4, T = 6-8
+# cases: measured <= 2.4e-3 per parameter (profiles/r6_s3/py_1_debug_greedy.log: both forms, seeded and injected masks,
+# with and without the ado head); against the plain fp32 oracle the same steps differ by up to 0.2 for some seeds
+# (bf16 rounding of the ReLU'd logits near zero), which is why the mirror is the reference here
+MIRROR_TOL = 1e-2
+
+
+def _mirror_fed(c, tokens):
+    with O.bf16_mirror():
+        return S._oracle_fed(c, tokens, torch.float64)
+
+
+def _assert_mirror(h, o, tol=MIRROR_TOL):
+    loss_m, g_m, _, preds_m, alphas_m = o
+    assert S.rel(h["preds"], preds_m) < 1e-2
+    assert S.rel(h["alphas"], alphas_m) < 1e-2
+    assert abs(h["loss"] - loss_m.item()) <= 1e-3 * abs(loss_m.item())
+    assert sorted(h["grads"]) == sorted(g_m)
+    errs = S._grad_errors(h, {n: g.float() for n, g in g_m.items()})
+    print("bf16 gradient errors vs the fed-token bf16 mirror:", {n: round(e, 5) for n, e in errs.items()})
+    bad = {n: e for n, e in errs.items() if e >= tol}
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("form", [0, 1])
 @pytest.mark.parametrize("ado", [True, False])
 def test_greedy_step_seeded_dropout_matches_oracle(sat, form, ado):
     """Both greedy forms (0 = fused, 1 = per-op) in training mode with seeded dropout: the masks rebuilt on the host
-    from the seed, the fed-token oracle, bf16 bounds (preds / alphas 3e-2, loss 1e-2, gradients 8e-2 of the norm at
-    B = 4 as in test_gpu_shapes)."""
+    from the seed, the fed-token bf16 mirror oracle."""
     D, Lf, E, V, T = 512, 196, 512, 2600, 8
     c = S._make_case(D, Lf, E, V, T, False, ado, False, 4, 23)
     dec, h = _greedy_seeded(sat, c, form)
     c = dict(c, masks=host_dropout_masks(dec._seed_host, 4, T - 1, E))
-    loss_f, g_f, _, preds_f, alphas_f = S._oracle_fed(c, h["tokens"], torch.float32)
-    assert S.rel(h["preds"], preds_f) < 3e-2
-    assert S.rel(h["alphas"], alphas_f) < 3e-2
-    assert abs(h["loss"] - loss_f.item()) <= 1e-2 * abs(loss_f.item())
-    assert sorted(h["grads"]) == sorted(g_f)
-    errs = S._grad_errors(h, g_f)
-    print(f"form {form} ado {ado}: bf16 gradient errors vs fed-token oracle:", {n: round(e, 4) for n, e in errs.items()})
-    for n, e in errs.items():
-        assert e < S.SHAPES_BF16_GRAD_TOL, (n, e)
+    _assert_mirror(h, _mirror_fed(c, h["tokens"]))
 
 
 def test_greedy_fused_tokens_are_argmax_of_preds(sat):
@@ -107,11 +122,7 @@ def test_greedy_fused_odd_vocabulary_and_small_batch(sat):
     c = S._make_case(D, Lf, E, V, T, False, True, False, 3, 29)
     h = S._hip_step(sat, c, torch.bfloat16)
     assert torch.equal(h["tokens"][:, 1:], h["preds"].argmax(2)[:, :-1])
-    loss_f, g_f, _, preds_f, alphas_f = S._oracle_fed(c, h["tokens"], torch.float32)
-    assert S.rel(h["preds"], preds_f) < 3e-2
-    assert abs(h["loss"] - loss_f.item()) <= 1e-2 * abs(loss_f.item())
-    for n, e in S._grad_errors(h, g_f).items():
-        assert e < S.SHAPES_BF16_GRAD_TOL, (n, e)
+    _assert_mirror(h, _mirror_fed(c, h["tokens"]))
 
 
 def _pad_heavy_case(Bn, T, seed):

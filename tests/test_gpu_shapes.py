@@ -246,6 +246,27 @@ def test_production_shape_bf16_close_to_oracle(sat, name):
     _assert_bf16(c, _hip_step(sat, c, torch.bfloat16), _oracle(c, torch.float32), grad_tol=SHAPES_BF16_GRAD_TOL)
 
 
+# the B = 4 shapes against the bf16 rounding mirror (fp64): the bound from the measured distribution
+SHAPES_BF16_MIRROR_TOL = 2e-2
+
+
+@pytest.mark.parametrize("name", list(SHAPES))
+def test_production_shape_bf16_close_to_rounding_oracle(sat, name):
+    c = _case(name)
+    h = _hip_step(sat, c, torch.bfloat16)
+    with O.bf16_mirror():
+        loss_m, g_m, _, preds_m, alphas_m = _oracle(c, torch.float64) if c["tf"] else \
+            _oracle_fed(c, h["tokens"], torch.float64)
+    e_preds, e_alphas = rel(h["preds"], preds_m), rel(h["alphas"], alphas_m)
+    e_loss = abs(h["loss"] - loss_m.item()) / abs(loss_m.item())
+    errs = _grad_errors(h, {n: g.float() for n, g in g_m.items()})
+    print(f"{name}: preds {e_preds:.2e} alphas {e_alphas:.2e} loss {e_loss:.2e}; gradient errors vs the bf16 mirror:",
+          {n: round(e, 5) for n, e in sorted(errs.items(), key=lambda kv: -kv[1])})
+    assert e_preds < 1e-2 and e_alphas < 1e-2 and e_loss < 1e-3
+    bad = {n: e for n, e in errs.items() if e >= SHAPES_BF16_MIRROR_TOL}
+    assert not bad, bad
+
+
 def _grad_errors(h, ref_grads):
     """relative gradient error norm per parameter (the non-vanishing ones)"""
     return {n: ((gr - ref_grads[n]).norm() / ref_grads[n].norm()).item() for n, gr in h["grads"].items()
