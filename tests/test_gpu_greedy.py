@@ -3,9 +3,10 @@
 * Fused greedy step (SatPolicy.greedy_step = 0, bf16, teacher forcing off: decoder.py:118-133 per step): the embedding
   half of the LSTM input GEMM from a token table built once per forward, dropout drawn inside the LSTM kernel, the ado
   head's f_z beside the context GEMM, f_h + ReLUs + combine in one launch, the vocabulary head writing per-block argmax
-  partials.  Checked, like every greedy case, against the fp32 oracle conditioned on the tokens the HIP decoder fed
-  itself (decoder.py:131-133: the argmax feedback is a constant for autograd), with the seeded dropout masks rebuilt
-  on the host from the decoder's seed -- so the in-kernel mask draw of both forms is pinned too.
+  partials.  Checked against the bf16 rounding mirror of the oracle (oracle/sat_oracle.py bf16_mirror, fp64)
+  conditioned on the tokens the HIP decoder fed itself (decoder.py:131-133: the argmax feedback is a constant for
+  autograd), with the seeded dropout masks rebuilt on the host from the decoder's seed -- so the in-kernel mask draw
+  of both forms is pinned too.
 * Dense embedding gradient (SatPolicy.embed_grad = 0): per-token sums in row order (one sort launch, piece sums, a
   fix-up for tokens whose rows span pieces), bit-identical across runs, against the fp32-atomic form and the oracle.
 
