@@ -522,9 +522,9 @@ struct StepTimer {
 
 // The fused greedy step (bf16, no teacher forcing; decoder.py:96-133 with tf off).  Per time step:
 //   h GEMM -> attention -> context GEMM (+ the ado head's f_z slabs in the same launch) -> LSTM cell (+ dropout of h)
-//   -> [ado: f_h + ReLUs + combine, one launch] -> vocabulary head (+ per-block argmax partials) -> argmax (the next
-//   token, its embedding row and its token-table row)
-// against the per-op form's per-step embedding-half GEMM, dropout, f_z / f_h GEMMs, combine, vocabulary GEMM and
+//   -> [ado: f_h + ReLUs + combine, one launch] -> vocabulary head (+ per-block argmax partials)
+// and the argmax itself folded into the next step's LSTM kernel (which reads the fed token's row of the token table and
+// writes its embedding row), against the per-op form's per-step embedding-half GEMM, dropout, f_z / f_h GEMMs, combine, vocabulary GEMM and
 // full-row argmax.  The embedding half of the gate GEMM depends only on the fed token, so it is one GEMM over the
 // vocabulary per forward (xt = emb W_ih[:, :E]^T + b_ih, once per weight version) and a row gather per step.
 int greedy_loop(const Ctx& c, const WS& w, const Splits& sp, const StepIO& io, void* preds, const uint8_t* mask_in,
@@ -574,6 +574,11 @@ int greedy_loop(const Ctx& c, const WS& w, const Splits& sp, const StepIO& io, v
       l.drop_training = d.training; l.drop_has_mask = d.has_dropout_mask; l.drop_t = t;
       l.mask_in = mask_in ? mask_in + oE : nullptr; l.mask_out = w.dmask + oE; l.mask_ld = c.T1 * E;
       l.seed = d.seed; l.seed_ptr = d.seed_ptr;
+      if (t > 0) {   // the token fed at t: the argmax of step t - 1's head partials, folded into this launch
+        l.am_val = w.am_val; l.am_idx = w.am_idx; l.am_ncb = sat_cdiv(V, 32); l.am_V = V;
+        l.xt = w.xt; l.emb = c.F(lay.embedding); l.emb_t = c.at(w.emb_t, oE); l.emb_t_ld = c.T1 * E;
+        l.tok_out = w.tok + t; l.tok_ld = T1;
+      }
       SAT_CHECK((hipError_t)sat_lstm_fwd_launch(l, s));
     }
     HeadOutArgs ho{};
@@ -600,10 +605,6 @@ int greedy_loop(const Ctx& c, const WS& w, const Splits& sp, const StepIO& io, v
     ho.preds = (bf16*)c.at(preds, (long)t * V); ho.preds_ld = c.T1 * V;
     ho.pval = w.am_val; ho.pidx = w.am_idx;
     SAT_CHECK((hipError_t)sat_greedy_head_out(ho, s));
-    if (t + 1 < T1)
-      SAT_CHECK((hipError_t)sat_greedy_argmax(w.am_val, w.am_idx, B, V, w.tok + t + 1, T1, c.F(lay.embedding), E,
-                                              (bf16*)c.at(w.emb_t, (long)(t + 1) * E), c.T1 * E, w.xt,
-                                              w.xg + (long)(t + 1) * 4 * E, c.T1 * 4 * E, s));
   }
   if (d.training && d.seed_ptr) SAT_CHECK((hipError_t)sat_bump_seed(d.seed_ptr, s));
   if (tokens) SAT_CHECK(hipMemcpyAsync(tokens, w.tok, c.R * sizeof(int32_t), hipMemcpyDeviceToDevice, s));

@@ -464,83 +464,112 @@ __global__ void embed_scatter_kernel(const float* __restrict__ dX, const int32_t
 }
 
 // ---- deterministic embedding backward: per-token sums in row order (sat_embed_scatter_add_sorted) ----
-// 1. one workgroup sorts the keys (tok << 14 | r) in LDS (bitonic): equal tokens end up adjacent, in row order;
-// 2. the sorted positions are cut into pieces of kEmbPiece: a piece sums each run of one token over its rows in order;
-//    a run that is a whole token segment is added to G[tok] directly, a run cut by a piece boundary goes to the
-//    piece's head (slot 0) or tail (slot 1) partial;
-// 3. the piece where a cut segment starts adds that segment's partials in piece order and adds the sum to G[tok].
+// 1. rank sort: every row's place in (token, row) order -- #rows with a smaller token + #earlier rows with the same
+//    token -- counted against all R tokens held in LDS (R^2 compares spread over R threads, no barriers between
+//    passes); it also records each sorted position's token segment [start, end);
+// 2. the sorted positions are cut into pieces of kEmbPiece: a piece loads its rows' gradients at once and sums each run
+//    of one token in row order; a run that is a whole segment is added to G[tok] directly, a run cut by a piece
+//    boundary goes to the piece's head (slot 0) or tail (slot 1) partial;
+// 3. the piece where a cut segment starts adds that segment's partials in a fixed tree order (four interleaved piece
+//    chains, then the chains in order) and adds the sum to G[tok].
 // Every G row is written by one thread per column, once: the same bits on every run.
 constexpr int kEmbSortMax = 16384, kEmbPiece = 32;
-__global__ __launch_bounds__(1024) void embed_sort_kernel(const int32_t* __restrict__ tok, int R,
-                                                          int32_t* __restrict__ perm, int32_t* __restrict__ stok) {
-  __shared__ uint32_t key[kEmbSortMax];
-  int NP = 1;
-  while (NP < R) NP <<= 1;
-  for (int i = threadIdx.x; i < NP; i += blockDim.x)
-    key[i] = i < R ? ((uint32_t)tok[i] << 14) | (uint32_t)i : 0xffffffffu;
+__global__ __launch_bounds__(256) void embed_rank_kernel(const int32_t* __restrict__ tok, int R,
+                                                         int32_t* __restrict__ perm, int32_t* __restrict__ stok,
+                                                         int32_t* __restrict__ seg) {
+  __shared__ __attribute__((aligned(16))) int32_t st[kEmbSortMax];
+  const int R4 = (R + 3) & ~3;
+  for (int i = threadIdx.x; i < R4; i += blockDim.x) st[i] = i < R ? tok[i] : 0x7fffffff;   // past R: no token
   __syncthreads();
-  for (int k = 2; k <= NP; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < NP; i += blockDim.x) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint32_t x = key[i], y = key[ixj];
-          if ((x > y) == ((i & k) == 0)) { key[i] = y; key[ixj] = x; }
-        }
-      }
-      __syncthreads();
-    }
-  for (int i = threadIdx.x; i < R; i += blockDim.x) {
-    perm[i] = (int32_t)(key[i] & 0x3fffu);
-    stok[i] = (int32_t)(key[i] >> 14);
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const int k = st[r];
+  int less = 0, before = 0, eq = 0;
+  for (int i = 0; i < R4; i += 4) {   // the same i for every lane: LDS broadcast reads, 4 tokens each
+    const int4 x = *(const int4*)(st + i);
+    less += (x.x < k) + (x.y < k) + (x.z < k) + (x.w < k);
+    eq += (x.x == k) + (x.y == k) + (x.z == k) + (x.w == k);
+    before += ((x.x == k) & (i < r)) + ((x.y == k) & (i + 1 < r)) + ((x.z == k) & (i + 2 < r)) + ((x.w == k) & (i + 3 < r));
   }
+  const int pos = less + before;
+  perm[pos] = r;
+  stok[pos] = k;
+  seg[2 * pos] = less;          // the token's segment of sorted positions: [less, less + eq)
+  seg[2 * pos + 1] = less + eq;
 }
 
 // grid (pieces, ceil(E / 256)), 64 threads: thread owns 4 columns
 __global__ __launch_bounds__(64) void embed_segsum_kernel(const float* __restrict__ dX, int E,
                                                           const int32_t* __restrict__ perm,
-                                                          const int32_t* __restrict__ stok, int R, float* G,
+                                                          const int32_t* __restrict__ stok,
+                                                          const int32_t* __restrict__ seg, int R, float* G,
                                                           float* __restrict__ part) {
   const int p = blockIdx.x, e = blockIdx.y * 256 + 4 * threadIdx.x;
-  const int s0 = p * kEmbPiece, s1 = min(R, s0 + kEmbPiece);
+  const int s0 = p * kEmbPiece, n = min(R - s0, kEmbPiece);
+  __shared__ int sr[kEmbPiece], stk[kEmbPiece], sa[kEmbPiece], sb[kEmbPiece];
+  if ((int)threadIdx.x < n) {
+    sr[threadIdx.x] = perm[s0 + threadIdx.x];
+    stk[threadIdx.x] = stok[s0 + threadIdx.x];
+    sa[threadIdx.x] = seg[2 * (s0 + threadIdx.x)];
+    sb[threadIdx.x] = seg[2 * (s0 + threadIdx.x) + 1];
+  }
+  __syncthreads();
   if (e >= E) return;
+  float4 x[kEmbPiece];   // every row of the piece requested before the first add
+#pragma unroll
+  for (int i = 0; i < kEmbPiece; ++i)
+    x[i] = i < n ? *(const float4*)(dX + (long)sr[i] * E + e) : make_float4(0.f, 0.f, 0.f, 0.f);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  int rs = s0;
-  for (int s = s0; s < s1; ++s) {
-    acc = f4add(acc, *(const float4*)(dX + (long)perm[s] * E + e));
-    const int tk = stok[s];
-    if (s + 1 == s1 || stok[s + 1] != tk) {   // the run [rs, s] of token tk ends in this piece
-      const bool starts = rs == 0 || stok[rs - 1] != tk, ends = s + 1 == R || stok[s + 1] != tk;
-      if (starts && ends) {
-        float4* g = (float4*)(G + (long)tk * E + e);
-        *g = f4add(*g, acc);
-      } else {
-        *(float4*)(part + ((long)p * 2 + (rs == s0 ? 0 : 1)) * E + e) = acc;
+  int rs = 0;
+#pragma unroll
+  for (int i = 0; i < kEmbPiece; ++i) {
+    if (i < n) {
+      acc = f4add(acc, x[i]);
+      if (i + 1 == n || stk[i + 1] != stk[i]) {   // the run [rs, i] of token stk[i] ends in this piece
+        if (sa[i] == s0 + rs && sb[i] == s0 + i + 1) {
+          float4* g = (float4*)(G + (long)stk[i] * E + e);
+          *g = f4add(*g, acc);
+        } else {
+          *(float4*)(part + ((long)p * 2 + (rs == 0 ? 0 : 1)) * E + e) = acc;
+        }
+        acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        rs = i + 1;
       }
-      acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      rs = s + 1;
     }
   }
 }
 
-__global__ __launch_bounds__(64) void embed_segfix_kernel(const int32_t* __restrict__ stok, int R, int E,
-                                                          const float* __restrict__ part, float* G) {
-  const int p = blockIdx.x, e = blockIdx.y * 256 + 4 * threadIdx.x;
+// grid (pieces, ceil(E / 256)), 256 threads = 4 chains x 64 threads
+__global__ __launch_bounds__(256) void embed_segfix_kernel(const int32_t* __restrict__ stok,
+                                                           const int32_t* __restrict__ seg, int R, int E,
+                                                           const float* __restrict__ part, float* G) {
+  const int p = blockIdx.x, chain = threadIdx.x >> 6, e = blockIdx.y * 256 + 4 * (threadIdx.x & 63);
   const int s0 = p * kEmbPiece, s1 = min(R, s0 + kEmbPiece);
-  if (e >= E) return;
-  const int tk = stok[s1 - 1];
-  if (s1 == R || stok[s1] != tk) return;   // the piece's last run ends here: complete, or another piece's segment
-  int rs = s1 - 1;
-  while (rs > s0 && stok[rs - 1] == tk) --rs;
-  if (rs == s0 && s0 > 0 && stok[s0 - 1] == tk) return;   // the segment started in an earlier piece
-  float4 acc = *(const float4*)(part + ((long)p * 2 + (rs == s0 ? 0 : 1)) * E + e);
-  for (int q = p + 1;; ++q) {   // the next pieces' head runs, in piece order
-    acc = f4add(acc, *(const float4*)(part + (long)q * 2 * E + e));
-    const int q1 = min(R, (q + 1) * kEmbPiece);
-    if (!(q1 < R && stok[q1 - 1] == tk && stok[q1] == tk)) break;   // the segment ends inside piece q
+  const int sa = seg[2 * (s1 - 1)], sb = seg[2 * (s1 - 1) + 1];   // the segment of the piece's last position
+  if (sb <= s1 || sa < s0) return;   // the segment ends in this piece, or started in an earlier one
+  __shared__ float4 cs[3][64];
+  const int p1 = (sb - 1) / kEmbPiece;   // the piece where the segment ends
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < E) {
+    // chain c: the head partials of pieces p + 1 + c, p + 5 + c, .. <= p1, eight loads in flight at a time
+    for (int q0 = p + 1 + chain; q0 <= p1; q0 += 32) {
+      float4 y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = q0 + 4 * u;
+        y[u] = q <= p1 ? *(const float4*)(part + (long)q * 2 * E + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = f4add(acc, y[u]);
+    }
   }
-  float4* g = (float4*)(G + (long)tk * E + e);
-  *g = f4add(*g, acc);
+  if (chain > 0) cs[chain - 1][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (chain != 0 || e >= E) return;
+  const float4 own = *(const float4*)(part + ((long)p * 2 + (sa == s0 ? 0 : 1)) * E + e);
+  const float4 sum = f4add(own, f4add(f4add(acc, cs[0][threadIdx.x]), f4add(cs[1][threadIdx.x], cs[2][threadIdx.x])));
+  float4* g = (float4*)(G + (long)stok[s1 - 1] * E + e);
+  *g = f4add(*g, sum);
 }
 
 // ---- greedy argmax over V (first index wins ties, decoder.py:132) ----------
@@ -786,9 +815,10 @@ int sat_embed_scatter_add(const float* dX, const int32_t* tok, int R, int E, flo
 }
 
 int sat_embed_sorted_max_rows() { return kEmbSortMax; }
+// workspace: perm [R], stok [R], seg [2R] (int32), then the piece partials [pieces][2][E] fp32
+static long embed_part_off(int R) { return (4L * R * 4 + 255) / 256 * 256; }
 size_t sat_embed_sorted_ws_bytes(int R, int E) {
-  const long pieces = sat_cdiv(R, kEmbPiece);
-  return (size_t)(2L * R * 4 + 64) / 64 * 64 + (size_t)pieces * 2 * E * 4;
+  return (size_t)(embed_part_off(R) + (long)sat_cdiv(R, kEmbPiece) * 2 * E * 4);
 }
 int sat_embed_scatter_add_sorted(const float* dX, const int32_t* tok, int R, int E, float* G, void* ws,
                                  hipStream_t s) {
@@ -796,12 +826,13 @@ int sat_embed_scatter_add_sorted(const float* dX, const int32_t* tok, int R, int
   if (R > kEmbSortMax || E % 4 || ((uintptr_t)dX & 15) || ((uintptr_t)G & 15) || !ws) return (int)hipErrorInvalidValue;
   int32_t* perm = (int32_t*)ws;
   int32_t* stok = perm + R;
-  float* part = (float*)((char*)ws + (2L * R * 4 + 64) / 64 * 64);
+  int32_t* seg = stok + R;
+  float* part = (float*)((char*)ws + embed_part_off(R));
   const int pieces = sat_cdiv(R, kEmbPiece);
-  hipLaunchKernelGGL(embed_sort_kernel, dim3(1), dim3(1024), 0, s, tok, R, perm, stok);
+  hipLaunchKernelGGL(embed_rank_kernel, dim3(sat_cdiv(R, 256)), dim3(256), 0, s, tok, R, perm, stok, seg);
   const dim3 g(pieces, sat_cdiv(E, 256));
-  hipLaunchKernelGGL(embed_segsum_kernel, g, dim3(64), 0, s, dX, E, perm, stok, R, G, part);
-  hipLaunchKernelGGL(embed_segfix_kernel, g, dim3(64), 0, s, stok, R, E, part, G);
+  hipLaunchKernelGGL(embed_segsum_kernel, g, dim3(64), 0, s, dX, E, perm, stok, seg, R, G, part);
+  hipLaunchKernelGGL(embed_segfix_kernel, g, dim3(256), 0, s, stok, seg, R, E, part, G);
   return (int)hipGetLastError();
 }
 

@@ -31,6 +31,8 @@ __device__ __forceinline__ uint8_t dropout_keep(uint64_t seed, int b, int t, int
 template <typename T>
 __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
   __shared__ float sg[4][64];
+  __shared__ float am_v[4];
+  __shared__ int am_i[4];
   const int E = a.E;
   const int q = threadIdx.x >> 6, u = threadIdx.x & 63;
   const long units = (long)a.B * E;
@@ -38,9 +40,33 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
     const long i = base + u;
     const bool ok = i < units;
     const int b = ok ? (int)(i / E) : 0, j = ok ? (int)(i - (long)b * E) : 0;
+    int id = 0;
+    if (a.am_val) {   // the token fold: the block's 64 units share one row (E % 64 == 0)
+      const int br = (int)(base / E);
+      float best = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int c = threadIdx.x; c < a.am_ncb; c += blockDim.x) {
+        const float x = a.am_val[(long)c * a.B + br];
+        const int xi = a.am_idx[(long)c * a.B + br];
+        if (sat_argmax_better(x, xi, best, bi)) { best = x; bi = xi; }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (sat_argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+      }
+      if (u == 0) { am_v[q] = best; am_i[q] = bi; }
+      __syncthreads();
+      best = am_v[0]; bi = am_i[0];
+#pragma unroll
+      for (int w = 1; w < 4; ++w)
+        if (sat_argmax_better(am_v[w], am_i[w], best, bi)) { best = am_v[w]; bi = am_i[w]; }
+      id = (bi < 0 || bi >= a.am_V) ? 0 : bi;
+    }
     if (ok) {
-      float v = a.xpart[(long)b * a.xpart_ld + q * E + j] +
-                sum_parts(a.hpart, (long)b * a.hpart_ld + q * E + j, a.h_splits, a.h_split_stride);
+      const float xv = a.am_val ? a.xt[(long)id * 4 * E + q * E + j] : a.xpart[(long)b * a.xpart_ld + q * E + j];
+      float v = xv + sum_parts(a.hpart, (long)b * a.hpart_ld + q * E + j, a.h_splits, a.h_split_stride);
       if (a.cpart) v += sum_parts(a.cpart, (long)b * a.cpart_ld + q * E + j, a.c_splits, a.c_split_stride);
       sg[q][u] = v;
       a.gates[(long)b * a.gates_ld + q * E + j] = v;
@@ -68,6 +94,10 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
           y = keep ? h * 2.f : 0.f;
         }
         ((T*)a.hd_t)[(long)b * a.hd_ld + j] = (T)y;
+      }
+      if (a.am_val) {   // the fed token's embedding row (the head's combine, the backward) and the token itself
+        ((T*)a.emb_t)[(long)b * a.emb_t_ld + j] = (T)a.emb[(long)id * E + j];
+        if (j == 0) a.tok_out[(long)b * a.tok_ld] = id;
       }
     }
     __syncthreads();

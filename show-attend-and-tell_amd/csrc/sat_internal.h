@@ -72,12 +72,7 @@ struct HeadOutArgs {
   float* pval; int32_t* pidx;
 };
 int sat_greedy_head_out(const HeadOutArgs& a, hipStream_t s);
-// the step's argmax from the block partials (first index on ties, NaN largest) -> the next fed token
-// (decoder.py:131-133), its embedding row (dtype emb_out) and its token-table row xt[id] (the embedding half of the
-// next step's LSTM input GEMM, + b_ih) into xg
-int sat_greedy_argmax(const float* pval, const int32_t* pidx, int B, int V, int32_t* tok, long tok_ld,
-                      const float* emb, int E, bf16* emb_out, long emb_ld, const float* xt, float* xg, long xg_ld,
-                      hipStream_t s);
+// the fused greedy step's shapes: B <= 128 rows, E a multiple of 64 (the LSTM kernel's token fold) up to 1024
 int sat_greedy_supported(int B, int E);
 int sat_cast_launch(const void* x, int xd, void* y, int yd, long n, hipStream_t s);
 
@@ -151,6 +146,13 @@ struct LstmFwdArgs {
   int drop_training, drop_has_mask, drop_t;
   const uint8_t* mask_in; uint8_t* mask_out; long mask_ld;
   uint64_t seed; const uint64_t* seed_ptr;
+  // nullable: the greedy step's token fold -- the token fed at this step is the argmax of the previous step's vocabulary
+  // head, reduced here from its per-block partials (am_val / am_idx [am_ncb][B], sat_greedy_head_out); the embedding
+  // half of the gate pre-activation is then read from the token table xt [V][4E] (xpart unused), and the row's
+  // embedding (emb_t, dtype) and the token (tok_out[b * tok_ld]) are written for the head and the backward.  E % 64 == 0
+  const float* am_val; const int32_t* am_idx; int am_ncb, am_V;
+  const float* xt; const float* emb; void* emb_t; long emb_t_ld;
+  int32_t* tok_out; long tok_ld;
   SatStamps st;                         // in-kernel launch timestamps (set by the launcher)
 };
 int sat_lstm_fwd_launch(const LstmFwdArgs& a, hipStream_t s);

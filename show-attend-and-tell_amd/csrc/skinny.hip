@@ -204,14 +204,21 @@ template <int NW>
 __global__ __launch_bounds__(NW * 64) void head_mid_kernel(HeadMidArgs a, int kw) {
   __shared__ __attribute__((aligned(16))) float red[2 * 16 * SK_RLD];
   const int bx = blockIdx.x, row0 = blockIdx.y * 32;
+  // the epilogue's operands of this thread's piece (32 rows x 8 pieces = 256: one per thread of the first four waves),
+  // requested before the tile's fragment loads so their latency hides under the MFMAs
+  const int q = threadIdx.x, rl = q >> 3, c4 = (q & 7) * 4, row = row0 + rl, n = bx * SK_COLS + c4;
+  const bool mine = q < 32 * 8 && row < a.B;
+  float4 bh = make_float4(0.f, 0.f, 0.f, 0.f), bz = bh, zp = bh;
+  uint2 eu = make_uint2(0u, 0u);
+  if (mine) {
+    bh = *(const float4*)(a.fh_b + n);
+    bz = *(const float4*)(a.fz_b + n);
+    zp = sum_parts4(a.fzp, (long)row * a.fzp_ld + n, a.fz_splits, a.fz_split_stride);
+    eu = *(const uint2*)(a.emb + (long)row * a.emb_ld + n);
+  }
   skinny_tile<2, NW>(a.hd, a.hd_ld, a.B, row0, a.fh_w, a.E, a.E, bx * SK_COLS, 0, a.E, kw, red);
-  for (int q = threadIdx.x; q < 32 * 8; q += NW * 64) {
-    const int rl = q >> 3, c4 = (q & 7) * 4, row = row0 + rl, n = bx * SK_COLS + c4;
-    if (row >= a.B) continue;
+  if (mine) {
     const float4 acc = *(const float4*)(red + rl * SK_RLD + c4);
-    const float4 bh = *(const float4*)(a.fh_b + n), bz = *(const float4*)(a.fz_b + n);
-    const float4 zp = sum_parts4(a.fzp, (long)row * a.fzp_ld + n, a.fz_splits, a.fz_split_stride);
-    const uint2 eu = *(const uint2*)(a.emb + (long)row * a.emb_ld + n);
     const bf16* ev = (const bf16*)&eu;
     const float h4[4] = {acc.x + bh.x, acc.y + bh.y, acc.z + bh.z, acc.w + bh.w};
     const float z4[4] = {zp.x + bz.x, zp.y + bz.y, zp.z + bz.z, zp.w + bz.w};
@@ -237,6 +244,14 @@ __global__ __launch_bounds__(NW * 64) void head_out_kernel(HeadOutArgs a, int kw
   const SatStampT0 t0 = sat_stamp_begin(st);
   __shared__ __attribute__((aligned(16))) float red[MB * 16 * SK_RLD];
   const int bx = blockIdx.x;
+  // this thread's four bias columns (the same in every pass of the epilogue: NW * 64 is a multiple of 8), requested
+  // before the tile's fragment loads
+  float bias4[4];
+  {
+    const int n = bx * SK_COLS + (threadIdx.x & 7) * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bias4[k] = n + k < a.V ? a.bias[n + k] : 0.f;
+  }
   skinny_tile<MB, NW>(a.x, a.x_ld, a.B, 0, a.w, a.E, a.V, bx * SK_COLS, 0, a.E, kw, red);
   constexpr int PIECES = MB * 16 * (SK_COLS / 4);   // a multiple of 64: whole waves take part in the shuffles
   const bool vec = (a.V & 3) == 0 && (((uintptr_t)a.preds | (uintptr_t)(a.preds_ld * 2)) & 7) == 0;
@@ -251,7 +266,7 @@ __global__ __launch_bounds__(NW * 64) void head_out_kernel(HeadOutArgs a, int kw
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int col = n + k;
-      float x = v[k] + (col < a.V ? a.bias[col] : 0.f);
+      float x = v[k] + bias4[k];
       if (a.relu) x = x > 0.f ? x : 0.f;
       pv[k] = (bf16)x;
       if (row < a.B && col < a.V) {
@@ -281,45 +296,6 @@ __global__ __launch_bounds__(NW * 64) void head_out_kernel(HeadOutArgs a, int kw
     }
   }
   sat_stamp_end(st, t0);
-}
-
-// one workgroup per row: the argmax over the block partials, then the next step's inputs of that row
-__global__ __launch_bounds__(256) void greedy_argmax_kernel(const float* __restrict__ pval,
-                                                            const int32_t* __restrict__ pidx, int ncb, int B, int V,
-                                                            int32_t* __restrict__ tok, long tok_ld,
-                                                            const float* __restrict__ emb, int E,
-                                                            bf16* __restrict__ emb_out, long emb_ld,
-                                                            const float* __restrict__ xt, float* __restrict__ xg,
-                                                            long xg_ld) {
-  const int b = blockIdx.x, tid = threadIdx.x;
-  float best = -INFINITY;
-  int bi = 0x7fffffff;
-  for (int c = tid; c < ncb; c += 256) {
-    const float x = pval[(long)c * B + b];
-    const int xi = pidx[(long)c * B + b];
-    if (sat_argmax_better(x, xi, best, bi)) { best = x; bi = xi; }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(best, o, 64);
-    const int oi = __shfl_xor(bi, o, 64);
-    if (sat_argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
-  }
-  __shared__ float sv[4];
-  __shared__ int si[4];
-  if ((tid & 63) == 0) { sv[tid >> 6] = best; si[tid >> 6] = bi; }
-  __syncthreads();
-  best = sv[0]; bi = si[0];
-#pragma unroll
-  for (int w = 1; w < 4; ++w)
-    if (sat_argmax_better(sv[w], si[w], best, bi)) { best = sv[w]; bi = si[w]; }
-  const int id = (bi < 0 || bi >= V) ? 0 : bi;
-  if (tid == 0) tok[(long)b * tok_ld] = id;
-  const float* er = emb + (long)id * E;
-  for (int e = tid; e < E; e += 256) emb_out[(long)b * emb_ld + e] = (bf16)er[e];
-  const float4* xr = (const float4*)(xt + (long)id * 4 * E);
-  float4* xo = (float4*)(xg + (long)b * xg_ld);
-  for (int i = tid; i < E; i += 256) xo[i] = xr[i];   // 4E floats = E float4
 }
 
 }  // namespace
@@ -370,7 +346,7 @@ int sat_skinny_splits(int M, int N, int K) {
 }
 
 
-int sat_greedy_supported(int B, int E) { return B >= 1 && B <= 128 && E % 32 == 0 && E >= 32 && E <= 1024; }
+int sat_greedy_supported(int B, int E) { return B >= 1 && B <= 128 && E % 64 == 0 && E >= 64 && E <= 1024; }
 
 int sat_greedy_head_mid(const HeadMidArgs& a, hipStream_t s) {
   if (!sat_greedy_supported(a.B, a.E)) return (int)hipErrorInvalidValue;
@@ -394,14 +370,5 @@ int sat_greedy_head_out(const HeadOutArgs& a, hipStream_t s) {
   else if (a.B <= 64) SAT_HEAD_OUT(4);
   else SAT_HEAD_OUT(8);
 #undef SAT_HEAD_OUT
-  return (int)hipGetLastError();
-}
-
-int sat_greedy_argmax(const float* pval, const int32_t* pidx, int B, int V, int32_t* tok, long tok_ld,
-                      const float* emb, int E, bf16* emb_out, long emb_ld, const float* xt, float* xg, long xg_ld,
-                      hipStream_t s) {
-  if (((uintptr_t)xt & 15) || ((uintptr_t)xg & 15) || (xg_ld & 3)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(greedy_argmax_kernel, dim3(B), dim3(256), 0, s, pval, pidx, sat_cdiv(V, SK_COLS), B, V, tok,
-                     tok_ld, emb, E, emb_out, emb_ld, xt, xg, xg_ld);
   return (int)hipGetLastError();
 }

@@ -247,7 +247,7 @@ def test_production_shape_bf16_close_to_oracle(sat, name):
 
 
 # the B = 4 shapes against the bf16 rounding mirror (fp64): the bound from the measured distribution
-SHAPES_BF16_MIRROR_TOL = 2e-2
+SHAPES_BF16_MIRROR_TOL = 1e-2   # measured <= 2.7e-3 (profiles/r6_s4/testsv_1.log)
 
 
 @pytest.mark.parametrize("name", list(SHAPES))
