@@ -1023,7 +1023,8 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
     SAT_CHECK((hipError_t)dgrad(13, R, E, 4 * E, dg_t, HG, c.W(lay->wih), E + D, w.demb, E, d.ado ? w.dcomb : nullptr,
                                 E));
     if (w.emb_ws)
-      SAT_CHECK((hipError_t)sat_embed_scatter_add_sorted(w.demb, w.tok, R, E, G(lay->embedding), w.emb_ws, s));
+      SAT_CHECK((hipError_t)sat_embed_scatter_add_sorted(w.demb, w.tok, R, E, G(lay->embedding), accumulate, w.emb_ws,
+                                                         s));
     else
       SAT_CHECK((hipError_t)sat_embed_scatter_add(w.demb, w.tok, R, E, G(lay->embedding), s));
   }

@@ -474,23 +474,36 @@ __global__ void embed_scatter_kernel(const float* __restrict__ dX, const int32_t
 //    chains, then the chains in order) and adds the sum to G[tok].
 // Every G row is written by one thread per column, once: the same bits on every run.
 constexpr int kEmbSortMax = 16384, kEmbPiece = 32;
+// 16 rows per workgroup x 16 parts of the token range per row (thread = part * 16 + row: the lanes of one part read
+// the same LDS words), the parts' counts summed in LDS
+constexpr int kRankRows = 16, kRankParts = 16;
 __global__ __launch_bounds__(256) void embed_rank_kernel(const int32_t* __restrict__ tok, int R,
                                                          int32_t* __restrict__ perm, int32_t* __restrict__ stok,
                                                          int32_t* __restrict__ seg) {
   __shared__ __attribute__((aligned(16))) int32_t st[kEmbSortMax];
+  __shared__ int cnt[3][kRankParts][kRankRows];
   const int R4 = (R + 3) & ~3;
   for (int i = threadIdx.x; i < R4; i += blockDim.x) st[i] = i < R ? tok[i] : 0x7fffffff;   // past R: no token
   __syncthreads();
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
-  const int k = st[r];
+  const int rl = threadIdx.x & (kRankRows - 1), part = threadIdx.x / kRankRows;
+  const int r = blockIdx.x * kRankRows + rl;
+  const int k = r < R ? st[r] : 0;
+  // this part's range of the (4-token) words
+  const int words = R4 / 4, per = (words + kRankParts - 1) / kRankParts;
+  const int w0 = part * per, w1 = min(words, w0 + per);
   int less = 0, before = 0, eq = 0;
-  for (int i = 0; i < R4; i += 4) {   // the same i for every lane: LDS broadcast reads, 4 tokens each
+#pragma unroll 4
+  for (int wi = w0; wi < w1; ++wi) {
+    const int i = 4 * wi;
     const int4 x = *(const int4*)(st + i);
     less += (x.x < k) + (x.y < k) + (x.z < k) + (x.w < k);
     eq += (x.x == k) + (x.y == k) + (x.z == k) + (x.w == k);
     before += ((x.x == k) & (i < r)) + ((x.y == k) & (i + 1 < r)) + ((x.z == k) & (i + 2 < r)) + ((x.w == k) & (i + 3 < r));
   }
+  cnt[0][part][rl] = less; cnt[1][part][rl] = eq; cnt[2][part][rl] = before;
+  __syncthreads();
+  if (part != 0 || r >= R) return;
+  for (int q = 1; q < kRankParts; ++q) { less += cnt[0][q][rl]; eq += cnt[1][q][rl]; before += cnt[2][q][rl]; }
   const int pos = less + before;
   perm[pos] = r;
   stok[pos] = k;
@@ -503,7 +516,7 @@ __global__ __launch_bounds__(64) void embed_segsum_kernel(const float* __restric
                                                           const int32_t* __restrict__ perm,
                                                           const int32_t* __restrict__ stok,
                                                           const int32_t* __restrict__ seg, int R, float* G,
-                                                          float* __restrict__ part) {
+                                                          float* __restrict__ part, int accumulate) {
   const int p = blockIdx.x, e = blockIdx.y * 256 + 4 * threadIdx.x;
   const int s0 = p * kEmbPiece, n = min(R - s0, kEmbPiece);
   __shared__ int sr[kEmbPiece], stk[kEmbPiece], sa[kEmbPiece], sb[kEmbPiece];
@@ -527,8 +540,9 @@ __global__ __launch_bounds__(64) void embed_segsum_kernel(const float* __restric
       acc = f4add(acc, x[i]);
       if (i + 1 == n || stk[i + 1] != stk[i]) {   // the run [rs, i] of token stk[i] ends in this piece
         if (sa[i] == s0 + rs && sb[i] == s0 + i + 1) {
+          // beta = 0: G was zeroed on this stream (the decoder's zeroing launch), 0 + acc is acc: store only
           float4* g = (float4*)(G + (long)stk[i] * E + e);
-          *g = f4add(*g, acc);
+          *g = accumulate ? f4add(*g, acc) : acc;
         } else {
           *(float4*)(part + ((long)p * 2 + (rs == 0 ? 0 : 1)) * E + e) = acc;
         }
@@ -542,7 +556,8 @@ __global__ __launch_bounds__(64) void embed_segsum_kernel(const float* __restric
 // grid (pieces, ceil(E / 256)), 256 threads = 4 chains x 64 threads
 __global__ __launch_bounds__(256) void embed_segfix_kernel(const int32_t* __restrict__ stok,
                                                            const int32_t* __restrict__ seg, int R, int E,
-                                                           const float* __restrict__ part, float* G) {
+                                                           const float* __restrict__ part, float* G,
+                                                           int accumulate) {
   const int p = blockIdx.x, chain = threadIdx.x >> 6, e = blockIdx.y * 256 + 4 * (threadIdx.x & 63);
   const int s0 = p * kEmbPiece, s1 = min(R, s0 + kEmbPiece);
   const int sa = seg[2 * (s1 - 1)], sb = seg[2 * (s1 - 1) + 1];   // the segment of the piece's last position
@@ -569,7 +584,7 @@ __global__ __launch_bounds__(256) void embed_segfix_kernel(const int32_t* __rest
   const float4 own = *(const float4*)(part + ((long)p * 2 + (sa == s0 ? 0 : 1)) * E + e);
   const float4 sum = f4add(own, f4add(f4add(acc, cs[0][threadIdx.x]), f4add(cs[1][threadIdx.x], cs[2][threadIdx.x])));
   float4* g = (float4*)(G + (long)stok[s1 - 1] * E + e);
-  *g = f4add(*g, sum);
+  *g = accumulate ? f4add(*g, sum) : sum;
 }
 
 // ---- greedy argmax over V (first index wins ties, decoder.py:132) ----------
@@ -820,7 +835,7 @@ static long embed_part_off(int R) { return (4L * R * 4 + 255) / 256 * 256; }
 size_t sat_embed_sorted_ws_bytes(int R, int E) {
   return (size_t)(embed_part_off(R) + (long)sat_cdiv(R, kEmbPiece) * 2 * E * 4);
 }
-int sat_embed_scatter_add_sorted(const float* dX, const int32_t* tok, int R, int E, float* G, void* ws,
+int sat_embed_scatter_add_sorted(const float* dX, const int32_t* tok, int R, int E, float* G, int accumulate, void* ws,
                                  hipStream_t s) {
   if (R <= 0) return 0;
   if (R > kEmbSortMax || E % 4 || ((uintptr_t)dX & 15) || ((uintptr_t)G & 15) || !ws) return (int)hipErrorInvalidValue;
@@ -829,10 +844,11 @@ int sat_embed_scatter_add_sorted(const float* dX, const int32_t* tok, int R, int
   int32_t* seg = stok + R;
   float* part = (float*)((char*)ws + embed_part_off(R));
   const int pieces = sat_cdiv(R, kEmbPiece);
-  hipLaunchKernelGGL(embed_rank_kernel, dim3(sat_cdiv(R, 256)), dim3(256), 0, s, tok, R, perm, stok, seg);
+  hipLaunchKernelGGL(embed_rank_kernel, dim3(sat_cdiv(R, kRankRows)), dim3(kRankRows * kRankParts), 0, s, tok, R,
+                     perm, stok, seg);
   const dim3 g(pieces, sat_cdiv(E, 256));
-  hipLaunchKernelGGL(embed_segsum_kernel, g, dim3(64), 0, s, dX, E, perm, stok, seg, R, G, part);
-  hipLaunchKernelGGL(embed_segfix_kernel, g, dim3(256), 0, s, stok, seg, R, E, part, G);
+  hipLaunchKernelGGL(embed_segsum_kernel, g, dim3(64), 0, s, dX, E, perm, stok, seg, R, G, part, accumulate);
+  hipLaunchKernelGGL(embed_segfix_kernel, g, dim3(256), 0, s, stok, seg, R, E, part, G, accumulate);
   return (int)hipGetLastError();
 }
 

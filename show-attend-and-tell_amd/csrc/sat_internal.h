@@ -45,7 +45,9 @@ __device__ __forceinline__ bool sat_argmax_better(float x, int xi, float y, int 
 // launch for tokens whose rows span several pieces), no fp32 atomics.  R <= sat_embed_sorted_max_rows(), V < 2^18.
 int sat_embed_sorted_max_rows();
 size_t sat_embed_sorted_ws_bytes(int R, int E);
-int sat_embed_scatter_add_sorted(const float* dX, const int32_t* tok, int R, int E, float* G, void* ws, hipStream_t s);
+// accumulate = 0: the caller zeroed G on this stream (each touched row is then stored, not read back)
+int sat_embed_scatter_add_sorted(const float* dX, const int32_t* tok, int R, int E, float* G, int accumulate, void* ws,
+                                 hipStream_t s);
 
 // ---- the greedy decoder step's output head (no teacher forcing, bf16; skinny.hip) ----
 // sat_skinny_dual_try: two skinny products of one shape in one launch (returns 1 when launched)
