@@ -196,8 +196,8 @@ size_t carve(const SatDecoderDims& d, char* base, WS* w) {
   if (greedy_fused(d)) {
     c.take(w->xt, V * 4 * E * f);
     c.take(w->fzp, sp.c * B * E * f);
-    c.take(w->am_val, (size_t)sat_cdiv(V, 32) * B * f);
-    c.take(w->am_idx, (size_t)sat_cdiv(V, 32) * B * 4);
+    c.take(w->am_val, (size_t)sat_greedy_head_blocks(d.B, d.V, d.E) * B * f);
+    c.take(w->am_idx, (size_t)sat_greedy_head_blocks(d.B, d.V, d.E) * B * 4);
   } else {
     w->xt = w->fzp = w->am_val = nullptr;
     w->am_idx = nullptr;
@@ -575,7 +575,7 @@ int greedy_loop(const Ctx& c, const WS& w, const Splits& sp, const StepIO& io, v
       l.mask_in = mask_in ? mask_in + oE : nullptr; l.mask_out = w.dmask + oE; l.mask_ld = c.T1 * E;
       l.seed = d.seed; l.seed_ptr = d.seed_ptr;
       if (t > 0) {   // the token fed at t: the argmax of step t - 1's head partials, folded into this launch
-        l.am_val = w.am_val; l.am_idx = w.am_idx; l.am_ncb = sat_cdiv(V, 32); l.am_V = V;
+        l.am_val = w.am_val; l.am_idx = w.am_idx; l.am_ncb = sat_greedy_head_blocks(B, V, E); l.am_V = V;
         l.xt = w.xt; l.emb = c.F(lay.embedding); l.emb_t = c.at(w.emb_t, oE); l.emb_t_ld = c.T1 * E;
         l.tok_out = w.tok + t; l.tok_ld = T1;
       }

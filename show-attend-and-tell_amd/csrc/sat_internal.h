@@ -64,8 +64,8 @@ struct HeadMidArgs {
   bf16* comb; long comb_ld;                   // out: f_out's input
 };
 int sat_greedy_head_mid(const HeadMidArgs& a, hipStream_t s);
-// vocabulary head of one step (decoder.py:125 / 157): preds = act(x W^T + b) in bf16, plus per 32-column block the
-// argmax of every row over the rounded logits (pval / pidx [ceil(V / 32)][B])
+// vocabulary head of one step (decoder.py:125 / 157): preds = act(x W^T + b) in bf16, plus per column block the
+// argmax of every row over the rounded logits (pval / pidx [sat_greedy_head_blocks][B])
 struct HeadOutArgs {
   int B, V, E, relu;
   const bf16* x; long x_ld;
@@ -74,6 +74,8 @@ struct HeadOutArgs {
   float* pval; int32_t* pidx;
 };
 int sat_greedy_head_out(const HeadOutArgs& a, hipStream_t s);
+// the number of argmax partials per row sat_greedy_head_out writes for these shapes (<= ceil(V / 16))
+int sat_greedy_head_blocks(int B, int V, int E);
 // the fused greedy step's shapes: B <= 128 rows, E a multiple of 64 (the LSTM kernel's token fold) up to 1024
 int sat_greedy_supported(int B, int E);
 int sat_cast_launch(const void* x, int xd, void* y, int yd, long n, hipStream_t s);

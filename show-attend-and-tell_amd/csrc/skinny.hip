@@ -298,6 +298,92 @@ __global__ __launch_bounds__(NW * 64) void head_out_kernel(HeadOutArgs a, int kw
   sat_stamp_end(st, t0);
 }
 
+// The vocabulary head at E = 512 with the step's input rows staged once in LDS: 64 columns per workgroup (157 at
+// V = 10000: one round on 256 CUs, where the skinny form above needs 313 workgroups), each of the four waves owning 16
+// columns over all of K -- its 16 weight fragments register-direct, the A fragments read from LDS -- so no wave-order
+// K fold; the 128 x 512 bf16 rows (128 KiB) land by LDS-DMA, 16-B chunk c of row r at chunk c ^ (r & 15) (one 1 KiB
+// instruction per row; the fragment reads of 16 rows x 4 k-chunks are then conflict-free).  Argmax partials per 16
+// columns.
+constexpr int HO_K = 512, HO_COLS = 64, HO_BLK = 16;
+typedef __attribute__((address_space(3))) void sk_lds_void;
+typedef __attribute__((address_space(1))) const void sk_gbl_void;
+template <int MB>
+__global__ __launch_bounds__(256) void head_out_lds_kernel(HeadOutArgs a, SatStamps st) {
+  const SatStampT0 t0 = sat_stamp_begin(st);
+  __shared__ __attribute__((aligned(16))) char sA[MB * 16 * HO_K * 2];
+  const int lane = threadIdx.x & 63, fr = lane & 15, fh = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n0 = blockIdx.x * HO_COLS + w * HO_BLK;   // this wave's 16 columns
+  // the wave's weight fragments (all 16 k-steps of 32) and bias, requested first
+  const bf16* wr = a.w + (long)min(n0 + fr, a.V - 1) * HO_K + 8 * fh;
+  bf16x8 bw[HO_K / 32];
+#pragma unroll
+  for (int ks = 0; ks < HO_K / 32; ++ks) bw[ks] = *(const bf16x8*)(wr + ks * 32);
+  float bias4[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bias4[r] = n0 + 4 * fh + r < a.V ? a.bias[n0 + 4 * fh + r] : 0.f;
+  // the rows by LDS-DMA: wave w issues rows w, w + 4, ..; lane s fills slot s with chunk s ^ (r & 15)
+  for (int r = w; r < MB * 16; r += 4) {
+    const int row = min(r, a.B - 1);
+    __builtin_amdgcn_global_load_lds((sk_gbl_void*)(a.x + (long)row * a.x_ld + 8 * (lane ^ (r & 15))),
+                                     (sk_lds_void*)(sA + r * HO_K * 2), 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  f32x4 acc[MB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < HO_K / 32; ++ks) {
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const bf16x8 af = *(const bf16x8*)(sA + (i * 16 + fr) * HO_K * 2 + 16 * ((4 * ks + fh) ^ fr));
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks], af, acc[i], 0, 0, 0);
+    }
+  }
+  // lane holds columns n0 + 4 fh .. + 3 of row i * 16 + fr
+  const bool vec = (a.V & 3) == 0 && (((uintptr_t)a.preds | (uintptr_t)(a.preds_ld * 2)) & 7) == 0;
+#pragma unroll
+  for (int i = 0; i < MB; ++i) {
+    const int row = i * 16 + fr, n = n0 + 4 * fh;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    uint2 pu;
+    bf16* pv = (bf16*)&pu;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x = acc[i][r] + bias4[r];
+      if (a.relu) x = x > 0.f ? x : 0.f;
+      pv[r] = (bf16)x;
+      if (row < a.B && n + r < a.V) {
+        const float xr = (float)pv[r];
+        if (sat_argmax_better(xr, n + r, best, bi)) { best = xr; bi = n + r; }
+      }
+    }
+    if (row < a.B) {
+      bf16* dst = a.preds + (long)row * a.preds_ld + n;
+      if (vec && n + 3 < a.V) {
+        *(uint2*)dst = pu;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < a.V) dst[r] = pv[r];
+      }
+    }
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {   // the 4 lanes (fh) of a row
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (sat_argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+    }
+    if (fh == 0 && row < a.B) {
+      const long cb = n0 / HO_BLK;
+      a.pval[cb * a.B + row] = best;
+      a.pidx[cb * a.B + row] = bi;
+    }
+  }
+  sat_stamp_end(st, t0);
+}
+
 }  // namespace
 
 int sat_skinny_try(const SatGemm& g, hipStream_t st, int* err) {
@@ -356,11 +442,24 @@ int sat_greedy_head_mid(const HeadMidArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// the vocabulary head's form for (B, V, E): the LDS-staged one at E = 512 (partials per 16 columns), else the skinny
+// tile (per 32)
+static bool head_out_lds(int B, int E) { return E == HO_K && B <= 128; }
+int sat_greedy_head_blocks(int B, int V, int E) { return sat_cdiv(V, head_out_lds(B, E) ? HO_BLK : SK_COLS); }
+
 int sat_greedy_head_out(const HeadOutArgs& a, hipStream_t s) {
   if (!sat_greedy_supported(a.B, a.E) || a.V < 1) return (int)hipErrorInvalidValue;
+  const SatStamps st = sat_launch_stamps();
+  if (head_out_lds(a.B, a.E)) {
+    if (((uintptr_t)a.x & 15) || (a.x_ld & 7) || ((uintptr_t)a.w & 15)) return (int)hipErrorInvalidValue;
+    const dim3 grid(sat_cdiv(a.V, HO_COLS));
+    if (a.B <= 32) hipLaunchKernelGGL(head_out_lds_kernel<2>, grid, dim3(256), 0, s, a, st);
+    else if (a.B <= 64) hipLaunchKernelGGL(head_out_lds_kernel<4>, grid, dim3(256), 0, s, a, st);
+    else hipLaunchKernelGGL(head_out_lds_kernel<8>, grid, dim3(256), 0, s, a, st);
+    return (int)hipGetLastError();
+  }
   const dim3 grid(sat_cdiv(a.V, SK_COLS));
   const int nw = head_waves(a.E), kw = head_kw(a.E);
-  const SatStamps st = sat_launch_stamps();
 #define SAT_HEAD_OUT(MB)                                                                                            \
   do {                                                                                                            \
     if (nw == 4) hipLaunchKernelGGL((head_out_kernel<MB, 4>), grid, dim3(256), 0, s, a, kw, st);                   \
