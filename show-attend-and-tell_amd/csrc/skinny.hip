@@ -21,6 +21,8 @@
 // Measured and not kept (profiles/r5_s10, r5_s16): an XCD-aware workgroup order (the column blocks of one split on
 // one XCD: fewer fabric reads of A, the h GEMM 7.5 -> 9.1 us), 64-column workgroups of eight waves (half the
 // workgroups and ~60 % of the bytes moved: 7.6 -> 11.9 us per product, step 6.40 -> 6.47-6.50 ms).
+#include <utility>
+
 #include "sat_common.h"
 #include "sat_internal.h"
 
@@ -301,45 +303,102 @@ __global__ __launch_bounds__(NW * 64) void head_out_kernel(HeadOutArgs a, int kw
 // The vocabulary head at E = 512 with the step's input rows staged once in LDS: 64 columns per workgroup (157 at
 // V = 10000: one round on 256 CUs, where the skinny form above needs 313 workgroups), each of the four waves owning 16
 // columns over all of K -- its 16 weight fragments register-direct, the A fragments read from LDS -- so no wave-order
-// K fold; the 128 x 512 bf16 rows (128 KiB) land by LDS-DMA, 16-B chunk c of row r at chunk c ^ (r & 15) (one 1 KiB
-// instruction per row; the fragment reads of 16 rows x 4 k-chunks are then conflict-free).  Argmax partials per 16
-// columns.
-constexpr int HO_K = 512, HO_COLS = 64, HO_BLK = 16;
+// K fold.  The rows (MB x 16 x 512 bf16, 128 KiB at B = 128) land by LDS-DMA in four K quarters, quarter-major
+// ([q][row][256 B], 16-B chunk c of a row at chunk c ^ (row & 15): one 1 KiB instruction = 4 rows of a quarter, the
+// fragment reads of 16 rows x 4 k-chunks conflict-free), each quarter waited for right before its k-steps, so the
+// MFMAs of the first quarters run while the later ones land.  Argmax partials per 64 columns (the waves' per-row
+// winners meet in LDS).
+constexpr int HO_K = 512, HO_COLS = 64, HO_BLK = 64, HO_Q = 4, HO_QB = HO_K * 2 / HO_Q;   // 256-B quarter rows
 typedef __attribute__((address_space(3))) void sk_lds_void;
-typedef __attribute__((address_space(1))) const void sk_gbl_void;
+// every wave's LDS-DMAs older than its N youngest vector-memory operations have landed, then a barrier
+template <int N>
+__device__ __forceinline__ void ho_vm_barrier() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)\n\ts_barrier" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+template <typename F, int... Ts>
+__device__ __forceinline__ void sk_static_for_impl(F&& f, std::integer_sequence<int, Ts...>) {
+  (f(std::integral_constant<int, Ts>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sk_static_for(F&& f) {
+  sk_static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 template <int MB>
 __global__ __launch_bounds__(256) void head_out_lds_kernel(HeadOutArgs a, SatStamps st) {
+  static_assert(MB % 2 == 0, "DMA instructions cover 4 rows: MB * 16 / 4 per quarter, a multiple of the 4 waves");
+  constexpr int MR = MB * 16, INSTR = MR / 4 / 4;   // DMA instructions per wave per quarter
   const SatStampT0 t0 = sat_stamp_begin(st);
-  __shared__ __attribute__((aligned(16))) char sA[MB * 16 * HO_K * 2];
+  // one LDS array per K quarter: distinct objects get distinct alias scopes, so the compiler's wait before a read of
+  // quarter q covers only quarter q's DMAs (with one array it waits for every pending LDS-DMA)
+  __shared__ __attribute__((aligned(16))) char sA0[MR * HO_QB];
+  __shared__ __attribute__((aligned(16))) char sA1[MR * HO_QB];
+  __shared__ __attribute__((aligned(16))) char sA2[MR * HO_QB];
+  __shared__ __attribute__((aligned(16))) char sA3[MR * HO_QB];
+  auto quarter = [&](int q) -> char* { return q == 0 ? sA0 : q == 1 ? sA1 : q == 2 ? sA2 : sA3; };
+  __shared__ float s_bv[4][MR];
+  __shared__ int s_bi[4][MR];
   const int lane = threadIdx.x & 63, fr = lane & 15, fh = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int n0 = blockIdx.x * HO_COLS + w * HO_BLK;   // this wave's 16 columns
+  const int n0 = blockIdx.x * HO_COLS + w * 16;   // this wave's 16 columns
   // the wave's weight fragments (all 16 k-steps of 32) and bias, requested first
   const bf16* wr = a.w + (long)min(n0 + fr, a.V - 1) * HO_K + 8 * fh;
   bf16x8 bw[HO_K / 32];
 #pragma unroll
   for (int ks = 0; ks < HO_K / 32; ++ks) bw[ks] = *(const bf16x8*)(wr + ks * 32);
+  // (branch-free: a predicated load splits the block, and the compiler's wait-count pass then waits for every load
+  // before the first MFMA instead of the quarter the asm waits name)
   float bias4[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) bias4[r] = n0 + 4 * fh + r < a.V ? a.bias[n0 + 4 * fh + r] : 0.f;
-  // the rows by LDS-DMA: wave w issues rows w, w + 4, ..; lane s fills slot s with chunk s ^ (r & 15)
-  for (int r = w; r < MB * 16; r += 4) {
-    const int row = min(r, a.B - 1);
-    __builtin_amdgcn_global_load_lds((sk_gbl_void*)(a.x + (long)row * a.x_ld + 8 * (lane ^ (r & 15))),
-                                     (sk_lds_void*)(sA + r * HO_K * 2), 16, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  for (int r = 0; r < 4; ++r) bias4[r] = a.bias[min(n0 + 4 * fh + r, a.V - 1)];
+  // the rows by LDS-DMA, quarter by quarter: instruction j of wave w covers rows 4 (w + 4 j) .. + 3; lane l fills slot
+  // l % 16 of row 4 (w + 4 j) + l / 16 with chunk (l % 16) ^ (row & 15) of the quarter
+  // (buffer_load ... lds through a resource over the rows, as convblock.hip stages its planes: the wait for quarter q
+  // is the asm's counted vmcnt, with no compiler-inserted vmcnt(0) in front of the first LDS read)
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, (short)0, (int)(2L * ((long)(a.B - 1) * a.x_ld + HO_K)), 0x00020000);
+#pragma unroll
+  for (int q = 0; q < HO_Q; ++q)
+#pragma unroll
+    for (int j = 0; j < INSTR; ++j) {
+      const int r0 = 4 * (w + 4 * j), row = r0 + (lane >> 4);
+      const int off = (int)(2L * ((long)min(row, a.B - 1) * a.x_ld + q * (HO_K / HO_Q) + 8 * ((lane & 15) ^ (row & 15))));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (sk_lds_void*)(quarter(q) + r0 * HO_QB), 16, off, 0, 0, 0);
+    }
   f32x4 acc[MB];
 #pragma unroll
   for (int i = 0; i < MB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][MB];
+  auto frag = [&](int ks, bf16x8 (&dst)[MB]) {
+    const int q = ks / 4, c = 4 * (ks % 4) + fh;
 #pragma unroll
-  for (int ks = 0; ks < HO_K / 32; ++ks) {
-#pragma unroll
-    for (int i = 0; i < MB; ++i) {
-      const bf16x8 af = *(const bf16x8*)(sA + (i * 16 + fr) * HO_K * 2 + 16 * ((4 * ks + fh) ^ fr));
-      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks], af, acc[i], 0, 0, 0);
+    for (int i = 0; i < MB; ++i) dst[i] = *(const bf16x8*)(quarter(q) + (i * 16 + fr) * HO_QB + 16 * (c ^ fr));
+  };
+  // quarter q is waited for (the DMAs of the later quarters, INSTR each, may stay in flight) right before its k-steps;
+  // within a quarter the next k-step's A fragments are read before this one's MFMAs
+  sk_static_for<HO_K / 32>([&](auto KS) {
+    constexpr int ks = decltype(KS)::value;
+    if constexpr (ks == 0) {
+      ho_vm_barrier<(HO_Q - 1) * INSTR>();
+      frag(0, af[0]);
     }
-  }
+    if constexpr (ks + 1 < HO_K / 32 && (ks + 1) % 4 != 0) frag(ks + 1, af[(ks + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);   // the next k-step's reads stay ahead of this k-step's MFMAs
+#pragma unroll
+    for (int i = 0; i < MB; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks], af[ks & 1][i], acc[i], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (ks + 1 < HO_K / 32 && (ks + 1) % 4 == 0) {
+      ho_vm_barrier<(HO_Q - 1 - (ks + 1) / 4) * INSTR>();
+      frag(ks + 1, af[(ks + 1) & 1]);
+    }
+  });
   // lane holds columns n0 + 4 fh .. + 3 of row i * 16 + fr
   const bool vec = (a.V & 3) == 0 && (((uintptr_t)a.preds | (uintptr_t)(a.preds_ld * 2)) & 7) == 0;
 #pragma unroll
@@ -375,11 +434,18 @@ __global__ __launch_bounds__(256) void head_out_lds_kernel(HeadOutArgs a, SatSta
       const int oi = __shfl_xor(bi, o, 64);
       if (sat_argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
     }
-    if (fh == 0 && row < a.B) {
-      const long cb = n0 / HO_BLK;
-      a.pval[cb * a.B + row] = best;
-      a.pidx[cb * a.B + row] = bi;
-    }
+    if (fh == 0) { s_bv[w][row] = best; s_bi[w][row] = bi; }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < min(MR, a.B)) {   // the four waves' winners of a row, in wave order
+    const int row = threadIdx.x;
+    float best = s_bv[0][row];
+    int bi = s_bi[0][row];
+#pragma unroll
+    for (int v = 1; v < 4; ++v)
+      if (sat_argmax_better(s_bv[v][row], s_bi[v][row], best, bi)) { best = s_bv[v][row]; bi = s_bi[v][row]; }
+    a.pval[(long)blockIdx.x * a.B + row] = best;
+    a.pidx[(long)blockIdx.x * a.B + row] = bi;
   }
   sat_stamp_end(st, t0);
 }
