@@ -28,7 +28,9 @@ __device__ __forceinline__ uint8_t dropout_keep(uint64_t seed, int b, int t, int
 // Gate-parallel forward: a 256-thread block covers 64 units; thread (q, u) sums gate q of unit u
 // over its split-K slabs (4x the loads in flight of a unit-per-thread kernel: 9.5 -> 5.7 us per
 // step at B=128, E=512, 4 + 8 slabs), the cell update reads the four gates back from LDS.
-template <typename T>
+// GREEDY: the fused greedy step's extras (dropout of h into hd_t, the token fold), compiled out of the teacher-forced
+// instance (with them in, its span went 3.5-3.7 -> 4.2 us per step, profiles/r6_s5 vs r6_s2)
+template <typename T, bool GREEDY>
 __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
   __shared__ float sg[4][64];
   __shared__ float am_v[4];
@@ -41,7 +43,7 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
     const bool ok = i < units;
     const int b = ok ? (int)(i / E) : 0, j = ok ? (int)(i - (long)b * E) : 0;
     int id = 0;
-    if (a.am_val) {   // the token fold: the block's 64 units share one row (E % 64 == 0)
+    if (GREEDY && a.am_val) {   // the token fold: the block's 64 units share one row (E % 64 == 0)
       const int br = (int)(base / E);
       float best = -INFINITY;
       int bi = 0x7fffffff;
@@ -65,7 +67,7 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
       id = (bi < 0 || bi >= a.am_V) ? 0 : bi;
     }
     if (ok) {
-      const float xv = a.am_val ? a.xt[(long)id * 4 * E + q * E + j] : a.xpart[(long)b * a.xpart_ld + q * E + j];
+      const float xv = GREEDY && a.am_val ? a.xt[(long)id * 4 * E + q * E + j] : a.xpart[(long)b * a.xpart_ld + q * E + j];
       float v = xv + sum_parts(a.hpart, (long)b * a.hpart_ld + q * E + j, a.h_splits, a.h_split_stride);
       if (a.cpart) v += sum_parts(a.cpart, (long)b * a.cpart_ld + q * E + j, a.c_splits, a.c_split_stride);
       sg[q][u] = v;
@@ -80,7 +82,7 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
       a.h_out[(long)b * a.h_out_ld + j] = h;
       if (a.h_out_t) ((T*)a.h_out_t)[(long)b * a.h_out_t_ld + j] = (T)h;
       if (a.h_next_in_t) ((T*)a.h_next_in_t)[(long)b * a.h_next_in_t_ld + j] = (T)h;
-      if (a.hd_t) {   // dropout(h) for the greedy step's head: dropout_kernel's arithmetic
+      if (GREEDY && a.hd_t) {   // dropout(h) for the greedy step's head: dropout_kernel's arithmetic
         float y = h;
         if (a.drop_training) {
           uint8_t keep;
@@ -95,7 +97,7 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
         }
         ((T*)a.hd_t)[(long)b * a.hd_ld + j] = (T)y;
       }
-      if (a.am_val) {   // the fed token's embedding row (the head's combine, the backward) and the token itself
+      if (GREEDY && a.am_val) {   // the fed token's embedding row (the head's combine, the backward) and the token itself
         ((T*)a.emb_t)[(long)b * a.emb_t_ld + j] = (T)a.emb[(long)id * E + j];
         if (j == 0) a.tok_out[(long)b * a.tok_ld] = id;
       }
@@ -104,10 +106,10 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
   }
 }
 
-template <typename T>
+template <typename T, bool GREEDY>
 __global__ __launch_bounds__(256) void lstm_fwd_gp_kernel(LstmFwdArgs a) {
   const SatStampT0 t0 = sat_stamp_begin(a.st);
-  lstm_fwd_gp_kernel_body<T>(a);
+  lstm_fwd_gp_kernel_body<T, GREEDY>(a);
   sat_stamp_end(a.st, t0);
 }
 
@@ -321,7 +323,14 @@ int sat_lstm_fwd_launch(const LstmFwdArgs& args, hipStream_t s) {
   LstmFwdArgs a = args;
   a.st = sat_launch_stamps();
   const long blocks = lstm_blocks(a.B, a.E);
-  DISPATCH_T(a.dtype, lstm_fwd_gp_kernel, dim3((int)blocks), a);
+  const bool greedy = a.hd_t || a.am_val;
+  if (a.dtype == SAT_BF16) {
+    if (greedy) hipLaunchKernelGGL((lstm_fwd_gp_kernel<bf16, true>), dim3((int)blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((lstm_fwd_gp_kernel<bf16, false>), dim3((int)blocks), dim3(256), 0, s, a);
+  } else {
+    if (greedy) hipLaunchKernelGGL((lstm_fwd_gp_kernel<float, true>), dim3((int)blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((lstm_fwd_gp_kernel<float, false>), dim3((int)blocks), dim3(256), 0, s, a);
+  }
   return (int)hipGetLastError();
 }
 int sat_lstm_bwd_launch(const LstmBwdArgs& args, hipStream_t s) {
