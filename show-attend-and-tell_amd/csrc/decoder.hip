@@ -942,7 +942,9 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
         SAT_CHECK((hipError_t)sat_zero_segs(seg, nseg, s));
       }
       SAT_CHECK((hipError_t)sat_gemm_launch(gdo, s));
-      SAT_CHECK((hipError_t)colsum(d_preds, d.dtype, V, R, V, G(lay->do_b)));
+      // the bias gradient from the padded copy when there is one: 16-B aligned rows take the vector column sum (the
+      // unpadded BERT rows took the scalar one: 206 us per step, profiles/r6_s13)
+      SAT_CHECK((hipError_t)colsum(dpre, d.dtype, ldp, R, V, G(lay->do_b)));
       SAT_CHECK((hipError_t)dgrad_launch(c, R, E, V, dpre, ldp, c.W(lay->do_w), E, w.dhd, E, s, nullptr, 0, 0, 0,
                                          VP != V, &sws[1]));
     }

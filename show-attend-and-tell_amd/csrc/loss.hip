@@ -58,7 +58,9 @@ __device__ __forceinline__ void write_row_stats(float* stats, int r, int T1, int
   st[4] = nonpad ? 1.f : 0.f;
 }
 
-template <typename TT>
+// PAIRS: the bf16 pair path for even V % 8 != 0 (its own instantiation: its 64-register row would lower the
+// occupancy of the others)
+template <typename TT, bool PAIRS = false>
 __global__ __launch_bounds__(256) void loss_rows_kernel(const TT* __restrict__ preds, const int64_t* __restrict__ caps,
                                                         int B, int T, int V, int pad_id, float* __restrict__ stats) {
   __shared__ float red_m[4], red_s[4], red_c[4];
@@ -117,6 +119,57 @@ __global__ __launch_bounds__(256) void loss_rows_kernel(const TT* __restrict__ p
       write_row_stats(stats, r, T1, t, M + logf(S), xt, C, tgt != pad_id);
     }
     return;
+  }
+  if constexpr (PAIRS) {
+    {
+      // bf16 rows of an even length that is not a multiple of 8 (BERT's V = 30522): 4-byte aligned, so the row goes
+      // into registers as bf16 pairs (up to 64 per thread, all requested up front), then the same two register
+      // passes as the 16-byte path -- the element loop below paid a 2-byte load and a branchy online update per logit
+      // (240 us per 3968 x 30522 logits, profiles/r6_s13)
+      constexpr int RD = 64;
+      const int ND = V / 2;
+      const unsigned* xd = (const unsigned*)x;
+      unsigned u[RD];
+#pragma unroll
+      for (int k = 0; k < RD; ++k) {
+        const int c = threadIdx.x + k * 256;
+        u[k] = c < ND ? xd[c] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < RD; ++k) {
+        const int c = threadIdx.x + k * 256;
+        if (c < ND) {
+          const TT* h = (const TT*)&u[k];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const float xv = (float)h[j];
+            m = fmaxf(m, xv);
+            cnt += (xv > xt || (xv == xt && c * 2 + j < tgt)) ? 1.f : 0.f;
+          }
+        }
+      }
+      const float M = block_max(m, red_m);
+#pragma unroll
+      for (int k = 0; k < RD; ++k) {
+        const int c = threadIdx.x + k * 256;
+        if (c < ND) {
+          const TT* h = (const TT*)&u[k];
+          se += __expf((float)h[0] - M);
+          se += __expf((float)h[1] - M);
+        }
+      }
+      se = wave_sum(se);
+      cnt = wave_sum(cnt);
+      const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+      if (lane == 0) { red_s[w] = se; red_c[w] = cnt; }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const float S = (red_s[0] + red_s[1]) + (red_s[2] + red_s[3]);
+        const float C = (red_c[0] + red_c[1]) + (red_c[2] + red_c[3]);
+        write_row_stats(stats, r, T1, t, M + logf(S), xt, C, tgt != pad_id);
+      }
+      return;
+    }
   }
   if (V % VEC == 0) {
     // LU vectors per thread in flight (the per-thread order c = tid, tid + 256, .. is unchanged)
@@ -280,6 +333,31 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const TT* __restrict__ pr
         sat_st16(rdx, (unsigned)((long)c * VEC * sizeof(TT)), o);   // write-through (sat_common.h)
       }
     }
+  } else if (sizeof(TT) == 2 && V % 2 == 0) {
+    // even bf16 rows (4-byte aligned): pairs, LU in flight per thread
+    constexpr int LU = 8;
+    const int ND = V / 2;
+    const unsigned* xd = (const unsigned*)x;
+    unsigned* dd = (unsigned*)dx;
+    for (int c0 = threadIdx.x; c0 < ND; c0 += LU * 256) {
+      unsigned u[LU];
+#pragma unroll
+      for (int k = 0; k < LU; ++k) {
+        const int c = c0 + k * 256;
+        u[k] = c < ND ? xd[c] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < LU; ++k) {
+        const int c = c0 + k * 256;
+        if (c >= ND) break;
+        const TT* h = (const TT*)&u[k];
+        unsigned o;
+        TT* q = (TT*)&o;
+        q[0] = (TT)grad((float)h[0], 2 * c);
+        q[1] = (TT)grad((float)h[1], 2 * c + 1);
+        dd[c] = o;
+      }
+    }
   } else {
     for (int v = threadIdx.x; v < V; v += blockDim.x) dx[v] = (TT)grad((float)x[v], v);
   }
@@ -300,7 +378,10 @@ extern "C" int sat_caption_loss_forward(int B, int T, int V, int L, int dtype, c
   const int R = B * (T - 1);
   float* stats = (float*)workspace;
   float* dreg = stats + (size_t)R * kStat;
-  if (dtype == SAT_BF16)
+  if (dtype == SAT_BF16 && V % 8 != 0 && V % 2 == 0 && V / 2 <= 64 * 256)
+    hipLaunchKernelGGL((loss_rows_kernel<bf16, true>), dim3(R), dim3(256), 0, s, (const bf16*)preds, captions, B, T, V,
+                       pad_id, stats);
+  else if (dtype == SAT_BF16)
     hipLaunchKernelGGL(loss_rows_kernel<bf16>, dim3(R), dim3(256), 0, s, (const bf16*)preds, captions, B, T, V, pad_id, stats);
   else
     hipLaunchKernelGGL(loss_rows_kernel<float>, dim3(R), dim3(256), 0, s, (const float*)preds, captions, B, T, V, pad_id, stats);
