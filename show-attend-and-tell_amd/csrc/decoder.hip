@@ -884,8 +884,9 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
                    long ldo, const float* add1 = nullptr, long ld_add1 = 0) {
     return dgrad_launch(c, M, N, K, X, ldx, Wt, ldw, out, ldo, s, add1, ld_add1, 0, 0, 0, &sws[blk]);
   };
-  auto colsum = [&](const void* X, int dt, long ld, int rows, int N, float* out, float* out2 = nullptr) {
-    return sat_colsum(X, dt, ld, rows, N, out, accumulate, out2, w.colsum, s);
+  auto colsum = [&](const void* X, int dt, long ld, int rows, int N, float* out, float* out2 = nullptr,
+                    int cols_readable = 0) {
+    return sat_colsum(X, dt, ld, rows, N, out, accumulate, out2, w.colsum, s, cols_readable);
   };
 
   if (phase & 1) {  // ---------------- output head (decoder.py:117-125,149-158) ----------------
@@ -919,7 +920,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
       SAT_CHECK((hipError_t)sat_gemm_launch(gfh, s));
       SAT_CHECK((hipError_t)sat_gemm_launch(gfz, s));
       // the three bias gradients (column sums of d logits, d f_h, d f_z) in one launch pair
-      const SatColsumSeg cs[3] = {{dpre, d.dtype, ldp, R, V, G(lay->fout_b), accumulate, nullptr},
+      const SatColsumSeg cs[3] = {{dpre, d.dtype, ldp, R, V, G(lay->fout_b), accumulate, nullptr, ldp != V},
                                   {w.dfh_t, d.dtype, E, R, E, G(lay->fh_b), accumulate, nullptr},
                                   {w.dfz_t, d.dtype, E, R, E, G(lay->fz_b), accumulate, nullptr}};
       SAT_CHECK((hipError_t)sat_colsum_multi(cs, 3, w.colsum, s));
@@ -944,7 +945,7 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
       SAT_CHECK((hipError_t)sat_gemm_launch(gdo, s));
       // the bias gradient from the padded copy when there is one: 16-B aligned rows take the vector column sum (the
       // unpadded BERT rows took the scalar one: 206 us per step, profiles/r6_s13)
-      SAT_CHECK((hipError_t)colsum(dpre, d.dtype, ldp, R, V, G(lay->do_b)));
+      SAT_CHECK((hipError_t)colsum(dpre, d.dtype, ldp, R, V, G(lay->do_b), nullptr, ldp != V));
       SAT_CHECK((hipError_t)dgrad_launch(c, R, E, V, dpre, ldp, c.W(lay->do_w), E, w.dhd, E, s, nullptr, 0, 0, 0,
                                          VP != V, &sws[1]));
     }

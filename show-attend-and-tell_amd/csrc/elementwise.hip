@@ -304,7 +304,9 @@ __global__ void colsum_partial_vec_kernel(const T* __restrict__ X, long ld, int 
   colsum_partial_vec_body<T>(X, ld, R, N, rows_per, part, blockIdx.x, blockIdx.y);
 }
 
-__device__ __forceinline__ void colsum_final_body(const float* __restrict__ part, int RS, int N,
+// N output columns; the partials have NP >= N columns per row chunk (NP > N: the vector partials ran over the padded
+// width)
+__device__ __forceinline__ void colsum_final_body(const float* __restrict__ part, int RS, int N, int NP,
                                                   float* __restrict__ out, int accumulate, float* __restrict__ out2,
                                                   int bx) {
   int n = bx * 256 + (int)threadIdx.x;
@@ -313,30 +315,34 @@ __device__ __forceinline__ void colsum_final_body(const float* __restrict__ part
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   int i = 0;
   for (; i + 4 <= RS; i += 4) {
-    s0 += part[(long)i * N + n];
-    s1 += part[(long)(i + 1) * N + n];
-    s2 += part[(long)(i + 2) * N + n];
-    s3 += part[(long)(i + 3) * N + n];
+    s0 += part[(long)i * NP + n];
+    s1 += part[(long)(i + 1) * NP + n];
+    s2 += part[(long)(i + 2) * NP + n];
+    s3 += part[(long)(i + 3) * NP + n];
   }
-  for (; i < RS; ++i) s0 += part[(long)i * N + n];
+  for (; i < RS; ++i) s0 += part[(long)i * NP + n];
   const float s = (s0 + s1) + (s2 + s3);
   out[n] = accumulate ? out[n] + s : s;
   if (out2) out2[n] = accumulate ? out2[n] + s : s;
 }
-__global__ void colsum_final_kernel(const float* __restrict__ part, int RS, int N, float* __restrict__ out,
+__global__ void colsum_final_kernel(const float* __restrict__ part, int RS, int N, int NP, float* __restrict__ out,
                                     int accumulate, float* __restrict__ out2) {
-  colsum_final_body(part, RS, N, out, accumulate, out2, blockIdx.x);
+  colsum_final_body(part, RS, N, NP, out, accumulate, out2, blockIdx.x);
 }
 
-// geometry of one column sum (shared by sat_colsum and sat_colsum_multi): RS row chunks of rows_per rows
+// geometry of one column sum (shared by sat_colsum and sat_colsum_multi): RS row chunks of rows_per rows; np columns
+// of partials (N, or N rounded up to the vector width when the caller's rows are readable that far: the decoder's
+// zero-padded d logits, whose odd BERT vocabulary otherwise took the scalar kernel)
 struct ColsumPlan {
   bool vok;
-  int colblocks, RS, rows_per;
+  int colblocks, RS, rows_per, np;
 };
-inline ColsumPlan colsum_plan(const void* X, int dtype, long ld, int R, int N) {
+inline ColsumPlan colsum_plan(const void* X, int dtype, long ld, int R, int N, int readable = 0) {
   ColsumPlan p;
   const int vec = dtype == SAT_BF16 ? 8 : 4;
-  p.vok = N % vec == 0 && ld % vec == 0 && ((uintptr_t)X & 15) == 0;
+  const int nr = (N + vec - 1) / vec * vec;
+  p.vok = (N % vec == 0 || (readable && nr <= ld)) && ld % vec == 0 && ((uintptr_t)X & 15) == 0;
+  p.np = p.vok ? nr : N;
   p.colblocks = sat_cdiv(N, 256 * (p.vok ? vec : 1));
   int RS = 1;
   while (p.colblocks * RS < 512 && RS < 64 && (R + RS * 2 - 1) / (RS * 2) >= 16) RS *= 2;
@@ -352,7 +358,7 @@ constexpr int kColsumMaxSegs = 8;
 struct ColsumMultiArgs {
   int n;
   struct Seg {
-    const void* X; long ld; int R, N, dtype, vok, colblocks, RS, rows_per, accumulate;
+    const void* X; long ld; int R, N, np, dtype, vok, colblocks, RS, rows_per, accumulate;
     int blk0, fblk0;            // first partial / final block of this segment
     float* part; float* out; float* out2;
   } seg[kColsumMaxSegs];
@@ -368,8 +374,8 @@ __global__ void colsum_multi_partial_kernel(ColsumMultiArgs a) {
   const auto& sg = a.seg[colsum_seg_of(a, b, false)];
   const int lb = b - sg.blk0, bx = lb % sg.colblocks, by = lb / sg.colblocks;
   if (sg.vok) {
-    if (sg.dtype == SAT_BF16) colsum_partial_vec_body<bf16>((const bf16*)sg.X, sg.ld, sg.R, sg.N, sg.rows_per, sg.part, bx, by);
-    else colsum_partial_vec_body<float>((const float*)sg.X, sg.ld, sg.R, sg.N, sg.rows_per, sg.part, bx, by);
+    if (sg.dtype == SAT_BF16) colsum_partial_vec_body<bf16>((const bf16*)sg.X, sg.ld, sg.R, sg.np, sg.rows_per, sg.part, bx, by);
+    else colsum_partial_vec_body<float>((const float*)sg.X, sg.ld, sg.R, sg.np, sg.rows_per, sg.part, bx, by);
   } else {
     if (sg.dtype == SAT_BF16) colsum_partial_body<bf16>((const bf16*)sg.X, sg.ld, sg.R, sg.N, sg.rows_per, sg.part, bx, by);
     else colsum_partial_body<float>((const float*)sg.X, sg.ld, sg.R, sg.N, sg.rows_per, sg.part, bx, by);
@@ -378,7 +384,7 @@ __global__ void colsum_multi_partial_kernel(ColsumMultiArgs a) {
 __global__ void colsum_multi_final_kernel(ColsumMultiArgs a) {
   const int b = blockIdx.x;
   const auto& sg = a.seg[colsum_seg_of(a, b, true)];
-  colsum_final_body(sg.part, sg.RS, sg.N, sg.out, sg.accumulate, sg.out2, b - sg.fblk0);
+  colsum_final_body(sg.part, sg.RS, sg.N, sg.np, sg.out, sg.accumulate, sg.out2, b - sg.fblk0);
 }
 
 // zero several fp32 row blocks (rows x cols at a row stride ld; contiguous ranges as one row) in one launch
@@ -730,20 +736,21 @@ int sat_mean_rows(const void* a, int B, int L, int D, int dtype, float* out_f32,
 }
 
 int sat_colsum(const void* X, int dtype, long ld, int R, int N, float* out, int accumulate, float* out2,
-               float* scratch, hipStream_t s) {
+               float* scratch, hipStream_t s, int cols_readable) {
   if (N <= 0) return 0;
-  const ColsumPlan p = colsum_plan(X, dtype, ld, R, N);
+  const ColsumPlan p = colsum_plan(X, dtype, ld, R, N, cols_readable);
   dim3 g1(p.colblocks, p.RS);
   if (p.vok) {
     if (dtype == SAT_BF16)
-      hipLaunchKernelGGL(colsum_partial_vec_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)X, ld, R, N, p.rows_per, scratch);
+      hipLaunchKernelGGL(colsum_partial_vec_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)X, ld, R, p.np, p.rows_per, scratch);
     else
-      hipLaunchKernelGGL(colsum_partial_vec_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ld, R, N, p.rows_per, scratch);
+      hipLaunchKernelGGL(colsum_partial_vec_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ld, R, p.np, p.rows_per, scratch);
   } else if (dtype == SAT_BF16)
     hipLaunchKernelGGL(colsum_partial_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)X, ld, R, N, p.rows_per, scratch);
   else
     hipLaunchKernelGGL(colsum_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ld, R, N, p.rows_per, scratch);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(sat_cdiv(N, 256)), dim3(256), 0, s, scratch, p.RS, N, out, accumulate, out2);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(sat_cdiv(N, 256)), dim3(256), 0, s, scratch, p.RS, N, p.np, out, accumulate,
+                     out2);
   return (int)hipGetLastError();
 }
 
@@ -756,15 +763,15 @@ int sat_colsum_multi(const SatColsumSeg* segs, int n, float* scratch, hipStream_
   for (int i = 0; i < n; ++i) {
     const SatColsumSeg& g = segs[i];
     if (g.N <= 0) continue;
-    const ColsumPlan p = colsum_plan(g.X, g.dtype, g.ld, g.R, g.N);
+    const ColsumPlan p = colsum_plan(g.X, g.dtype, g.ld, g.R, g.N, g.cols_readable);
     auto& sg = a.seg[k++];
-    sg.X = g.X; sg.ld = g.ld; sg.R = g.R; sg.N = g.N; sg.dtype = g.dtype; sg.vok = p.vok;
+    sg.X = g.X; sg.ld = g.ld; sg.R = g.R; sg.N = g.N; sg.np = p.np; sg.dtype = g.dtype; sg.vok = p.vok;
     sg.colblocks = p.colblocks; sg.RS = p.RS; sg.rows_per = p.rows_per; sg.accumulate = g.accumulate;
     sg.blk0 = blk; sg.fblk0 = fblk;
     sg.part = scratch + off; sg.out = g.out; sg.out2 = g.out2;
     blk += p.colblocks * p.RS;
     fblk += sat_cdiv(g.N, 256);
-    off += (long)p.RS * g.N;
+    off += (long)p.RS * p.np;
   }
   a.n = k;
   if (k == 0) return 0;
@@ -795,7 +802,8 @@ int sat_zero_multi(float* const* ptrs, const long* counts, int n, hipStream_t s)
   for (int i = 0; i < n; ++i) seg[i] = SatZeroSeg{ptrs[i], 1, counts[i], counts[i]};
   return sat_zero_segs(seg, n, s);
 }
-size_t sat_colsum_scratch_floats(int R, int N) { (void)R; return (size_t)64 * (N > 0 ? N : 1); }
+// up to 64 row chunks of the (possibly padded: + up to 7 columns per segment, <= 8 segments) partial width
+size_t sat_colsum_scratch_floats(int R, int N) { (void)R; return (size_t)64 * ((N > 0 ? N : 1) + 64); }
 
 int sat_embed_gather(const float* W, const int32_t* tok, int B, int T1, long tok_stride_b, int E, int dtype,
                      void* out, long out_ld, hipStream_t s) {

@@ -3,13 +3,16 @@
 #include "sat_common.h"
 
 int sat_mean_rows(const void* a, int B, int L, int D, int dtype, float* out_f32, void* out_t, hipStream_t s);
+// cols_readable: X's rows may be read up to N rounded up to the vector width (zero-padded or harmless columns that
+// are summed and dropped), so an N that is not a multiple of it still takes the vector kernel
 int sat_colsum(const void* X, int dtype, long ld, int R, int N, float* out, int accumulate, float* out2,
-               float* scratch, hipStream_t s);
+               float* scratch, hipStream_t s, int cols_readable = 0);
 size_t sat_colsum_scratch_floats(int R, int N);
 // several column sums in one partial + one final launch (<= 8 segments, same arithmetic as sat_colsum); the
 // scratch holds sum_i 64 * N_i floats
 struct SatColsumSeg {
   const void* X; int dtype; long ld; int R, N; float* out; int accumulate; float* out2;
+  int cols_readable;   // as sat_colsum's
 };
 int sat_colsum_multi(const SatColsumSeg* segs, int n, float* scratch, hipStream_t s);
 // zero n (<= 8) fp32 ranges in one launch (graph-safe memset)
