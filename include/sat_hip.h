@@ -255,7 +255,9 @@ int sat_decoder_backward(const SatDecoderDims* d, const SatDecoderLayout* lay, c
                          const void* params_lp, const void* img_features, void* workspace,
                          size_t workspace_bytes, const void* preds, const float* alphas,
                          const void* d_preds, const float* d_alphas, float* grads, int accumulate,
-                         int phase, void* stream);   /* phase 1 | 2 | 3, + 4: d_preds already ReLU-masked (ado) */
+                         int phase, void* stream);   /* phase 1 | 2 | 3, + 4: d_preds already ReLU-masked (ado),
+                                                     + 8: d_preds rows zero-padded to the bf16 head's
+                                                     stride (sat_caption_loss_backward_ld; ado needs 4) */
 
 /* --- beam-search captioning (decoder.py:160-269, Decoder.caption; generate_caption.py:86-88) ---
  * img_features: DEVICE [beam_size, L, D] (the reference expands one image to beam rows).
@@ -292,6 +294,14 @@ int sat_caption_loss_backward(int B, int T, int V, int L, int dtype, const void*
 int sat_caption_loss_backward_relu(int B, int T, int V, int L, int dtype, const void* preds,
                               const int64_t* captions, float alpha_c, void* workspace,
                               const float* grad_out, void* d_preds, float* d_alphas, void* stream);
+/* either of the two with d_preds rows ld_dpreds >= V elements apart and columns V..ld_dpreds-1
+ * written as zeros (relu_mask != 0: the _relu form).  The bf16 decoder head pads odd vocabularies
+ * to a multiple of 8 (16-B rows, e.g. BERT's 30522 -> 30528); a gradient handed over in that
+ * layout skips the decoder's copy into padded rows (sat_decoder_backward phase bit 8). */
+int sat_caption_loss_backward_ld(int B, int T, int V, int L, int dtype, const void* preds,
+                                 const int64_t* captions, float alpha_c, void* workspace,
+                                 const float* grad_out, void* d_preds, int64_t ld_dpreds,
+                                 float* d_alphas, int relu_mask, void* stream);
 
 /* --- streaming image input (train.py:27-32 transform, dataset.py:9-12 decode on the host) ------
  * Decoded uint8 RGB images of any size, packed HWC (image b at pixels + offsets[b], sizes[b] =

@@ -126,6 +126,8 @@ _SIGNATURES = [
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("sat_caption_loss_backward_relu", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float,
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("sat_caption_loss_backward_ld", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float,
+                                             c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     ("sat_images_workspace_bytes", c_size_t, [c_int, c_int, c_int]),
     ("sat_images_max_downscale", c_int, []),
     ("sat_images_to_input", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,

@@ -823,8 +823,9 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
                                     int phase, void* stream) {
   SAT_CHECK((hipError_t)check_dims(dp));
   SAT_REQUIRE(lay && params && img_features && workspace && preds && alphas && d_preds && d_alphas && grads);
-  // bit 4: d_preds already ReLU-masked (sat_caption_loss_backward_relu)
-  SAT_REQUIRE((phase & 3) != 0 && phase >= 1 && phase <= 7);
+  // bit 4: d_preds already ReLU-masked (sat_caption_loss_backward_relu); bit 8: d_preds rows at the head's padded
+  // stride with zero pad columns (sat_caption_loss_backward_ld), so no copy into padded rows
+  SAT_REQUIRE((phase & 3) != 0 && phase >= 1 && phase <= 15);
   SAT_REQUIRE(dp->dtype == SAT_F32 || params_lp);
   SatPolicyScope scope(dp->policy);
   SatStampScope no_stamps(nullptr, 0);   // only the per-step groups of the BPTT loop record timestamps
@@ -895,7 +896,10 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
       // already masked (sat_caption_loss_backward_relu fused it)
       const void* dpre = d_preds;
       long ldp = V;
-      if (VP != V) {
+      if (phase & 8) {
+        SAT_REQUIRE(phase & 4);   // the padded layout comes from the loss, which masks
+        ldp = VP;
+      } else if (VP != V) {
         SAT_CHECK((hipError_t)sat_pad_rows(d_preds, (phase & 4) ? nullptr : preds, R, V, VP, d.dtype, w.dpre_t, s));
         dpre = w.dpre_t; ldp = VP;
       } else if (!(phase & 4)) {
@@ -928,8 +932,8 @@ extern "C" int sat_decoder_backward(const SatDecoderDims* dp, const SatDecoderLa
       if (att) SAT_CHECK((hipError_t)dgrad(5, R, D, E, w.dfz_t, E, c.W(lay->fz_w), D, w.dctx_head, D));
     } else {
       const void* dpre = d_preds;
-      long ldp = V;
-      if (VP != V) {
+      long ldp = (phase & 8) ? VP : V;
+      if (VP != V && !(phase & 8)) {
         SAT_CHECK((hipError_t)sat_pad_rows(d_preds, nullptr, R, V, VP, d.dtype, w.dpre_t, s));
         dpre = w.dpre_t; ldp = VP;
       }

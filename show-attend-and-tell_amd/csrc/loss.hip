@@ -291,13 +291,13 @@ template <typename TT, bool MASK>
 __global__ __launch_bounds__(256) void loss_bwd_kernel(const TT* __restrict__ preds, const int64_t* __restrict__ caps,
                                                        int B, int T, int V, int L, const float* __restrict__ stats,
                                                        const float* __restrict__ dreg, const float* __restrict__ grad_out,
-                                                       TT* __restrict__ dpreds, float* __restrict__ dalphas) {
+                                                       TT* __restrict__ dpreds, long ldo, float* __restrict__ dalphas) {
   const int r = blockIdx.x;
   const int T1 = T - 1;
   const int b = r / T1, t = r - b * T1;
   const float g = grad_out ? grad_out[0] : 1.f;
   const TT* x = preds + (long)r * V;
-  TT* dx = dpreds + (long)r * V;
+  TT* dx = dpreds + (long)r * ldo;
   const bool scored = t < T1 - 1;
   const int tgt = scored ? (int)caps[(long)b * T + t + 1] : -1;
   const float lse = scored ? stats[(long)r * kStat] : 0.f;
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const TT* __restrict__ pr
     return d;
   };
   constexpr int VEC = 16 / sizeof(TT);
-  if (V % VEC == 0) {
+  if (V % VEC == 0 && ldo % VEC == 0) {
     const __amdgpu_buffer_rsrc_t rdx = sat_out_rsrc(dx, (long)sizeof(TT) * V);   // this row: offsets < 2 GiB
     constexpr int LU = 4;   // vectors per thread in flight
     const int NV = V / VEC;
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const TT* __restrict__ pr
         sat_st16(rdx, (unsigned)((long)c * VEC * sizeof(TT)), o);   // write-through (sat_common.h)
       }
     }
-  } else if (sizeof(TT) == 2 && V % 2 == 0) {
+  } else if (sizeof(TT) == 2 && V % 2 == 0 && ldo % 2 == 0) {
     // even bf16 rows (4-byte aligned): pairs, LU in flight per thread
     constexpr int LU = 8;
     const int ND = V / 2;
@@ -361,6 +361,8 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(const TT* __restrict__ pr
   } else {
     for (int v = threadIdx.x; v < V; v += blockDim.x) dx[v] = (TT)grad((float)x[v], v);
   }
+  // a padded destination (sat_caption_loss_backward_ld): zero columns V..ldo-1
+  for (long v = V + threadIdx.x; v < ldo; v += blockDim.x) dx[v] = (TT)0.f;
   for (int l = threadIdx.x; l < L; l += blockDim.x) dalphas[(long)r * L + l] = g * dreg[(long)b * L + l];
 }
 
@@ -397,25 +399,25 @@ extern "C" int sat_caption_loss_forward(int B, int T, int V, int L, int dtype, c
 
 namespace {
 int loss_backward(int B, int T, int V, int L, int dtype, const void* preds, const int64_t* captions, void* workspace,
-                  const float* grad_out, void* d_preds, float* d_alphas, bool relu_mask, hipStream_t s) {
-  SAT_REQUIRE(preds && captions && workspace && d_preds && d_alphas && B > 0 && T >= 3);
+                  const float* grad_out, void* d_preds, long ldo, float* d_alphas, bool relu_mask, hipStream_t s) {
+  SAT_REQUIRE(preds && captions && workspace && d_preds && d_alphas && B > 0 && T >= 3 && ldo >= V);
   const int R = B * (T - 1);
   const float* stats = (const float*)workspace;
   const float* dreg = stats + (size_t)R * kStat;
   if (dtype == SAT_BF16) {
     if (relu_mask)
       hipLaunchKernelGGL((loss_bwd_kernel<bf16, true>), dim3(R), dim3(256), 0, s, (const bf16*)preds, captions, B, T,
-                         V, L, stats, dreg, grad_out, (bf16*)d_preds, d_alphas);
+                         V, L, stats, dreg, grad_out, (bf16*)d_preds, ldo, d_alphas);
     else
       hipLaunchKernelGGL((loss_bwd_kernel<bf16, false>), dim3(R), dim3(256), 0, s, (const bf16*)preds, captions, B,
-                         T, V, L, stats, dreg, grad_out, (bf16*)d_preds, d_alphas);
+                         T, V, L, stats, dreg, grad_out, (bf16*)d_preds, ldo, d_alphas);
   } else {
     if (relu_mask)
       hipLaunchKernelGGL((loss_bwd_kernel<float, true>), dim3(R), dim3(256), 0, s, (const float*)preds, captions, B,
-                         T, V, L, stats, dreg, grad_out, (float*)d_preds, d_alphas);
+                         T, V, L, stats, dreg, grad_out, (float*)d_preds, ldo, d_alphas);
     else
       hipLaunchKernelGGL((loss_bwd_kernel<float, false>), dim3(R), dim3(256), 0, s, (const float*)preds, captions,
-                         B, T, V, L, stats, dreg, grad_out, (float*)d_preds, d_alphas);
+                         B, T, V, L, stats, dreg, grad_out, (float*)d_preds, ldo, d_alphas);
   }
   return (int)hipGetLastError();
 }
@@ -425,7 +427,7 @@ extern "C" int sat_caption_loss_backward(int B, int T, int V, int L, int dtype, 
                                          const int64_t* captions, float alpha_c, void* workspace,
                                          const float* grad_out, void* d_preds, float* d_alphas, void* stream) {
   (void)alpha_c;
-  return loss_backward(B, T, V, L, dtype, preds, captions, workspace, grad_out, d_preds, d_alphas, false,
+  return loss_backward(B, T, V, L, dtype, preds, captions, workspace, grad_out, d_preds, V, d_alphas, false,
                        (hipStream_t)stream);
 }
 
@@ -433,6 +435,15 @@ extern "C" int sat_caption_loss_backward_relu(int B, int T, int V, int L, int dt
                                               const int64_t* captions, float alpha_c, void* workspace,
                                               const float* grad_out, void* d_preds, float* d_alphas, void* stream) {
   (void)alpha_c;
-  return loss_backward(B, T, V, L, dtype, preds, captions, workspace, grad_out, d_preds, d_alphas, true,
+  return loss_backward(B, T, V, L, dtype, preds, captions, workspace, grad_out, d_preds, V, d_alphas, true,
                        (hipStream_t)stream);
+}
+
+extern "C" int sat_caption_loss_backward_ld(int B, int T, int V, int L, int dtype, const void* preds,
+                                            const int64_t* captions, float alpha_c, void* workspace,
+                                            const float* grad_out, void* d_preds, int64_t ld_dpreds,
+                                            float* d_alphas, int relu_mask, void* stream) {
+  (void)alpha_c;
+  return loss_backward(B, T, V, L, dtype, preds, captions, workspace, grad_out, d_preds, (long)ld_dpreds, d_alphas,
+                       relu_mask != 0, (hipStream_t)stream);
 }

@@ -448,13 +448,21 @@ class _DecoderFn(torch.autograd.Function):
             d_preds = torch.zeros_like(preds)
         if d_alphas is None:
             d_alphas = torch.zeros_like(alphas)
-        d_preds = d_preds.contiguous()
+        masked = 4 if getattr(d_preds, "_sat_relu_masked", False) else 0   # phase bit: d_preds already ReLU-masked
+        # phase bit 8: caption_loss wrote d_preds into rows zero-padded to the bf16 head's stride (its [..., :V]
+        # view), the layout the head's backward GEMMs read: no copy into padded rows
+        ld = getattr(d_preds, "_sat_padded_ld", 0)
+        V = preds.shape[-1]
+        if (ld and d_preds.dtype == torch.bfloat16 and ld == (V + 7) // 8 * 8 and d_preds.shape == preds.shape
+                and d_preds.stride() == (preds.shape[1] * ld, ld, 1) and (masked or not dec.use_advanced_deep_output)):
+            masked |= 8
+        else:
+            d_preds = d_preds.contiguous()
         d_alphas = d_alphas.contiguous().float()
         if d_preds.dtype != preds.dtype:
             raise TypeError("sat_amd.Decoder.backward: grad dtype must match preds")
         accumulate = dec._attach_grads()
         lib = L.lib()
-        masked = 4 if getattr(d_preds, "_sat_relu_masked", False) else 0   # phase bit: d_preds already ReLU-masked
         if dec._defer_phase2:
             phases = (1,)
         elif dec._grad_hooks:   # a hook (DDP bucket all-reduce) runs between the phases

@@ -51,16 +51,27 @@ class _CaptionLossFn(torch.autograd.Function):
     def backward(ctx, g_loss, g_metrics):
         preds, caps = ctx.saved_tensors
         B, T, V, Lf = ctx.dims
-        d_preds = torch.empty_like(preds)
+        # bf16 logits whose rows are not 16-B multiples: the gradient goes into rows zero-padded to a multiple of 8,
+        # the layout the decoder head's backward GEMMs read (sat_decoder_backward phase bit 8), and is handed on as
+        # the [..., :V] view, tagged -- any other consumer sees an ordinary strided tensor
+        ld = (V + 7) // 8 * 8 if preds.dtype == torch.bfloat16 and V % 8 else V
+        if ld != V:
+            d_pad = torch.empty(B, T - 1, ld, device=preds.device, dtype=preds.dtype)
+            d_preds = d_pad[..., :V]
+        else:
+            d_pad = d_preds = torch.empty_like(preds)
         d_alphas = torch.empty(B, T - 1, Lf, device=preds.device, dtype=torch.float32)
         g = (g_loss if g_loss is not None else torch.ones((), device=preds.device)).float().contiguous()
         # with ReLU'd logits the mask of that ReLU is applied here, and the gradient says so
-        fn = L.lib().sat_caption_loss_backward_relu if ctx.relu else L.lib().sat_caption_loss_backward
-        L.check(fn(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds), L.ptr(caps), ctx.alpha_c, L.ptr(ctx.ws),
-                   L.ptr(g), L.ptr(d_preds), L.ptr(d_alphas), L.stream_of(d_preds)),
+        L.check(L.lib().sat_caption_loss_backward_ld(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds),
+                                                     L.ptr(caps), ctx.alpha_c, L.ptr(ctx.ws), L.ptr(g),
+                                                     L.ptr(d_pad), ld, L.ptr(d_alphas), int(ctx.relu),
+                                                     L.stream_of(d_preds)),
                 "sat_caption_loss_backward")
         if ctx.relu:
             d_preds._sat_relu_masked = True
+        if ld != V:
+            d_preds._sat_padded_ld = ld
         ctx.ws = None
         return d_preds, d_alphas, None, None, None, None
 

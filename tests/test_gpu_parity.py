@@ -461,6 +461,50 @@ def test_caption_loss_relu_fused_mask(sat):
     assert (grads[0] * (1 - mask)).abs().sum() > 0   # the plain gradient is not masked
 
 
+@pytest.mark.parametrize("V", [30522, 1003, 1000])
+@pytest.mark.parametrize("relu", [False, True])
+def test_caption_loss_backward_padded_rows(sat, V, relu):
+    """sat_caption_loss_backward_ld writes the same gradient into rows ld apart with zero pad columns (the bf16
+    head's layout for vocabularies not a multiple of 8: BERT's 30522 even -> the pair path, 1003 odd -> the scalar
+    one, 1000 -> the 16-B path with ld = V); caption_loss hands on the [..., :V] view of the padded rows, tagged."""
+    from sat_amd import _lib as L
+    torch.manual_seed(1)
+    B, T, Lf = 3, 6, 49
+    preds = torch.relu(torch.randn(B, T - 1, V, device=DEV)).bfloat16()
+    alphas = torch.softmax(torch.randn(B, T - 1, Lf, device=DEV), -1)
+    caps = torch.randint(0, V, (B, T), device=DEV)
+    lib = L.lib()
+    ws = torch.empty(lib.sat_caption_loss_workspace_bytes(B, T, Lf), device=DEV, dtype=torch.uint8)
+    out = torch.empty(8, device=DEV)
+    L.check(lib.sat_caption_loss_forward(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds), L.ptr(alphas),
+                                         L.ptr(caps), 1.0, 3, 3, 0, 1, L.ptr(ws), L.ptr(out), None), "fwd")
+    g = torch.full((), 0.75, device=DEV)
+    ref, da_ref = torch.empty_like(preds), torch.empty(B, T - 1, Lf, device=DEV)
+    fn = lib.sat_caption_loss_backward_relu if relu else lib.sat_caption_loss_backward
+    L.check(fn(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds), L.ptr(caps), 1.0, L.ptr(ws), L.ptr(g),
+               L.ptr(ref), L.ptr(da_ref), None), "bwd")
+    ld = (V + 7) // 8 * 8
+    pad = torch.full((B, T - 1, ld), float("nan"), device=DEV).bfloat16()
+    da = torch.empty_like(da_ref)
+    L.check(lib.sat_caption_loss_backward_ld(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds), L.ptr(caps), 1.0,
+                                             L.ptr(ws), L.ptr(g), L.ptr(pad), ld, L.ptr(da), int(relu), None), "ld")
+    torch.cuda.synchronize()
+    assert torch.equal(pad[..., :V], ref)
+    assert torch.equal(pad[..., V:], torch.zeros_like(pad[..., V:]))
+    assert torch.equal(da, da_ref)
+    # through autograd: the same values, the padded view when V % 8 != 0
+    p = preds.clone().requires_grad_(True)
+    if relu:
+        p._sat_relu_logits = True
+    seen = {}
+    p.register_hook(lambda gr: seen.setdefault("g", gr))
+    loss, _ = sat.caption_loss(p, alphas, caps)
+    (0.75 * loss).backward()
+    gr = seen["g"]
+    assert torch.equal(gr, ref)
+    assert getattr(gr, "_sat_padded_ld", V) == ld if V % 8 else not hasattr(gr, "_sat_padded_ld")
+
+
 def test_decoder_split_target(sat):
     """The per-step split-K workgroup target (64 when the decoder shares the GPU with the encoder
     stream) changes only the fp32 summation order of the bf16 path: loss and gradients agree."""
