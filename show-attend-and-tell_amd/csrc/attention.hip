@@ -494,8 +494,7 @@ __device__ __forceinline__ void attn_bwd2_kernel_body(AttnBwdArgs a, int NS) {
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < BEV; ++j) s_red[w][lane * BEV + j] = dv[j];
-  dbv = wave_sum(dbv);
-  if (lane == 0) s_tmp[w] = dbv;
+  if (lane == 0) s_tmp[w] = dbv;   // every lane added the same de per slot: lane 0 holds the wave's sum
   __syncthreads();
   if (tid < BSLICE && eo < E) {
     float v = 0.f;
@@ -534,7 +533,7 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   constexpr int VN = V16<T>::N;
   constexpr int EC = 64 * VN * ECH;
   __shared__ float s_dctx[64 * VN * DCH];
-  __shared__ float s_de[kMaxL];
+  __shared__ float s_al[kMaxL], s_dax[kMaxL];
   __shared__ float s_red[FBW][EC];
   __shared__ float s_tmp[FBW];
   __shared__ int s_last;
@@ -558,6 +557,16 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
       if (a.d_ctx_ext) dx = a.d_ctx_ext[(long)b * a.d_ctx_ext_ld + d];
     }
     dcol[k][0] = dg; dcol[k][1] = g; dcol[k][2] = cx; dcol[k][3] = dx;
+  }
+  // alpha (and dL/dalpha from outside) of every slot: staged in LDS by phase A, read per slot by the walk
+  constexpr int LPT = kMaxL / (FBW * 64);
+  const float* alpha = a.alpha + (long)b * a.alpha_ld;
+  float al_r[LPT], dax_r[LPT];
+#pragma unroll
+  for (int k = 0; k < LPT; ++k) {
+    const int l = k * FBW * 64 + tid;
+    al_r[k] = l < L ? alpha[l] : 0.f;
+    dax_r[k] = l < L && a.d_alpha_ext ? a.d_alpha_ext[(long)b * a.d_alpha_ext_ld + l] : 0.f;
   }
   uint4 xa[FBU][DCH];
 #pragma unroll
@@ -591,7 +600,6 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
     }
   }
   // ---- A: dL/dcontext, the gate gradient (chunk 0), ctx . dctx + sum_k alpha_k dalpha_ext_k ----
-  const float* alpha = a.alpha + (long)b * a.alpha_ld;
   float loc = 0.f;
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
@@ -611,8 +619,15 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
       s_dctx[d] = dctx;
     }
   }
-  if (a.d_alpha_ext)
-    for (int l = tid; l < L; l += FBW * 64) loc += alpha[l] * a.d_alpha_ext[(long)b * a.d_alpha_ext_ld + l];
+#pragma unroll
+  for (int k = 0; k < LPT; ++k) {
+    const int l = k * FBW * 64 + tid;
+    if (l < L) {
+      if (a.d_alpha_ext) loc += al_r[k] * dax_r[k];
+      s_al[l] = al_r[k];
+      s_dax[l] = dax_r[k];
+    }
+  }
   loc = wave_sum(loc);
   if (lane == 0) s_tmp[w] = loc;
   lds_barrier();   // the annotation / Ws rows stay in flight
@@ -624,20 +639,35 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   for (int q = 0; q < DCH; ++q)
 #pragma unroll
     for (int j = 0; j < VN; ++j) dctx[q][j] = s_dctx[q * 64 * VN + lane * VN + j];
-  // ---- B + C: dL/dalpha and de per slot of the chunk ----
-  // PIPE (a chunk deeper than one batch of loads, e.g. L = 196): the next batch's rows are requested before the
-  // current batch's arithmetic (two register buffers of half the batch: the same registers), as in the forward
+  // ---- B-D in one walk over the chunk's slots: per slot dL/dalpha_l (a_l . dctx), de_l = alpha_l (dL/dalpha_l -
+  // sum), and at once its tanh backward over E (partial dL/d(U h), dL/dv, dL/dv.bias) -- the wave that scored a
+  // slot owns it through the tanh, so a slot's annotation and Ws rows are requested together and the walk is one
+  // pass of dependent batches instead of two.  PIPE (a chunk deeper than one batch of loads, e.g. L = 196): the
+  // next batch's rows are requested before the current batch's arithmetic (two register buffers of half a batch)
+  float duh[ECH][VN], dv[ECH][VN];
+#pragma unroll
+  for (int q = 0; q < ECH; ++q)
+#pragma unroll
+    for (int j = 0; j < VN; ++j) duh[q][j] = dv[q][j] = 0.f;
+  float dbv = 0.f;   // the same in every lane (de is wave-uniform)
   constexpr int BST = FBW * FBU;
-  auto load_xa = [&](int l0, uint4 (&dst)[FBU][DCH]) {
+  auto load_rows = [&](int l0, uint4 (&da)[FBU][DCH], uint4 (&dw)[FBU][ECH]) {
 #pragma unroll
     for (int u = 0; u < FBU; ++u)
 #pragma unroll
       for (int q = 0; q < DCH; ++q) {
         const int l = l0 + FBW * u, d = q * 64 * VN + lane * VN;
-        dst[u][q] = ld16(ab + (long)l * D + q * 64 * VN, l < l_end && d < D);
+        da[u][q] = ld16(ab + (long)l * D + q * 64 * VN, l < l_end && d < D);
+      }
+#pragma unroll
+    for (int u = 0; u < FBU; ++u)
+#pragma unroll
+      for (int q = 0; q < ECH; ++q) {
+        const int l = l0 + FBW * u, e = q * 64 * VN + lane * VN;
+        dw[u][q] = ld16(Ws + (long)l * E + q * 64 * VN, l < l_end && e < E);
       }
   };
-  auto dalpha = [&](int l0, const uint4 (&src)[FBU][DCH]) {
+  auto slots = [&](int l0, const uint4 (&sa)[FBU][DCH], const uint4 (&sw)[FBU][ECH]) {
 #pragma unroll
     for (int u = 0; u < FBU; ++u) {
       const int l = l0 + FBW * u;
@@ -645,60 +675,17 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
       float p = 0.f;
 #pragma unroll
       for (int q = 0; q < DCH; ++q) {
-        const T* h = (const T*)&src[u][q];
+        const T* h = (const T*)&sa[u][q];
 #pragma unroll
         for (int j = 0; j < VN; ++j) p = fmaf(dctx[q][j], (float)h[j], p);
       }
       p = wave_sum(p);
-      if (lane == 0) {
-        const float da = p + (a.d_alpha_ext ? a.d_alpha_ext[(long)b * a.d_alpha_ext_ld + l] : 0.f);
-        const float de = alpha[l] * (da - sad);
-        s_de[l - l_beg] = de;
-        a.de_out[(long)b * a.de_ld + l] = de;
-      }
-    }
-  };
-  if constexpr (PIPE) {
-    for (int l0 = l_beg + w; l0 < l_end; l0 += 2 * BST) {
-      uint4 xn[FBU][DCH];
-      if (l0 + BST < l_end) load_xa(l0 + BST, xn);
-      dalpha(l0, xa);
-      if (l0 + 2 * BST < l_end) load_xa(l0 + 2 * BST, xa);
-      if (l0 + BST < l_end) dalpha(l0 + BST, xn);
-    }
-  } else {
-    for (int l0 = l_beg + w; l0 < l_end; l0 += BST) {
-      if (l0 != l_beg + w) load_xa(l0, xa);
-      dalpha(l0, xa);
-    }
-  }
-  __syncthreads();
-  // ---- D: tanh backward over E for the chunk's slots ----
-  float duh[ECH][VN], dv[ECH][VN];
-#pragma unroll
-  for (int q = 0; q < ECH; ++q)
-#pragma unroll
-    for (int j = 0; j < VN; ++j) duh[q][j] = dv[q][j] = 0.f;
-  float dbv = 0.f;
-  auto load_xw = [&](int l0, uint4 (&dst)[FBU][ECH]) {
-#pragma unroll
-    for (int u = 0; u < FBU; ++u)
-#pragma unroll
-      for (int q = 0; q < ECH; ++q) {
-        const int l = l0 + FBW * u, e = q * 64 * VN + lane * VN;
-        dst[u][q] = ld16(Ws + (long)l * E + q * 64 * VN, l < l_end && e < E);
-      }
-  };
-  auto tanh_bwd = [&](int l0, const uint4 (&src)[FBU][ECH]) {
-#pragma unroll
-    for (int u = 0; u < FBU; ++u) {
-      const int l = l0 + FBW * u;
-      if (l >= l_end) break;   // wave-uniform
-      const float de = s_de[l - l_beg];
+      const float de = s_al[l] * ((p + s_dax[l]) - sad);
+      if (lane == 0) a.de_out[(long)b * a.de_ld + l] = de;
       dbv += de;
 #pragma unroll
       for (int q = 0; q < ECH; ++q) {
-        const T* h = (const T*)&src[u][q];
+        const T* h = (const T*)&sw[u][q];
 #pragma unroll
         for (int j = 0; j < VN; ++j) {
           const float t = tanh_t<T>((float)h[j] + uu[q][j]);
@@ -710,16 +697,16 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   };
   if constexpr (PIPE) {
     for (int l0 = l_beg + w; l0 < l_end; l0 += 2 * BST) {
-      uint4 xn[FBU][ECH];
-      if (l0 + BST < l_end) load_xw(l0 + BST, xn);
-      tanh_bwd(l0, xw);
-      if (l0 + 2 * BST < l_end) load_xw(l0 + 2 * BST, xw);
-      if (l0 + BST < l_end) tanh_bwd(l0 + BST, xn);
+      uint4 an[FBU][DCH], wn[FBU][ECH];
+      if (l0 + BST < l_end) load_rows(l0 + BST, an, wn);
+      slots(l0, xa, xw);
+      if (l0 + 2 * BST < l_end) load_rows(l0 + 2 * BST, xa, xw);
+      if (l0 + BST < l_end) slots(l0 + BST, an, wn);
     }
   } else {
     for (int l0 = l_beg + w; l0 < l_end; l0 += BST) {
-      if (l0 != l_beg + w) load_xw(l0, xw);
-      tanh_bwd(l0, xw);
+      if (l0 != l_beg + w) load_rows(l0, xa, xw);
+      slots(l0, xa, xw);
     }
   }
   // fold the waves in a fixed order: dL/d(U h) into registers of threads e < E, then dL/dv
@@ -745,7 +732,6 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   for (int q = 0; q < ECH; ++q)
 #pragma unroll
     for (int j = 0; j < VN; ++j) s_red[w][q * 64 * VN + lane * VN + j] = dv[q][j];
-  dbv = wave_sum(dbv);
   if (lane == 0) s_tmp[w] = dbv;
   __syncthreads();
 #pragma unroll
