@@ -40,6 +40,8 @@ __device__ __forceinline__ void load4(const T* p, float* o) {
   }
 }
 
+__device__ __forceinline__ float f4get(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+
 // tanh: exact libm in the fp32 parity path; exp-based (v_exp_f32 + v_rcp_f32, ~1e-6 abs) in bf16 mode.
 template <typename T>
 __device__ __forceinline__ float tanh_t(float x) {
@@ -101,22 +103,66 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   const int b = blockIdx.x, s = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = a.L, D = a.D, E = a.E;
-  const T* Ws = (const T*)a.Ws + (long)b * L * E;
-  const float* uh = a.uh + (long)b * a.uh_ld;
   const int c0 = s * COLS;
-  const T* ab = (const T*)a.a + (long)b * L * D + c0 + lane * VN;
-
-  // Issue order = order of first use (vmcnt retires loads in order): the first batch of score
-  // rows, then U h + b and v, then the context rows and the gate pre-activation, which stay in
-  // flight while the scores and the softmax are computed.
+  // Every load of the step is requested here, branch-free (buffer loads: a guarded-off load reads past the resource
+  // and returns zeros -- exec-masked branches made the compiler wait for a row right after requesting it), in order
+  // of first use (vmcnt retires loads in order): the U h + b slabs and v, the first batch of score rows, the context
+  // rows, the gate pre-activation slabs -- the context rows and the gate slabs stay in flight while the scores and the
+  // softmax are computed.
+  constexpr int kHP = 2;   // U h / gate slabs requested up front (the decoder's h GEMM: 1-2; more: the looped sum)
+  const int hp = a.hg_splits < 1 ? 1 : a.hg_splits;
+  const bool hp_up = hp <= kHP;
+  const float* uh = a.uh + (long)b * a.uh_ld;
+  const __amdgpu_buffer_rsrc_t rU = sat_in_rsrc(uh, ((long)(hp - 1) * a.hg_split_stride + E) * 4);
+  const __amdgpu_buffer_rsrc_t rV = sat_in_rsrc(a.v_w, (long)E * 4);
+  const __amdgpu_buffer_rsrc_t rW = sat_in_rsrc((const T*)a.Ws + (long)b * L * E, (long)L * E * sizeof(T));
+  const __amdgpu_buffer_rsrc_t rA = sat_in_rsrc((const T*)a.a + (long)b * L * D, (long)L * D * sizeof(T));
+  constexpr int Q4 = VN / 4;   // float4 groups per 16-B vector of T
+  float4 up[CH][Q4][kHP], vp[CH][Q4];
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int q = 0; q < Q4; ++q) {
+      const int e = c * 64 * VN + lane * VN + 4 * q;
+#pragma unroll
+      for (int p = 0; p < kHP; ++p)
+        up[c][q][p] = sat_ld16f(rU, hp_up && p < hp && e < E ? (unsigned)((p * a.hg_split_stride + e) * 4) : kSatOOB);
+      vp[c][q] = sat_ld16f(rV, e < E ? (unsigned)(e * 4) : kSatOOB);
+    }
+  float4 uf[CH][Q4];   // more slabs than requested up front: the looped sum, before the rows are requested
+  if (!hp_up) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int q = 0; q < Q4; ++q) {
+        const int e = c * 64 * VN + lane * VN + 4 * q;
+        uf[c][q] = e < E ? sum_parts4(uh, e, a.hg_splits, a.hg_split_stride) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+  }
+  auto ws_off = [&](int l, int e) { return l < L && e < E ? (unsigned)(((long)l * E + e) * sizeof(T)) : kSatOOB; };
+  auto a_off = [&](int l, int d) { return l < L && d < D ? (unsigned)(((long)l * D + d) * sizeof(T)) : kSatOOB; };
   uint4 xv[FU][CH];
 #pragma unroll
   for (int u = 0; u < FU; ++u)
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int l = w + NW * u, e = c * 64 * VN + lane * VN;
-      xv[u][c] = ld16(Ws + (long)l * E + e, l < L && e < E);
-    }
+    for (int c = 0; c < CH; ++c) xv[u][c] = sat_ld16(rW, ws_off(w + NW * u, c * 64 * VN + lane * VN));
+  // context rows of the first batch
+  uint4 xa[FU][FDV];
+#pragma unroll
+  for (int u = 0; u < FU; ++u)
+#pragma unroll
+    for (int v = 0; v < FDV; ++v) xa[u][v] = sat_ld16(rA, a_off(w + NW * u, c0 + v * 64 * VN + lane * VN));
+  // the epilogue's threads own 4 consecutive columns each (col4 = 4 tid: 16-B write-through stores)
+  static_assert(COLS <= 4 * NT && COLS % 4 == 0, "four columns per epilogue thread");
+  const int col4 = 4 * tid;
+  const bool ep = col4 < COLS && c0 + col4 < D;   // D % 4 == 0 (host-checked): a quad is all in or all out
+  float4 gp[kHP];
+  const __amdgpu_buffer_rsrc_t rG = sat_in_rsrc(a.gate_pre ? a.gate_pre + (long)b * a.gate_ld : a.uh,
+                                                ((long)(hp - 1) * a.hg_split_stride + D) * 4);
+#pragma unroll
+  for (int p = 0; p < kHP; ++p)
+    gp[p] = sat_ld16f(rG, a.gate_pre && ep && hp_up && p < hp ? (unsigned)((p * a.hg_split_stride + c0 + col4) * 4)
+                                                             : kSatOOB);
 
   // ---- scores: lane owns VN consecutive e per chunk; (U h + b) and v live in registers ----
   float u_r[CH][VN], v_r[CH][VN];
@@ -124,31 +170,14 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   for (int c = 0; c < CH; ++c) {
     const int e = c * 64 * VN + lane * VN;
 #pragma unroll
-    for (int j = 0; j < VN; j += 4) {
-      float4 u4 = make_float4(0.f, 0.f, 0.f, 0.f), v4 = u4;
-      if (e < E) {
-        u4 = sum_parts4(uh, e + j, a.hg_splits, a.hg_split_stride);
-        v4 = *(const float4*)(a.v_w + e + j);
-      }
-      u_r[c][j] = u4.x; u_r[c][j + 1] = u4.y; u_r[c][j + 2] = u4.z; u_r[c][j + 3] = u4.w;
-      v_r[c][j] = v4.x; v_r[c][j + 1] = v4.y; v_r[c][j + 2] = v4.z; v_r[c][j + 3] = v4.w;
+    for (int q = 0; q < Q4; ++q) {
+      const float4 u4 = hp_up ? sum_loaded_parts4(up[c][q], hp) : uf[c][q];
+      const float4 v4 = vp[c][q];
+      u_r[c][4 * q] = u4.x; u_r[c][4 * q + 1] = u4.y; u_r[c][4 * q + 2] = u4.z; u_r[c][4 * q + 3] = u4.w;
+      v_r[c][4 * q] = v4.x; v_r[c][4 * q + 1] = v4.y; v_r[c][4 * q + 2] = v4.z; v_r[c][4 * q + 3] = v4.w;
     }
   }
-
-  // context rows of the first batch and the epilogue's gate pre-activation (this thread's column)
-  uint4 xa[FU][FDV];
-#pragma unroll
-  for (int u = 0; u < FU; ++u)
-#pragma unroll
-    for (int v = 0; v < FDV; ++v)
-      xa[u][v] = ld16(ab + (long)(w + NW * u) * D + v * 64 * VN,
-                      w + NW * u < L && c0 + v * 64 * VN + lane * VN < D);
-  // the epilogue's threads own 4 consecutive columns each (col4 = 4 tid: 16-B write-through stores)
-  static_assert(COLS <= 4 * NT && COLS % 4 == 0, "four columns per epilogue thread");
-  const int col4 = 4 * tid;
-  const bool ep = col4 < COLS && c0 + col4 < D;   // D % 4 == 0 (host-checked): a quad is all in or all out
-  float4 gpre4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (a.gate_pre && ep) gpre4 = sum_parts4(a.gate_pre + (long)b * a.gate_ld, c0 + col4, a.hg_splits, a.hg_split_stride);
+  float4 gpre4 = make_float4(0.f, 0.f, 0.f, 0.f);   // summed in the epilogue (its slabs arrive last)
 
   const float bv = a.v_b[0];
   // (the per-slot and per-column accumulations are explicit FMAs: the compiler's own contraction choice can differ
@@ -161,10 +190,7 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
 #pragma unroll
     for (int u = 0; u < FU; ++u)
 #pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        const int l = l0 + NW * u, e = c * 64 * VN + lane * VN;
-        dst[u][c] = ld16(Ws + (long)l * E + e, l < L && e < E);
-      }
+      for (int c = 0; c < CH; ++c) dst[u][c] = sat_ld16(rW, ws_off(l0 + NW * u, c * 64 * VN + lane * VN));
   };
   auto scores = [&](int l0, const uint4 (&src)[FU][CH]) {
 #pragma unroll
@@ -185,9 +211,10 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   if constexpr (PIPE) {
     for (int l0 = w; l0 < L; l0 += 2 * STEP) {
       uint4 xn[FU][CH];
-      if (l0 + STEP < L) load_ws(l0 + STEP, xn);
+      load_ws(l0 + STEP, xn);   // unconditional: rows past L read zeros (a guarded load let the compiler
+                                 // hoist the rows' unpacking next to it, waiting on them at once)
       scores(l0, xv);
-      if (l0 + 2 * STEP < L) load_ws(l0 + 2 * STEP, xv);
+      load_ws(l0 + 2 * STEP, xv);
       if (l0 + STEP < L) scores(l0 + STEP, xn);
     }
   } else {
@@ -237,8 +264,7 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
 #pragma unroll
     for (int u = 0; u < FU; ++u)
 #pragma unroll
-      for (int v = 0; v < FDV; ++v)
-        dst[u][v] = ld16(ab + (long)(l0 + NW * u) * D + v * 64 * VN, l0 + NW * u < L && c0 + v * 64 * VN + lane * VN < D);
+      for (int v = 0; v < FDV; ++v) dst[u][v] = sat_ld16(rA, a_off(l0 + NW * u, c0 + v * 64 * VN + lane * VN));
   };
   auto context = [&](int l0, const uint4 (&src)[FU][FDV]) {
 #pragma unroll
@@ -258,9 +284,9 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
   if constexpr (PIPE) {   // the same two-buffer overlap as the scores
     for (int l0 = w; l0 < L; l0 += 2 * STEP) {
       uint4 an[FU][FDV];
-      if (l0 + STEP < L) load_a(l0 + STEP, an);
+      load_a(l0 + STEP, an);
       context(l0, xa);
-      if (l0 + 2 * STEP < L) load_a(l0 + 2 * STEP, xa);
+      load_a(l0 + 2 * STEP, xa);
       if (l0 + STEP < L) context(l0 + STEP, an);
     }
   } else {
@@ -290,6 +316,9 @@ __device__ __forceinline__ void attn_fwd_kernel_body(AttnFwdArgs a) {
     }
     if (half + 1 < NW / 8) __syncthreads();
   }
+  if (a.gate_pre && ep)
+    gpre4 = hp_up ? sum_loaded_parts4(gp, hp)
+                  : sum_parts4(a.gate_pre + (long)b * a.gate_ld, c0 + col4, a.hg_splits, a.hg_split_stride);
   if (ep) {
     const int dout = c0 + col4;
     // fp32 outputs through 16-B write-through stores (sat_common.h): this step's end-of-kernel L2 writeback, on the
@@ -541,63 +570,84 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int L = a.L, D = a.D, E = a.E;
   const int LC = (L + NL - 1) / NL, l_beg = c * LC, l_end = min(L, l_beg + LC);
-  const T* ab = (const T*)a.a + (long)b * L * D + lane * VN;
-  const T* Ws = (const T*)a.Ws + (long)b * L * E + lane * VN;
-  // ---- requests in order of first use ----
+  // ---- requests in order of first use, branch-free (buffer loads: a guarded-off load reads past its resource and
+  // returns zeros -- the exec-masked loads and the looped slab sums before made the compiler wait for each column's
+  // slabs before requesting the next, several round trips ahead of the annotation rows) ----
   constexpr int CPT = (64 * VN * DCH + FBW * 64 - 1) / (FBW * 64);
-  float dcol[CPT][4];   // dg, g, cx, dx of this thread's columns
+  constexpr int kDP = 8;   // d(gated context) slabs requested up front (the transposed skinny GEMM's: 4-6; more: looped)
+  const int dp = a.dg_splits < 1 ? 1 : a.dg_splits;
+  const bool dp_up = dp <= kDP;
+  const __amdgpu_buffer_rsrc_t rDG =
+      sat_in_rsrc(a.d_gated + (long)b * a.d_gated_ld, ((long)(dp - 1) * a.dg_split_stride + D) * 4);
+  const __amdgpu_buffer_rsrc_t rGt = sat_in_rsrc(a.gate + (long)b * a.gate_ld, (long)D * 4);
+  const __amdgpu_buffer_rsrc_t rCx = sat_in_rsrc(a.ctx + (long)b * a.ctx_ld, (long)D * 4);
+  const __amdgpu_buffer_rsrc_t rDx =
+      sat_in_rsrc(a.d_ctx_ext ? a.d_ctx_ext + (long)b * a.d_ctx_ext_ld : a.ctx, (long)D * 4);
+  float dgp[CPT][kDP], dcol[CPT][4];   // d(gated) slabs; dg, g, cx, dx of this thread's columns
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
     const int d = k * FBW * 64 + tid;
-    float dg = 0.f, g = 0.f, cx = 0.f, dx = 0.f;
-    if (d < D) {
-      dg = sum_parts(a.d_gated, (long)b * a.d_gated_ld + d, a.dg_splits, a.dg_split_stride);
-      g = a.gate[(long)b * a.gate_ld + d];
-      cx = a.ctx[(long)b * a.ctx_ld + d];
-      if (a.d_ctx_ext) dx = a.d_ctx_ext[(long)b * a.d_ctx_ext_ld + d];
+    const bool ok = d < D;
+#pragma unroll
+    for (int p = 0; p < kDP; ++p)
+      dgp[k][p] = sat_ld4f(rDG, ok && dp_up && p < dp ? (unsigned)((p * a.dg_split_stride + d) * 4) : kSatOOB);
+    dcol[k][1] = sat_ld4f(rGt, ok ? (unsigned)(d * 4) : kSatOOB);
+    dcol[k][2] = sat_ld4f(rCx, ok ? (unsigned)(d * 4) : kSatOOB);
+    dcol[k][3] = sat_ld4f(rDx, ok && a.d_ctx_ext ? (unsigned)(d * 4) : kSatOOB);
+  }
+  if (!dp_up) {   // more slabs than requested up front: the looped sum, before the rows are requested
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int d = k * FBW * 64 + tid;
+      dcol[k][0] = d < D ? sum_parts(a.d_gated, (long)b * a.d_gated_ld + d, a.dg_splits, a.dg_split_stride) : 0.f;
     }
-    dcol[k][0] = dg; dcol[k][1] = g; dcol[k][2] = cx; dcol[k][3] = dx;
   }
   // alpha (and dL/dalpha from outside) of every slot: staged in LDS by phase A, read per slot by the walk
   constexpr int LPT = kMaxL / (FBW * 64);
-  const float* alpha = a.alpha + (long)b * a.alpha_ld;
+  const __amdgpu_buffer_rsrc_t rAl = sat_in_rsrc(a.alpha + (long)b * a.alpha_ld, (long)L * 4);
+  const __amdgpu_buffer_rsrc_t rDa =
+      sat_in_rsrc(a.d_alpha_ext ? a.d_alpha_ext + (long)b * a.d_alpha_ext_ld : a.alpha, (long)L * 4);
   float al_r[LPT], dax_r[LPT];
 #pragma unroll
   for (int k = 0; k < LPT; ++k) {
     const int l = k * FBW * 64 + tid;
-    al_r[k] = l < L ? alpha[l] : 0.f;
-    dax_r[k] = l < L && a.d_alpha_ext ? a.d_alpha_ext[(long)b * a.d_alpha_ext_ld + l] : 0.f;
+    al_r[k] = sat_ld4f(rAl, l < L ? (unsigned)(l * 4) : kSatOOB);
+    dax_r[k] = sat_ld4f(rDa, l < L && a.d_alpha_ext ? (unsigned)(l * 4) : kSatOOB);
   }
+  const __amdgpu_buffer_rsrc_t rA = sat_in_rsrc((const T*)a.a + (long)b * L * D, (long)L * D * sizeof(T));
+  const __amdgpu_buffer_rsrc_t rW = sat_in_rsrc((const T*)a.Ws + (long)b * L * E, (long)L * E * sizeof(T));
+  auto a_off = [&](int l, int q) {
+    const int d = q * 64 * VN + lane * VN;
+    return l < l_end && d < D ? (unsigned)(((long)l * D + d) * sizeof(T)) : kSatOOB;
+  };
+  auto w_off = [&](int l, int q) {
+    const int e = q * 64 * VN + lane * VN;
+    return l < l_end && e < E ? (unsigned)(((long)l * E + e) * sizeof(T)) : kSatOOB;
+  };
   uint4 xa[FBU][DCH];
 #pragma unroll
   for (int u = 0; u < FBU; ++u)
 #pragma unroll
-    for (int q = 0; q < DCH; ++q) {
-      const int l = l_beg + w + FBW * u, d = q * 64 * VN + lane * VN;
-      xa[u][q] = ld16(ab + (long)l * D + q * 64 * VN, l < l_end && d < D);
+    for (int q = 0; q < DCH; ++q) xa[u][q] = sat_ld16(rA, a_off(l_beg + w + FBW * u, q));
+  const __amdgpu_buffer_rsrc_t rU = sat_in_rsrc(a.uh + (long)b * a.uh_ld, (long)E * 4);
+  const __amdgpu_buffer_rsrc_t rV = sat_in_rsrc(a.v_w, (long)E * 4);
+  float4 uu4[ECH][VN / 4], vw4[ECH][VN / 4];
+#pragma unroll
+  for (int q = 0; q < ECH; ++q)
+#pragma unroll
+    for (int j = 0; j < VN / 4; ++j) {
+      const int e = q * 64 * VN + lane * VN + 4 * j;
+      uu4[q][j] = sat_ld16f(rU, e < E ? (unsigned)(e * 4) : kSatOOB);
+      vw4[q][j] = sat_ld16f(rV, e < E ? (unsigned)(e * 4) : kSatOOB);
     }
   uint4 xw[FBU][ECH];
 #pragma unroll
   for (int u = 0; u < FBU; ++u)
 #pragma unroll
-    for (int q = 0; q < ECH; ++q) {
-      const int l = l_beg + w + FBW * u, e = q * 64 * VN + lane * VN;
-      xw[u][q] = ld16(Ws + (long)l * E + q * 64 * VN, l < l_end && e < E);
-    }
-  float uu[ECH][VN], vw[ECH][VN];
+    for (int q = 0; q < ECH; ++q) xw[u][q] = sat_ld16(rW, w_off(l_beg + w + FBW * u, q));
+  if (dp_up) {
 #pragma unroll
-  for (int q = 0; q < ECH; ++q) {
-    const int e = q * 64 * VN + lane * VN;
-#pragma unroll
-    for (int j = 0; j < VN; j += 4) {
-      float4 u4 = make_float4(0.f, 0.f, 0.f, 0.f), v4 = u4;
-      if (e < E) {
-        u4 = *(const float4*)(a.uh + (long)b * a.uh_ld + e + j);
-        v4 = *(const float4*)(a.v_w + e + j);
-      }
-      uu[q][j] = u4.x; uu[q][j + 1] = u4.y; uu[q][j + 2] = u4.z; uu[q][j + 3] = u4.w;
-      vw[q][j] = v4.x; vw[q][j + 1] = v4.y; vw[q][j + 2] = v4.z; vw[q][j + 3] = v4.w;
-    }
+    for (int k = 0; k < CPT; ++k) dcol[k][0] = sum_loaded_parts(dgp[k], dp);
   }
   // ---- A: dL/dcontext, the gate gradient (chunk 0), ctx . dctx + sum_k alpha_k dalpha_ext_k ----
   float loc = 0.f;
@@ -655,17 +705,11 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
 #pragma unroll
     for (int u = 0; u < FBU; ++u)
 #pragma unroll
-      for (int q = 0; q < DCH; ++q) {
-        const int l = l0 + FBW * u, d = q * 64 * VN + lane * VN;
-        da[u][q] = ld16(ab + (long)l * D + q * 64 * VN, l < l_end && d < D);
-      }
+      for (int q = 0; q < DCH; ++q) da[u][q] = sat_ld16(rA, a_off(l0 + FBW * u, q));
 #pragma unroll
     for (int u = 0; u < FBU; ++u)
 #pragma unroll
-      for (int q = 0; q < ECH; ++q) {
-        const int l = l0 + FBW * u, e = q * 64 * VN + lane * VN;
-        dw[u][q] = ld16(Ws + (long)l * E + q * 64 * VN, l < l_end && e < E);
-      }
+      for (int q = 0; q < ECH; ++q) dw[u][q] = sat_ld16(rW, w_off(l0 + FBW * u, q));
   };
   auto slots = [&](int l0, const uint4 (&sa)[FBU][DCH], const uint4 (&sw)[FBU][ECH]) {
 #pragma unroll
@@ -688,8 +732,8 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
         const T* h = (const T*)&sw[u][q];
 #pragma unroll
         for (int j = 0; j < VN; ++j) {
-          const float t = tanh_t<T>((float)h[j] + uu[q][j]);
-          duh[q][j] = fmaf(de * vw[q][j], fmaf(-t, t, 1.f), duh[q][j]);
+          const float t = tanh_t<T>((float)h[j] + f4get(uu4[q][j / 4], j % 4));
+          duh[q][j] = fmaf(de * f4get(vw4[q][j / 4], j % 4), fmaf(-t, t, 1.f), duh[q][j]);
           dv[q][j] = fmaf(de, t, dv[q][j]);
         }
       }
@@ -698,9 +742,10 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   if constexpr (PIPE) {
     for (int l0 = l_beg + w; l0 < l_end; l0 += 2 * BST) {
       uint4 an[FBU][DCH], wn[FBU][ECH];
-      if (l0 + BST < l_end) load_rows(l0 + BST, an, wn);
+      load_rows(l0 + BST, an, wn);   // unconditional: rows past the chunk read zeros (a guarded load let the
+                                      // compiler hoist the rows' unpacking next to it, waiting on them at once)
       slots(l0, xa, xw);
-      if (l0 + 2 * BST < l_end) load_rows(l0 + 2 * BST, xa, xw);
+      load_rows(l0 + 2 * BST, xa, xw);
       if (l0 + BST < l_end) slots(l0 + BST, an, wn);
     }
   } else {
@@ -919,6 +964,10 @@ int sat_attention_fwd_launch(const AttnFwdArgs& args, hipStream_t s) {
   SAT_REQUIRE(a.L <= kMaxL && a.E % VD == 0 && a.E <= 1024);
   SAT_REQUIRE((a.uh_ld % 4) == 0 && (a.hg_splits <= 1 || a.hg_split_stride % 4 == 0));
   SAT_REQUIRE(a.D % VD == 0);
+  // the kernel's buffer resources (one batch row each) address < 2 GiB
+  const long elt = a.dtype == SAT_BF16 ? 2 : 4, hp = a.hg_splits < 1 ? 1 : a.hg_splits;
+  SAT_REQUIRE((long)a.L * a.D * elt < 0x7fffffffL && (long)a.L * a.E * elt < 0x7fffffffL);
+  SAT_REQUIRE(hp > 2 || ((hp - 1) * a.hg_split_stride + (a.D > a.E ? a.D : a.E)) * 4 < 0x7fffffffL);
   // one workgroup of 16 waves per (row, 1024 bf16 columns).  Measured and removed (profiles/r3_s14, r3_s19): 512-column
   // slices (twice the workgroups; bit-identical) -- no faster at B = 64, 15.2 vs 10.3 us per step at B = 128; 8 waves
   // x 8 slots per workgroup (half the resident waves) -- 6.61-6.66 vs 6.57-6.58 ms per overlapped step
@@ -989,6 +1038,11 @@ int sat_attention_bwd_launch(const AttnBwdArgs& args, hipStream_t s) {
   const int VD = a.dtype == SAT_BF16 ? 8 : 4;
   SAT_REQUIRE(a.L <= kMaxL && a.E % VD == 0 && a.E <= 1024);
   SAT_REQUIRE(a.D % VD == 0);
+  // the split kernel's buffer resources (one batch row each) address < 2 GiB
+  const long dp = a.dg_splits < 1 ? 1 : a.dg_splits;
+  const long elt = a.dtype == SAT_BF16 ? 2 : 4;
+  SAT_REQUIRE((long)a.L * a.D * elt < 0x7fffffffL && (long)a.L * a.E * elt < 0x7fffffffL);
+  SAT_REQUIRE(dp > 8 || ((dp - 1) * a.dg_split_stride + a.D) * 4 < 0x7fffffffL);
   if (sat_policy().attn_bwd != 1 && (a.uh_ld % 4) == 0 && (a.E % 4) == 0) {
     const bool ok = a.dtype == SAT_BF16 ? launch_bwd_split<bf16>(a, s) : launch_bwd_split<float>(a, s);
     if (ok) return (int)hipGetLastError();

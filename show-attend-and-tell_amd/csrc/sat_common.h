@@ -116,6 +116,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t sat_out_rsrc(const void* base,
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
                                            0x00020000);
 }
+// loads through a buffer resource: an offset past the resource's bytes reads zeros, so a guarded load needs no
+// exec-masked branch (whose register copies can make the compiler wait for a load right after issuing it)
+constexpr unsigned kSatOOB = 0x80000000u;   // an offset no resource covers (num_records < 2^31)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sat_in_rsrc(const void* base, long bytes) { return sat_out_rsrc(base, bytes); }
+__device__ __forceinline__ uint4 sat_ld16(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  const sat_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float4 sat_ld16f(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  const uint4 u = sat_ld16(r, byte_off);
+  return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+}
+__device__ __forceinline__ float sat_ld4f(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  return __uint_as_float((unsigned)__builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, 0));
+}
 template <int CPOL = SAT_OUT_CPOL>
 __device__ __forceinline__ void sat_st16(__amdgpu_buffer_rsrc_t r, unsigned byte_off, uint4 u) {
   __builtin_amdgcn_raw_buffer_store_b128(sat_u32x4{u.x, u.y, u.z, u.w}, r, (int)byte_off, 0, CPOL);

@@ -236,6 +236,39 @@ __device__ __forceinline__ float4 sum_parts4(const float* p, long idx, int n, lo
   return f4add(f4add(a0, a1), f4add(a2, a3));
 }
 
+// sum_parts4 over slabs already loaded (x[q] = slab q, zeros past n; n <= NP): the same additions in the same order,
+// so a kernel can request its slabs with the rest of its loads and sum them later
+template <int NP>
+__device__ __forceinline__ float4 sum_loaded_parts4(const float4 (&x)[NP], int n) {
+  if (n <= 1) return x[0];
+  const int full = 3 * ((n - 1) / 3);   // slabs 1 .. full: three accumulators in turn; the rest: the first
+  float4 a1 = make_float4(0.f, 0.f, 0.f, 0.f), a2 = a1, a3 = a1;
+#pragma unroll
+  for (int q = 1; q < NP; ++q) {
+    if (q >= n) break;
+    if (q <= full && (q - 1) % 3 == 1) a2 = f4add(a2, x[q]);
+    else if (q <= full && (q - 1) % 3 == 2) a3 = f4add(a3, x[q]);
+    else a1 = f4add(a1, x[q]);
+  }
+  return f4add(f4add(x[0], a1), f4add(a2, a3));
+}
+
+// the scalar form (sum_parts's order)
+template <int NP>
+__device__ __forceinline__ float sum_loaded_parts(const float (&x)[NP], int n) {
+  if (n <= 1) return x[0];
+  const int full = 3 * ((n - 1) / 3);
+  float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+  for (int q = 1; q < NP; ++q) {
+    if (q >= n) break;
+    if (q <= full && (q - 1) % 3 == 1) a2 += x[q];
+    else if (q <= full && (q - 1) % 3 == 2) a3 += x[q];
+    else a1 += x[q];
+  }
+  return (x[0] + a1) + (a2 + a3);
+}
+
 // ---- LSTM cell arithmetic (nn.LSTMCell, gate order i, f, g, o; decoder.py:115) of the pointwise kernels
 // (lstm.hip) ----
 __device__ __forceinline__ void lstm_cell_fwd(float gi, float gf, float gg, float go, float c_prev, float& c, float& h) {
