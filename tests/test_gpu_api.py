@@ -83,10 +83,14 @@ def test_policy_edit_between_forward_and_deferred_backward(sat):
         torch.cuda.synchronize()
         return _grads(dec)
     a, b = step(False), step(True)
-    # a backward that read the edited policy would place the workspace regions at other offsets (garbage
-    # gradients); the forward's own copy keeps them within run-to-run rounding (fp32 atomics in the embedding
-    # scatter-add); attention.v.bias's gradient is zero up to rounding (softmax is shift-invariant), so the absolute
-    # floor is also tied to the largest gradient of the model
-    top = max(g.abs().max().item() for g in a.values())
+    # a backward that read the edited policy would place the workspace regions at other offsets (garbage gradients,
+    # O(1) off); the forward's own copy keeps them within run-to-run rounding.  At this B = 3 shape the step is not
+    # bit-reproducible: the tile GEMM's fp32-atomic split-K orders a few sums differently run to run (~1e-7), and
+    # where that flips a bf16 rounding of a per-step operand (d(U h), the context) a whole weight gradient moves by
+    # up to ~1e-3 relative (measured 7.3e-4 on attention.U.weight, tools/repeat_policy_edit.py, profiles/r6_s27) --
+    # so the bound is on each gradient's norm; attention.v.bias's gradient is zero up to rounding (softmax is
+    # shift-invariant) and is compared at the scale of attention.v.weight's
     for n in a:
-        assert torch.allclose(a[n], b[n], rtol=1e-4, atol=1e-5 * a[n].abs().max().item() + 1e-7 * top), n
+        scale = a["attention.v.weight"].norm() if n == "attention.v.bias" else a[n].norm()
+        err = ((a[n] - b[n]).norm() / scale).item()
+        assert err < 1e-2, (n, err)
