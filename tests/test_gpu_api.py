@@ -85,11 +85,11 @@ def test_policy_edit_between_forward_and_deferred_backward(sat):
     a, b = step(False), step(True)
     # a backward that read the edited policy would place the workspace regions at other offsets (garbage gradients,
     # O(1) off); the forward's own copy keeps them within run-to-run rounding.  At this B = 3 shape the step is not
-    # bit-reproducible: the tile GEMM's fp32-atomic split-K orders a few sums differently run to run (~1e-7), and
-    # where that flips a bf16 rounding of a per-step operand (d(U h), the context) a whole weight gradient moves by
-    # up to ~1e-3 relative (measured 7.3e-4 on attention.U.weight, tools/repeat_policy_edit.py, profiles/r6_s27) --
-    # so the bound is on each gradient's norm; attention.v.bias's gradient is zero up to rounding (softmax is
-    # shift-invariant) and is compared at the scale of attention.v.weight's
+    # bit-reproducible: a few fp32 sums differ run to run (~1e-7), and where that flips a bf16 rounding of a per-step
+    # operand a whole weight gradient moves by up to ~1e-3 relative (measured 7.3e-4 on attention.U.weight,
+    # tools/repeat_policy_edit.py, profiles/r6_s27) -- so the bound is on each gradient's norm;
+    # attention.v.bias's gradient is zero up to rounding (softmax is shift-invariant) and is compared at the scale of
+    # attention.v.weight's
     for n in a:
         scale = a["attention.v.weight"].norm() if n == "attention.v.bias" else a[n].norm()
         err = ((a[n] - b[n]).norm() / scale).item()
