@@ -30,7 +30,9 @@ __device__ __forceinline__ uint8_t dropout_keep(uint64_t seed, int b, int t, int
 // step at B=128, E=512, 4 + 8 slabs), the cell update reads the four gates back from LDS.
 // GREEDY: the fused greedy step's extras (dropout of h into hd_t, the token fold), compiled out of the teacher-forced
 // instance (with them in, its span went 3.5-3.7 -> 4.2 us per step, profiles/r6_s5 vs r6_s2)
-template <typename T, bool GREEDY>
+// HS, CS: the h and context products' split counts when compile-time (CS = 0 with HS > 0: no context part); HS = 0:
+// any counts, looped sums
+template <typename T, bool GREEDY, int HS, int CS>
 __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
   __shared__ float sg[4][64];
   __shared__ float am_v[4];
@@ -42,6 +44,28 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
     const long i = base + u;
     const bool ok = i < units;
     const int b = ok ? (int)(i / E) : 0, j = ok ? (int)(i - (long)b * E) : 0;
+    // every load this thread needs is requested here (HS / CS > 0: the products' split counts, compile-time, so
+    // the slab loads are unconditional and branch-free; buffer loads, a guarded-off one reads zeros): the gate's x
+    // part, its split-K slabs of the h and context products (summed after they arrive, in sum_parts's order), and
+    // c_prev for the cell update after the barrier -- one memory round trip where the looped slab sums and the
+    // post-barrier c_prev load took several.  HS = 0: the looped sums (any split count).
+    const bool xt_mode = GREEDY && a.am_val;
+    const __amdgpu_buffer_rsrc_t rX = sat_in_rsrc(a.xpart, ((long)(a.B - 1) * a.xpart_ld + 4L * E) * 4);
+    const __amdgpu_buffer_rsrc_t rH =
+        sat_in_rsrc(a.hpart, ((long)(HS > 1 ? HS - 1 : 0) * a.h_split_stride + (long)(a.B - 1) * a.hpart_ld + 4L * E) * 4);
+    const __amdgpu_buffer_rsrc_t rC =
+        sat_in_rsrc(a.cpart, ((long)(CS > 1 ? CS - 1 : 0) * a.c_split_stride + (long)(a.B - 1) * a.cpart_ld + 4L * E) * 4);
+    const __amdgpu_buffer_rsrc_t rP = sat_in_rsrc(a.c_prev, ((long)(a.B - 1) * a.c_prev_ld + E) * 4);
+    const long gi = (long)q * E + j;   // the gate's column
+    float xv = sat_ld4f(rX, ok && !xt_mode ? (unsigned)(((long)b * a.xpart_ld + gi) * 4) : kSatOOB);
+    float hp[HS > 0 ? HS : 1], cpv[CS > 0 ? CS : 1];
+#pragma unroll
+    for (int p = 0; p < HS; ++p)
+      hp[p] = sat_ld4f(rH, ok ? (unsigned)(((long)b * a.hpart_ld + gi + p * a.h_split_stride) * 4) : kSatOOB);
+#pragma unroll
+    for (int p = 0; p < CS; ++p)
+      cpv[p] = sat_ld4f(rC, ok ? (unsigned)(((long)b * a.cpart_ld + gi + p * a.c_split_stride) * 4) : kSatOOB);
+    const float cprev = sat_ld4f(rP, ok && q == 0 ? (unsigned)(((long)b * a.c_prev_ld + j) * 4) : kSatOOB);
     int id = 0;
     if (GREEDY && a.am_val) {   // the token fold: the block's 64 units share one row (E % 64 == 0)
       const int br = (int)(base / E);
@@ -65,18 +89,20 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
       for (int w = 1; w < 4; ++w)
         if (sat_argmax_better(am_v[w], am_i[w], best, bi)) { best = am_v[w]; bi = am_i[w]; }
       id = (bi < 0 || bi >= a.am_V) ? 0 : bi;
+      if (ok) xv = a.xt[(long)id * 4 * E + q * E + j];
     }
     if (ok) {
-      const float xv = GREEDY && a.am_val ? a.xt[(long)id * 4 * E + q * E + j] : a.xpart[(long)b * a.xpart_ld + q * E + j];
-      float v = xv + sum_parts(a.hpart, (long)b * a.hpart_ld + q * E + j, a.h_splits, a.h_split_stride);
-      if (a.cpart) v += sum_parts(a.cpart, (long)b * a.cpart_ld + q * E + j, a.c_splits, a.c_split_stride);
+      float v = xv + (HS > 0 ? sum_loaded_parts(hp, HS)
+                             : sum_parts(a.hpart, (long)b * a.hpart_ld + q * E + j, a.h_splits, a.h_split_stride));
+      if (CS > 0) v += sum_loaded_parts(cpv, CS);
+      else if (HS == 0 && a.cpart) v += sum_parts(a.cpart, (long)b * a.cpart_ld + q * E + j, a.c_splits, a.c_split_stride);
       sg[q][u] = v;
       a.gates[(long)b * a.gates_ld + q * E + j] = v;
     }
     __syncthreads();
     if (q == 0 && ok) {
       float c, h;
-      lstm_cell_fwd(sg[0][u], sg[1][u], sg[2][u], sg[3][u], a.c_prev[(long)b * a.c_prev_ld + j], c, h);
+      lstm_cell_fwd(sg[0][u], sg[1][u], sg[2][u], sg[3][u], cprev, c, h);
       a.c_out[(long)b * a.c_out_ld + j] = c;
       if (a.c_next_in) a.c_next_in[(long)b * a.c_next_in_ld + j] = c;
       a.h_out[(long)b * a.h_out_ld + j] = h;
@@ -106,10 +132,10 @@ __device__ __forceinline__ void lstm_fwd_gp_kernel_body(LstmFwdArgs a) {
   }
 }
 
-template <typename T, bool GREEDY>
+template <typename T, bool GREEDY, int HS, int CS>
 __global__ __launch_bounds__(256) void lstm_fwd_gp_kernel(LstmFwdArgs a) {
   const SatStampT0 t0 = sat_stamp_begin(a.st);
-  lstm_fwd_gp_kernel_body<T, GREEDY>(a);
+  lstm_fwd_gp_kernel_body<T, GREEDY, HS, CS>(a);
   sat_stamp_end(a.st, t0);
 }
 
@@ -125,20 +151,46 @@ __device__ __forceinline__ void lstm_bwd_gp_kernel_body(LstmBwdArgs a) {
     const long i = base + u;
     const bool ok = i < units;
     const int b = ok ? (int)(i / E) : 0, j = ok ? (int)(i - (long)b * E) : 0;
-    float cp = 0.f, cn = 0.f, dcin = 0.f, hh = 0.f;
+    // every load requested up front, branch-free (buffer loads; zeros past the resource): the gate, this thread's
+    // recurrent-dh slabs s = q, q + 4, .. (summed in that order after they arrive), c_prev, c_new, dc, the head's dh
+    // and its dropout mask
+    constexpr int kQ = 4;   // slabs per thread requested up front (dh_splits <= 16; more: the looped sum)
+    const int ds = a.dh_rec ? a.dh_splits : 0;
+    const bool d_up = ds <= 4 * kQ;
+    const __amdgpu_buffer_rsrc_t rG = sat_in_rsrc(a.gates, ((long)(a.B - 1) * a.gates_ld + 4L * E) * 4);
+    const __amdgpu_buffer_rsrc_t rD =
+        sat_in_rsrc(a.dh_rec, ((long)(ds > 0 ? ds - 1 : 0) * a.dh_split_stride + (long)(a.B - 1) * a.dh_rec_ld + E) * 4);
+    const __amdgpu_buffer_rsrc_t rCp = sat_in_rsrc(a.c_prev, ((long)(a.B - 1) * a.c_prev_ld + E) * 4);
+    const __amdgpu_buffer_rsrc_t rCn = sat_in_rsrc(a.c_new, ((long)(a.B - 1) * a.c_new_ld + E) * 4);
+    const __amdgpu_buffer_rsrc_t rDc = sat_in_rsrc(a.dc, units * 4);
+    const __amdgpu_buffer_rsrc_t rHh = sat_in_rsrc(a.dh_head, ((long)(a.B - 1) * a.dh_head_ld + E) * 4);
+    const float gv = sat_ld4f(rG, ok ? (unsigned)(((long)b * a.gates_ld + q * E + j) * 4) : kSatOOB);
+    float dp[kQ];
+#pragma unroll
+    for (int k = 0; k < kQ; ++k) {
+      const int sp = q + 4 * k;
+      dp[k] = sat_ld4f(rD, ok && d_up && sp < ds ? (unsigned)(((long)b * a.dh_rec_ld + j + sp * a.dh_split_stride) * 4)
+                                                 : kSatOOB);
+    }
+    float cp = sat_ld4f(rCp, ok ? (unsigned)(((long)b * a.c_prev_ld + j) * 4) : kSatOOB);
+    float cn = sat_ld4f(rCn, ok ? (unsigned)(((long)b * a.c_new_ld + j) * 4) : kSatOOB);
+    float dcin = sat_ld4f(rDc, ok && !a.dc_zero ? (unsigned)(i * 4) : kSatOOB);
+    float hh = sat_ld4f(rHh, ok && a.dh_head ? (unsigned)(((long)b * a.dh_head_ld + j) * 4) : kSatOOB);
+    const __amdgpu_buffer_rsrc_t rM = sat_in_rsrc(a.mask, (long)(a.B - 1) * a.mask_ld + E);
+    const bool mk = __builtin_amdgcn_raw_buffer_load_b8(
+                        rM, ok && a.dh_head && a.mask ? (int)((long)b * a.mask_ld + j) : (int)kSatOOB, 0, 0) != 0;
     if (ok) {
-      sg[q][u] = a.gates[(long)b * a.gates_ld + q * E + j];
+      sg[q][u] = gv;
       float p = 0.f;
-      if (a.dh_rec)
-        for (int sp = q; sp < a.dh_splits; sp += 4) p += a.dh_rec[(long)b * a.dh_rec_ld + j + sp * a.dh_split_stride];
-      sdh[q][u] = p;
-      cp = a.c_prev[(long)b * a.c_prev_ld + j];
-      cn = a.c_new[(long)b * a.c_new_ld + j];
-      dcin = a.dc_zero ? 0.f : a.dc[i];
-      if (a.dh_head) {
-        hh = a.dh_head[(long)b * a.dh_head_ld + j];
-        if (a.mask) hh = a.mask[(long)b * a.mask_ld + j] ? hh * 2.f : 0.f;
+      if (d_up) {
+#pragma unroll
+        for (int k = 0; k < kQ; ++k)
+          if (q + 4 * k < ds) p += dp[k];
+      } else {
+        for (int sp = q; sp < ds; sp += 4) p += a.dh_rec[(long)b * a.dh_rec_ld + j + sp * a.dh_split_stride];
       }
+      sdh[q][u] = p;
+      if (a.dh_head && a.mask) hh = mk ? hh * 2.f : 0.f;
     }
     __syncthreads();
     if (ok) {
@@ -319,17 +371,41 @@ inline long lstm_blocks(int B, int E) {
   const long blocks = ((long)B * E + 63) / 64;
   return blocks > 4096 ? 4096 : blocks;
 }
+template <typename T, bool GREEDY, int HS>
+bool lstm_fwd_cs(int cs, dim3 grid, hipStream_t s, const LstmFwdArgs& a) {
+  switch (cs) {   // the decoder's context-product split counts (0: no context part)
+    case 0: hipLaunchKernelGGL((lstm_fwd_gp_kernel<T, GREEDY, HS, 0>), grid, dim3(256), 0, s, a); return true;
+    case 1: hipLaunchKernelGGL((lstm_fwd_gp_kernel<T, GREEDY, HS, 1>), grid, dim3(256), 0, s, a); return true;
+    case 2: hipLaunchKernelGGL((lstm_fwd_gp_kernel<T, GREEDY, HS, 2>), grid, dim3(256), 0, s, a); return true;
+    case 4: hipLaunchKernelGGL((lstm_fwd_gp_kernel<T, GREEDY, HS, 4>), grid, dim3(256), 0, s, a); return true;
+    case 8: hipLaunchKernelGGL((lstm_fwd_gp_kernel<T, GREEDY, HS, 8>), grid, dim3(256), 0, s, a); return true;
+    default: return false;
+  }
+}
+template <typename T, bool GREEDY>
+void lstm_fwd_launch_t(dim3 grid, hipStream_t s, const LstmFwdArgs& a) {
+  const int hs = a.h_splits < 1 ? 1 : a.h_splits, cs = a.cpart ? (a.c_splits < 1 ? 1 : a.c_splits) : 0;
+  // the buffer resources of the compile-time forms address < 2 GiB
+  const bool fits = ((long)(hs - 1) * a.h_split_stride + (long)a.B * a.hpart_ld) * 4 < 0x7fffffffL &&
+                    (!a.cpart || ((long)(cs - 1) * a.c_split_stride + (long)a.B * a.cpart_ld) * 4 < 0x7fffffffL) &&
+                    (a.xt || ((long)a.B * a.xpart_ld) * 4 < 0x7fffffffL);
+  if (sizeof(T) == 2 && fits) {
+    if (hs == 1 && lstm_fwd_cs<T, GREEDY, 1>(cs, grid, s, a)) return;
+    if (hs == 2 && lstm_fwd_cs<T, GREEDY, 2>(cs, grid, s, a)) return;
+  }
+  hipLaunchKernelGGL((lstm_fwd_gp_kernel<T, GREEDY, 0, 0>), grid, dim3(256), 0, s, a);
+}
 int sat_lstm_fwd_launch(const LstmFwdArgs& args, hipStream_t s) {
   LstmFwdArgs a = args;
   a.st = sat_launch_stamps();
-  const long blocks = lstm_blocks(a.B, a.E);
+  const dim3 grid((unsigned)lstm_blocks(a.B, a.E));
   const bool greedy = a.hd_t || a.am_val;
   if (a.dtype == SAT_BF16) {
-    if (greedy) hipLaunchKernelGGL((lstm_fwd_gp_kernel<bf16, true>), dim3((int)blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((lstm_fwd_gp_kernel<bf16, false>), dim3((int)blocks), dim3(256), 0, s, a);
+    if (greedy) lstm_fwd_launch_t<bf16, true>(grid, s, a);
+    else lstm_fwd_launch_t<bf16, false>(grid, s, a);
   } else {
-    if (greedy) hipLaunchKernelGGL((lstm_fwd_gp_kernel<float, true>), dim3((int)blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((lstm_fwd_gp_kernel<float, false>), dim3((int)blocks), dim3(256), 0, s, a);
+    if (greedy) lstm_fwd_launch_t<float, true>(grid, s, a);
+    else lstm_fwd_launch_t<float, false>(grid, s, a);
   }
   return (int)hipGetLastError();
 }
