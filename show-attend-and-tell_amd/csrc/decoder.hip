@@ -63,18 +63,36 @@ struct Splits { int h, c, g, dh, i; };
 // decoder prefers 192: 10.24 vs 10.48 ms sequential).  SatDecoderDims::split_target, 0 = 192.
 constexpr int kSplitTargetDefault = 192;
 
+// A single split on a bf16 per-step product with K >= 1024 sends it to the tile kernel's atomic split-K, whose fp32
+// atomics add in arrival order: run-to-run rounding differences in the recurrent chain (dh, d gates, dc), which the
+// bf16 copies of the next products amplify into whole-ulp flips at small batch.  Where no whole-k-tile divisor of K
+// fits, the product splits raggedly instead: S slabs of cdiv(kt, S) k-tiles, the last one shorter (the partial-output
+// kernels write an empty k range as zeros), at most 8 slabs.
+constexpr int kChainAtomicK = 1024;
+inline int ragged_splits(int K, long want) {
+  const int kt = sat_cdiv(K, 64);
+  const int cap = want < 2 ? 2 : (want > 8 ? 8 : (int)want);
+  const int kc = sat_cdiv(kt, cap);
+  return sat_cdiv(kt, kc);
+}
 inline int pick_splits(int M, int N, int K, int dtype, bool kmajor_w, int target) {
-  if (dtype != SAT_BF16 || K % 64) return 1;
+  if (dtype != SAT_BF16) return 1;
   const long tiles = (long)sat_cdiv(M, 128) * sat_cdiv(N, kmajor_w ? 128 : 64);
   long want = (target + tiles - 1) / tiles;
   if (want > 32) want = 32;
   const int kt = K / 64;
   int best = 1;
-  for (int s = 1; s <= kt && s <= want; ++s)
-    if (kt % s == 0) best = s;
+  if (K % 64 == 0)
+    for (int s = 1; s <= kt && s <= want; ++s)
+      if (kt % s == 0) best = s;
+  if (best == 1 && K >= kChainAtomicK) best = ragged_splits(K, want);
   return best;
 }
-inline int forced(int f, int K, int auto_s) { return (f > 0 && K % 64 == 0 && (K / 64) % f == 0) ? f : auto_s; }
+// a policy override that divides K into whole k-tiles; 1 on a K >= 1024 product keeps the automatic count (see above)
+inline int forced(int f, int K, int auto_s) {
+  if (f == 1 && K >= kChainAtomicK) return auto_s;
+  return (f > 0 && K % 64 == 0 && (K / 64) % f == 0) ? f : auto_s;
+}
 // tr: the backward's dL/d(gated context) and dL/dh products read the transposed weight copies
 // (SatDecoderLayout::wih_ctx_t / hcat_t, k-contiguous) and run on the skinny kernel with its own K split
 inline Splits splits_for(const SatDecoderDims& d, bool tr) {
