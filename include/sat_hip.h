@@ -75,7 +75,9 @@ typedef struct {
   int attn_pipe;        /* attention forward / split backward over more slots than one batch of loads (L = 196):
                          * 0 auto (slot batches double-buffered), 1 one batch at a time */
   int decoder_splits[4];/* split-K counts of the per-step bf16 decoder GEMMs -- h: [U; f_beta; W_hh] h, c: context
-                         * part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic */
+                         * part of the gate GEMM, g: dL/d(gated context), dh: recurrent dL/dh; 0 = automatic; a count
+                         * that does not divide K into whole 64-deep k-tiles, or 1 on a K >= 1024 product (it would
+                         * take the tile kernel's fp32-atomic split-K), keeps the automatic count */
   int greedy_step;      /* bf16 forward without teacher forcing (decoder.py:118-133 per step): 0 the fused greedy step
                          * (token table for the embedding half of the gate GEMM, dropout in the LSTM kernel, f_z beside
                          * the context GEMM, f_h + combine in one launch, the vocabulary head with in-launch argmax
