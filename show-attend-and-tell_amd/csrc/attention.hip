@@ -557,6 +557,19 @@ __global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int 
 // slots: partial dL/d(U h), dL/dv, dL/dv.bias.  With NL > 1 the partials meet in the last-arriving
 // workgroup of the row (agent-scope ticket; payload stored and loaded sc1, so no cache fence is needed:
 // MI355X_MICROARCH.md, visibility, first row of the sc1 table), summed in chunk order (deterministic).
+// Diagnostics builds only (tools/build_variant.sh, -DSAT_ATTN_MARK=k): the attention backward's stamp records the time
+// every wave of the workgroup has reached phase boundary k instead of the kernel's end (bench.py's per-step spans then
+// measure start -> boundary k).  The product build defines no marker.
+#ifdef SAT_ATTN_MARK
+#define SAT_MARK(k)                                                                                                  \
+  if ((k) == SAT_ATTN_MARK && a.st.p && a.st.p[0]) {                                                                 \
+    __syncthreads();                                                                                                 \
+    const int w_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);                                   \
+    if (threadIdx.x == 0 && w_ < a.st.cap) a.st.p[2 + 2 * (long)w_ + 1] = __builtin_amdgcn_s_memrealtime();          \
+  }
+#else
+#define SAT_MARK(k)
+#endif
 template <typename T, int DCH, int ECH, int FBW, int FBU, bool PIPE>
 __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   constexpr int VN = V16<T>::N;
@@ -649,6 +662,7 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) dcol[k][0] = sum_loaded_parts(dgp[k], dp);
   }
+  SAT_MARK(1)
   // ---- A: dL/dcontext, the gate gradient (chunk 0), ctx . dctx + sum_k alpha_k dalpha_ext_k ----
   float loc = 0.f;
 #pragma unroll
@@ -681,6 +695,7 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   loc = wave_sum(loc);
   if (lane == 0) s_tmp[w] = loc;
   lds_barrier();   // the annotation / Ws rows stay in flight
+  SAT_MARK(2)
   float sad = 0.f;
 #pragma unroll
   for (int i = 0; i < FBW; i += 2) sad += s_tmp[i] + s_tmp[i + 1];
@@ -754,6 +769,7 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
       slots(l0, xa, xw);
     }
   }
+  SAT_MARK(3)
   // fold the waves in a fixed order: dL/d(U h) into registers of threads e < E, then dL/dv
 #pragma unroll
   for (int q = 0; q < ECH; ++q)
@@ -792,6 +808,7 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   float fb = 0.f;
 #pragma unroll
   for (int i = 0; i < FBW; i += 2) fb += s_tmp[i] + s_tmp[i + 1];
+  SAT_MARK(4)
   if (NL == 1) {   // the whole row here: write directly
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
@@ -862,7 +879,14 @@ template <typename T, int DCH, int ECH, int FBW, int FBU, bool PIPE = false>
 __global__ __launch_bounds__(FBW * 64) void attn_bwd_split_kernel(AttnBwdArgs a) {
   const SatStampT0 t0 = sat_stamp_begin(a.st);
   attn_bwd_split_kernel_body<T, DCH, ECH, FBW, FBU, PIPE>(a);
+#ifdef SAT_ATTN_MARK
+  if (t0.on) {   // the marker wrote the record's end; the start is written here
+    const int w_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (threadIdx.x == 0 && w_ < a.st.cap) a.st.p[2 + 2 * (long)w_] = t0.t0;
+  }
+#else
   sat_stamp_end(a.st, t0);
+#endif
 }
 
 // After the time loop: dWs[b,l,e] = sum over t = T1-1 .. 0 of de[b,t,l] v[e] (1 - tanh^2(Ws[b,l,e] +
