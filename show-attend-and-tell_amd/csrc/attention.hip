@@ -557,6 +557,15 @@ __global__ __launch_bounds__(BNW * 64) void attn_bwd2_kernel(AttnBwdArgs a, int 
 // slots: partial dL/d(U h), dL/dv, dL/dv.bias.  With NL > 1 the partials meet in the last-arriving
 // workgroup of the row (agent-scope ticket; payload stored and loaded sc1, so no cache fence is needed:
 // MI355X_MICROARCH.md, visibility, first row of the sc1 table), summed in chunk order (deterministic).
+// The split backward's chunk hand-off without agent-scope fences: the partials are stored `sc1` (agent relaxed
+// atomic stores, 4 B), every storing wave waits vmcnt(0) before the barrier, lane 0 adds to the row's ticket, the
+// workgroup whose add returned NL - 1 reads the partials with `sc1` loads (agent relaxed atomic loads) after that add
+// returned / after the barrier: the first row of MI355X_MICROARCH.md's table of hand-offs measured valid without the
+// acquire, and with an `sc1` payload without the release (one workgroup per CU, hipMalloc'd workspace).  cfg5
+// (L = 196, two chunks per row) attention backward span 21.7 -> 19.8 us (profiles/r6_s64); 1 = the fenced form.
+#ifndef SAT_ATTN_FENCES
+#define SAT_ATTN_FENCES 0
+#endif
 // Diagnostics builds only (tools/build_variant.sh, -DSAT_ATTN_MARK=k): the attention backward's stamp records the time
 // every wave of the workgroup has reached phase boundary k instead of the kernel's end (bench.py's per-step spans then
 // measure start -> boundary k).  The product build defines no marker.
@@ -836,18 +845,21 @@ __device__ __forceinline__ void attn_bwd_split_kernel_body(AttnBwdArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its sc1 stores are done
   __syncthreads();
   if (tid == 0) {
-    // agent-scope release before the ticket (the payload is already write-through and drained -- MI355X_MICROARCH.md
-    // "Valid forms" -- the fence makes the hand-off a release / acquire pair under the memory model as well; the
-    // second wait keeps the compiler from dropping the fence's own, cdna_hip_programming.md Guideline 16 Pitfall 12)
+    // (SAT_ATTN_FENCES: an agent-scope release before the ticket; the second wait keeps the compiler from dropping
+    // the fence's own, cdna_hip_programming.md Guideline 16 Pitfall 12)
+#if SAT_ATTN_FENCES
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     const unsigned prev = __hip_atomic_fetch_add(a.ticket + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool last = prev == (unsigned)(NL - 1);
+#if SAT_ATTN_FENCES
     if (last) {   // agent-scope acquire on the reading CU besides the sc1 loads below (cdna_hip_programming.md §6
                   // Guideline 16): one fence per row's last arriver, only on the NL > 1 path (small batches)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+#endif
     s_last = last;
   }
   __syncthreads();

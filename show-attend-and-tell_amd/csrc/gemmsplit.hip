@@ -28,8 +28,19 @@
 #include "sat_common.h"
 #include "sat_internal.h"
 
-#ifndef SAT_SPLIT_RELEASE   // diagnostics builds: 0 = no release fence on the writers (sc1 payload only)
-#define SAT_SPLIT_RELEASE 1
+// The partial-tile hand-off without agent-scope fences: every partial is stored `sc1` (write-through, 16 B), every
+// storing wave waits vmcnt(0) before the workgroup barrier, one lane per workgroup then adds to the tile's ticket
+// (agent atomic), the workgroup whose add returned splits - 1 is the reader, and every load of the partials is a 16-B
+// `sc1` buffer load issued after that add returned (the other waves after the barrier the adding wave joins): the
+// first row of MI355X_MICROARCH.md's table of hand-offs measured valid with `sc1` loads in place of the acquire, whose
+// condition (2) makes the release redundant too (one workgroup per CU, hipMalloc'd workspace).  The fences cost a
+// `buffer_wbl2` / `buffer_inv` per tile: bench line 6.111-6.136 -> 6.069-6.088 ms with both hand-offs fence-free
+// (profiles/r6_s65, with the attention backward's); 1 = the fenced forms (A/B builds).
+#ifndef SAT_SPLIT_RELEASE
+#define SAT_SPLIT_RELEASE 0
+#endif
+#ifndef SAT_SPLIT_ACQUIRE
+#define SAT_SPLIT_ACQUIRE 0
 #endif
 #ifndef SAT_SPLIT_DEBUG     // diagnostics builds: 1 = record every ticket draw (tools/debug_split_tickets.py)
 #define SAT_SPLIT_DEBUG 0
@@ -300,10 +311,12 @@ __device__ __forceinline__ void split_gemm_body(const SArgs& a) {
         }
       }
 #endif
-      if (prev == (unsigned)(a.splits - 1)) {
-        // the last arriver: agent-scope acquire before it reads the other partial tiles
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (SAT_SPLIT_ACQUIRE) {
+        if (prev == (unsigned)(a.splits - 1)) {
+          // the last arriver: agent-scope acquire before it reads the other partial tiles
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
       }
       *flag = prev;
     }
