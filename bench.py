@@ -763,6 +763,7 @@ def main():
         stamped: every conv launch and every per-step decoder launch writes in-kernel timestamps (the diagnostic
         copies captured after the timed region; the timed graphs carry no stamp pointers at all)."""
         G = dict(enc=[], dec=[], rec=[], feats=[], loss=[], stamps_enc=[], stamps_dec=[])
+        one = torch.ones((), device=dev)
         for k in range(nbuf):
             if stamped:
                 G["stamps_enc"].append(LaunchStamps(len(launches), dev, base=policy))
@@ -783,7 +784,7 @@ def main():
             with torch.cuda.graph(gd, capture_error_mode=CAPTURE_MODE):
                 preds, alphas = dec(G["feats"][k], caps)
                 loss_k, _ = sat_amd.caption_loss(preds, alphas, caps, pad_id=pad_id, skip_ids=skip_ids)
-                loss_k.backward()
+                loss_k.backward(one)   # d loss / d loss = 1 from a constant made before capture (no fill node)
             if split_bwd:
                 gr = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gr, capture_error_mode=CAPTURE_MODE):

@@ -287,6 +287,12 @@ int sat_caption_loss_forward(int B, int T, int V, int L, int dtype, const void* 
                              const float* alphas, const int64_t* captions, float alpha_c,
                              int pad_id, int skip0, int skip1, int skip2, void* workspace,
                              float* out, void* stream);
+/* the same, the loss (out[0]) also written to loss_out (its own 4-byte buffer: the autograd wrapper hands it out
+ * as a tensor a caller may scale in place, without a device copy of out[0]) */
+int sat_caption_loss_forward_loss_out(int B, int T, int V, int L, int dtype, const void* preds,
+                                      const float* alphas, const int64_t* captions, float alpha_c,
+                                      int pad_id, int skip0, int skip1, int skip2, void* workspace,
+                                      float* out, float* loss_out, void* stream);
 int sat_caption_loss_backward(int B, int T, int V, int L, int dtype, const void* preds,
                               const int64_t* captions, float alpha_c, void* workspace,
                               const float* grad_out, void* d_preds, float* d_alphas, void* stream);

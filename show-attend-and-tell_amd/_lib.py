@@ -122,6 +122,9 @@ _SIGNATURES = [
     ("sat_caption_loss_workspace_bytes", c_size_t, [c_int, c_int, c_int]),
     ("sat_caption_loss_forward", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_float,
                                          c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    ("sat_caption_loss_forward_loss_out", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                                  c_float, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                                  c_void_p]),
     ("sat_caption_loss_backward", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float,
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("sat_caption_loss_backward_relu", c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float,

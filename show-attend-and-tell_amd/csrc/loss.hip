@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void loss_reg_kernel(const float* __restrict__
 __global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* __restrict__ stats, const float* __restrict__ part,
                                                            int nparts, const int64_t* __restrict__ caps, int B, int T,
                                                            int L, float alpha_c, int s0, int s1, int s2,
-                                                           float* __restrict__ out) {
+                                                           float* __restrict__ out, float* __restrict__ loss_out) {
   __shared__ float red[16];
   const int T1 = T - 1, R = B * T1;
   float ce = 0.f, c1 = 0.f, c5 = 0.f, np = 0.f;
@@ -276,6 +276,7 @@ __global__ __launch_bounds__(1024) void loss_reduce_kernel(const float* __restri
     const float cem = ce / (float)(B * (T1 - 1));
     const float regm = alpha_c * (reg * (1.0f / (float)(B * L)));
     out[0] = cem + regm;
+    if (loss_out) loss_out[0] = cem + regm;
     out[1] = cem;
     out[2] = regm;
     out[3] = c1; out[4] = c5; out[5] = np; out[6] = cl;
@@ -372,9 +373,10 @@ extern "C" size_t sat_caption_loss_workspace_bytes(int B, int T, int L) {
   return ((size_t)B * (T - 1) * kStat + (size_t)B * L + sat_cdiv((long)B * L, 256) + 64) * sizeof(float);
 }
 
-extern "C" int sat_caption_loss_forward(int B, int T, int V, int L, int dtype, const void* preds, const float* alphas,
-                                        const int64_t* captions, float alpha_c, int pad_id, int skip0, int skip1,
-                                        int skip2, void* workspace, float* out, void* stream) {
+namespace {
+int loss_forward(int B, int T, int V, int L, int dtype, const void* preds, const float* alphas, const int64_t* captions,
+                 float alpha_c, int pad_id, int skip0, int skip1, int skip2, void* workspace, float* out,
+                 float* loss_out, void* stream) {
   SAT_REQUIRE(preds && alphas && captions && workspace && out && B > 0 && T >= 3 && V > 0 && L > 0);
   hipStream_t s = (hipStream_t)stream;
   const int R = B * (T - 1);
@@ -393,8 +395,25 @@ extern "C" int sat_caption_loss_forward(int B, int T, int V, int L, int dtype, c
   hipLaunchKernelGGL(loss_reg_kernel, dim3(nparts), dim3(256), 0, s, alphas, B, T - 1, L, alpha_c, dreg, part);
   SAT_LAUNCH_CHECK();
   hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(1024), 0, s, stats, (const float*)part, nparts, captions, B, T,
-                     L, alpha_c, skip0, skip1, skip2, out);
+                     L, alpha_c, skip0, skip1, skip2, out, loss_out);
   return (int)hipGetLastError();
+}
+}  // namespace
+
+extern "C" int sat_caption_loss_forward(int B, int T, int V, int L, int dtype, const void* preds, const float* alphas,
+                                        const int64_t* captions, float alpha_c, int pad_id, int skip0, int skip1,
+                                        int skip2, void* workspace, float* out, void* stream) {
+  return loss_forward(B, T, V, L, dtype, preds, alphas, captions, alpha_c, pad_id, skip0, skip1, skip2, workspace, out,
+                      nullptr, stream);
+}
+
+extern "C" int sat_caption_loss_forward_loss_out(int B, int T, int V, int L, int dtype, const void* preds,
+                                                 const float* alphas, const int64_t* captions, float alpha_c,
+                                                 int pad_id, int skip0, int skip1, int skip2, void* workspace,
+                                                 float* out, float* loss_out, void* stream) {
+  SAT_REQUIRE(loss_out);
+  return loss_forward(B, T, V, L, dtype, preds, alphas, captions, alpha_c, pad_id, skip0, skip1, skip2, workspace, out,
+                      loss_out, stream);
 }
 
 namespace {

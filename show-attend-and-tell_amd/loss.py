@@ -24,6 +24,8 @@ class _CaptionLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, preds, alphas, captions, alpha_c, pad_id, skip):
         L.require_device(preds, alphas, captions)
+        # no zero-filled gradient for the metrics output (non-differentiable): one fill launch less per backward
+        ctx.set_materialize_grads(False)
         B, T1, V = preds.shape
         T = captions.shape[1]
         if T1 != T - 1 or alphas.shape[:2] != (B, T1):
@@ -32,18 +34,20 @@ class _CaptionLossFn(torch.autograd.Function):
         lib = L.lib()
         ws = torch.empty(lib.sat_caption_loss_workspace_bytes(B, T, Lf), device=preds.device, dtype=torch.uint8)
         out = torch.empty(8, device=preds.device, dtype=torch.float32)
+        # the loss in its own 4-byte tensor (a caller may scale it in place: gradient accumulation, loss.mul_ -- a
+        # view of a custom Function's output buffer would make autograd reject that), written by the kernel itself
+        loss = torch.empty((), device=preds.device, dtype=torch.float32)
         preds_c, alphas_c, caps = preds.contiguous(), alphas.contiguous().float(), captions.contiguous().long()
-        L.check(lib.sat_caption_loss_forward(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds_c), L.ptr(alphas_c),
-                                             L.ptr(caps), float(alpha_c), int(pad_id), int(skip[0]), int(skip[1]),
-                                             int(skip[2]), L.ptr(ws), L.ptr(out), L.stream_of(out)),
+        L.check(lib.sat_caption_loss_forward_loss_out(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds_c),
+                                                      L.ptr(alphas_c), L.ptr(caps), float(alpha_c), int(pad_id),
+                                                      int(skip[0]), int(skip[1]), int(skip[2]), L.ptr(ws), L.ptr(out),
+                                                      L.ptr(loss), L.stream_of(out)),
                 "sat_caption_loss_forward")
         ctx.save_for_backward(preds_c, caps)
         ctx.ws, ctx.dims, ctx.alpha_c = ws, (B, T, V, Lf), float(alpha_c)
         ctx.relu = bool(getattr(preds, "_sat_relu_logits", False))   # set by sat_amd.Decoder (ado)
-        # metrics: a view of the kernel's output (never modified by callers); loss: its own 4-byte tensor, so a
-        # caller may scale it in place (gradient accumulation, loss.mul_) -- a view of a custom Function's output
-        # buffer would make autograd reject that
-        loss, metrics = out[0].clone(), out[1:7]
+        # metrics: a view of the kernel's output (never modified by callers)
+        metrics = out[1:7]
         ctx.mark_non_differentiable(metrics)
         return loss, metrics
 

@@ -461,6 +461,36 @@ def test_caption_loss_relu_fused_mask(sat):
     assert (grads[0] * (1 - mask)).abs().sum() > 0   # the plain gradient is not masked
 
 
+def test_caption_loss_forward_loss_out(sat):
+    """sat_caption_loss_forward_loss_out writes out[0..6] exactly as sat_caption_loss_forward and the loss also into its
+    own buffer (caption_loss's loss tensor, no device copy of out[0]); the autograd loss is a separate tensor a caller
+    may scale in place."""
+    from sat_amd import _lib as L
+    torch.manual_seed(2)
+    B, T, Lf, V = 4, 7, 49, 1000
+    preds = torch.randn(B, T - 1, V, device=DEV).bfloat16()
+    alphas = torch.softmax(torch.randn(B, T - 1, Lf, device=DEV), -1)
+    caps = torch.randint(0, V, (B, T), device=DEV)
+    lib = L.lib()
+    ws = torch.empty(lib.sat_caption_loss_workspace_bytes(B, T, Lf), device=DEV, dtype=torch.uint8)
+    out_a, out_b = torch.empty(8, device=DEV), torch.empty(8, device=DEV)
+    loss = torch.full((), float("nan"), device=DEV)
+    L.check(lib.sat_caption_loss_forward(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds), L.ptr(alphas),
+                                         L.ptr(caps), 1.0, 3, 3, 0, 1, L.ptr(ws), L.ptr(out_a), None), "fwd")
+    L.check(lib.sat_caption_loss_forward_loss_out(B, T, V, Lf, L.dtype_code(preds.dtype), L.ptr(preds), L.ptr(alphas),
+                                                  L.ptr(caps), 1.0, 3, 3, 0, 1, L.ptr(ws), L.ptr(out_b), L.ptr(loss),
+                                                  None), "fwd loss_out")
+    torch.cuda.synchronize()
+    assert torch.equal(out_a[:7], out_b[:7])
+    assert torch.equal(loss, out_a[0])
+    p = preds.clone().requires_grad_(True)
+    l2, metrics = sat.caption_loss(p, alphas, caps)
+    assert torch.equal(l2.detach(), out_a[0]) and torch.equal(metrics, out_a[1:7])
+    l2.mul_(0.5)   # its own storage: in-place scaling is allowed
+    l2.backward()
+    assert p.grad is not None and torch.isfinite(p.grad.float()).all()
+
+
 @pytest.mark.parametrize("V", [30522, 1003, 1000])
 @pytest.mark.parametrize("relu", [False, True])
 def test_caption_loss_backward_padded_rows(sat, V, relu):
