@@ -55,6 +55,7 @@ def host_dropout_masks(seed, B, T1, E):
 
 def _greedy_seeded(sat, c, form):
     """A bf16 greedy train-mode forward + backward with dropout drawn from the decoder's seed (no injected mask)."""
+    torch.manual_seed(1234)   # the decoder's dropout seed is drawn from torch's generator: one draw for every process
     dec = S._decoder(sat, c).train()
     dec.policy = sat.Policy(greedy_step=form)
     caps = c["caps"].to(DEV)
@@ -73,10 +74,12 @@ def _greedy_seeded(sat, c, form):
 # bounds against the bf16 rounding mirror of the oracle (oracle/sat_oracle.py bf16_mirror, fp64) at these B <= 4, T = 6-8
 # cases: measured <= 2.4e-3 per parameter (profiles/r6_s3/py_1_debug_greedy.log: both forms, seeded and injected masks,
 # with and without the ado head); against the plain fp32 oracle the same steps differ by up to 0.2 for some seeds
-# (bf16 rounding of the ReLU'd logits near zero), which is why the mirror is the reference here.  Until r6_s55 the
-# step was not bit-reproducible at these batches (a one-split per-step product on fp32 atomics) and a
-# flipped bf16 rounding moved the head's gradients by up to 1.9e-2 (profiles/r6_s29, r6_s30); it is deterministic now
-MIRROR_TOL = 1e-2
+# (bf16 rounding of the ReLU'd logits near zero), which is why the mirror is the reference here.  The step is
+# bit-reproducible run to run, but with dropout drawn from the decoder's seed the error depends on the
+# draw: where a draw flips a bf16 rounding of a per-step operand the head and LSTM gradients move by up to 2.9e-2
+# ([True-1], profiles/r6_s70: torch's default generator is seeded per process here, so each process drew other
+# masks; profiles/r6_s71: 1 of 3 processes) -- hence 3e-2, and _greedy_seeded now fixes the draw
+MIRROR_TOL = 3e-2
 
 
 def _mirror_fed(c, tokens):
