@@ -118,6 +118,16 @@ inline Splits splits_for(const SatDecoderDims& d, bool tr) {
     // against 256-deep, profiles/r3_s11_decoder_splits.txt)
     if (tr && (k = sat_skinny_splits(d.B, D, 4 * E)) && (4 * E) % 512 == 0) s.g = k / 2;
     if (tr && (k = sat_skinny_splits(d.B, E, KH)) && KH % 512 == 0) s.dh = k / 2;
+    // dL/dh has only E / 32 column blocks (16 at E = 512): 512-deep splits left 112 of 256 CUs idle at K = 4608
+    // (ResNet152 features, 144 workgroups).  There the most 128-multiple-deep splits that keep the launch within one
+    // workgroup per CU (and the LSTM backward's up-front slab loads, <= 16): 12 (192 workgroups), span 7.33 -> 6.40 us
+    // at B = 128, 4.71 -> 4.04 at B = 64 (profiles/r6_s77, r6_s78).  At K = 3072 (VGG19, 6 -> 12 splits) it measured
+    // slower (10.85 -> 10.97 us, the cfg5 chain +2.7 us), so only K >= 4096 takes it.
+    if (tr && s.dh > 1 && KH % 128 == 0 && KH >= 4096) {
+      const int cols = E / 32, kt = KH / 128;
+      for (int c = 16; c > s.dh; --c)
+        if (kt % c == 0 && c * cols <= 256 && KH / c <= 1024) { s.dh = c; break; }
+    }
   }
   if (bf) {   // per-call overrides (SatPolicy::decoder_splits, 0 = automatic)
     const int* f = sat_policy().decoder_splits;

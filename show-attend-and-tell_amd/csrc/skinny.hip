@@ -157,9 +157,12 @@ bool skinny_shape(const SatGemm& g, int mode, SkArgs* a, int* nw) {
   // whole 256-deep slabs: the context GEMM 9.2 vs 10.9 us per step; the backward's products through the
   // transposed weight copies); the [U; f_beta; W_hh] h GEMM (one split) stays on the tile kernel (8.2 vs 8.6
   // us: with K = 512 every workgroup reads all of A); mode 2: every eligible problem (tests)
-  if (mode == 0 && !(g.partial_splits > 1 && g.K % g.partial_splits == 0 && (g.K / g.partial_splits) % 256 == 0 &&
-                     g.K / g.partial_splits <= 1024))
-    return false;
+  // (and, for narrow products, N <= 1024, 128-multiple-deep ones from 256 on: dL/dh at K = 4608 over 12, r6_s78;
+  // the wide h GEMM keeps 256-multiples -- cfg5's, K = 768 over 2, was 7.25 vs 9.58 us as a 384-deep skinny product)
+  if (mode == 0) {
+    const int kd = g.partial_splits > 1 && g.K % g.partial_splits == 0 ? g.K / g.partial_splits : 0;
+    if (!(kd > 0 && kd <= 1024 && (kd % 256 == 0 || (kd % 128 == 0 && kd >= 256 && g.N <= 1024)))) return false;
+  }
   if (g.dtype != SAT_BF16 || g.c_dtype != SAT_F32 || g.batch != 1 || g.conv.C > 0) return false;
   if (g.transA || g.transB || g.aux || g.add1 || g.act != SAT_ACT_NONE || g.beta != 0.f || g.alpha != 1.f) return false;
   if (g.M < 1 || g.M > 128 || g.N % SK_COLS || g.K % 32 || g.K <= 0) return false;
